@@ -1,0 +1,152 @@
+/*
+ * icp_capi.h — C-ABI of the MI355X-native ICP engine (libicp_hip.so).
+ *
+ * Drop-in boundary for the reference's src/GPU layer (yassram/iterative-closest-point).
+ * The reference exposes C++ free functions over Eigen matrices (src/GPU/gpu.hh:110-116)
+ * and the GPU::ICP class (src/GPU/gpu.hh:41-104).  This header replaces them with plain
+ * pointers + sizes; INTEGRATION.md shows the shim a maintainer adds to src/GPU so that
+ * host code written against gpu.hh relinks unchanged.
+ *
+ * Data layout at the boundary: a cloud of n points is 3 x n column-major doubles, i.e.
+ * interleaved xyz (Eigen MatrixXd::data() of the reference's 3 x n matrices):
+ * point j = (a[3j], a[3j+1], a[3j+2]).  Device layout is private to the engine.
+ *
+ * Errors: every entry point returns ICP_OK (0) or a negative ICP_E_* code; the library
+ * never calls exit().  icp_last_error(ctx) gives a message.  Calls are synchronous
+ * (results are on the host when the call returns) and not re-entrant per context.
+ */
+#ifndef ICP_CAPI_H
+#define ICP_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------- */
+#define ICP_OK 0
+#define ICP_E_ARG (-1)            /* bad argument / null pointer                    */
+#define ICP_E_HIP (-2)            /* HIP runtime failure (message in icp_last_error) */
+#define ICP_E_SIZE_MISMATCH (-3)  /* np != nm      (src/cpu.cc:44-47, src/GPU/gpu.cc:54-57) */
+#define ICP_E_TOO_FEW_POINTS (-4) /* np < 4        (src/cpu.cc:49-52, src/GPU/gpu.cc:59-62) */
+#define ICP_E_NO_MODEL (-5)       /* icp_set_model / icp_set_scene not called        */
+#define ICP_E_RCCL (-6)           /* RCCL failure                                   */
+#define ICP_E_NO_DEVICE (-7)      /* no HIP device / bad device ordinal             */
+#define ICP_E_IO (-8)             /* file could not be opened (src/load.cc:11-14)   */
+#define ICP_E_RANGE (-9)          /* coordinates outside the engine's domain        */
+
+/* ---- nearest-neighbour arithmetic -------------------------------------- */
+/* Both modes return the SAME indices: the first (lowest-index) minimum of the fp64
+ * squared distance ((dx*dx + dy*dy) + dz*dz) — the reference's opti GPU rule
+ * (src/GPU/compute.cu:112-117,137) == CPU minCoeff first-min (src/cpu.cc:22).       */
+#define ICP_NN_CERTIFIED 0 /* fp32 filter + per-query certificate + fp64 resolution (fast) */
+#define ICP_NN_FP64 1      /* fp64 brute force (reference-faithful cross-check)           */
+
+typedef struct icp_ctx icp_ctx;
+
+typedef struct icp_result {
+    int iterations; /* ICP iterations executed                                       */
+    int converged;  /* 1 if err < threshold stopped the loop (src/GPU/gpu.cc:79-80)   */
+    double err;     /* last err = (e_align + e_apply) / np, as printed (gpu.cc:76)    */
+    double s;       /* last increment's scale       (GPU::ICP::s, gpu.hh:91)          */
+    double R[9];    /* last increment's rotation, row-major (GPU::ICP::r, gpu.hh:93)  */
+    double t[3];    /* last increment's translation (GPU::ICP::t, gpu.hh:92)          */
+} icp_result;
+
+typedef struct icp_stats {
+    double nn_ms;          /* summed device time of the NN search kernels (HIP events) */
+    long long nn_launches; /* number of NN searches timed                               */
+    long long nn_pairs;    /* sum over searches of np_local * nm                        */
+    long long ambiguous;   /* queries the fp32 certificate sent to fp64 resolution      */
+    double iter_ms;        /* host wall time inside icp_run                             */
+    long long iterations;  /* iterations executed by icp_run                            */
+} icp_stats;
+
+/* ---- context ------------------------------------------------------------ */
+/* Single-GPU context on HIP device `device` (replaces the stateless wrappers of
+ * src/GPU/compute.cu, which re-allocate and re-upload everything per call). */
+int icp_ctx_create(int device, int nn_mode, icp_ctx **out);
+
+/* One rank of a world_size-rank job (one process per GPU).  The scene is sharded,
+ * the model replicated; per iteration the partial centroid / cross-covariance / error
+ * sums are all-reduced with RCCL.  `rccl_id` = 128 bytes from icp_rccl_unique_id() on
+ * rank 0, broadcast to all ranks by the caller. */
+int icp_ctx_create_dist(int device, int nn_mode, int rank, int world_size, const void *rccl_id,
+                        icp_ctx **out);
+int icp_rccl_unique_id(void *out128);
+void icp_ctx_destroy(icp_ctx *ctx);
+const char *icp_last_error(const icp_ctx *ctx);
+const char *icp_strerror(int code);
+int icp_device_count(int *count);
+
+/* ---- resident clouds (GPU::ICP constructor, src/GPU/gpu.hh:44-56) -------- */
+/* Model ("ref", m) is uploaded once and replicated on every rank. */
+int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm);
+/* Scene ("transform", p): this rank's np_local points of an np_total-point cloud.
+ * Resets new_p = p (gpu.hh:47).  Single-GPU: np_local == np_total. */
+int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total);
+/* Copy this rank's current new_p (gpu.hh:88) back to the host. */
+int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
+/* Reference behaviour is to refuse np != nm (gpu.cc:54-57); 1 lifts that check. */
+int icp_set_allow_unequal(icp_ctx *ctx, int allow);
+
+/* ---- the ICP loop: GPU::ICP::find_corresponding_opti (src/GPU/gpu.cc:52-83) -- */
+/* Runs up to max_iter iterations on the resident clouds; stops after the iteration
+ * whose err < threshold (pass threshold < 0 to run exactly max_iter iterations).
+ * err_trace (nullable, length max_iter) receives every iteration's err.
+ * Returns ICP_E_SIZE_MISMATCH / ICP_E_TOO_FEW_POINTS like the reference's checks. */
+int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res);
+
+/* ---- per-operation surface (src/GPU/gpu.hh:110-116) ---------------------- */
+/* compute_Y_w_opti (compute.cu:154-245): Y[:, j] = m[:, NN(p_j)] on the resident model.
+ * y_xyz_out and idx_out are each nullable. */
+int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_xyz_out,
+                       int32_t *idx_out);
+/* rowwise().mean() + substract_col_w (gpu.cc:98-102, compute.cu:381-416):
+ * mu = mean of the n points; centred_out (nullable) = points - mu. */
+int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3],
+                         double *centred_out);
+/* y_p_norm_w (compute.cu:418-469): d_caps = sum ||y_j||^2, sp = sum ||p_j||^2 */
+int icp_y_p_norm(icp_ctx *ctx, const double *y_xyz, const double *p_xyz, size_t n,
+                 double *d_caps, double *sp);
+/* compute_err_w (compute.cu:315-379): q_j = sR p_j + t; returns sum ||y_j - q_j||^2;
+ * if in_place, p_xyz is overwritten with q (the reference writes p back, :367-368).
+ * sR is the row-major 3x3 product s*R, t a 3-vector. */
+int icp_err_compute(icp_ctx *ctx, const double *y_xyz, double *p_xyz, size_t n, int in_place,
+                    const double sR[9], const double t[3], double *err);
+/* ICP::find_alignment (gpu.cc:95-151): Horn's closed form aligning p onto y.
+ * Outputs s, R (row-major), t and err = sum ||y - (sRp + t)||^2 (p is not modified). */
+int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, size_t n,
+                       double *s, double R[9], double t[3], double *err);
+
+/* ---- host-only helpers (no device work) --------------------------------- */
+/* The host half of find_alignment (gpu.cc:104-146) from the reduced sums:
+ * S = sum p' y'^T (row-major), mu_p, mu_y, d_caps = sum ||y'||^2, sp = sum ||p'||^2. */
+int icp_horn_solve(const double S[9], const double mu_p[3], const double mu_y[3], double d_caps,
+                   double sp, double *s, double R[9], double t[3]);
+/* max_element_index (gpu.cc:85-93) exactly as the reference writes it. */
+int icp_max_element_index(const double ev[4]);
+/* Contiguous shard of the scene for `rank` of `world_size` (first n % w ranks get +1). */
+int icp_shard_range(size_t n_total, int rank, int world_size, size_t *begin, size_t *count);
+/* Synthetic pair: n model points uniform in [-1,1]^3 from
+ * std::mt19937_64(seed), rounded to fp32-representable doubles; scene = R(axis,angle) m + t
+ * (computed in fp64, then rounded to fp32), same point order. */
+int icp_synthetic_pair(uint64_t seed, size_t n, double angle_deg, const double axis[3],
+                       const double t[3], double *model_xyz_out, double *scene_xyz_out);
+/* load_matrix (src/load.cc:3-33): n = #lines - 1, header skipped, "%lf,%lf,%lf" per row.
+ * *xyz_out is allocated with malloc; release with icp_free.  ICP_E_IO if unopenable. */
+int icp_load_matrix(const char *path, double **xyz_out, size_t *n_out);
+/* write_matrix (src/load.cc:68-81): header + 6-significant-digit rows. */
+int icp_write_matrix(const char *path, const double *xyz, size_t n);
+void icp_free(void *p);
+
+/* ---- instrumentation ----------------------------------------------------- */
+int icp_get_stats(const icp_ctx *ctx, icp_stats *out);
+int icp_reset_stats(icp_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICP_CAPI_H */

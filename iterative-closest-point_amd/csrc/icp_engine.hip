@@ -1,0 +1,674 @@
+// icp_engine.hip — the device-resident ICP engine behind include/icp_capi.h.
+//
+// Replaces the reference's src/GPU layer: GPU::ICP::find_corresponding_opti
+// (src/GPU/gpu.cc:52-83), GPU::ICP::find_alignment (gpu.cc:95-151) and the wrappers of
+// src/GPU/compute.cu.  Differences in structure (same results):
+//  * clouds live in HBM for the context's lifetime (the reference re-allocates and
+//    re-uploads the model every call, compute.cu:160);
+//  * the NN search is one fused pass + a tiny exact-resolution pass, no N x M matrix
+//    (compute.cu:176-203 materialises batch x M fp64 distances);
+//  * per iteration only 18 fp64 sums cross PCIe (the reference round-trips whole clouds
+//    ~30 times per iteration);
+//  * multi-GPU: the scene is sharded across ranks, the sums are all-reduced with RCCL.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "icp_kernels.h"
+
+using namespace icp;
+
+namespace {
+
+struct DevCloud {
+    double *x = nullptr, *y = nullptr, *z = nullptr;
+    float4 *f = nullptr;
+    size_t n = 0, cap = 0;
+};
+
+} // namespace
+
+struct icp_ctx {
+    int device = 0;
+    int nn_mode = ICP_NN_CERTIFIED;
+    int rank = 0, world = 1;
+    bool allow_unequal = false;
+    hipStream_t st = nullptr;
+    ncclComm_t comm = nullptr;
+
+    // model (replicated)
+    DevCloud model;
+    float4 *m32 = nullptr; // centred fp32 model, padded to nm_pad with far points
+    size_t nm = 0, nm_pad = 0, m32_cap = 0;
+    double c[3] = {0, 0, 0}; // centring point = model centroid
+    double rm = 0.0;         // max |centred fp32 model coordinate|
+    bool has_model = false;
+
+    // scene (this rank's shard), its correspondences
+    DevCloud scene, Y;
+    size_t np_total = 0;
+    bool has_scene = false;
+
+    // scratch clouds for the per-operation surface
+    DevCloud qa, qb;
+
+    // NN workspace
+    int *idx = nullptr;
+    size_t idx_cap = 0;
+    void *part = nullptr;
+    size_t part_cap = 0;
+    int *amb_count = nullptr, *amb_list = nullptr;
+    double *amb_T = nullptr;
+    size_t amb_cap = 0;
+
+    // reductions
+    double *partials = nullptr;
+    double *sums = nullptr;
+    double *h_sums = nullptr; // pinned
+    int *h_amb = nullptr;     // pinned
+    double *stage = nullptr;
+    size_t stage_cap = 0;
+
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    icp_stats stats{};
+    std::string err;
+};
+
+namespace {
+
+int fail(icp_ctx *ctx, int code, const std::string &msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(ctx, ICP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+#define LAUNCHCHK(what)                                                                       \
+    do {                                                                                      \
+        hipError_t e_ = hipGetLastError();                                                    \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(ctx, ICP_E_HIP, std::string(what) + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+#define TRY(expr)                                                                             \
+    do {                                                                                      \
+        int rc_ = (expr);                                                                     \
+        if (rc_ != ICP_OK) return rc_;                                                        \
+    } while (0)
+
+#define RCCLCHK(expr)                                                                         \
+    do {                                                                                      \
+        ncclResult_t r_ = (expr);                                                             \
+        if (r_ != ncclSuccess)                                                                \
+            return fail(ctx, ICP_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+template <class T> int grow(icp_ctx *ctx, T **p, size_t *cap, size_t count)
+{
+    if (*cap >= count && *p) return ICP_OK;
+    if (*p) HIPCHK(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    size_t bytes = sizeof(T) * (count ? count : 1);
+    HIPCHK(hipMalloc((void **)p, bytes));
+    *cap = count;
+    return ICP_OK;
+}
+
+int grow_cloud(icp_ctx *ctx, DevCloud &c, size_t n, bool with_f32)
+{
+    if (c.cap < n || !c.x || (with_f32 && !c.f)) {
+        for (void *p : {(void *)c.x, (void *)c.y, (void *)c.z, (void *)c.f})
+            if (p) HIPCHK(hipFree(p));
+        c = DevCloud{};
+        const size_t m = n ? n : 1;
+        HIPCHK(hipMalloc((void **)&c.x, sizeof(double) * m));
+        HIPCHK(hipMalloc((void **)&c.y, sizeof(double) * m));
+        HIPCHK(hipMalloc((void **)&c.z, sizeof(double) * m));
+        HIPCHK(hipMalloc((void **)&c.f, sizeof(float4) * m));
+        c.cap = m;
+    }
+    c.n = n;
+    return ICP_OK;
+}
+
+void free_cloud(DevCloud &c)
+{
+    for (void *p : {(void *)c.x, (void *)c.y, (void *)c.z, (void *)c.f})
+        if (p) (void)hipFree(p);
+    c = DevCloud{};
+}
+
+// host AoS (3 x n col-major) -> device SoA fp64 (+ centred fp32 copy)
+int upload_cloud(icp_ctx *ctx, DevCloud &c, const double *xyz, size_t n, bool make_f32)
+{
+    TRY(grow_cloud(ctx, c, n, true));
+    if (!n) return ICP_OK;
+    TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * n));
+    HIPCHK(hipMemcpyAsync(ctx->stage, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice, ctx->st));
+    launch_aos_to_soa(ctx->stage, n, c.x, c.y, c.z, ctx->st);
+    if (make_f32) launch_make_f32(c.x, c.y, c.z, n, ctx->c[0], ctx->c[1], ctx->c[2], c.f, ctx->st);
+    LAUNCHCHK("upload_cloud");
+    return ICP_OK;
+}
+
+int download_cloud(icp_ctx *ctx, const DevCloud &c, size_t n, double *xyz)
+{
+    if (!n) return ICP_OK;
+    TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * n));
+    launch_soa_to_aos(c.x, c.y, c.z, n, ctx->stage, ctx->st);
+    LAUNCHCHK("download_cloud");
+    HIPCHK(hipMemcpyAsync(xyz, ctx->stage, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    return ICP_OK;
+}
+
+int ensure_reduction_space(icp_ctx *ctx)
+{
+    if (ctx->partials) return ICP_OK;
+    HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocks * 12));
+    HIPCHK(hipMalloc((void **)&ctx->sums, sizeof(double) * 32));
+    HIPCHK(hipHostMalloc((void **)&ctx->h_sums, sizeof(double) * 32, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));
+    return ICP_OK;
+}
+
+// queue of queries the fp32 certificate could not settle (list + window T + counter)
+int ensure_queue(icp_ctx *ctx, size_t n)
+{
+    if (!ctx->amb_count) HIPCHK(hipMalloc((void **)&ctx->amb_count, sizeof(int) * 4));
+    if (ctx->amb_cap >= n && ctx->amb_list) return ICP_OK;
+    if (ctx->amb_list) HIPCHK(hipFree(ctx->amb_list));
+    if (ctx->amb_T) HIPCHK(hipFree(ctx->amb_T));
+    ctx->amb_list = nullptr;
+    ctx->amb_T = nullptr;
+    ctx->amb_cap = 0;
+    const size_t m = n ? n : 1;
+    HIPCHK(hipMalloc((void **)&ctx->amb_list, sizeof(int) * m));
+    HIPCHK(hipMalloc((void **)&ctx->amb_T, sizeof(double) * m));
+    ctx->amb_cap = m;
+    return ICP_OK;
+}
+
+// NN search of the n queries in q against the resident model -> ctx->idx[0..n).
+// Timed with HIP events on the context stream (ev[0]..ev[1] = the O(N*M) kernel).
+int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
+{
+    TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
+    if (!n) return ICP_OK;
+    if (ctx->nn_mode == ICP_NN_FP64) {
+        const NNPlan pl = plan_nn64(n, ctx->nm);
+        const size_t need = (size_t)pl.splits * n * (sizeof(double) + sizeof(int));
+        TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap, need));
+        double *pb = (double *)ctx->part;
+        int *pi = (int *)(pb + (size_t)pl.splits * n);
+        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        launch_nn_fp64(q.x, q.y, q.z, (int)n, ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm,
+                       pl, pb, pi, ctx->st);
+        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
+        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
+        LAUNCHCHK("nn_fp64");
+    } else {
+        const NNPlan pl = plan_nn32(n, ctx->nm_pad);
+        const size_t need = (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int));
+        TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap, need));
+        float *pb = (float *)ctx->part;
+        float *ps = pb + (size_t)pl.splits * n;
+        int *pi = (int *)(ps + (size_t)pl.splits * n);
+        TRY(ensure_queue(ctx, n));
+        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int), ctx->st));
+        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        CertParams cp{ctx->rm};
+        launch_nn_finalize(pb, ps, pi, pl.splits, q.f, (int)n, cp, ctx->idx, ctx->amb_count,
+                           ctx->amb_list, ctx->amb_T, ctx->st);
+        launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx,
+                          ctx->st);
+        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
+        LAUNCHCHK("nn_certified");
+    }
+    return ICP_OK;
+}
+
+// after the stream has been synchronised: fold the NN events into the stats
+void account_nn(icp_ctx *ctx, size_t n)
+{
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->stats.nn_ms += ms;
+    ctx->stats.nn_launches += 1;
+    ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
+}
+
+int allreduce(icp_ctx *ctx, double *buf, size_t count)
+{
+    if (ctx->world <= 1 || !ctx->comm) return ICP_OK;
+    RCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, ctx->st));
+    return ICP_OK;
+}
+
+int check_ready(icp_ctx *ctx, bool need_scene)
+{
+    if (!ctx) return ICP_E_ARG;
+    if (!ctx->has_model || (need_scene && !ctx->has_scene))
+        return fail(ctx, ICP_E_NO_MODEL, "model/scene not set (icp_set_model / icp_set_scene)");
+    HIPCHK(hipSetDevice(ctx->device));
+    return ensure_reduction_space(ctx);
+}
+
+} // namespace
+
+// ===================================================================================
+extern "C" {
+
+int icp_device_count(int *count)
+{
+    if (!count) return ICP_E_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return ICP_OK;
+}
+
+static int ctx_init(icp_ctx *ctx)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(ctx, ICP_E_NO_DEVICE, "no HIP device visible");
+    if (ctx->device < 0 || ctx->device >= ndev)
+        return fail(ctx, ICP_E_NO_DEVICE, "device ordinal out of range");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking));
+    for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e));
+    return ensure_reduction_space(ctx);
+}
+
+int icp_ctx_create(int device, int nn_mode, icp_ctx **out)
+{
+    if (!out || (nn_mode != ICP_NN_CERTIFIED && nn_mode != ICP_NN_FP64)) return ICP_E_ARG;
+    *out = nullptr;
+    icp_ctx *ctx = new icp_ctx();
+    ctx->device = device;
+    ctx->nn_mode = nn_mode;
+    int rc = ctx_init(ctx);
+    if (rc != ICP_OK) {
+        icp_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return ICP_OK;
+}
+
+int icp_rccl_unique_id(void *out128)
+{
+    if (!out128) return ICP_E_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return ICP_E_RCCL;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(out128, &id, sizeof(id));
+    return ICP_OK;
+}
+
+int icp_ctx_create_dist(int device, int nn_mode, int rank, int world_size, const void *rccl_id,
+                        icp_ctx **out)
+{
+    if (!out || world_size < 1 || rank < 0 || rank >= world_size ||
+        (nn_mode != ICP_NN_CERTIFIED && nn_mode != ICP_NN_FP64) || (world_size > 1 && !rccl_id))
+        return ICP_E_ARG;
+    *out = nullptr;
+    icp_ctx *ctx = new icp_ctx();
+    ctx->device = device;
+    ctx->nn_mode = nn_mode;
+    ctx->rank = rank;
+    ctx->world = world_size;
+    int rc = ctx_init(ctx);
+    if (rc == ICP_OK && world_size > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, rccl_id, sizeof(id));
+        ncclResult_t r = ncclCommInitRank(&ctx->comm, world_size, id, rank);
+        if (r != ncclSuccess) rc = fail(ctx, ICP_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    if (rc != ICP_OK) {
+        icp_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return ICP_OK;
+}
+
+void icp_ctx_destroy(icp_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->st) (void)hipStreamSynchronize(ctx->st);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    free_cloud(ctx->model);
+    free_cloud(ctx->scene);
+    free_cloud(ctx->Y);
+    free_cloud(ctx->qa);
+    free_cloud(ctx->qb);
+    for (void *p : {(void *)ctx->m32, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
+                    (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
+                    (void *)ctx->sums, (void *)ctx->stage})
+        if (p) (void)hipFree(p);
+    if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
+    if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->st) (void)hipStreamDestroy(ctx->st);
+    delete ctx;
+}
+
+const char *icp_last_error(const icp_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int icp_set_allow_unequal(icp_ctx *ctx, int allow)
+{
+    if (!ctx) return ICP_E_ARG;
+    ctx->allow_unequal = allow != 0;
+    return ICP_OK;
+}
+
+int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
+{
+    if (!ctx || (!m_xyz && nm) || nm == 0) return ICP_E_ARG;
+    if (nm > (size_t)0x7fffffff - kTile32) return fail(ctx, ICP_E_ARG, "model too large");
+    HIPCHK(hipSetDevice(ctx->device));
+    // centring point c = model centroid (any c is valid for the certificate; the centroid
+    // keeps |coordinates| and hence the fp32 error bound small)
+    double s[3] = {0, 0, 0};
+    for (size_t j = 0; j < nm; ++j)
+        for (int k = 0; k < 3; ++k) s[k] += m_xyz[3 * j + k];
+    for (int k = 0; k < 3; ++k) ctx->c[k] = s[k] / (double)nm;
+    // centred fp32 model, padded to a whole number of LDS tiles with far points
+    const size_t nm_pad = (nm + kTile32 - 1) / kTile32 * kTile32;
+    std::vector<float4> h(nm_pad);
+    double rm = 0.0;
+    for (size_t j = 0; j < nm; ++j) {
+        float4 v;
+        v.x = (float)(m_xyz[3 * j] - ctx->c[0]);
+        v.y = (float)(m_xyz[3 * j + 1] - ctx->c[1]);
+        v.z = (float)(m_xyz[3 * j + 2] - ctx->c[2]);
+        v.w = 0.f;
+        if (!std::isfinite(v.x) || !std::isfinite(v.y) || !std::isfinite(v.z))
+            return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
+        rm = std::fmax(rm, std::fmax(std::fabs((double)v.x), std::fmax(std::fabs((double)v.y), std::fabs((double)v.z))));
+        h[j] = v;
+    }
+    if (rm > 1e15) return fail(ctx, ICP_E_RANGE, "model coordinates exceed 1e15 around the centroid");
+    for (size_t j = nm; j < nm_pad; ++j) h[j] = make_float4(1.0e18f, 1.0e18f, 1.0e18f, 0.f);
+    ctx->rm = rm;
+    TRY(grow(ctx, &ctx->m32, &ctx->m32_cap, nm_pad));
+    HIPCHK(hipMemcpyAsync(ctx->m32, h.data(), sizeof(float4) * nm_pad, hipMemcpyHostToDevice, ctx->st));
+    TRY(upload_cloud(ctx, ctx->model, m_xyz, nm, false));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    ctx->nm = nm;
+    ctx->nm_pad = nm_pad;
+    ctx->has_model = true;
+    // the scene's fp32 copy depends on c: refresh it
+    if (ctx->has_scene && ctx->scene.n) {
+        launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1],
+                        ctx->c[2], ctx->scene.f, ctx->st);
+        LAUNCHCHK("make_f32");
+        HIPCHK(hipStreamSynchronize(ctx->st));
+    }
+    return ICP_OK;
+}
+
+int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total)
+{
+    if (!ctx || (!p_xyz && np_local) || np_local > np_total) return ICP_E_ARG;
+    if (np_total > (size_t)0x7fffffff) return fail(ctx, ICP_E_ARG, "scene too large");
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    TRY(upload_cloud(ctx, ctx->scene, p_xyz, np_local, true));
+    TRY(grow_cloud(ctx, ctx->Y, np_local, false));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    ctx->np_total = np_total;
+    ctx->has_scene = true;
+    return ICP_OK;
+}
+
+int icp_get_scene(icp_ctx *ctx, double *p_xyz_out)
+{
+    if (!ctx || (!p_xyz_out && ctx->scene.n)) return ICP_E_ARG;
+    if (!ctx->has_scene) return fail(ctx, ICP_E_NO_MODEL, "scene not set");
+    HIPCHK(hipSetDevice(ctx->device));
+    return download_cloud(ctx, ctx->scene, ctx->scene.n, p_xyz_out);
+}
+
+int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res)
+{
+    TRY(check_ready(ctx, true));
+    // alignement_check (gpu.cc:54-62)
+    if (ctx->np_total != ctx->nm && !ctx->allow_unequal)
+        return fail(ctx, ICP_E_SIZE_MISMATCH, "Point sets need to have the same number of points.");
+    if (ctx->np_total < 4) return fail(ctx, ICP_E_TOO_FEW_POINTS, "Need at least 4 point pairs");
+
+    const auto wall0 = std::chrono::steady_clock::now();
+    const size_t n = ctx->scene.n;
+    const double N = (double)ctx->np_total;
+    DevCloud &P = ctx->scene, &Y = ctx->Y;
+    icp_result r{};
+    r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55)
+    r.R[0] = r.R[4] = r.R[8] = 1.0;
+    long long amb = 0;
+
+    for (int it = 0; it < max_iter; ++it) {
+        // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
+        TRY(nn_search(ctx, P, n));
+        // 2. centroids (gpu.cc:98-99): sum p, sum y   [+ RCCL all-reduce, 6 doubles]
+        const int nb = red_blocks(n);
+        launch_gather_moments(ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, P.x, P.y, P.z,
+                              (int)n, Y.x, Y.y, Y.z, ctx->partials, ctx->st);
+        launch_reduce(ctx->partials, nb, 6, ctx->sums + kSumP, ctx->st);
+        LAUNCHCHK("moments");
+        TRY(allreduce(ctx, ctx->sums + kSumP, 6));
+        // 3. centred cross-covariance + norms (gpu.cc:101-104, :142) [+ all-reduce, 11]
+        launch_centred_moments(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, ctx->sums, N, ctx->partials,
+                               ctx->st);
+        launch_reduce(ctx->partials, nb, 11, ctx->sums + kSumS, ctx->st);
+        LAUNCHCHK("centred_moments");
+        TRY(allreduce(ctx, ctx->sums + kSumS, 11));
+        HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * kSumErr, hipMemcpyDeviceToHost,
+                              ctx->st));
+        if (ctx->nn_mode == ICP_NN_CERTIFIED)
+            HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        account_nn(ctx, n);
+        if (ctx->nn_mode == ICP_NN_CERTIFIED) amb += ctx->h_amb[0];
+
+        // 4. host Horn solve (gpu.cc:106-146)
+        const double *h = ctx->h_sums;
+        const double mu_p[3] = {h[kSumP] / N, h[kSumP + 1] / N, h[kSumP + 2] / N};
+        const double mu_y[3] = {h[kSumY] / N, h[kSumY + 1] / N, h[kSumY + 2] / N};
+        horn_solve(h + kSumS, mu_p, mu_y, h[kSumDcaps], h[kSumSp], &r.s, r.R, r.t);
+
+        // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2.
+        //    find_alignment's own residual (gpu.cc:148) is the identical sum, so
+        //    err = (e + e) / np exactly.
+        Xform xf;
+        for (int k = 0; k < 9; ++k) xf.sR[k] = r.s * r.R[k];
+        for (int k = 0; k < 3; ++k) {
+            xf.t[k] = r.t[k];
+            xf.c[k] = ctx->c[k];
+        }
+        launch_transform_err(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, xf, 1, P.f, ctx->partials, ctx->st);
+        launch_reduce(ctx->partials, nb, 1, ctx->sums + kSumErr, ctx->st);
+        LAUNCHCHK("transform_err");
+        TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
+        HIPCHK(hipMemcpyAsync(ctx->h_sums + kSumErr, ctx->sums + kSumErr, sizeof(double),
+                              hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        const double e = ctx->h_sums[kSumErr];
+        const double err = (e + e) / N; // gpu.cc:71-76
+        if (err_trace) err_trace[it] = err;
+        r.err = err;
+        r.iterations = it + 1;
+        ctx->stats.iterations += 1;
+        if (err < threshold) { // gpu.cc:79-80
+            r.converged = 1;
+            break;
+        }
+    }
+    ctx->stats.ambiguous += amb;
+    ctx->stats.iter_ms +=
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+    if (res) *res = r;
+    return ICP_OK;
+}
+
+// ---- per-operation surface ------------------------------------------------------------
+
+int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_xyz_out,
+                       int32_t *idx_out)
+{
+    TRY(check_ready(ctx, false));
+    if (!p_xyz && np) return ICP_E_ARG;
+    TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
+    TRY(nn_search(ctx, ctx->qa, np));
+    if (np && y_xyz_out) {
+        TRY(grow_cloud(ctx, ctx->qb, np, false));
+        launch_gather_moments(ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, ctx->qa.x,
+                              ctx->qa.y, ctx->qa.z, (int)np, ctx->qb.x, ctx->qb.y, ctx->qb.z,
+                              ctx->partials, ctx->st);
+        LAUNCHCHK("gather");
+        TRY(download_cloud(ctx, ctx->qb, np, y_xyz_out));
+    }
+    if (np && idx_out)
+        HIPCHK(hipMemcpyAsync(idx_out, ctx->idx, sizeof(int32_t) * np, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (np) account_nn(ctx, np);
+    return ICP_OK;
+}
+
+int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3], double *centred_out)
+{
+    if (!ctx || !mu || (!xyz && n) || n == 0) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    TRY(upload_cloud(ctx, ctx->qa, xyz, n, false));
+    launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, red_blocks(n), 3, ctx->sums, ctx->st);
+    LAUNCHCHK("sum3");
+    HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    for (int k = 0; k < 3; ++k) mu[k] = ctx->h_sums[k] / (double)n;
+    if (centred_out) {
+        launch_subtract(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, mu[0], mu[1], mu[2], ctx->st);
+        LAUNCHCHK("subtract");
+        TRY(download_cloud(ctx, ctx->qa, n, centred_out));
+    }
+    return ICP_OK;
+}
+
+int icp_y_p_norm(icp_ctx *ctx, const double *y_xyz, const double *p_xyz, size_t n, double *d_caps,
+                 double *sp)
+{
+    if (!ctx || !d_caps || !sp || ((!y_xyz || !p_xyz) && n)) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
+    TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
+    launch_norms(ctx->qa.x, ctx->qa.y, ctx->qa.z, ctx->qb.x, ctx->qb.y, ctx->qb.z, (int)n,
+                 ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, red_blocks(n), 2, ctx->sums, ctx->st);
+    LAUNCHCHK("norms");
+    HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    *d_caps = ctx->h_sums[0];
+    *sp = ctx->h_sums[1];
+    return ICP_OK;
+}
+
+int icp_err_compute(icp_ctx *ctx, const double *y_xyz, double *p_xyz, size_t n, int in_place,
+                    const double sR[9], const double t[3], double *err)
+{
+    if (!ctx || !sR || !t || !err || ((!y_xyz || !p_xyz) && n)) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
+    TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
+    Xform xf;
+    std::memcpy(xf.sR, sR, sizeof(xf.sR));
+    std::memcpy(xf.t, t, sizeof(xf.t));
+    std::memcpy(xf.c, ctx->c, sizeof(xf.c));
+    launch_transform_err(ctx->qb.x, ctx->qb.y, ctx->qb.z, ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, xf,
+                         in_place ? 1 : 0, nullptr, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, red_blocks(n), 1, ctx->sums, ctx->st);
+    LAUNCHCHK("transform_err");
+    HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    *err = ctx->h_sums[0];
+    if (in_place) TRY(download_cloud(ctx, ctx->qb, n, p_xyz));
+    return ICP_OK;
+}
+
+int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, size_t n, double *s,
+                       double R[9], double t[3], double *err)
+{
+    if (!ctx || !s || !R || !t || !err || !p_xyz || !y_xyz || n == 0) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
+    TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
+    const int nb = red_blocks(n);
+    launch_sum3(ctx->qb.x, ctx->qb.y, ctx->qb.z, (int)n, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, nb, 3, ctx->sums + kSumP, ctx->st);
+    launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, nb, 3, ctx->sums + kSumY, ctx->st);
+    launch_centred_moments(ctx->qb.x, ctx->qb.y, ctx->qb.z, ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n,
+                           ctx->sums, (double)n, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, nb, 11, ctx->sums + kSumS, ctx->st);
+    LAUNCHCHK("find_alignment moments");
+    HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * kSumErr, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    const double N = (double)n;
+    const double *h = ctx->h_sums;
+    const double mu_p[3] = {h[kSumP] / N, h[kSumP + 1] / N, h[kSumP + 2] / N};
+    const double mu_y[3] = {h[kSumY] / N, h[kSumY + 1] / N, h[kSumY + 2] / N};
+    horn_solve(h + kSumS, mu_p, mu_y, h[kSumDcaps], h[kSumSp], s, R, t);
+    double sR[9];
+    for (int k = 0; k < 9; ++k) sR[k] = *s * R[k];
+    Xform xf;
+    std::memcpy(xf.sR, sR, sizeof(sR));
+    std::memcpy(xf.t, t, sizeof(xf.t));
+    std::memcpy(xf.c, ctx->c, sizeof(xf.c));
+    launch_transform_err(ctx->qb.x, ctx->qb.y, ctx->qb.z, ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, xf,
+                         0, nullptr, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, nb, 1, ctx->sums + kSumErr, ctx->st);
+    LAUNCHCHK("find_alignment err");
+    HIPCHK(hipMemcpyAsync(ctx->h_sums + kSumErr, ctx->sums + kSumErr, sizeof(double),
+                          hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    *err = ctx->h_sums[kSumErr];
+    return ICP_OK;
+}
+
+int icp_get_stats(const icp_ctx *ctx, icp_stats *out)
+{
+    if (!ctx || !out) return ICP_E_ARG;
+    *out = ctx->stats;
+    return ICP_OK;
+}
+
+int icp_reset_stats(icp_ctx *ctx)
+{
+    if (!ctx) return ICP_E_ARG;
+    ctx->stats = icp_stats{};
+    return ICP_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,286 @@
+// icp_host.cpp — host-side pieces of the ICP engine that need no device:
+// Horn's closed-form alignment solve, scene sharding, the synthetic cloud generator
+// and CSV point-cloud I/O.  Part of libicp_hip.so (product code, not the oracle).
+//
+// Reference: src/GPU/gpu.cc:95-151 (find_alignment, host half), gpu.cc:85-93
+// (max_element_index), src/load.cc:3-97 (I/O).
+#include "icp_internal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+namespace icp {
+
+// Eigenvector of the largest eigenvalue of a symmetric 4x4 (row-major), by cyclic
+// Jacobi rotations.  Eigen's EigenSolver (gpu.cc:113-115) is a general real solver
+// whose eigenvalue order decides max_element_index's quirk; on symmetric Horn
+// matrices we take the true maximum (on every bundled configuration
+// the quirk selects the maximum too).
+void largest_eigvec_sym4(const double Nin[16], double q[4], double evals[4])
+{
+    double a[4][4], v[4][4];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) {
+            a[r][c] = 0.5 * (Nin[4 * r + c] + Nin[4 * c + r]);
+            v[r][c] = r == c ? 1.0 : 0.0;
+        }
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        double off = 0.0, tot = 0.0;
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) {
+                double x = a[r][c] * a[r][c];
+                tot += x;
+                if (r != c) off += x;
+            }
+        if (!(off > 1e-64 * tot)) break;
+        for (int p = 0; p < 3; ++p)
+            for (int k = p + 1; k < 4; ++k) {
+                const double apk = a[p][k];
+                if (apk == 0.0) continue;
+                const double th = (a[k][k] - a[p][p]) / (2.0 * apk);
+                const double tn = std::copysign(1.0, th) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                const double cs = 1.0 / std::sqrt(tn * tn + 1.0), sn = tn * cs;
+                for (int i = 0; i < 4; ++i) {
+                    const double ip = a[i][p], ik = a[i][k];
+                    a[i][p] = cs * ip - sn * ik;
+                    a[i][k] = sn * ip + cs * ik;
+                }
+                for (int i = 0; i < 4; ++i) {
+                    const double pi = a[p][i], ki = a[k][i];
+                    a[p][i] = cs * pi - sn * ki;
+                    a[k][i] = sn * pi + cs * ki;
+                }
+                for (int i = 0; i < 4; ++i) {
+                    const double ip = v[i][p], ik = v[i][k];
+                    v[i][p] = cs * ip - sn * ik;
+                    v[i][k] = sn * ip + cs * ik;
+                }
+            }
+    }
+    int best = 0;
+    for (int k = 0; k < 4; ++k) {
+        evals[k] = a[k][k];
+        if (a[k][k] > a[best][best]) best = k;
+    }
+    double nrm = 0.0;
+    for (int r = 0; r < 4; ++r) nrm += v[r][best] * v[r][best];
+    nrm = std::sqrt(nrm);
+    for (int r = 0; r < 4; ++r) q[r] = v[r][best] / nrm;
+}
+
+// 3x3 row-major matrix times vector in the reference's accumulation order
+// ((a0 x0 + a1 x1) + a2 x2) — this file is compiled with -ffp-contract=off.
+static void matvec3(const double A[9], const double x[3], double out[3])
+{
+    for (int i = 0; i < 3; ++i) {
+        const double a = A[3 * i] * x[0], b = A[3 * i + 1] * x[1], c = A[3 * i + 2] * x[2];
+        out[i] = (a + b) + c;
+    }
+}
+
+void horn_solve(const double S[9], const double mu_p[3], const double mu_y[3], double d_caps,
+                double sp, double *s_out, double R[9], double t[3])
+{
+    auto s = [&](int r, int c) { return S[3 * r + c]; };
+    // Horn's symmetric 4x4 (gpu.cc:106-111)
+    const double N[16] = {
+        s(0, 0) + s(1, 1) + s(2, 2), s(1, 2) - s(2, 1), -1 * s(0, 2) + s(2, 0), s(0, 1) - s(1, 0),
+        -1 * s(2, 1) + s(1, 2), s(0, 0) - s(2, 2) - s(1, 1), s(0, 1) + s(1, 0), s(0, 2) + s(2, 0),
+        s(2, 0) - s(0, 2), s(1, 0) + s(0, 1), s(1, 1) - s(2, 2) - s(0, 0), s(1, 2) + s(2, 1),
+        -1 * s(1, 0) + s(0, 1), s(2, 0) + s(0, 2), s(2, 1) + s(1, 2), s(2, 2) - s(1, 1) - s(0, 0)};
+    double q[4], ev[4];
+    largest_eigvec_sym4(N, q, ev);
+    // R = (Qbar^T Q)[1:4, 1:4]  (gpu.cc:119-133)
+    const double qb[16] = {q[0], -q[1], -q[2], -q[3], q[1], q[0], q[3], -q[2],
+                           q[2], -q[3], q[0], q[1], q[3], q[2], -q[1], q[0]};
+    const double qc[16] = {q[0], -q[1], -q[2], -q[3], q[1], q[0], -q[3], q[2],
+                           q[2], q[3], q[0], -q[1], q[3], -q[2], q[1], q[0]};
+    for (int r = 1; r < 4; ++r)
+        for (int c = 1; c < 4; ++c) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; ++k) acc += qb[4 * k + r] * qc[4 * k + c];
+            R[3 * (r - 1) + (c - 1)] = acc;
+        }
+    // Horn's symmetric scale and the translation (gpu.cc:140-146)
+    const double sc = std::sqrt(d_caps / sp);
+    double sR[9], smu[3];
+    for (int k = 0; k < 9; ++k) sR[k] = sc * R[k];
+    matvec3(sR, mu_p, smu);
+    for (int k = 0; k < 3; ++k) t[k] = mu_y[k] - smu[k];
+    *s_out = sc;
+}
+
+void shard_range(size_t n, int rank, int world, size_t *begin, size_t *count)
+{
+    const size_t base = n / (size_t)world, rem = n % (size_t)world;
+    const size_t r = (size_t)rank;
+    *begin = r * base + (r < rem ? r : rem);
+    *count = base + (r < rem ? 1 : 0);
+}
+
+// ---- CSV I/O (src/load.cc) ---------------------------------------------------
+// Row parse = sscanf(line, "%lf,%lf,%lf") (load.cc:27): %lf skips leading whitespace
+// and converts with strtod; each ',' must follow its number directly; fields that do
+// not parse stay 0 (load.cc:26).
+static void parse_row(char *s, double out[3])
+{
+    for (int k = 0; k < 3; ++k) {
+        char *e = nullptr;
+        const double v = std::strtod(s, &e);
+        if (e == s) return;
+        out[k] = v;
+        if (k < 2) {
+            if (*e != ',') return;
+            s = e + 1;
+        }
+    }
+}
+
+int load_matrix(const char *path, std::vector<double> &xyz, size_t *n_out)
+{
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return ICP_E_IO;
+    std::fseek(f, 0, SEEK_END);
+    const long sz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    std::vector<char> buf(sz > 0 ? (size_t)sz + 1 : 1, '\0');
+    const size_t got = sz > 0 ? std::fread(buf.data(), 1, (size_t)sz, f) : 0;
+    std::fclose(f);
+    buf[got] = '\0';
+    // load.cc:15-17: getline() count minus the header
+    size_t lines = 0;
+    for (size_t i = 0; i < got; ++i) lines += buf[i] == '\n';
+    if (got && buf[got - 1] != '\n') ++lines;
+    const size_t n = lines > 0 ? lines - 1 : 0;
+    xyz.assign(3 * n, 0.0);
+    char *cur = buf.data(), *end = buf.data() + got;
+    char *nl = (char *)std::memchr(cur, '\n', (size_t)(end - cur));
+    cur = nl ? nl + 1 : end; // load.cc:21: skip the header line
+    for (size_t i = 0; i < n; ++i) {
+        char *le = cur < end ? (char *)std::memchr(cur, '\n', (size_t)(end - cur)) : nullptr;
+        if (le) *le = '\0';
+        parse_row(cur, &xyz[3 * i]);
+        cur = le ? le + 1 : end;
+    }
+    *n_out = n;
+    return ICP_OK;
+}
+
+int write_matrix(const char *path, const double *xyz, size_t n)
+{
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return ICP_E_IO;
+    std::fputs("Points_0,Points_1,Points_2\n", f); // load.cc:73
+    for (size_t j = 0; j < n; ++j)                 // ostream default: %g, precision 6
+        std::fprintf(f, "%g,%g,%g\n", xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2]);
+    std::fclose(f);
+    return ICP_OK;
+}
+
+void synthetic_pair(uint64_t seed, size_t n, double angle_deg, const double axis_in[3],
+                    const double tr[3], double *model, double *scene)
+{
+    std::mt19937_64 gen(seed);
+    for (size_t i = 0; i < 3 * n; ++i) {
+        // 53 random bits -> [0,1) -> [-1,1), rounded to an fp32-representable double
+        const double u = (double)(gen() >> 11) * 0x1.0p-53;
+        model[i] = (double)(float)(2.0 * u - 1.0);
+    }
+    double ax[3] = {axis_in[0], axis_in[1], axis_in[2]};
+    const double nrm = std::sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+    for (double &a : ax) a /= nrm;
+    const double th = angle_deg * M_PI / 180.0, c = std::cos(th), s = std::sin(th), C = 1.0 - c;
+    const double R[9] = {c + ax[0] * ax[0] * C,         ax[0] * ax[1] * C - ax[2] * s, ax[0] * ax[2] * C + ax[1] * s,
+                         ax[1] * ax[0] * C + ax[2] * s, c + ax[1] * ax[1] * C,         ax[1] * ax[2] * C - ax[0] * s,
+                         ax[2] * ax[0] * C - ax[1] * s, ax[2] * ax[1] * C + ax[0] * s, c + ax[2] * ax[2] * C};
+    for (size_t j = 0; j < n; ++j) {
+        double q[3];
+        matvec3(R, model + 3 * j, q);
+        for (int k = 0; k < 3; ++k) scene[3 * j + k] = (double)(float)(q[k] + tr[k]);
+    }
+}
+
+} // namespace icp
+
+// ---- C-ABI wrappers for the host-only entry points ------------------------------
+extern "C" {
+
+int icp_horn_solve(const double S[9], const double mu_p[3], const double mu_y[3], double d_caps,
+                   double sp, double *s, double R[9], double t[3])
+{
+    if (!S || !mu_p || !mu_y || !s || !R || !t) return ICP_E_ARG;
+    icp::horn_solve(S, mu_p, mu_y, d_caps, sp, s, R, t);
+    return ICP_OK;
+}
+
+int icp_max_element_index(const double ev[4])
+{
+    // gpu.cc:85-93 as written: `max` is never updated, so this is the LAST i in 1..3
+    // with ev[i] > ev[0] (not the argmax in general).
+    int index = 0;
+    const double max = ev[0];
+    for (int i = 1; i < 4; ++i)
+        if (ev[i] > max) index = i;
+    return index;
+}
+
+int icp_shard_range(size_t n_total, int rank, int world_size, size_t *begin, size_t *count)
+{
+    if (world_size < 1 || rank < 0 || rank >= world_size || !begin || !count) return ICP_E_ARG;
+    icp::shard_range(n_total, rank, world_size, begin, count);
+    return ICP_OK;
+}
+
+int icp_synthetic_pair(uint64_t seed, size_t n, double angle_deg, const double axis[3],
+                       const double t[3], double *model_xyz_out, double *scene_xyz_out)
+{
+    if (!axis || !t || !model_xyz_out || !scene_xyz_out) return ICP_E_ARG;
+    icp::synthetic_pair(seed, n, angle_deg, axis, t, model_xyz_out, scene_xyz_out);
+    return ICP_OK;
+}
+
+int icp_load_matrix(const char *path, double **xyz_out, size_t *n_out)
+{
+    if (!path || !xyz_out || !n_out) return ICP_E_ARG;
+    std::vector<double> v;
+    size_t n = 0;
+    int rc = icp::load_matrix(path, v, &n);
+    if (rc != ICP_OK) return rc;
+    double *out = (double *)std::malloc(sizeof(double) * (v.size() ? v.size() : 1));
+    if (!out) return ICP_E_ARG;
+    if (!v.empty()) std::memcpy(out, v.data(), sizeof(double) * v.size());
+    *xyz_out = out;
+    *n_out = n;
+    return ICP_OK;
+}
+
+int icp_write_matrix(const char *path, const double *xyz, size_t n)
+{
+    if (!path || (!xyz && n)) return ICP_E_ARG;
+    return icp::write_matrix(path, xyz, n);
+}
+
+void icp_free(void *p) { std::free(p); }
+
+const char *icp_strerror(int code)
+{
+    switch (code) {
+    case ICP_OK: return "ok";
+    case ICP_E_ARG: return "invalid argument";
+    case ICP_E_HIP: return "HIP runtime error";
+    case ICP_E_SIZE_MISMATCH: return "Point sets need to have the same number of points.";
+    case ICP_E_TOO_FEW_POINTS: return "Need at least 4 point pairs";
+    case ICP_E_NO_MODEL: return "model or scene not set";
+    case ICP_E_RCCL: return "RCCL error";
+    case ICP_E_NO_DEVICE: return "no HIP device";
+    case ICP_E_IO: return "file could not be opened";
+    case ICP_E_RANGE: return "coordinates outside the supported range";
+    default: return "unknown error";
+    }
+}
+
+} // extern "C"

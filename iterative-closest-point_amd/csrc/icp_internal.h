@@ -1,0 +1,37 @@
+// icp_internal.h — private declarations shared by the engine's translation units.
+#pragma once
+
+#include "../../include/icp_capi.h"
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace icp {
+
+// ---- host-only (icp_host.cpp) ------------------------------------------------
+void largest_eigvec_sym4(const double N[16], double q[4], double evals[4]);
+void horn_solve(const double S[9], const double mu_p[3], const double mu_y[3], double d_caps,
+                double sp, double *s, double R[9], double t[3]);
+void shard_range(size_t n, int rank, int world, size_t *begin, size_t *count);
+int load_matrix(const char *path, std::vector<double> &xyz, size_t *n_out);
+int write_matrix(const char *path, const double *xyz, size_t n);
+void synthetic_pair(uint64_t seed, size_t n, double angle_deg, const double axis[3],
+                    const double t[3], double *model, double *scene);
+
+// ---- NN kernel geometry (icp_kernels.hip) -----------------------------------------
+constexpr int kBlock = 256;   // threads per workgroup (4 waves of 64)
+constexpr int kTile32 = 1024; // model points per LDS tile, fp32 filter (16 KiB)
+constexpr int kTile64 = 512;  // model points per LDS tile, fp64 path (16 KiB)
+constexpr int kSub = 32;      // sub-block granularity of the running-argmin bookkeeping
+constexpr int kRedMaxBlocks = 1024; // max workgroups of a streaming reduction pass
+
+// Slots of the per-iteration reduced-sum vector (device `sums`, fp64):
+//  [0..2]  sum p        [3..5]  sum y
+//  [6..14] S = sum (p-mu_p)(y-mu_y)^T, row-major
+//  [15]    d_caps = sum ||y - mu_y||^2      [16] sp = sum ||p - mu_p||^2
+//  [17]    e = sum ||y - (sR p + t)||^2
+constexpr int kSumP = 0, kSumY = 3, kSumS = 6, kSumDcaps = 15, kSumSp = 16, kSumErr = 17,
+              kNumSums = 18;
+
+} // namespace icp

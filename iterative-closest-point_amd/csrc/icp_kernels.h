@@ -1,0 +1,87 @@
+// icp_kernels.h — host-callable launchers for the engine's HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "icp_internal.h"
+
+namespace icp {
+
+// Parameters of the fp32 certificate (see icp_kernels.hip, "certified NN").
+struct CertParams {
+    double rm; // max |coordinate| of the centred fp32 model (real points only)
+};
+
+// ---- layout conversion -------------------------------------------------------
+void launch_aos_to_soa(const double *aos, size_t n, double *x, double *y, double *z,
+                       hipStream_t st);
+void launch_soa_to_aos(const double *x, const double *y, const double *z, size_t n, double *aos,
+                       hipStream_t st);
+// f[j] = (float)(p_j - c) (xyz), w = 0
+void launch_make_f32(const double *x, const double *y, const double *z, size_t n, double cx,
+                     double cy, double cz, float4 *f, hipStream_t st);
+
+// ---- nearest neighbour -------------------------------------------------------------
+// Workspace sizes for a search of np queries against nm_pad (padded) model points.
+struct NNPlan {
+    int q_per_lane; // queries per lane (register blocking)
+    int qblocks;    // workgroups along the query axis
+    int splits;     // workgroups along the model axis
+    int chunk;      // model points per split (multiple of the tile)
+};
+NNPlan plan_nn32(size_t np, size_t nm_pad);
+NNPlan plan_nn64(size_t np, size_t nm_pad);
+
+// fp32 filter: partial (best, second, argbest) per (split, query).
+void launch_nn_filter(const float4 *p32, int np, const float4 *m32, int nm_pad,
+                      const NNPlan &plan, float *part_best, float *part_second, int *part_idx,
+                      hipStream_t st);
+// merge splits, certify, write idx for certified queries, queue the rest.
+void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
+                        int splits, const float4 *p32, int np, CertParams cp, int *idx,
+                        int *amb_count, int *amb_list, double *amb_T, hipStream_t st);
+// exact fp64 resolution of the queued queries (candidates d32 <= T only).
+void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
+                       const float4 *p32, const double *px, const double *py, const double *pz,
+                       const float4 *m32, const double *mx, const double *my, const double *mz,
+                       int nm, int max_items, int *idx, hipStream_t st);
+// fp64 brute force: partial (best d64, argbest) per (split, query), then merge.
+void launch_nn_fp64(const double *px, const double *py, const double *pz, int np,
+                    const double *mx, const double *my, const double *mz, int nm,
+                    const NNPlan &plan, double *part_best, int *part_idx, hipStream_t st);
+void launch_nn_finalize64(const double *part_best, const int *part_idx, int splits, int np,
+                          int *idx, hipStream_t st);
+
+// ---- streaming reductions (deterministic two-stage, fp64) --------------------------
+int red_blocks(size_t n);
+// y = m[idx]; partial [sum p (3), sum y (3)]
+void launch_gather_moments(const int *idx, const double *mx, const double *my, const double *mz,
+                           const double *px, const double *py, const double *pz, int n,
+                           double *yx, double *yy, double *yz, double *partials, hipStream_t st);
+// partial [sum p (3)] of one cloud
+void launch_sum3(const double *x, const double *y, const double *z, int n, double *partials,
+                 hipStream_t st);
+// partial [S (9), d_caps, sp] around mu = sums[kSumP..]/n_total, sums[kSumY..]/n_total
+void launch_centred_moments(const double *px, const double *py, const double *pz,
+                            const double *yx, const double *yy, const double *yz, int n,
+                            const double *sums, double n_total, double *partials,
+                            hipStream_t st);
+// p' = p - mu in place (substract_col)
+void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
+                     hipStream_t st);
+// partial [sum ||y||^2, sum ||p||^2] (y_p_norm)
+void launch_norms(const double *yx, const double *yy, const double *yz, const double *px,
+                  const double *py, const double *pz, int n, double *partials, hipStream_t st);
+// q = sR p + t; partial [sum ||y - q||^2]; if write_p: p <- q and p32 <- (float)(q - c)
+struct Xform {
+    double sR[9];
+    double t[3];
+    double c[3];
+};
+void launch_transform_err(double *px, double *py, double *pz, const double *yx, const double *yy,
+                          const double *yz, int n, Xform xf, int write_p, float4 *p32,
+                          double *partials, hipStream_t st);
+// out[k] = sum_b partials[b*K + k], fixed order, one workgroup
+void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);
+
+} // namespace icp

@@ -1,0 +1,666 @@
+// icp_kernels.hip — CDNA4 (gfx950) kernels of the ICP hot path.
+//
+// Replaces the reference's src/GPU/compute.cu kernels:
+//   compute_distance + find_Y (compute.cu:94-150)   -> fused NN search (no N x M matrix)
+//   substract_col (:381-398), y_p_norm (:418-440),
+//   compute_err (:315-346)                           -> two-stage fp64 block reductions
+//
+// Compiled with -ffp-contract=off: every fp64 expression below rounds exactly as
+// written (the reference's host build never fused), and fp32 FMAs are spelled out
+// explicitly with __builtin_fmaf where they are wanted.
+//
+// ---------------------------------------------------------------------------------
+// Certified NN ("ICP_NN_CERTIFIED").  The NN answer is DEFINED as the fp64 first-min:
+//   idx(p) = min { k : D64(p, m_k) = min_l D64(p, m_l) },
+//   D64 = ((dx*dx + dy*dy) + dz*dz) in fp64, no FMA   (compute.cu:112-117, :137).
+// Pass 1 (nn_filter) evaluates every pair in fp32 on coordinates centred on the model
+// centroid c:  D32 = fma(dz,dz, fma(dy,dy, dx*dx)), dx = (float)(px-cx) - (float)(mx-cx),
+// and keeps per query the smallest two D32 values (v_min_f32 + v_med3_f32) and the
+// 32-point sub-block holding the smallest.  With u = 2^-24, A = max|p~|, Rm = max|m~| and
+// E = 2u(A + Rm)(1 + 2^-20) (per-axis bound on |dx~ - dx|),
+//   |D32 - D| <= f(D32),   f(x) = 6u x + 3.5 E sqrt(x) (1 + 4u) + 3 E^2,
+// where D is the exact squared distance.  Every fp64 minimiser m* then satisfies
+// D32(m*) <= T := b' + f(max(4b', 400 E^2)),  b' = (b + f(b))(1 + 2^-49), b = min D32
+// (DESIGN.md §3 has the proof).  If the second-smallest D32 exceeds T the fp32 argmin
+// is the unique candidate and therefore the exact answer; otherwise the query is
+// queued and nn_resolve re-scans it, computing D64 for the candidates D32 <= T only.
+// Result: bit-identical indices to the fp64 brute force, at fp32 VALU cost.
+// ---------------------------------------------------------------------------------
+#include "icp_kernels.h"
+
+#include <cmath>
+
+namespace icp {
+
+namespace {
+
+
+__device__ __forceinline__ float d32(float px, float py, float pz, float4 m)
+{
+    const float dx = px - m.x;
+    const float dy = py - m.y;
+    const float dz = pz - m.z;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+__device__ __forceinline__ double d64(double px, double py, double pz, double mx, double my,
+                                      double mz)
+{
+    const double dx = px - mx;
+    const double dy = py - my;
+    const double dz = pz - mz;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+// Certificate window T(b) for a query with centred fp32 coordinates p (see header).
+__device__ double cert_window(float b32, float4 p, double rm)
+{
+    const double u = 0x1.0p-24;
+    const double A = fmax(fabs((double)p.x), fmax(fabs((double)p.y), fabs((double)p.z)));
+    const double E = 2.0 * u * (A + rm) * (1.0 + 0x1.0p-20);
+    auto f = [&](double x) { return 6.0 * u * x + 3.5 * E * sqrt(x) * (1.0 + 4.0 * u) + 3.0 * E * E; };
+    const double b = (double)b32;
+    const double bp = (b + f(b)) * (1.0 + 0x1.0p-49);
+    const double X = fmax(4.0 * bp, 400.0 * E * E);
+    return (bp + f(X)) * (1.0 + 1e-12);
+}
+
+// Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
+// out[k].  Fixed shuffle tree + fixed LDS order: deterministic.
+template <int K>
+__device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
+{
+    __shared__ double sh[kBlock / 64][K];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += __shfl_down(a[k], off, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
+    }
+}
+
+// ---- layout ------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const double *__restrict__ aos,
+                                                            size_t n, double *x, double *y,
+                                                            double *z)
+{
+    for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * kBlock) {
+        x[i] = aos[3 * i];
+        y[i] = aos[3 * i + 1];
+        z[i] = aos[3 * i + 2];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(const double *__restrict__ x,
+                                                            const double *__restrict__ y,
+                                                            const double *__restrict__ z,
+                                                            size_t n, double *aos)
+{
+    for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * kBlock) {
+        aos[3 * i] = x[i];
+        aos[3 * i + 1] = y[i];
+        aos[3 * i + 2] = z[i];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void make_f32_kernel(const double *__restrict__ x,
+                                                          const double *__restrict__ y,
+                                                          const double *__restrict__ z,
+                                                          size_t n, double cx, double cy,
+                                                          double cz, float4 *f)
+{
+    for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * kBlock)
+        f[i] = make_float4((float)(x[i] - cx), (float)(y[i] - cy), (float)(z[i] - cz), 0.0f);
+}
+
+// ---- NN: fp32 filter ----------------------------------------------------------------
+// grid = (qblocks, splits).  Lane owns Q queries (j = blockIdx.x*256*Q + q*256 + tid);
+// the workgroup streams its model chunk through a 1024-point LDS tile; every lane reads
+// the same model point (LDS broadcast, one ds_read_b128 feeds 64*Q pairs).
+template <int Q>
+__global__ __launch_bounds__(kBlock) void nn_filter_kernel(
+    const float4 *__restrict__ p32, int np, const float4 *__restrict__ m32, int nm_pad, int chunk,
+    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx)
+{
+    __shared__ float4 tile[kTile32];
+    const int tid = threadIdx.x;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm_pad);
+    const int qbase = blockIdx.x * (kBlock * Q) + tid;
+
+    float px[Q], py[Q], pz[Q], best[Q], second[Q];
+    int bsub[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = qbase + q * kBlock;
+        const float4 v = j < np ? p32[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        px[q] = v.x;
+        py[q] = v.y;
+        pz[q] = v.z;
+        best[q] = INFINITY;
+        second[q] = INFINITY;
+        bsub[q] = m0;
+    }
+
+    for (int t0 = m0; t0 < m1; t0 += kTile32) {
+        __syncthreads();
+#pragma unroll
+        for (int k = tid; k < kTile32; k += kBlock) tile[k] = m32[t0 + k];
+        __syncthreads();
+        for (int sb = 0; sb < kTile32; sb += kSub) {
+            float prev[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) prev[q] = best[q];
+#pragma unroll 8
+            for (int k = 0; k < kSub; ++k) {
+                const float4 m = tile[sb + k];
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const float d = d32(px[q], py[q], pz[q], m);
+                    second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d);
+                    best[q] = __builtin_fminf(best[q], d);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) bsub[q] = best[q] < prev[q] ? (t0 + sb) : bsub[q];
+        }
+    }
+
+    // Recover the index of `best` inside its sub-block (lowest k with d == best).
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        int found = bsub[q];
+#pragma unroll
+        for (int k = kSub - 1; k >= 0; --k) {
+            const float d = d32(px[q], py[q], pz[q], m32[bsub[q] + k]);
+            found = (d == best[q]) ? bsub[q] + k : found;
+        }
+        const int j = qbase + q * kBlock;
+        if (j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = best[q];
+            part_second[o] = second[q];
+            part_idx[o] = found;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
+    const float *__restrict__ part_best, const float *__restrict__ part_second,
+    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
+    double rm, int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    float b = part_best[j], s2 = part_second[j];
+    int id = part_idx[j];
+    for (int sp = 1; sp < splits; ++sp) {
+        const size_t o = (size_t)sp * np + j;
+        const float b2 = part_best[o], s22 = part_second[o];
+        if (b2 < b) { // strict: the earlier split keeps ties (lower indices)
+            s2 = fminf(b, s22);
+            b = b2;
+            id = part_idx[o];
+        } else {
+            s2 = fminf(s2, b2);
+        }
+    }
+    const double T = cert_window(b, p32[j], rm);
+    if ((double)s2 > T) {
+        idx[j] = id; // unique candidate => exact fp64 first-min
+    } else {
+        const int slot = atomicAdd(amb_count, 1);
+        amb_list[slot] = j;
+        amb_T[slot] = T;
+    }
+}
+
+// One workgroup per queued query (grid-stride over the queue): exact fp64 D on the
+// candidates D32 <= T, lexicographic (D64, index) minimum = first minimum.
+__global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
+    const int *__restrict__ amb_count, const int *__restrict__ amb_list,
+    const double *__restrict__ amb_T, const float4 *__restrict__ p32,
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    const float4 *__restrict__ m32, const double *__restrict__ mx, const double *__restrict__ my,
+    const double *__restrict__ mz, int nm, int *__restrict__ idx)
+{
+    __shared__ double shd[kBlock];
+    __shared__ int shi[kBlock];
+    const int count = *amb_count;
+    for (int item = blockIdx.x; item < count; item += gridDim.x) {
+        const int j = amb_list[item];
+        const double T = amb_T[item];
+        const float4 p = p32[j];
+        const double qx = px[j], qy = py[j], qz = pz[j];
+        double bd = INFINITY;
+        int bi = 0x7fffffff;
+        for (int k = threadIdx.x; k < nm; k += kBlock) {
+            const float d = d32(p.x, p.y, p.z, m32[k]);
+            if ((double)d <= T) {
+                const double e = d64(qx, qy, qz, mx[k], my[k], mz[k]);
+                if (e < bd) { // k increases per thread: strict keeps the first
+                    bd = e;
+                    bi = k;
+                }
+            }
+        }
+        shd[threadIdx.x] = bd;
+        shi[threadIdx.x] = bi;
+        __syncthreads();
+        for (int s = kBlock / 2; s > 0; s >>= 1) {
+            if (threadIdx.x < s) {
+                const double od = shd[threadIdx.x + s];
+                const int oi = shi[threadIdx.x + s];
+                if (od < shd[threadIdx.x] || (od == shd[threadIdx.x] && oi < shi[threadIdx.x])) {
+                    shd[threadIdx.x] = od;
+                    shi[threadIdx.x] = oi;
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) idx[j] = shi[0];
+        __syncthreads();
+    }
+}
+
+// ---- NN: fp64 brute force ------------------------------------------------------------
+struct D4 {
+    double x, y, z, w;
+};
+
+template <int Q>
+__global__ __launch_bounds__(kBlock) void nn_fp64_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, const double *__restrict__ mx, const double *__restrict__ my,
+    const double *__restrict__ mz, int nm, int chunk, double *__restrict__ part_best,
+    int *__restrict__ part_idx)
+{
+    __shared__ D4 tile[kTile64];
+    const int tid = threadIdx.x;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm);
+    const int qbase = blockIdx.x * (kBlock * Q) + tid;
+    double qx[Q], qy[Q], qz[Q], best[Q];
+    int bsub[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = qbase + q * kBlock;
+        const bool ok = j < np;
+        qx[q] = ok ? px[j] : 0.0;
+        qy[q] = ok ? py[j] : 0.0;
+        qz[q] = ok ? pz[j] : 0.0;
+        best[q] = INFINITY;
+        bsub[q] = m0;
+    }
+    for (int t0 = m0; t0 < m1; t0 += kTile64) {
+        __syncthreads();
+        for (int k = tid; k < kTile64; k += kBlock) {
+            const int g = t0 + k;
+            D4 v;
+            if (g < m1) {
+                v.x = mx[g];
+                v.y = my[g];
+                v.z = mz[g];
+            } else {
+                v.x = v.y = v.z = 1.0e150;
+            }
+            v.w = 0.0;
+            tile[k] = v;
+        }
+        __syncthreads();
+        for (int sb = 0; sb < kTile64; sb += kSub) {
+            double prev[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) prev[q] = best[q];
+#pragma unroll 8
+            for (int k = 0; k < kSub; ++k) {
+                const D4 m = tile[sb + k];
+#pragma unroll
+                for (int q = 0; q < Q; ++q) best[q] = fmin(best[q], d64(qx[q], qy[q], qz[q], m.x, m.y, m.z));
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) bsub[q] = best[q] < prev[q] ? (t0 + sb) : bsub[q];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        int found = bsub[q];
+        for (int k = kSub - 1; k >= 0; --k) {
+            const int g = bsub[q] + k;
+            if (g < m1) {
+                const double d = d64(qx[q], qy[q], qz[q], mx[g], my[g], mz[g]);
+                found = (d == best[q]) ? g : found;
+            }
+        }
+        const int j = qbase + q * kBlock;
+        if (j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = best[q];
+            part_idx[o] = found;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void nn_finalize64_kernel(const double *__restrict__ part_best,
+                                                               const int *__restrict__ part_idx,
+                                                               int splits, int np,
+                                                               int *__restrict__ idx)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    double b = part_best[j];
+    int id = part_idx[j];
+    for (int sp = 1; sp < splits; ++sp) {
+        const size_t o = (size_t)sp * np + j;
+        if (part_best[o] < b) {
+            b = part_best[o];
+            id = part_idx[o];
+        }
+    }
+    idx[j] = id;
+}
+
+// ---- streaming reductions ----------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void gather_moments_kernel(
+    const int *__restrict__ idx, const double *__restrict__ mx, const double *__restrict__ my,
+    const double *__restrict__ mz, const double *__restrict__ px, const double *__restrict__ py,
+    const double *__restrict__ pz, int n, double *__restrict__ yx, double *__restrict__ yy,
+    double *__restrict__ yz, double *__restrict__ partials)
+{
+    double a[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const int k = idx[i];
+        const double y0 = mx[k], y1 = my[k], y2 = mz[k];
+        yx[i] = y0;
+        yy[i] = y1;
+        yz[i] = y2;
+        a[0] += px[i];
+        a[1] += py[i];
+        a[2] += pz[i];
+        a[3] += y0;
+        a[4] += y1;
+        a[5] += y2;
+    }
+    block_sum_store<6>(a, partials + (size_t)blockIdx.x * 6);
+}
+
+__global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__ x,
+                                                     const double *__restrict__ y,
+                                                     const double *__restrict__ z, int n,
+                                                     double *__restrict__ partials)
+{
+    double a[3] = {0, 0, 0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        a[0] += x[i];
+        a[1] += y[i];
+        a[2] += z[i];
+    }
+    block_sum_store<3>(a, partials + (size_t)blockIdx.x * 3);
+}
+
+__global__ __launch_bounds__(kBlock) void centred_moments_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
+    int n, const double *__restrict__ sums, double n_total, double *__restrict__ partials)
+{
+    // mu = rowwise().mean() (gpu.cc:98-99), identical in every thread and on the host
+    const double mpx = sums[kSumP] / n_total, mpy = sums[kSumP + 1] / n_total,
+                 mpz = sums[kSumP + 2] / n_total;
+    const double myx = sums[kSumY] / n_total, myy = sums[kSumY + 1] / n_total,
+                 myz = sums[kSumY + 2] / n_total;
+    double a[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) a[k] = 0.0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const double p0 = px[i] - mpx, p1 = py[i] - mpy, p2 = pz[i] - mpz; // substract_col
+        const double y0 = yx[i] - myx, y1 = yy[i] - myy, y2 = yz[i] - myz;
+        a[0] += p0 * y0; // S = P' Y'^T (gpu.cc:104)
+        a[1] += p0 * y1;
+        a[2] += p0 * y2;
+        a[3] += p1 * y0;
+        a[4] += p1 * y1;
+        a[5] += p1 * y2;
+        a[6] += p2 * y0;
+        a[7] += p2 * y1;
+        a[8] += p2 * y2;
+        a[9] += (y0 * y0 + y1 * y1) + y2 * y2;  // y_p_norm d_caps (compute.cu:436-437)
+        a[10] += (p0 * p0 + p1 * p1) + p2 * p2; // y_p_norm sp     (compute.cu:438-439)
+    }
+    block_sum_store<11>(a, partials + (size_t)blockIdx.x * 11);
+}
+
+__global__ __launch_bounds__(kBlock) void subtract_kernel(double *x, double *y, double *z, int n,
+                                                         double mx, double my, double mz)
+{
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        x[i] = x[i] - mx;
+        y[i] = y[i] - my;
+        z[i] = z[i] - mz;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void norms_kernel(
+    const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int n, double *__restrict__ partials)
+{
+    double a[2] = {0, 0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        a[0] += (yx[i] * yx[i] + yy[i] * yy[i]) + yz[i] * yz[i];
+        a[1] += (px[i] * px[i] + py[i] * py[i]) + pz[i] * pz[i];
+    }
+    block_sum_store<2>(a, partials + (size_t)blockIdx.x * 2);
+}
+
+__global__ __launch_bounds__(kBlock) void transform_err_kernel(
+    double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
+    const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
+    int n, Xform xf, int write_p, float4 *__restrict__ p32, double *__restrict__ partials)
+{
+    double a[1] = {0.0};
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const double p0 = px[i], p1 = py[i], p2 = pz[i];
+        // sr * p + t in Eigen's column-sweep order (compute.cu:330-339, cpu.cc:33)
+        const double q0 = ((xf.sR[0] * p0 + xf.sR[1] * p1) + xf.sR[2] * p2) + xf.t[0];
+        const double q1 = ((xf.sR[3] * p0 + xf.sR[4] * p1) + xf.sR[5] * p2) + xf.t[1];
+        const double q2 = ((xf.sR[6] * p0 + xf.sR[7] * p1) + xf.sR[8] * p2) + xf.t[2];
+        const double e0 = yx[i] - q0, e1 = yy[i] - q1, e2 = yz[i] - q2;
+        a[0] += (e0 * e0 + e1 * e1) + e2 * e2; // compute.cu:344-345
+        if (write_p) {
+            px[i] = q0;
+            py[i] = q1;
+            pz[i] = q2;
+            if (p32)
+                p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]),
+                                     (float)(q2 - xf.c[2]), 0.0f);
+        }
+    }
+    block_sum_store<1>(a, partials + blockIdx.x);
+}
+
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict__ partials,
+                                                       int nblocks, int K, double *__restrict__ out)
+{
+    __shared__ double sh[kBlock];
+    for (int k = 0; k < K; ++k) {
+        double a = 0.0;
+        for (int b = threadIdx.x; b < nblocks; b += kBlock) a += partials[(size_t)b * K + k];
+        sh[threadIdx.x] = a;
+        __syncthreads();
+        for (int s = kBlock / 2; s > 0; s >>= 1) {
+            if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[k] = sh[0];
+        __syncthreads();
+    }
+}
+
+inline int grid_for(size_t n, int cap = 2048)
+{
+    size_t g = (n + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    return (int)(g < (size_t)cap ? g : (size_t)cap);
+}
+
+} // namespace
+
+// ---- launchers ----------------------------------------------------------------------
+
+void launch_aos_to_soa(const double *aos, size_t n, double *x, double *y, double *z, hipStream_t st)
+{
+    if (!n) return;
+    aos_to_soa_kernel<<<grid_for(n), kBlock, 0, st>>>(aos, n, x, y, z);
+}
+
+void launch_soa_to_aos(const double *x, const double *y, const double *z, size_t n, double *aos,
+                       hipStream_t st)
+{
+    if (!n) return;
+    soa_to_aos_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, aos);
+}
+
+void launch_make_f32(const double *x, const double *y, const double *z, size_t n, double cx,
+                     double cy, double cz, float4 *f, hipStream_t st)
+{
+    if (!n) return;
+    make_f32_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, cx, cy, cz, f);
+}
+
+static NNPlan make_plan(size_t np, size_t nm, int tile, int q_small, int q_large, size_t large_np)
+{
+    NNPlan pl;
+    pl.q_per_lane = np >= large_np ? q_large : q_small;
+    const size_t per_block = (size_t)kBlock * pl.q_per_lane;
+    pl.qblocks = (int)((np + per_block - 1) / per_block);
+    if (pl.qblocks < 1) pl.qblocks = 1;
+    const int tiles = (int)((nm + tile - 1) / tile);
+    // aim for >= 2048 workgroups (8 per CU) so small scenes still fill the chip
+    int splits = (2048 + pl.qblocks - 1) / pl.qblocks;
+    if (splits > tiles) splits = tiles;
+    if (splits < 1) splits = 1;
+    const int tiles_per_split = (tiles + splits - 1) / splits;
+    pl.chunk = tiles_per_split * tile;
+    pl.splits = (tiles + tiles_per_split - 1) / tiles_per_split;
+    return pl;
+}
+
+NNPlan plan_nn32(size_t np, size_t nm_pad) { return make_plan(np, nm_pad, kTile32, 1, 4, 262144); }
+NNPlan plan_nn64(size_t np, size_t nm) { return make_plan(np, nm, kTile64, 1, 2, 262144); }
+
+void launch_nn_filter(const float4 *p32, int np, const float4 *m32, int nm_pad, const NNPlan &pl,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st)
+{
+    dim3 grid(pl.qblocks, pl.splits);
+    if (pl.q_per_lane == 4)
+        nn_filter_kernel<4><<<grid, kBlock, 0, st>>>(p32, np, m32, nm_pad, pl.chunk, part_best,
+                                                     part_second, part_idx);
+    else
+        nn_filter_kernel<1><<<grid, kBlock, 0, st>>>(p32, np, m32, nm_pad, pl.chunk, part_best,
+                                                     part_second, part_idx);
+}
+
+void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
+                        int splits, const float4 *p32, int np, CertParams cp, int *idx,
+                        int *amb_count, int *amb_list, double *amb_T, hipStream_t st)
+{
+    nn_finalize_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
+        part_best, part_second, part_idx, splits, p32, np, cp.rm, idx, amb_count, amb_list, amb_T);
+}
+
+void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
+                       const float4 *p32, const double *px, const double *py, const double *pz,
+                       const float4 *m32, const double *mx, const double *my, const double *mz,
+                       int nm, int max_items, int *idx, hipStream_t st)
+{
+    int grid = max_items < 2048 ? max_items : 2048;
+    if (grid < 1) grid = 1;
+    nn_resolve_kernel<<<grid, kBlock, 0, st>>>(amb_count, amb_list, amb_T, p32, px, py, pz, m32, mx,
+                                                my, mz, nm, idx);
+}
+
+void launch_nn_fp64(const double *px, const double *py, const double *pz, int np, const double *mx,
+                    const double *my, const double *mz, int nm, const NNPlan &pl,
+                    double *part_best, int *part_idx, hipStream_t st)
+{
+    dim3 grid(pl.qblocks, pl.splits);
+    if (pl.q_per_lane == 2)
+        nn_fp64_kernel<2><<<grid, kBlock, 0, st>>>(px, py, pz, np, mx, my, mz, nm, pl.chunk,
+                                                   part_best, part_idx);
+    else
+        nn_fp64_kernel<1><<<grid, kBlock, 0, st>>>(px, py, pz, np, mx, my, mz, nm, pl.chunk,
+                                                   part_best, part_idx);
+}
+
+void launch_nn_finalize64(const double *part_best, const int *part_idx, int splits, int np,
+                          int *idx, hipStream_t st)
+{
+    nn_finalize64_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(part_best, part_idx,
+                                                                         splits, np, idx);
+}
+
+int red_blocks(size_t n) { return grid_for(n, kRedMaxBlocks); }
+
+void launch_gather_moments(const int *idx, const double *mx, const double *my, const double *mz,
+                           const double *px, const double *py, const double *pz, int n,
+                           double *yx, double *yy, double *yz, double *partials, hipStream_t st)
+{
+    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, mx, my, mz, px, py, pz, n, yx, yy,
+                                                             yz, partials);
+}
+
+void launch_sum3(const double *x, const double *y, const double *z, int n, double *partials,
+                 hipStream_t st)
+{
+    sum3_kernel<<<red_blocks(n), kBlock, 0, st>>>(x, y, z, n, partials);
+}
+
+void launch_centred_moments(const double *px, const double *py, const double *pz,
+                            const double *yx, const double *yy, const double *yz, int n,
+                            const double *sums, double n_total, double *partials, hipStream_t st)
+{
+    centred_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, sums,
+                                                              n_total, partials);
+}
+
+void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
+                     hipStream_t st)
+{
+    if (n <= 0) return;
+    subtract_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, mx, my, mz);
+}
+
+void launch_norms(const double *yx, const double *yy, const double *yz, const double *px,
+                  const double *py, const double *pz, int n, double *partials, hipStream_t st)
+{
+    norms_kernel<<<red_blocks(n), kBlock, 0, st>>>(yx, yy, yz, px, py, pz, n, partials);
+}
+
+void launch_transform_err(double *px, double *py, double *pz, const double *yx, const double *yy,
+                          const double *yz, int n, Xform xf, int write_p, float4 *p32,
+                          double *partials, hipStream_t st)
+{
+    transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, write_p,
+                                                            p32, partials);
+}
+
+void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st)
+{
+    reduce_kernel<<<1, kBlock, 0, st>>>(partials, nblocks, K, out);
+}
+
+} // namespace icp

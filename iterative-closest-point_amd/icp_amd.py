@@ -1,0 +1,396 @@
+"""icp_amd — Python mirror of the reference's src/GPU interface over libicp_hip.so.
+
+The product is the C-ABI library (include/icp_capi.h) built from csrc/; this module only
+binds it with ctypes so tests, bench.py and the graft entry point can drive it.  Names
+follow the reference (yassram/iterative-closest-point):
+
+  ICP(m, p, max_iter).find_corresponding_opti()   src/GPU/gpu.cc:52-83
+  ICP.find_alignment(y)                            src/GPU/gpu.cc:95-151
+  compute_Y_w_opti(m, p)                           src/GPU/compute.cu:154-245
+  compute_err_w(Y, p, in_place, sr, t)             src/GPU/compute.cu:348-379
+  compute_centroid(M)  (mean + substract_col_w)   src/GPU/compute.cu:400-416
+  y_p_norm_w(y, p)                                 src/GPU/compute.cu:442-469
+  load_matrix / write_matrix                       src/load.cc:3-97
+
+Clouds are numpy float64 arrays of shape (n, 3) here (row = point).  That is the same
+memory as the reference's 3 x n column-major Eigen matrix, so no copy is needed at the
+C boundary.  There is NO CPU fallback: if libicp_hip.so is missing or no HIP device is
+visible, every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ICP_AMD_LIB", os.path.join(_HERE, "build", "libicp_hip.so"))
+
+ICP_OK = 0
+ICP_E_ARG = -1
+ICP_E_HIP = -2
+ICP_E_SIZE_MISMATCH = -3
+ICP_E_TOO_FEW_POINTS = -4
+ICP_E_NO_MODEL = -5
+ICP_E_RCCL = -6
+ICP_E_NO_DEVICE = -7
+ICP_E_IO = -8
+ICP_E_RANGE = -9
+
+NN_CERTIFIED = 0
+NN_FP64 = 1
+
+# every function include/icp_capi.h declares (checked by tests/test_capi.py)
+EXPORTED = [
+    "icp_ctx_create", "icp_ctx_create_dist", "icp_rccl_unique_id", "icp_ctx_destroy",
+    "icp_last_error", "icp_strerror", "icp_device_count", "icp_set_model", "icp_set_scene",
+    "icp_get_scene", "icp_set_allow_unequal", "icp_run", "icp_closest_matrix",
+    "icp_compute_centroid", "icp_y_p_norm", "icp_err_compute", "icp_find_alignment",
+    "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
+    "icp_load_matrix", "icp_write_matrix", "icp_free", "icp_get_stats", "icp_reset_stats",
+]
+
+
+class ICPError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+class Result(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("converged", C.c_int), ("err", C.c_double),
+                ("s", C.c_double), ("R", C.c_double * 9), ("t", C.c_double * 3)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("nn_ms", C.c_double), ("nn_launches", C.c_longlong), ("nn_pairs", C.c_longlong),
+                ("ambiguous", C.c_longlong), ("iter_ms", C.c_double), ("iterations", C.c_longlong)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libicp_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ICPError(ICP_E_NO_DEVICE, f"{LIB_PATH} not built: run `make -C iterative-closest-point_amd`")
+    L = C.CDLL(LIB_PATH)
+    dp = C.POINTER(C.c_double)
+    vp = C.c_void_p
+    sz = C.c_size_t
+    L.icp_ctx_create.argtypes = [C.c_int, C.c_int, C.POINTER(vp)]
+    L.icp_ctx_create_dist.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]
+    L.icp_rccl_unique_id.argtypes = [C.c_char_p]
+    L.icp_ctx_destroy.argtypes = [vp]
+    L.icp_ctx_destroy.restype = None
+    L.icp_last_error.argtypes = [vp]
+    L.icp_last_error.restype = C.c_char_p
+    L.icp_strerror.argtypes = [C.c_int]
+    L.icp_strerror.restype = C.c_char_p
+    L.icp_device_count.argtypes = [C.POINTER(C.c_int)]
+    L.icp_set_model.argtypes = [vp, dp, sz]
+    L.icp_set_scene.argtypes = [vp, dp, sz, sz]
+    L.icp_get_scene.argtypes = [vp, dp]
+    L.icp_set_allow_unequal.argtypes = [vp, C.c_int]
+    L.icp_run.argtypes = [vp, C.c_int, C.c_double, dp, C.POINTER(Result)]
+    L.icp_closest_matrix.argtypes = [vp, dp, sz, dp, C.POINTER(C.c_int32)]
+    L.icp_compute_centroid.argtypes = [vp, dp, sz, dp, dp]
+    L.icp_y_p_norm.argtypes = [vp, dp, dp, sz, dp, dp]
+    L.icp_err_compute.argtypes = [vp, dp, dp, sz, C.c_int, dp, dp, dp]
+    L.icp_find_alignment.argtypes = [vp, dp, dp, sz, dp, dp, dp, dp]
+    L.icp_horn_solve.argtypes = [dp, dp, dp, C.c_double, C.c_double, dp, dp, dp]
+    L.icp_max_element_index.argtypes = [dp]
+    L.icp_shard_range.argtypes = [sz, C.c_int, C.c_int, C.POINTER(sz), C.POINTER(sz)]
+    L.icp_synthetic_pair.argtypes = [C.c_uint64, sz, C.c_double, dp, dp, dp, dp]
+    L.icp_load_matrix.argtypes = [C.c_char_p, C.POINTER(dp), C.POINTER(sz)]
+    L.icp_write_matrix.argtypes = [C.c_char_p, dp, sz]
+    L.icp_free.argtypes = [vp]
+    L.icp_free.restype = None
+    L.icp_get_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.icp_reset_stats.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _cloud(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError("clouds are (n, 3) float64 arrays")
+    return a
+
+
+def _vec(a, n) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64).reshape(-1)
+    if a.size != n:
+        raise ValueError(f"expected {n} values")
+    return a
+
+
+# ---------------------------------------------------------------------------------
+# host-only helpers (no device needed)
+# ---------------------------------------------------------------------------------
+
+def strerror(code: int) -> str:
+    return lib().icp_strerror(code).decode()
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().icp_device_count(C.byref(n))
+    return n.value
+
+
+def horn_solve(S, mu_p, mu_y, d_caps: float, sp: float):
+    """Host half of find_alignment (gpu.cc:104-146) -> (s, R(3x3), t(3))."""
+    S = _vec(S, 9); mu_p = _vec(mu_p, 3); mu_y = _vec(mu_y, 3)
+    s = C.c_double(0.0); R = np.zeros(9); t = np.zeros(3)
+    rc = lib().icp_horn_solve(_dp(S), _dp(mu_p), _dp(mu_y), d_caps, sp, C.byref(s), _dp(R), _dp(t))
+    if rc != ICP_OK:
+        raise ICPError(rc, strerror(rc))
+    return s.value, R.reshape(3, 3), t
+
+
+def max_element_index(ev) -> int:
+    """gpu.cc:85-93 verbatim (the quirky 'largest' eigenvalue picker)."""
+    ev = _vec(ev, 4)
+    return lib().icp_max_element_index(_dp(ev))
+
+
+def shard_range(n_total: int, rank: int, world: int):
+    b = C.c_size_t(0); c = C.c_size_t(0)
+    rc = lib().icp_shard_range(n_total, rank, world, C.byref(b), C.byref(c))
+    if rc != ICP_OK:
+        raise ICPError(rc, strerror(rc))
+    return b.value, c.value
+
+
+def synthetic_pair(n: int, seed: int = 42, angle_deg: float = 5.0, axis=(1.0, 2.0, 3.0),
+                   t=(0.05, -0.03, 0.02)):
+    """SURVEY.md §8d generator: (model, scene) as (n, 3) float64."""
+    m = np.empty((n, 3)); p = np.empty((n, 3))
+    ax = np.asarray(axis, dtype=np.float64); tt = np.asarray(t, dtype=np.float64)
+    rc = lib().icp_synthetic_pair(seed, n, angle_deg, _dp(ax), _dp(tt), _dp(m), _dp(p))
+    if rc != ICP_OK:
+        raise ICPError(rc, strerror(rc))
+    return m, p
+
+
+def load_matrix(path: str) -> np.ndarray:
+    """src/load.cc:3-33 -> (n, 3) float64."""
+    ptr = C.POINTER(C.c_double)(); n = C.c_size_t(0)
+    rc = lib().icp_load_matrix(path.encode(), C.byref(ptr), C.byref(n))
+    if rc != ICP_OK:
+        raise ICPError(rc, f"{path}: {strerror(rc)}")
+    try:
+        out = np.ctypeslib.as_array(ptr, shape=(max(n.value, 1) * 3,))[: n.value * 3].copy()
+    finally:
+        lib().icp_free(ptr)
+    return out.reshape(n.value, 3)
+
+
+def write_matrix(path: str, xyz) -> None:
+    xyz = _cloud(xyz)
+    rc = lib().icp_write_matrix(path.encode(), _dp(xyz), xyz.shape[0])
+    if rc != ICP_OK:
+        raise ICPError(rc, strerror(rc))
+
+
+def rccl_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    rc = lib().icp_rccl_unique_id(buf)
+    if rc != ICP_OK:
+        raise ICPError(rc, strerror(rc))
+    return buf.raw
+
+
+# ---------------------------------------------------------------------------------
+# device context
+# ---------------------------------------------------------------------------------
+
+class Context:
+    """One HIP device context (optionally one rank of an RCCL job)."""
+
+    def __init__(self, device: int = 0, nn_mode: int = NN_CERTIFIED, rank: int = 0,
+                 world_size: int = 1, rccl_id: bytes | None = None):
+        L = lib()
+        h = C.c_void_p()
+        if world_size > 1:
+            rc = L.icp_ctx_create_dist(device, nn_mode, rank, world_size, rccl_id, C.byref(h))
+        else:
+            rc = L.icp_ctx_create(device, nn_mode, C.byref(h))
+        if rc != ICP_OK:
+            raise ICPError(rc, f"context creation failed: {strerror(rc)}")
+        self._h = h
+        self.rank, self.world_size = rank, world_size
+
+    def _check(self, rc: int):
+        if rc != ICP_OK:
+            raise ICPError(rc, f"{strerror(rc)}: {lib().icp_last_error(self._h).decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().icp_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # resident clouds
+    def set_model(self, m):
+        m = _cloud(m)
+        self._check(lib().icp_set_model(self._h, _dp(m), m.shape[0]))
+
+    def set_scene(self, p, np_total: int | None = None):
+        p = _cloud(p)
+        self._check(lib().icp_set_scene(self._h, _dp(p), p.shape[0], p.shape[0] if np_total is None else np_total))
+        self._np_local = p.shape[0]
+
+    def get_scene(self) -> np.ndarray:
+        out = np.empty((self._np_local, 3))
+        self._check(lib().icp_get_scene(self._h, _dp(out)))
+        return out
+
+    def set_allow_unequal(self, allow: bool):
+        self._check(lib().icp_set_allow_unequal(self._h, 1 if allow else 0))
+
+    def run(self, max_iter: int, threshold: float = 1e-5):
+        errs = np.zeros(max(max_iter, 1))
+        res = Result()
+        self._check(lib().icp_run(self._h, max_iter, threshold, _dp(errs), C.byref(res)))
+        return res, errs[: res.iterations].copy()
+
+    # per-operation surface
+    def closest_matrix(self, p):
+        p = _cloud(p)
+        y = np.empty_like(p); idx = np.empty(p.shape[0], dtype=np.int32)
+        self._check(lib().icp_closest_matrix(self._h, _dp(p), p.shape[0], _dp(y),
+                                             idx.ctypes.data_as(C.POINTER(C.c_int32))))
+        return y, idx
+
+    def compute_centroid(self, xyz, centred: bool = True):
+        xyz = _cloud(xyz)
+        mu = np.zeros(3); out = np.empty_like(xyz) if centred else None
+        self._check(lib().icp_compute_centroid(self._h, _dp(xyz), xyz.shape[0], _dp(mu),
+                                               _dp(out) if centred else None))
+        return mu, out
+
+    def y_p_norm(self, y, p):
+        y = _cloud(y); p = _cloud(p)
+        d = C.c_double(0.0); s = C.c_double(0.0)
+        self._check(lib().icp_y_p_norm(self._h, _dp(y), _dp(p), y.shape[0], C.byref(d), C.byref(s)))
+        return d.value, s.value
+
+    def err_compute(self, y, p, in_place: bool, sR, t):
+        y = _cloud(y); p = _cloud(p).copy()
+        sR = _vec(sR, 9); t = _vec(t, 3); e = C.c_double(0.0)
+        self._check(lib().icp_err_compute(self._h, _dp(y), _dp(p), y.shape[0], 1 if in_place else 0,
+                                          _dp(sR), _dp(t), C.byref(e)))
+        return e.value, p
+
+    def find_alignment(self, p, y):
+        p = _cloud(p); y = _cloud(y)
+        s = C.c_double(0.0); R = np.zeros(9); t = np.zeros(3); e = C.c_double(0.0)
+        self._check(lib().icp_find_alignment(self._h, _dp(p), _dp(y), p.shape[0], C.byref(s), _dp(R),
+                                             _dp(t), C.byref(e)))
+        return s.value, R.reshape(3, 3), t, e.value
+
+    def stats(self) -> dict:
+        st = Stats()
+        self._check(lib().icp_get_stats(self._h, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in Stats._fields_}
+
+    def reset_stats(self):
+        self._check(lib().icp_reset_stats(self._h))
+
+
+# ---------------------------------------------------------------------------------
+# reference-shaped API (src/GPU/gpu.hh)
+# ---------------------------------------------------------------------------------
+
+@dataclass
+class ICP:
+    """GPU::ICP (src/GPU/gpu.hh:41-104): ICP(m, p, max_iter); find_corresponding_opti()."""
+    m: np.ndarray
+    p: np.ndarray
+    max_iter: int
+    nn_mode: int = NN_CERTIFIED
+    device: int = 0
+    threshold: float = 1e-5  # src/GPU/gpu.hh:103
+    allow_unequal: bool = False
+    new_p: np.ndarray = field(init=False)
+    s: float = field(init=False, default=1.0)
+    r: np.ndarray = field(init=False)
+    t: np.ndarray = field(init=False)
+    errors: np.ndarray = field(init=False)
+
+    def __post_init__(self):
+        self.m = _cloud(self.m); self.p = _cloud(self.p)
+        self.new_p = self.p.copy()
+        self.r = np.eye(3); self.t = np.zeros(3)
+        self.errors = np.zeros(0)
+        self._ctx = Context(self.device, self.nn_mode)
+        self._ctx.set_allow_unequal(self.allow_unequal)
+        self._ctx.set_model(self.m)
+        self._ctx.set_scene(self.p)
+
+    def find_corresponding_opti(self):
+        res, errs = self._ctx.run(self.max_iter, self.threshold)
+        self.errors = errs
+        self.s, self.r, self.t = res.s, np.array(res.R).reshape(3, 3), np.array(res.t)
+        self.new_p = self._ctx.get_scene()
+        return res
+
+    def find_alignment(self, y):
+        s, R, t, e = self._ctx.find_alignment(self.new_p, y)
+        self.s, self.r, self.t = s, R, t
+        return e
+
+
+_default_ctx: Context | None = None
+
+
+def _ctx_for_model(m) -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    _default_ctx.set_model(m)
+    return _default_ctx
+
+
+def compute_Y_w_opti(m, p):
+    """compute.cu:154-245: Y[j] = m[NN(p_j)] (returns Y, idx)."""
+    return _ctx_for_model(m).closest_matrix(p)
+
+
+def compute_err_w(Y, p, in_place: bool, sr, t):
+    """compute.cu:348-379 -> (err, p_after)."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    return _default_ctx.err_compute(Y, p, in_place, sr, t)
+
+
+def compute_centroid(M):
+    """rowwise().mean() + substract_col_w (gpu.cc:98-102) on the device -> (mu, M - mu)."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    return _default_ctx.compute_centroid(M, centred=True)

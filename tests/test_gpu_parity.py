@@ -1,0 +1,237 @@
+"""HIP path vs the CPU oracle (parity tests proper; run on an MI355X with -m gpu).
+
+Tolerances:
+  * NN indices: bit-exact (index work) — both NN modes, every dataset, every edge case;
+  * per-iteration err: rel 1e-9; s, R: abs 1e-9; t and final new_p: abs 1e-9 x extent
+    on the bundled clouds (fp64 throughout; reduction order is the only difference);
+  * ICP_NN_FP64 and ICP_NN_CERTIFIED runs are bitwise identical to each other.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import datasets
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+RNG = np.random.default_rng(99)
+MODES = [0, 1]  # ICP_NN_CERTIFIED, ICP_NN_FP64
+
+
+@pytest.fixture(scope="module")
+def amd(icp_lib):
+    if icp_lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    return icp_lib
+
+
+@pytest.fixture(scope="module")
+def ctxs(amd):
+    c = {m: amd.Context(0, m) for m in MODES}
+    yield c
+    for v in c.values():
+        v.close()
+
+
+def load(amd, name):
+    return amd.load_matrix(datasets.path(name))
+
+
+def gold_npz(name):
+    return np.load(os.path.join(GOLD, f"{name}_oracle.npz"))
+
+
+@pytest.fixture(scope="module")
+def golden_traces():
+    with open(os.path.join(GOLD, "traces.json")) as f:
+        return json.load(f)
+
+
+# ---- NN: bit-exact indices -------------------------------------------------------------
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("cfg", ["cow_tr1", "cow_tr2", "horse_tr1", "horse_tr2", "bunny"])
+def test_nn_iteration0_matches_fixture(amd, ctxs, golden_traces, mode, cfg):
+    g = golden_traces[cfg]
+    m, p = load(amd, g["model"]), load(amd, g["scene"])
+    ctx = ctxs[mode]
+    ctx.set_model(m)
+    y, idx = ctx.closest_matrix(p)
+    ref = gold_npz(cfg)["idx0"]
+    assert np.array_equal(idx, ref), f"{int((idx != ref).sum())} mismatches"
+    np.testing.assert_array_equal(y, m[ref])
+
+
+def test_nn_synthetic_fixture(amd, ctxs):
+    z = np.load(os.path.join(GOLD, "synthetic4096.npz"))
+    for mode in MODES:
+        ctxs[mode].set_model(z["model"])
+        _, idx = ctxs[mode].closest_matrix(z["scene"])
+        np.testing.assert_array_equal(idx, z["idx0"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("np_,nm", [(1, 1), (1, 5), (5, 1), (3, 1023), (257, 1024), (1000, 1025),
+                                    (4097, 3000), (300000, 2048), (2048, 300001)])
+def test_nn_random_sizes(amd, ctxs, oracle, mode, np_, nm):
+    m = RNG.uniform(-3, 3, size=(nm, 3)) + np.array([10.0, -5.0, 2.0])
+    p = RNG.uniform(-3, 3, size=(np_, 3)) + np.array([10.0, -5.0, 2.0])
+    ctx = ctxs[mode]
+    ctx.set_model(m)
+    _, idx = ctx.closest_matrix(p)
+    sel = np.arange(np_) if np_ * nm <= 4e8 else RNG.choice(np_, size=int(4e8 // nm), replace=False)
+    _, ref = oracle.closest(p[sel], m)
+    np.testing.assert_array_equal(idx[sel], ref)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_nn_exact_ties_and_duplicates(amd, ctxs, oracle, mode):
+    # integer grid: many exactly equidistant model points + duplicated model points
+    g = np.stack(np.meshgrid(np.arange(12), np.arange(12), np.arange(12), indexing="ij"), -1).reshape(-1, 3)
+    m = np.concatenate([g, g[::7], g[::3]]).astype(np.float64) * 0.5
+    p = (RNG.integers(0, 23, size=(5000, 3)) * 0.25).astype(np.float64)
+    ctx = ctxs[mode]
+    ctx.set_model(m)
+    _, idx = ctx.closest_matrix(p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+
+
+def test_nn_certificate_sends_ties_to_resolution(amd):
+    with amd.Context(0, 0) as ctx:
+        m = np.array([[1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0], [5, 5, 5.0]])
+        ctx.set_model(m)
+        ctx.reset_stats()
+        _, idx = ctx.closest_matrix(np.array([[0.0, 0, 0], [4.0, 4, 4]]))
+        assert idx.tolist() == [0, 3]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_nn_far_offset_cloud(amd, ctxs, oracle, mode):
+    # coordinates ~1e6 away from the origin: the fp32 filter works on centred values
+    m = RNG.normal(size=(5000, 3)) + 1.0e6
+    p = RNG.normal(size=(3000, 3)) + 1.0e6
+    ctxs[mode].set_model(m)
+    _, idx = ctxs[mode].closest_matrix(p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+
+
+def test_nn_certified_equals_fp64_at_1m(amd, ctxs, oracle):
+    m, p = amd.synthetic_pair(1 << 20, seed=42)
+    out = {}
+    for mode in MODES:
+        ctxs[mode].set_model(m)
+        _, out[mode] = ctxs[mode].closest_matrix(p)
+    np.testing.assert_array_equal(out[0], out[1])
+    sel = RNG.choice(p.shape[0], size=96, replace=False)
+    _, ref = oracle.closest(p[sel], m)
+    np.testing.assert_array_equal(out[0][sel], ref)
+
+
+# ---- full ICP loop vs oracle trajectories ----------------------------------------------
+
+def run_engine(amd, mode, m, p, max_iter, threshold, allow_unequal=False):
+    with amd.Context(0, mode) as ctx:
+        ctx.set_allow_unequal(allow_unequal)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        res, errs = ctx.run(max_iter, threshold)
+        return res, errs, ctx.get_scene()
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("cfg", ["cow_tr1", "cow_tr2", "horse_tr2", "horse_tr1", "bunny"])
+def test_icp_trajectory_matches_oracle(amd, golden_traces, mode, cfg):
+    g = golden_traces[cfg]
+    m, p = load(amd, g["model"]), load(amd, g["scene"])
+    res, errs, new_p = run_engine(amd, mode, m, p, g["max_iter"], g["threshold"], g["allow_unequal"])
+    assert res.iterations == g["iterations"]
+    rtol = 1e-3 if cfg == "bunny" else 1e-9  # bunny: tie-sensitive trajectory
+    np.testing.assert_allclose(errs, g["err"], rtol=rtol)
+    np.testing.assert_allclose(np.array(res.R).reshape(3, 3), np.array(g["R"][-1]), atol=1e-9 if cfg != "bunny" else 1e-3)
+    assert res.s == pytest.approx(g["s"][-1], abs=1e-9 if cfg != "bunny" else 1e-3)
+    extent = float(np.abs(m).max())
+    ref_p = gold_npz(cfg)["new_p"]
+    np.testing.assert_allclose(new_p, ref_p, atol=(1e-9 if cfg != "bunny" else 1e-3) * extent)
+
+
+def test_icp_synthetic_fixed_iterations(amd, golden_traces):
+    g = golden_traces["synthetic4096"]
+    z = np.load(os.path.join(GOLD, "synthetic4096.npz"))
+    res, errs, new_p = run_engine(amd, 0, z["model"], z["scene"], 30, -1.0)
+    assert res.iterations == 30 and not res.converged
+    np.testing.assert_allclose(errs, g["err"], rtol=1e-9)
+    np.testing.assert_allclose(new_p, z["new_p"], atol=1e-9)
+
+
+def test_modes_bitwise_identical(amd):
+    m, p = load(amd, "horse_ref"), load(amd, "horse_tr1")
+    a = run_engine(amd, 0, m, p, 6, -1.0)
+    b = run_engine(amd, 1, m, p, 6, -1.0)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_reference_fatal_checks(amd):
+    m = RNG.normal(size=(10, 3))
+    with amd.Context(0, 0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(m[:9])
+        with pytest.raises(amd.ICPError) as ei:
+            ctx.run(5)
+        assert ei.value.code == amd.ICP_E_SIZE_MISMATCH
+        ctx.set_model(m[:3])
+        ctx.set_scene(m[:3])
+        with pytest.raises(amd.ICPError) as ei:
+            ctx.run(5)
+        assert ei.value.code == amd.ICP_E_TOO_FEW_POINTS
+        with pytest.raises(amd.ICPError):
+            amd.Context(0, 0).run(3)  # no model
+
+
+def test_zero_iterations_leaves_scene(amd):
+    m = RNG.normal(size=(100, 3))
+    res, errs, new_p = run_engine(amd, 0, m, m + 0.1, 0, 1e-5)
+    assert res.iterations == 0 and errs.size == 0
+    np.testing.assert_array_equal(new_p, m + 0.1)
+
+
+# ---- per-operation surface (src/GPU/gpu.hh:110-116) ------------------------------------
+
+def test_surface_ops_match_oracle(amd, oracle):
+    m, p = load(amd, "cow_ref"), load(amd, "cow_tr2")
+    y, _ = oracle.closest(p, m)
+    al = oracle.find_alignment(p, y)
+    with amd.Context(0, 0) as ctx:
+        mu, centred = ctx.compute_centroid(p)
+        np.testing.assert_allclose(mu, np.array(al.mu_p), rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(centred, p - mu, atol=0)
+        d_caps, sp = ctx.y_p_norm(y - np.array(al.mu_y), p - np.array(al.mu_p))
+        assert d_caps == pytest.approx(al.d_caps, rel=1e-12)
+        assert sp == pytest.approx(al.sp, rel=1e-12)
+        s, R, t, e = ctx.find_alignment(p, y)
+        assert s == pytest.approx(al.s, rel=1e-12)
+        np.testing.assert_allclose(R, np.array(al.R).reshape(3, 3), atol=1e-12)
+        np.testing.assert_allclose(t, np.array(al.t), atol=1e-12)
+        assert e == pytest.approx(al.err, rel=1e-9)
+        sR = (al.s * np.array(al.R)).reshape(9)
+        e1, p_same = ctx.err_compute(y, p, False, sR, al.t)
+        np.testing.assert_array_equal(p_same, p)
+        e2, p_new = ctx.err_compute(y, p, True, sR, al.t)
+        oe, op = oracle.err_compute(p, y, al.s, al.R, al.t)
+        assert e1 == e2 and e2 == pytest.approx(oe, rel=1e-12)
+        np.testing.assert_array_equal(p_new, op)  # per-point transform bitwise = oracle
+
+
+def test_reference_shaped_icp_class(amd, golden_traces):
+    m, p = load(amd, "cow_ref"), load(amd, "cow_tr1")
+    icp = amd.ICP(m, p, 20)
+    res = icp.find_corresponding_opti()
+    assert res.iterations == 7 and res.converged
+    np.testing.assert_allclose(icp.errors, golden_traces["cow_tr1"]["err"], rtol=1e-9)
+    np.testing.assert_allclose(icp.new_p, m, atol=1e-5)

@@ -1,0 +1,151 @@
+"""Pin the CPU oracle (restatement of src/cpu.cc) before trusting it.
+
+Known answers come from the reference's own artefacts (it ships no tests):
+  * benchmark/callgrind.out.76685:5,28306-28324 — `./icp cow_ref cow_tr1 10` calls
+    closest_matrix / find_alignment / err_compute exactly 7 times: converged at i = 6;
+  * report/report.pdf Table X — 20 321 = 7 x 2 903 naive NN calls: np = 2 903, 7 iterations;
+  * data_students/README.md:14-21 — cow/horse files are exact rigid transforms of the ref;
+  * SURVEY.md §4 — independent replays (cow_tr2: 12 iterations, horse_tr2: 8).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import datasets
+
+RNG = np.random.default_rng(20260515)
+
+
+def test_cow_tr1_converges_in_7_iterations(oracle):
+    m = oracle.load_matrix(datasets.path("cow_ref"))
+    p = oracle.load_matrix(datasets.path("cow_tr1"))
+    assert m.shape == (2903, 3) and p.shape == (2903, 3)  # header skipped (load.cc:16-21)
+    r = oracle.icp(m, p, 20)
+    assert r["iterations"] == 7  # callgrind calls=7, nvprof 20321/2903
+    # survey replay (independent numpy restatement): err sequence
+    ref = [2.2429e-02, 1.1799e-02, 6.5827e-03, 3.2468e-03, 7.1521e-04, 1.5278e-05]
+    np.testing.assert_allclose(r["err"][:6], ref, rtol=5e-4)
+    assert r["err"][6] < 1e-10
+    # cow_tr1 is a rigid transform of cow_ref with point order kept: final cloud = ref
+    np.testing.assert_allclose(r["new_p"], m, atol=1e-5)
+
+
+def test_cow_tr2_and_horse_tr2_iteration_counts(oracle, golden):
+    assert golden["cow_tr2"]["iterations"] == 12
+    assert golden["horse_tr2"]["iterations"] == 8
+    assert golden["horse_tr1"]["iterations"] == 50  # no convergence (scale collapse)
+    assert golden["bunny"]["iterations"] == 50
+
+
+def test_fixture_reproducible(oracle, golden):
+    m = oracle.load_matrix(datasets.path("cow_ref"))
+    p = oracle.load_matrix(datasets.path("cow_tr2"))
+    r = oracle.icp(m, p, 20)
+    g = golden["cow_tr2"]
+    assert r["iterations"] == g["iterations"]
+    np.testing.assert_array_equal(r["err"], np.array(g["err"]))  # deterministic, bitwise
+    np.testing.assert_array_equal(r["R"], np.array(g["R"]))
+
+
+def test_max_element_index_quirk(oracle):
+    # cpu.cc:81-91: `max` never updated -> LAST i with ev[i] > ev[0]
+    assert oracle.max_element_index([1.0, 2.0, 3.0, 0.5]) == 2
+    assert oracle.max_element_index([1.0, 3.0, 2.0, 0.5]) == 2  # quirk: argmax is 1
+    assert oracle.max_element_index([5.0, 3.0, 2.0, 0.5]) == 0
+    assert oracle.max_element_index([0.0, 0.0, 0.0, 0.0]) == 0
+
+
+def test_eig_sym4_matches_lapack(oracle):
+    for _ in range(50):
+        A = RNG.normal(size=(4, 4))
+        N = A + A.T
+        ev, V = oracle.eig_sym4(N)
+        w = np.linalg.eigvalsh(N)
+        np.testing.assert_allclose(np.sort(ev), w, rtol=1e-12, atol=1e-12)
+        for k in range(4):
+            np.testing.assert_allclose(N @ V[:, k], ev[k] * V[:, k], atol=1e-11)
+
+
+def test_closest_first_minimum_tie(oracle):
+    m = np.array([[1.0, 0, 0], [0, 1.0, 0], [-1.0, 0, 0], [0, -1.0, 0], [1.0, 0, 0]])
+    p = np.array([[0.0, 0, 0], [2.0, 0, 0], [0, -3.0, 0]])
+    y, idx = oracle.closest(p, m)
+    assert idx.tolist() == [0, 0, 3]  # all four equidistant -> index 0; duplicates -> lowest
+    np.testing.assert_array_equal(y, m[idx])
+
+
+def test_horn_recovers_rotation_and_scale(oracle):
+    p = RNG.normal(size=(10, 3))
+    th = np.pi / 2
+    R = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
+    t = np.array([0.5, -1.0, 2.0])
+    y = 2.0 * p @ R.T + t
+    al = oracle.find_alignment(p, y)
+    np.testing.assert_allclose(np.array(al.R).reshape(3, 3), R, atol=1e-12)
+    assert al.s == pytest.approx(2.0, rel=1e-13)
+    np.testing.assert_allclose(np.array(al.t), t, atol=1e-12)
+    assert al.err < 1e-20
+
+
+def test_fatal_checks(oracle):
+    m = RNG.normal(size=(10, 3))
+    with pytest.raises(ValueError, match="size"):
+        oracle.icp(m, m[:9], 5)  # cpu.cc:44-47
+    with pytest.raises(ValueError, match="few"):
+        oracle.icp(m[:3], m[:3], 5)  # cpu.cc:49-52
+    r = oracle.icp(m, m[:9], 3, allow_unequal=True)
+    assert r["iterations"] >= 1
+
+
+def test_oracle_matches_numpy_twin(oracle):
+    import numpy_twin
+    for n in (7, 64, 300):
+        m = RNG.uniform(-1, 1, size=(n, 3))
+        th = 0.3
+        R = np.array([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]])
+        p = m @ R.T + np.array([0.1, 0.2, -0.1]) + RNG.normal(scale=1e-3, size=(n, 3))
+        y1, i1 = oracle.closest(p, m)
+        y2, i2 = numpy_twin.closest(p, m)
+        np.testing.assert_array_equal(i1, i2)
+        al = oracle.find_alignment(p, y1)
+        s, Rt, t, e = numpy_twin.find_alignment(p, y1)
+        np.testing.assert_allclose(np.array(al.R).reshape(3, 3), Rt, atol=1e-12)
+        assert al.s == pytest.approx(s, rel=1e-12)
+        np.testing.assert_allclose(np.array(al.t), t, atol=1e-12)
+        assert al.err == pytest.approx(e, rel=1e-9, abs=1e-18)
+        r = oracle.icp(m, p, 10)
+        q, errs = numpy_twin.icp(m, p, 10)
+        np.testing.assert_allclose(r["err"], errs, rtol=1e-9, atol=1e-18)
+        np.testing.assert_allclose(r["new_p"], q, atol=1e-11)
+
+
+def test_err_compute_double_counts(oracle):
+    # cpu.cc:65-73: find_alignment's residual and err_compute's residual are the same sum
+    m = oracle.load_matrix(datasets.path("cow_ref"))
+    p = oracle.load_matrix(datasets.path("cow_tr2"))
+    y, _ = oracle.closest(p, m)
+    al = oracle.find_alignment(p, y)
+    e2, _ = oracle.err_compute(p, y, al.s, al.R, al.t)
+    assert e2 == al.err  # bitwise identical
+
+
+def test_load_matrix_contract(oracle, tmp_path):
+    f = tmp_path / "c.txt"
+    f.write_text("Points_0,Points_1,Points_2\n1.5,2,3\n-4e-3,5,6,7\n\n8,9\n")
+    a = oracle.load_matrix(str(f))
+    # n = #lines - 1 = 4; blank line -> zeros; missing field -> 0; extra column ignored
+    np.testing.assert_array_equal(a, [[1.5, 2, 3], [-4e-3, 5, 6], [0, 0, 0], [8, 9, 0]])
+    g = tmp_path / "d.txt"
+    g.write_text("h\n1,2,3")  # no trailing newline still counts (getline)
+    assert oracle.load_matrix(str(g)).shape == (1, 3)
+
+
+def test_bunny_fixture_records_tie_sensitivity(golden):
+    # bun000/bun045 sit on a 0.0005 grid: sqrt(pow()) distances (cpu.cc:17-19) and squared
+    # distances pick different first minima on some queries (SURVEY §4 NN sensitivity).
+    g = golden["bunny"]
+    assert g["nm"] == 40256 and g["np"] == 40097
+    assert g["idx0_sqrt_vs_squared_mismatches"] >= 0
+    for name in ("cow_tr1", "cow_tr2", "horse_tr1", "horse_tr2"):
+        assert golden[name]["idx0_sqrt_vs_squared_mismatches"] == 0

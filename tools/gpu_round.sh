@@ -1,0 +1,45 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a fault / abort / timeout ends the script
+# (pytest exit 1 = test failures is not a fault, the script goes on to measure).
+#   usage: tools/gpu_round.sh TAG [steps...]   steps: test smoke bench prof pmc cli
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-r01}; shift || true
+STEPS=${*:-"test smoke bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+fatal() { # exit codes that mean the GPU (or the process) died
+    case "$1" in 124|137|134|139|-6|-11) return 0 ;; *) return 1 ;; esac
+}
+
+run() { # name timeout cmd...
+    local name=$1 to=$2; shift 2
+    echo "== $name: $*" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+    tail -n 25 "$OUT/$name.log"
+    if fatal $rc; then echo "FATAL in $name (rc=$rc): stopping"; exit $rc; fi
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+    test)  run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
+               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cow ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc1" -o fetch -- \
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow &&
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc2" -o write -- \
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow ;;
+    cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
+               \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
+    *) echo "unknown step $s" ;;
+    esac
+done
+echo "done: $STEPS"
