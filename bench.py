@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--nn", choices=["certified", "fp64"], default="certified")
+    ap.add_argument("--variant", choices=["auto", "valu", "mfma"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
     args = ap.parse_args()
@@ -117,8 +118,11 @@ def main():
     else:
         ctx = icp_amd.Context(local, nn_mode)
 
+    variant = {"auto": icp_amd.VARIANT_AUTO, "valu": icp_amd.VARIANT_VALU, "mfma": icp_amd.VARIANT_MFMA}[args.variant]
+    ctx.set_nn_variant(variant)
     m, p = icp_amd.synthetic_pair(args.n, seed=42)
     b, c = icp_amd.shard_range(args.n, rank, world)
+    uses_mfma = args.nn == "certified" and (args.variant == "mfma" or (args.variant == "auto" and c >= 65536 and args.n >= 65536))
     ctx.set_model(m)
     ctx.set_scene(p[b:b + c], np_total=args.n)
 
@@ -155,15 +159,19 @@ def main():
             "dtype": "f32 NN filter + f64 certificate/reductions",
             "data": "synthetic (mt19937_64 seed 42, uniform [-1,1]^3; scene = 5deg rotation + translation)",
             "config": {"workload": f"C4 synthetic {args.n}-pt model vs rigid-transformed copy, fixed iterations",
-                       "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn,
+                       "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
                        "parallelism": f"scene-sharded x{world}, model replicated, RCCL all-reduce of 18 fp64 sums/iter"},
-            "roofline": {"bound": "mfma", "compute_unit": "VALU fp32 (peak = f32 MFMA peak)",
-                         "kernel": "nn_filter_kernel", "achieved": achieved,
+            "roofline": {"bound": "mfma",
+                         "compute_unit": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)" if uses_mfma
+                         else ("VALU fp64" if args.nn == "fp64" else "VALU fp32 direct form (peak = f32 MFMA peak)"),
+                         "kernel": "nn_mfma_kernel" if uses_mfma else ("nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel"),
+                         "achieved": achieved,
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
                          "avg_launch_ms": nn_avg_ms, "flop_per_launch": flops,
                          "flop_definition": "8 flop per (query, model) pair"},
-            "ambiguous_queries_per_iter": st["ambiguous"] / max(st["iterations"], 1),
+            "mfma_uncertified_per_iter": st["level1_queued"] / max(st["iterations"], 1),
+            "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
         }
         if world == 1 and not args.no_cow:

@@ -44,6 +44,15 @@ extern "C" {
 #define ICP_NN_CERTIFIED 0 /* fp32 filter + per-query certificate + fp64 resolution (fast) */
 #define ICP_NN_FP64 1      /* fp64 brute force (reference-faithful cross-check)           */
 
+/* Filter used by ICP_NN_CERTIFIED (results identical; speed differs):
+ * VALU: direct-form fp32 distances on the vector ALUs (8 VALU ops per pair);
+ * MFMA: expanded form |m|^2 - 2 p.m on v_mfma_f32_16x16x4_f32 (256 pairs per instruction),
+ *       uncertified queries cascade to the VALU filter, then to fp64;
+ * AUTO: MFMA when both clouds have >= 65536 points, else VALU. */
+#define ICP_NN_VARIANT_AUTO 0
+#define ICP_NN_VARIANT_VALU 1
+#define ICP_NN_VARIANT_MFMA 2
+
 typedef struct icp_ctx icp_ctx;
 
 typedef struct icp_result {
@@ -60,6 +69,7 @@ typedef struct icp_stats {
     long long nn_launches; /* number of NN searches timed                               */
     long long nn_pairs;    /* sum over searches of np_local * nm                        */
     long long ambiguous;   /* queries the fp32 certificate sent to fp64 resolution      */
+    long long level1_queued; /* queries the MFMA certificate sent to the VALU filter     */
     double iter_ms;        /* host wall time inside icp_run                             */
     long long iterations;  /* iterations executed by icp_run                            */
 } icp_stats;
@@ -76,6 +86,14 @@ int icp_ctx_create(int device, int nn_mode, icp_ctx **out);
 int icp_ctx_create_dist(int device, int nn_mode, int rank, int world_size, const void *rccl_id,
                         icp_ctx **out);
 int icp_rccl_unique_id(void *out128);
+/* Same sharded engine, but the per-iteration sums are combined by a caller-supplied
+ * host all-reduce instead of RCCL: `fn(buf, count, user)` must replace buf[0..count) by
+ * its element-wise sum over all ranks (identically on every rank) and return 0.  Used to
+ * run several ranks on ONE device (RCCL refuses duplicate GPUs) and by embedders that
+ * own their communicator. */
+typedef int (*icp_allreduce_fn)(double *buf, size_t count, void *user);
+int icp_ctx_create_sharded(int device, int nn_mode, int rank, int world_size, icp_allreduce_fn fn,
+                           void *user, icp_ctx **out);
 void icp_ctx_destroy(icp_ctx *ctx);
 const char *icp_last_error(const icp_ctx *ctx);
 const char *icp_strerror(int code);
@@ -91,6 +109,8 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
 int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
 /* Reference behaviour is to refuse np != nm (gpu.cc:54-57); 1 lifts that check. */
 int icp_set_allow_unequal(icp_ctx *ctx, int allow);
+/* ICP_NN_VARIANT_* (default AUTO). */
+int icp_set_nn_variant(icp_ctx *ctx, int variant);
 
 /* ---- the ICP loop: GPU::ICP::find_corresponding_opti (src/GPU/gpu.cc:52-83) -- */
 /* Runs up to max_iter iterations on the resident clouds; stops after the iteration

@@ -40,11 +40,17 @@ struct icp_ctx {
     bool allow_unequal = false;
     hipStream_t st = nullptr;
     ncclComm_t comm = nullptr;
+    icp_allreduce_fn host_reduce = nullptr; // alternative to RCCL (icp_ctx_create_sharded)
+    void *host_reduce_user = nullptr;
 
     // model (replicated)
     DevCloud model;
-    float4 *m32 = nullptr; // centred fp32 model, padded to nm_pad with far points
-    size_t nm = 0, nm_pad = 0, m32_cap = 0;
+    float4 *m32 = nullptr;   // centred fp32 model, padded to nm_pad with far points
+    float4 *mperm = nullptr; // same, (mm, x, y, z) permuted for the MFMA operands
+    float *mm = nullptr;     // |m~|^2 rounded to fp32 (the MFMA's k = 0 operand)
+    size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0;
+    int nn_variant = ICP_NN_VARIANT_AUTO;
+    int level1_queued = 0; // queries the last MFMA pass could not certify
     double c[3] = {0, 0, 0}; // centring point = model centroid
     double rm = 0.0;         // max |centred fp32 model coordinate|
     bool has_model = false;
@@ -60,8 +66,10 @@ struct icp_ctx {
     // NN workspace
     int *idx = nullptr;
     size_t idx_cap = 0;
-    void *part = nullptr;
-    size_t part_cap = 0;
+    void *part = nullptr, *part2 = nullptr;
+    size_t part_cap = 0, part2_cap = 0;
+    int *amb1 = nullptr; // queue of the MFMA certificate
+    size_t amb1_cap = 0;
     int *amb_count = nullptr, *amb_list = nullptr;
     double *amb_T = nullptr;
     size_t amb_cap = 0;
@@ -201,6 +209,15 @@ int ensure_queue(icp_ctx *ctx, size_t n)
     return ICP_OK;
 }
 
+// The MFMA filter pays off once both clouds are large (its uncertified queries cost a
+// host round trip to size the second-level launch).
+bool use_mfma(const icp_ctx *ctx, size_t n)
+{
+    if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return true;
+    if (ctx->nn_variant == ICP_NN_VARIANT_VALU) return false;
+    return n >= 65536 && ctx->nm >= 65536;
+}
+
 // NN search of the n queries in q against the resident model -> ctx->idx[0..n).
 // Timed with HIP events on the context stream (ev[0]..ev[1] = the O(N*M) kernel).
 int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
@@ -220,6 +237,59 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
         LAUNCHCHK("nn_fp64");
+    } else if (use_mfma(ctx, n)) {
+        // level 1: MFMA expanded-form filter over every query
+        const NNPlan pl = plan_nn_mfma(n, ctx->nm_pad);
+        TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap,
+                 (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int))));
+        float *pb = (float *)ctx->part;
+        float *ps = pb + (size_t)pl.splits * n;
+        int *pi = (int *)(ps + (size_t)pl.splits * n);
+        TRY(ensure_queue(ctx, n));
+        TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
+        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 2, ctx->st));
+        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
+                                ctx->amb_count + 1, ctx->amb1, ctx->st);
+        LAUNCHCHK("nn_mfma");
+        HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        const int c1 = ctx->h_amb[1];
+        ctx->level1_queued = c1;
+        if (c1 > 0) {
+            // level 2: direct-form fp32 filter on the uncertified queries only
+            const NNPlan p2 = plan_nn32((size_t)c1, ctx->nm_pad);
+            NNPlan p2l = p2;
+            p2l.q_per_lane = 1;
+            const size_t per_block = kBlock;
+            p2l.qblocks = (int)(((size_t)c1 + per_block - 1) / per_block);
+            {
+                const int tiles = (int)(ctx->nm_pad / kTile32);
+                int splits = (2048 + p2l.qblocks - 1) / p2l.qblocks;
+                if (splits > tiles) splits = tiles;
+                if (splits < 1) splits = 1;
+                const int tps = (tiles + splits - 1) / splits;
+                p2l.chunk = tps * kTile32;
+                p2l.splits = (tiles + tps - 1) / tps;
+            }
+            TRY(grow(ctx, (char **)&ctx->part2, &ctx->part2_cap,
+                     (size_t)p2l.splits * c1 * (2 * sizeof(float) + sizeof(int))));
+            float *qb = (float *)ctx->part2;
+            float *qs = qb + (size_t)p2l.splits * c1;
+            int *qi = (int *)(qs + (size_t)p2l.splits * c1);
+            launch_nn_filter(q.f, ctx->amb1, c1, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi, ctx->st);
+            CertParams cp{ctx->rm};
+            launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->amb1, c1, cp, ctx->idx, ctx->amb_count,
+                               ctx->amb_list, ctx->amb_T, ctx->st);
+            // level 3: exact fp64 on the candidates of what is still open
+            launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, c1, ctx->idx,
+                              ctx->st);
+        }
+        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
+        LAUNCHCHK("nn_mfma levels 2-3");
     } else {
         const NNPlan pl = plan_nn32(n, ctx->nm_pad);
         const size_t need = (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int));
@@ -230,10 +300,10 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         TRY(ensure_queue(ctx, n));
         HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int), ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
-        launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        launch_nn_filter(q.f, nullptr, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
         CertParams cp{ctx->rm};
-        launch_nn_finalize(pb, ps, pi, pl.splits, q.f, (int)n, cp, ctx->idx, ctx->amb_count,
+        launch_nn_finalize(pb, ps, pi, pl.splits, q.f, nullptr, (int)n, cp, ctx->idx, ctx->amb_count,
                            ctx->amb_list, ctx->amb_T, ctx->st);
         launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx,
@@ -253,10 +323,23 @@ void account_nn(icp_ctx *ctx, size_t n)
     ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
 }
 
+// Sum `count` device doubles over the ranks: RCCL on the context stream, or the caller's
+// host all-reduce (device -> host, fn, host -> device).
 int allreduce(icp_ctx *ctx, double *buf, size_t count)
 {
-    if (ctx->world <= 1 || !ctx->comm) return ICP_OK;
-    RCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, ctx->st));
+    if (ctx->world <= 1) return ICP_OK;
+    if (ctx->comm) {
+        RCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, ctx->st));
+        return ICP_OK;
+    }
+    if (!ctx->host_reduce) return fail(ctx, ICP_E_ARG, "world_size > 1 without a communicator");
+    double tmp[32];
+    HIPCHK(hipMemcpyAsync(tmp, buf, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (ctx->host_reduce(tmp, count, ctx->host_reduce_user) != 0)
+        return fail(ctx, ICP_E_RCCL, "host all-reduce callback failed");
+    HIPCHK(hipMemcpyAsync(buf, tmp, sizeof(double) * count, hipMemcpyHostToDevice, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
 }
 
@@ -349,6 +432,29 @@ int icp_ctx_create_dist(int device, int nn_mode, int rank, int world_size, const
     return ICP_OK;
 }
 
+int icp_ctx_create_sharded(int device, int nn_mode, int rank, int world_size, icp_allreduce_fn fn,
+                           void *user, icp_ctx **out)
+{
+    if (!out || world_size < 1 || rank < 0 || rank >= world_size || (world_size > 1 && !fn) ||
+        (nn_mode != ICP_NN_CERTIFIED && nn_mode != ICP_NN_FP64))
+        return ICP_E_ARG;
+    *out = nullptr;
+    icp_ctx *ctx = new icp_ctx();
+    ctx->device = device;
+    ctx->nn_mode = nn_mode;
+    ctx->rank = rank;
+    ctx->world = world_size;
+    ctx->host_reduce = fn;
+    ctx->host_reduce_user = user;
+    int rc = ctx_init(ctx);
+    if (rc != ICP_OK) {
+        icp_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return ICP_OK;
+}
+
 void icp_ctx_destroy(icp_ctx *ctx)
 {
     if (!ctx) return;
@@ -360,7 +466,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
     free_cloud(ctx->Y);
     free_cloud(ctx->qa);
     free_cloud(ctx->qb);
-    for (void *p : {(void *)ctx->m32, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
+    for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, ctx->part2,
+                    (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
                     (void *)ctx->sums, (void *)ctx->stage})
         if (p) (void)hipFree(p);
@@ -373,6 +480,13 @@ void icp_ctx_destroy(icp_ctx *ctx)
 }
 
 const char *icp_last_error(const icp_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int icp_set_nn_variant(icp_ctx *ctx, int variant)
+{
+    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_MFMA) return ICP_E_ARG;
+    ctx->nn_variant = variant;
+    return ICP_OK;
+}
 
 int icp_set_allow_unequal(icp_ctx *ctx, int allow)
 {
@@ -412,6 +526,22 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     ctx->rm = rm;
     TRY(grow(ctx, &ctx->m32, &ctx->m32_cap, nm_pad));
     HIPCHK(hipMemcpyAsync(ctx->m32, h.data(), sizeof(float4) * nm_pad, hipMemcpyHostToDevice, ctx->st));
+    // MFMA operand image: point P = 64g + 16t + i, component k (mm, x, y, z) at float
+    // g*256 + k*64 + 4i + t  (lane l = 16k + i reads its 4 operands as one float4)
+    std::vector<float> hp(4 * nm_pad), hmm(nm_pad);
+    for (size_t P = 0; P < nm_pad; ++P) {
+        const float4 v = h[P];
+        const bool real = P < nm;
+        const float mmv = real ? (float)((double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z) : 1.0e30f;
+        const float comp[4] = {mmv, real ? v.x : 0.f, real ? v.y : 0.f, real ? v.z : 0.f};
+        const size_t g = P >> 6, t = (P >> 4) & 3, i = P & 15;
+        for (int k = 0; k < 4; ++k) hp[g * 256 + k * 64 + i * 4 + t] = comp[k];
+        hmm[P] = mmv;
+    }
+    TRY(grow(ctx, &ctx->mperm, &ctx->mperm_cap, nm_pad));
+    TRY(grow(ctx, &ctx->mm, &ctx->mm_cap, nm_pad));
+    HIPCHK(hipMemcpyAsync(ctx->mperm, hp.data(), sizeof(float) * 4 * nm_pad, hipMemcpyHostToDevice, ctx->st));
+    HIPCHK(hipMemcpyAsync(ctx->mm, hmm.data(), sizeof(float) * nm_pad, hipMemcpyHostToDevice, ctx->st));
     TRY(upload_cloud(ctx, ctx->model, m_xyz, nm, false));
     HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->nm = nm;
@@ -488,7 +618,10 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
         account_nn(ctx, n);
-        if (ctx->nn_mode == ICP_NN_CERTIFIED) amb += ctx->h_amb[0];
+        if (ctx->nn_mode == ICP_NN_CERTIFIED) {
+            amb += ctx->h_amb[0];
+            ctx->stats.level1_queued += use_mfma(ctx, n) ? ctx->level1_queued : 0;
+        }
 
         // 4. host Horn solve (gpu.cc:106-146)
         const double *h = ctx->h_sums;

@@ -32,14 +32,24 @@ struct NNPlan {
 NNPlan plan_nn32(size_t np, size_t nm_pad);
 NNPlan plan_nn64(size_t np, size_t nm_pad);
 
-// fp32 filter: partial (best, second, argbest) per (split, query).
-void launch_nn_filter(const float4 *p32, int np, const float4 *m32, int nm_pad,
+// fp32 direct-form filter: partial (best, second, argbest) per (split, slot); slot s is
+// query s, or query list[s] when list != nullptr.
+void launch_nn_filter(const float4 *p32, const int *list, int nslots, const float4 *m32, int nm_pad,
                       const NNPlan &plan, float *part_best, float *part_second, int *part_idx,
                       hipStream_t st);
-// merge splits, certify, write idx for certified queries, queue the rest.
+// merge splits, certify, write idx for certified queries, queue the rest (with window T).
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
-                        int splits, const float4 *p32, int np, CertParams cp, int *idx,
-                        int *amb_count, int *amb_list, double *amb_T, hipStream_t st);
+                        int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
+                        int *idx, int *amb_count, int *amb_list, double *amb_T, hipStream_t st);
+// MFMA expanded-form filter (G = |m|^2 - 2 p.m) and its certificate; uncertified queries
+// are appended to amb_list (no window: they go through the direct-form filter next).
+constexpr int kMfmaQG = 4; // 16-query groups per wave
+NNPlan plan_nn_mfma(size_t np, size_t nm_pad);
+void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, const NNPlan &plan,
+                    float *part_best, float *part_second, int *part_idx, hipStream_t st);
+void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
+                             int splits, const float4 *p32, int np, const float *mm, int *idx,
+                             int *amb_count, int *amb_list, hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,

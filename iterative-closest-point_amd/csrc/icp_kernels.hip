@@ -65,6 +65,15 @@ __device__ double cert_window(float b32, float4 p, double rm)
     return (bp + f(X)) * (1.0 + 1e-12);
 }
 
+// v_min_f32 without the canonicalising v_max hipcc puts in front of fminf on MFMA
+// results (one per operand; the values here are never NaN / denormal-sensitive)
+__device__ __forceinline__ float min_nocanon(float a, float b)
+{
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
 // out[k].  Fixed shuffle tree + fixed LDS order: deterministic.
 template <int K>
@@ -125,27 +134,31 @@ __global__ __launch_bounds__(kBlock) void make_f32_kernel(const double *__restri
 }
 
 // ---- NN: fp32 filter ----------------------------------------------------------------
-// grid = (qblocks, splits).  Lane owns Q queries (j = blockIdx.x*256*Q + q*256 + tid);
-// the workgroup streams its model chunk through a 1024-point LDS tile; every lane reads
-// the same model point (LDS broadcast, one ds_read_b128 feeds 64*Q pairs).
-template <int Q>
+// grid = (qblocks, splits).  Lane owns Q query slots (s = blockIdx.x*256*Q + q*256 + tid);
+// slot s is query s, or query list[s] when LIST (second-level filter of the queries the
+// MFMA certificate could not settle).  The workgroup streams its model chunk through a
+// 1024-point LDS tile; every lane reads the same model point (LDS broadcast: one
+// ds_read_b96 feeds 64*Q pairs).  Per pair: 3 v_sub + v_mul + 2 v_fma + v_min + v_med3.
+template <int Q, bool LIST>
 __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
-    const float4 *__restrict__ p32, int np, const float4 *__restrict__ m32, int nm_pad, int chunk,
-    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx)
+    const float4 *__restrict__ p32, const int *__restrict__ list, int nslots,
+    const float4 *__restrict__ m32, int nm_pad, int chunk, float *__restrict__ part_best,
+    float *__restrict__ part_second, int *__restrict__ part_idx)
 {
     __shared__ float4 tile[kTile32];
     const int tid = threadIdx.x;
     const int split = blockIdx.y;
     const int m0 = split * chunk;
     const int m1 = min(m0 + chunk, nm_pad);
-    const int qbase = blockIdx.x * (kBlock * Q) + tid;
+    const int sbase = blockIdx.x * (kBlock * Q) + tid;
 
     float px[Q], py[Q], pz[Q], best[Q], second[Q];
     int bsub[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const int j = qbase + q * kBlock;
-        const float4 v = j < np ? p32[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int s = sbase + q * kBlock;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s < nslots) v = p32[LIST ? list[s] : s];
         px[q] = v.x;
         py[q] = v.y;
         pz[q] = v.z;
@@ -187,9 +200,9 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
             const float d = d32(px[q], py[q], pz[q], m32[bsub[q] + k]);
             found = (d == best[q]) ? bsub[q] + k : found;
         }
-        const int j = qbase + q * kBlock;
-        if (j < np) {
-            const size_t o = (size_t)split * np + j;
+        const int s = sbase + q * kBlock;
+        if (s < nslots) {
+            const size_t o = (size_t)split * nslots + s;
             part_best[o] = best[q];
             part_second[o] = second[q];
             part_idx[o] = found;
@@ -197,19 +210,19 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
     }
 }
 
-__global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
-    const float *__restrict__ part_best, const float *__restrict__ part_second,
-    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
-    double rm, int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T)
+// merge the per-split partial (best, second, idx) of slot s; earlier split keeps ties
+__device__ __forceinline__ void merge_splits(const float *__restrict__ part_best,
+                                             const float *__restrict__ part_second,
+                                             const int *__restrict__ part_idx, int splits,
+                                             int nslots, int s, float &b, float &s2, int &id)
 {
-    const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= np) return;
-    float b = part_best[j], s2 = part_second[j];
-    int id = part_idx[j];
+    b = part_best[s];
+    s2 = part_second[s];
+    id = part_idx[s];
     for (int sp = 1; sp < splits; ++sp) {
-        const size_t o = (size_t)sp * np + j;
+        const size_t o = (size_t)sp * nslots + s;
         const float b2 = part_best[o], s22 = part_second[o];
-        if (b2 < b) { // strict: the earlier split keeps ties (lower indices)
+        if (b2 < b) {
             s2 = fminf(b, s22);
             b = b2;
             id = part_idx[o];
@@ -217,6 +230,21 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
             s2 = fminf(s2, b2);
         }
     }
+}
+
+template <bool LIST>
+__global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
+    const float *__restrict__ part_best, const float *__restrict__ part_second,
+    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32,
+    const int *__restrict__ list, int nslots, double rm, int *__restrict__ idx, int *amb_count,
+    int *amb_list, double *amb_T)
+{
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= nslots) return;
+    const int j = LIST ? list[s] : s;
+    float b, s2;
+    int id;
+    merge_splits(part_best, part_second, part_idx, splits, nslots, s, b, s2, id);
     const double T = cert_window(b, p32[j], rm);
     if ((double)s2 > T) {
         idx[j] = id; // unique candidate => exact fp64 first-min
@@ -224,6 +252,155 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
         const int slot = atomicAdd(amb_count, 1);
         amb_list[slot] = j;
         amb_T[slot] = T;
+    }
+}
+
+// ---- NN: MFMA filter ---------------------------------------------------------------
+// G(p, m) = |m~|^2 - 2 p~.m~ (= D - |p~|^2: same argmin) for 16 model points x 16 queries
+// per v_mfma_f32_16x16x4_f32:  A[i][k] = (mm, x, y, z) of model point i,
+// B[k][j] = (1, -2px, -2py, -2pz) of query j;  D[i][j] = fma chain k = 0..3 from C = 0.
+// Lane l: query column j = l & 15 of each of its QG query groups, model rows
+// 4(l >> 4) + r (r = 0..3) of each MFMA; the 4 lane groups are merged at the end.
+// The model is pre-permuted (icp_set_model) so that lane l's A operands for the 4 MFMAs
+// of a 64-point group are one contiguous float4: mperm[g*256 + 4*l + t] =
+// component (l >> 4) of point 64g + 16t + (l & 15)  ->  one conflict-free ds_read_b128
+// per 4*QG MFMAs.  Numerics and the certificate: nn_finalize_mfma_kernel.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+template <int QG>
+__global__ __launch_bounds__(kBlock) void nn_mfma_kernel(
+    const float4 *__restrict__ p32, int np, const float4 *__restrict__ mperm4, int nm_pad,
+    int chunk, float *__restrict__ part_best, float *__restrict__ part_second,
+    int *__restrict__ part_idx)
+{
+    __shared__ float4 tile[kTile32];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 4, col = lane & 15;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm_pad);
+    const int qbase = blockIdx.x * (4 * QG * 16) + wave * (QG * 16) + col;
+
+    float bq[QG], best[QG], second[QG];
+    int bgrp[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int j = qbase + q * 16;
+        const float4 v = j < np ? p32[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        bq[q] = h == 0 ? 1.0f : -2.0f * (h == 1 ? v.x : (h == 2 ? v.y : v.z));
+        best[q] = INFINITY;
+        second[q] = INFINITY;
+        bgrp[q] = m0 >> 6;
+    }
+    const f32x4_t zero = {0.f, 0.f, 0.f, 0.f};
+
+    for (int t0 = m0; t0 < m1; t0 += kTile32) {
+        __syncthreads();
+#pragma unroll
+        for (int k = tid; k < kTile32; k += kBlock) tile[k] = mperm4[t0 + k];
+        __syncthreads();
+        for (int g = 0; g < kTile32 / 64; ++g) {
+            const float4 a4 = tile[g * 64 + lane];
+            float prev[QG];
+#pragma unroll
+            for (int q = 0; q < QG; ++q) prev[q] = best[q];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float a = t == 0 ? a4.x : (t == 1 ? a4.y : (t == 2 ? a4.z : a4.w));
+#pragma unroll
+                for (int q = 0; q < QG; ++q) {
+                    const f32x4_t d = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq[q], zero, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d[r]);
+                        best[q] = min_nocanon(best[q], d[r]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < QG; ++q) bgrp[q] = best[q] < prev[q] ? ((t0 >> 6) + g) : bgrp[q];
+        }
+    }
+
+    const float *mperm = (const float *)mperm4;
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int j = qbase + q * 16;
+        const float4 v = j < np ? p32[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float bx = -2.0f * v.x, by = -2.0f * v.y, bz = -2.0f * v.z;
+        // rescan this lane's 16 points of the best group with the MFMA's own fma chain
+        // (k = 0..3 from 0); lowest index with G == best, -1 if none (=> not certified)
+        int id = -1;
+        const int base = bgrp[q] * 256;
+#pragma unroll
+        for (int t = 3; t >= 0; --t)
+#pragma unroll
+            for (int r = 3; r >= 0; --r) {
+                const int i = 4 * h + r;
+                const float mm = mperm[base + 0 * 64 + i * 4 + t];
+                const float mx = mperm[base + 1 * 64 + i * 4 + t];
+                const float my = mperm[base + 2 * 64 + i * 4 + t];
+                const float mz = mperm[base + 3 * 64 + i * 4 + t];
+                const float gv = __builtin_fmaf(mz, bz, __builtin_fmaf(my, by, __builtin_fmaf(mx, bx, __builtin_fmaf(mm, 1.0f, 0.0f))));
+                id = (gv == best[q]) ? bgrp[q] * 64 + 16 * t + i : id;
+            }
+        float b = best[q], s2 = second[q];
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {
+            const float ob = __shfl_xor(b, off, 64), os = __shfl_xor(s2, off, 64);
+            const int oi = __shfl_xor(id, off, 64);
+            if (ob < b) {
+                s2 = fminf(b, os);
+                b = ob;
+                id = oi;
+            } else {
+                s2 = fminf(s2, ob);
+            }
+        }
+        if (h == 0 && j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = b;
+            part_second[o] = s2;
+            part_idx[o] = id;
+        }
+    }
+}
+
+// Certificate of the MFMA filter.  With u = 2^-24, a~ / b~ the centred fp32 query / model
+// point and A = |a~|: |G^(m) - G(m)| <= delta(|b~|), delta(R) = 8u (R^2 + 2AR) (operand
+// rounding 2u(R^2 + 2AR) + mm rounding and three fma roundings 4u(R^2 + 2AR)).  For the
+// best point m_b (G^ = b): D(m_b) <= Db = b + delta_b + |a|^2.  Every fp64 minimiser m*
+// has |b*| <= |a| + sqrt(D(m*)) <= Rc := A(1+2u) + sqrt(Db (1 + 2^-40)), hence
+// G^(m*) <= T := b + delta_b + delta(Rc) + 2^-48 Db.  second > T  =>  m_b is the answer.
+__global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
+    const float *__restrict__ part_best, const float *__restrict__ part_second,
+    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
+    const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    float b, s2;
+    int id;
+    merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    bool ok = id >= 0;
+    if (ok) {
+        const double u = 0x1.0p-24;
+        const float4 p = p32[j];
+        const double a2 = (double)p.x * p.x + (double)p.y * p.y + (double)p.z * p.z;
+        const double A = sqrt(a2);
+        auto delta = [&](double R) { return 8.0 * u * (R * R + 2.0 * A * R) * (1.0 + 1e-6); };
+        const double db = delta(sqrt((double)mm[id]) * (1.0 + u));
+        const double Db = fmax((double)b + db + a2 * (1.0 + 4.0 * u), 0.0);
+        const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
+        double T = (double)b + db + delta(Rc) + 0x1.0p-48 * Db;
+        T += fabs(T) * 1e-12 + 1e-300;
+        ok = (double)s2 > T;
+    }
+    if (ok) {
+        idx[j] = id;
+    } else {
+        const int slot = atomicAdd(amb_count, 1);
+        amb_list[slot] = j;
     }
 }
 
@@ -562,24 +739,69 @@ static NNPlan make_plan(size_t np, size_t nm, int tile, int q_small, int q_large
 NNPlan plan_nn32(size_t np, size_t nm_pad) { return make_plan(np, nm_pad, kTile32, 1, 4, 262144); }
 NNPlan plan_nn64(size_t np, size_t nm) { return make_plan(np, nm, kTile64, 1, 2, 262144); }
 
-void launch_nn_filter(const float4 *p32, int np, const float4 *m32, int nm_pad, const NNPlan &pl,
-                      float *part_best, float *part_second, int *part_idx, hipStream_t st)
+void launch_nn_filter(const float4 *p32, const int *list, int nslots, const float4 *m32, int nm_pad,
+                      const NNPlan &pl, float *part_best, float *part_second, int *part_idx,
+                      hipStream_t st)
 {
     dim3 grid(pl.qblocks, pl.splits);
-    if (pl.q_per_lane == 4)
-        nn_filter_kernel<4><<<grid, kBlock, 0, st>>>(p32, np, m32, nm_pad, pl.chunk, part_best,
-                                                     part_second, part_idx);
-    else
-        nn_filter_kernel<1><<<grid, kBlock, 0, st>>>(p32, np, m32, nm_pad, pl.chunk, part_best,
-                                                     part_second, part_idx);
+    if (list) {
+        nn_filter_kernel<1, true><<<grid, kBlock, 0, st>>>(p32, list, nslots, m32, nm_pad, pl.chunk,
+                                                           part_best, part_second, part_idx);
+    } else if (pl.q_per_lane == 4) {
+        nn_filter_kernel<4, false><<<grid, kBlock, 0, st>>>(p32, nullptr, nslots, m32, nm_pad,
+                                                            pl.chunk, part_best, part_second, part_idx);
+    } else {
+        nn_filter_kernel<1, false><<<grid, kBlock, 0, st>>>(p32, nullptr, nslots, m32, nm_pad,
+                                                            pl.chunk, part_best, part_second, part_idx);
+    }
 }
 
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
-                        int splits, const float4 *p32, int np, CertParams cp, int *idx,
-                        int *amb_count, int *amb_list, double *amb_T, hipStream_t st)
+                        int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
+                        int *idx, int *amb_count, int *amb_list, double *amb_T, hipStream_t st)
 {
-    nn_finalize_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-        part_best, part_second, part_idx, splits, p32, np, cp.rm, idx, amb_count, amb_list, amb_T);
+    const int grid = (nslots + kBlock - 1) / kBlock;
+    if (list)
+        nn_finalize_kernel<true><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32,
+                                                          list, nslots, cp.rm, idx, amb_count,
+                                                          amb_list, amb_T);
+    else
+        nn_finalize_kernel<false><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits,
+                                                           p32, nullptr, nslots, cp.rm, idx,
+                                                           amb_count, amb_list, amb_T);
+}
+
+NNPlan plan_nn_mfma(size_t np, size_t nm_pad)
+{
+    NNPlan pl;
+    pl.q_per_lane = kMfmaQG;
+    const size_t per_block = (size_t)4 * kMfmaQG * 16;
+    pl.qblocks = (int)((np + per_block - 1) / per_block);
+    if (pl.qblocks < 1) pl.qblocks = 1;
+    const int tiles = (int)((nm_pad + kTile32 - 1) / kTile32);
+    int splits = (2048 + pl.qblocks - 1) / pl.qblocks;
+    if (splits > tiles) splits = tiles;
+    if (splits < 1) splits = 1;
+    const int tps = (tiles + splits - 1) / splits;
+    pl.chunk = tps * kTile32;
+    pl.splits = (tiles + tps - 1) / tps;
+    return pl;
+}
+
+void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, const NNPlan &pl,
+                    float *part_best, float *part_second, int *part_idx, hipStream_t st)
+{
+    dim3 grid(pl.qblocks, pl.splits);
+    nn_mfma_kernel<kMfmaQG><<<grid, kBlock, 0, st>>>(p32, np, mperm, nm_pad, pl.chunk, part_best,
+                                                     part_second, part_idx);
+}
+
+void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
+                             int splits, const float4 *p32, int np, const float *mm, int *idx,
+                             int *amb_count, int *amb_list, hipStream_t st)
+{
+    nn_finalize_mfma_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
+        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list);
 }
 
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,

@@ -41,12 +41,16 @@ ICP_E_RANGE = -9
 
 NN_CERTIFIED = 0
 NN_FP64 = 1
+VARIANT_AUTO = 0
+VARIANT_VALU = 1
+VARIANT_MFMA = 2
 
 # every function include/icp_capi.h declares (checked by tests/test_capi.py)
 EXPORTED = [
-    "icp_ctx_create", "icp_ctx_create_dist", "icp_rccl_unique_id", "icp_ctx_destroy",
+    "icp_ctx_create", "icp_ctx_create_dist", "icp_rccl_unique_id", "icp_ctx_create_sharded",
+    "icp_ctx_destroy",
     "icp_last_error", "icp_strerror", "icp_device_count", "icp_set_model", "icp_set_scene",
-    "icp_get_scene", "icp_set_allow_unequal", "icp_run", "icp_closest_matrix",
+    "icp_get_scene", "icp_set_allow_unequal", "icp_set_nn_variant", "icp_run", "icp_closest_matrix",
     "icp_compute_centroid", "icp_y_p_norm", "icp_err_compute", "icp_find_alignment",
     "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
     "icp_load_matrix", "icp_write_matrix", "icp_free", "icp_get_stats", "icp_reset_stats",
@@ -66,8 +70,10 @@ class Result(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("nn_ms", C.c_double), ("nn_launches", C.c_longlong), ("nn_pairs", C.c_longlong),
-                ("ambiguous", C.c_longlong), ("iter_ms", C.c_double), ("iterations", C.c_longlong)]
+                ("ambiguous", C.c_longlong), ("level1_queued", C.c_longlong), ("iter_ms", C.c_double), ("iterations", C.c_longlong)]
 
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
 
 _lib = None
 
@@ -86,6 +92,7 @@ def lib() -> C.CDLL:
     L.icp_ctx_create.argtypes = [C.c_int, C.c_int, C.POINTER(vp)]
     L.icp_ctx_create_dist.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]
     L.icp_rccl_unique_id.argtypes = [C.c_char_p]
+    L.icp_ctx_create_sharded.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, ALLREDUCE_FN, vp, C.POINTER(vp)]
     L.icp_ctx_destroy.argtypes = [vp]
     L.icp_ctx_destroy.restype = None
     L.icp_last_error.argtypes = [vp]
@@ -97,6 +104,7 @@ def lib() -> C.CDLL:
     L.icp_set_scene.argtypes = [vp, dp, sz, sz]
     L.icp_get_scene.argtypes = [vp, dp]
     L.icp_set_allow_unequal.argtypes = [vp, C.c_int]
+    L.icp_set_nn_variant.argtypes = [vp, C.c_int]
     L.icp_run.argtypes = [vp, C.c_int, C.c_double, dp, C.POINTER(Result)]
     L.icp_closest_matrix.argtypes = [vp, dp, sz, dp, C.POINTER(C.c_int32)]
     L.icp_compute_centroid.argtypes = [vp, dp, sz, dp, dp]
@@ -220,10 +228,21 @@ class Context:
     """One HIP device context (optionally one rank of an RCCL job)."""
 
     def __init__(self, device: int = 0, nn_mode: int = NN_CERTIFIED, rank: int = 0,
-                 world_size: int = 1, rccl_id: bytes | None = None):
+                 world_size: int = 1, rccl_id: bytes | None = None, host_allreduce=None):
+        """host_allreduce(np.ndarray) -> None: in-place sum over ranks (instead of RCCL)."""
         L = lib()
         h = C.c_void_p()
-        if world_size > 1:
+        self._cb = None
+        if host_allreduce is not None:
+            def _cb(buf, count, _user):
+                try:
+                    host_allreduce(np.ctypeslib.as_array(buf, shape=(count,)))
+                    return 0
+                except Exception:  # a failed rendezvous must not unwind through C
+                    return 1
+            self._cb = ALLREDUCE_FN(_cb)
+            rc = L.icp_ctx_create_sharded(device, nn_mode, rank, world_size, self._cb, None, C.byref(h))
+        elif world_size > 1:
             rc = L.icp_ctx_create_dist(device, nn_mode, rank, world_size, rccl_id, C.byref(h))
         else:
             rc = L.icp_ctx_create(device, nn_mode, C.byref(h))
@@ -267,6 +286,9 @@ class Context:
         out = np.empty((self._np_local, 3))
         self._check(lib().icp_get_scene(self._h, _dp(out)))
         return out
+
+    def set_nn_variant(self, variant: int):
+        self._check(lib().icp_set_nn_variant(self._h, variant))
 
     def set_allow_unequal(self, allow: bool):
         self._check(lib().icp_set_allow_unequal(self._h, 1 if allow else 0))

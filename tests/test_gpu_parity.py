@@ -19,7 +19,10 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
 RNG = np.random.default_rng(99)
-MODES = [0, 1]  # ICP_NN_CERTIFIED, ICP_NN_FP64
+# (nn_mode, filter variant): certified with the VALU filter, certified with the MFMA filter
+# (+ VALU second level + fp64), fp64 brute force
+MODES = ["valu", "mfma", "fp64"]
+_MODE_ARGS = {"valu": (0, 1), "mfma": (0, 2), "fp64": (1, 0)}
 
 
 @pytest.fixture(scope="module")
@@ -31,7 +34,10 @@ def amd(icp_lib):
 
 @pytest.fixture(scope="module")
 def ctxs(amd):
-    c = {m: amd.Context(0, m) for m in MODES}
+    c = {}
+    for m in MODES:
+        c[m] = amd.Context(0, _MODE_ARGS[m][0])
+        c[m].set_nn_variant(_MODE_ARGS[m][1])
     yield c
     for v in c.values():
         v.close()
@@ -101,8 +107,10 @@ def test_nn_exact_ties_and_duplicates(amd, ctxs, oracle, mode):
     np.testing.assert_array_equal(idx, ref)
 
 
-def test_nn_certificate_sends_ties_to_resolution(amd):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_nn_certificate_sends_ties_to_resolution(amd, variant):
     with amd.Context(0, 0) as ctx:
+        ctx.set_nn_variant(variant)
         m = np.array([[1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0], [5, 5, 5.0]])
         ctx.set_model(m)
         ctx.reset_stats()
@@ -126,17 +134,36 @@ def test_nn_certified_equals_fp64_at_1m(amd, ctxs, oracle):
     out = {}
     for mode in MODES:
         ctxs[mode].set_model(m)
+        ctxs[mode].reset_stats()
         _, out[mode] = ctxs[mode].closest_matrix(p)
-    np.testing.assert_array_equal(out[0], out[1])
+    np.testing.assert_array_equal(out["valu"], out["fp64"])
+    np.testing.assert_array_equal(out["mfma"], out["fp64"])
     sel = RNG.choice(p.shape[0], size=96, replace=False)
     _, ref = oracle.closest(p[sel], m)
-    np.testing.assert_array_equal(out[0][sel], ref)
+    np.testing.assert_array_equal(out["fp64"][sel], ref)
+
+
+def test_mfma_rescan_matches_mfma_bits(amd):
+    # the MFMA filter recovers its argmin by recomputing G with a VALU fma chain; if the
+    # MFMA's rounding ever differed, those queries would all fall back to level 2.  On
+    # random data essentially every query must be certified at level 1 or 2.
+    m, p = amd.synthetic_pair(1 << 17, seed=3)
+    with amd.Context(0, 0) as ctx:
+        ctx.set_nn_variant(amd.VARIANT_MFMA)
+        ctx.set_model(m)
+        ctx.set_scene(p, np_total=p.shape[0])
+        ctx.set_allow_unequal(True)
+        ctx.run(1, -1.0)
+        st = ctx.stats()
+    assert st["level1_queued"] < 0.1 * p.shape[0], st
+    assert st["ambiguous"] < 0.01 * p.shape[0], st
 
 
 # ---- full ICP loop vs oracle trajectories ----------------------------------------------
 
 def run_engine(amd, mode, m, p, max_iter, threshold, allow_unequal=False):
-    with amd.Context(0, mode) as ctx:
+    with amd.Context(0, _MODE_ARGS[mode][0]) as ctx:
+        ctx.set_nn_variant(_MODE_ARGS[mode][1])
         ctx.set_allow_unequal(allow_unequal)
         ctx.set_model(m)
         ctx.set_scene(p)
@@ -163,7 +190,7 @@ def test_icp_trajectory_matches_oracle(amd, golden_traces, mode, cfg):
 def test_icp_synthetic_fixed_iterations(amd, golden_traces):
     g = golden_traces["synthetic4096"]
     z = np.load(os.path.join(GOLD, "synthetic4096.npz"))
-    res, errs, new_p = run_engine(amd, 0, z["model"], z["scene"], 30, -1.0)
+    res, errs, new_p = run_engine(amd, "mfma", z["model"], z["scene"], 30, -1.0)
     assert res.iterations == 30 and not res.converged
     np.testing.assert_allclose(errs, g["err"], rtol=1e-9)
     np.testing.assert_allclose(new_p, z["new_p"], atol=1e-9)
@@ -171,10 +198,11 @@ def test_icp_synthetic_fixed_iterations(amd, golden_traces):
 
 def test_modes_bitwise_identical(amd):
     m, p = load(amd, "horse_ref"), load(amd, "horse_tr1")
-    a = run_engine(amd, 0, m, p, 6, -1.0)
-    b = run_engine(amd, 1, m, p, 6, -1.0)
-    np.testing.assert_array_equal(a[1], b[1])
-    np.testing.assert_array_equal(a[2], b[2])
+    a = run_engine(amd, "valu", m, p, 6, -1.0)
+    for mode in ("mfma", "fp64"):
+        b = run_engine(amd, mode, m, p, 6, -1.0)
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[2], b[2])
 
 
 def test_reference_fatal_checks(amd):
@@ -196,7 +224,7 @@ def test_reference_fatal_checks(amd):
 
 def test_zero_iterations_leaves_scene(amd):
     m = RNG.normal(size=(100, 3))
-    res, errs, new_p = run_engine(amd, 0, m, m + 0.1, 0, 1e-5)
+    res, errs, new_p = run_engine(amd, "valu", m, m + 0.1, 0, 1e-5)
     assert res.iterations == 0 and errs.size == 0
     np.testing.assert_array_equal(new_p, m + 0.1)
 

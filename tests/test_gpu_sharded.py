@@ -1,0 +1,98 @@
+"""Sharded (multi-rank) engine path on ONE GPU: W virtual ranks = W threads, each with its
+own context/stream on device 0 and a scene shard; the per-iteration sums are combined by a
+host all-reduce (icp_ctx_create_sharded) instead of RCCL, which refuses duplicate GPUs.
+Everything but the ncclAllReduce call itself is the code the 8-GPU run executes."""
+import threading
+
+import numpy as np
+import pytest
+
+import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+class HostAllReduce:
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world, timeout=120)
+        self.bufs = [None] * world
+
+    def for_rank(self, r):
+        def reduce(buf):
+            self.bufs[r] = buf.copy()
+            self.bar.wait()
+            acc = self.bufs[0].copy()
+            for k in range(1, self.world):  # fixed rank order: identical on every rank
+                acc += self.bufs[k]
+            self.bar.wait()
+            buf[:] = acc
+        return reduce
+
+
+def run_sharded(amd, m, p, world, iters, threshold, mode=0):
+    red = HostAllReduce(world)
+    results = [None] * world
+    errors = []
+
+    def worker(r):
+        try:
+            b, c = amd.shard_range(p.shape[0], r, world)
+            with amd.Context(0, mode, rank=r, world_size=world, host_allreduce=red.for_rank(r)) as ctx:
+                ctx.set_model(m)
+                ctx.set_scene(p[b:b + c], np_total=p.shape[0])
+                res, errs = ctx.run(iters, threshold)
+                results[r] = (res, errs, ctx.get_scene())
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+            red.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errors, errors
+    return results
+
+
+def run_single(amd, m, p, iters, threshold, mode=0):
+    with amd.Context(0, mode) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        res, errs = ctx.run(iters, threshold)
+        return res, errs, ctx.get_scene()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_matches_single_horse(icp_lib, world):
+    amd = icp_lib
+    m = amd.load_matrix(datasets.path("horse_ref"))
+    p = amd.load_matrix(datasets.path("horse_tr2"))
+    ref = run_single(amd, m, p, 20, 1e-5)
+    out = run_sharded(amd, m, p, world, 20, 1e-5)
+    for res, errs, _ in out:  # identical decisions and solves on every rank
+        assert res.iterations == ref[0].iterations
+        np.testing.assert_array_equal(errs, out[0][1])
+        np.testing.assert_array_equal(np.array(res.R), np.array(out[0][0].R))
+    np.testing.assert_allclose(out[0][1], ref[1], rtol=1e-11)
+    np.testing.assert_allclose(np.concatenate([o[2] for o in out]), ref[2], atol=1e-12)
+
+
+def test_sharded_synthetic_fixed_iterations(icp_lib):
+    amd = icp_lib
+    m, p = amd.synthetic_pair(1 << 16, seed=42)
+    ref = run_single(amd, m, p, 5, -1.0)
+    out = run_sharded(amd, m, p, 4, 5, -1.0)
+    np.testing.assert_allclose(out[0][1], ref[1], rtol=1e-11)
+    np.testing.assert_allclose(np.concatenate([o[2] for o in out]), ref[2], atol=1e-12)
+
+
+def test_uneven_shards_including_empty(icp_lib):
+    amd = icp_lib
+    m = amd.load_matrix(datasets.path("cow_ref"))
+    p = amd.load_matrix(datasets.path("cow_tr1"))
+    # 2903 points over 5 ranks: 581/581/581/580/580
+    out = run_sharded(amd, m, p, 5, 20, 1e-5)
+    assert out[0][0].iterations == 7
+    np.testing.assert_allclose(np.concatenate([o[2] for o in out]), m, atol=1e-5)

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""NN-only probe for profiling: repeated icp_closest_matrix on the C4 synthetic pair.
+
+    python tools/nn_probe.py --variant mfma|valu|fp64 [--n 1048576] [--reps 3]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "iterative-closest-point_amd"))
+import icp_amd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", default="mfma", choices=["valu", "mfma", "fp64"])
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    mode = icp_amd.NN_FP64 if a.variant == "fp64" else icp_amd.NN_CERTIFIED
+    with icp_amd.Context(0, mode) as ctx:
+        ctx.set_nn_variant({"valu": 1, "mfma": 2, "fp64": 0}[a.variant])
+        m, p = icp_amd.synthetic_pair(a.n, seed=42)
+        ctx.set_model(m)
+        ctx.closest_matrix(p)
+        ctx.reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            ctx.closest_matrix(p)
+        dt = (time.perf_counter() - t0) / a.reps
+        st = ctx.stats()
+    ms = st["nn_ms"] / max(st["nn_launches"], 1)
+    print(f"{a.variant}: wall {dt * 1e3:.2f} ms/search, filter kernel {ms:.2f} ms, "
+          f"{8.0 * a.n * a.n / (ms * 1e-3) / 1e12:.1f} TF(8 flop/pair)")
+
+
+if __name__ == "__main__":
+    main()
