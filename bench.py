@@ -34,7 +34,9 @@ import numpy as np  # noqa: E402
 import icp_amd  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32 MFMA peak
-FLOP_PER_PAIR = 8
+PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
+FLOP_PER_PAIR = 8          # SURVEY.md §8d (algorithmic: 3 sub + 1 mul + 2 fma)
+MFMA16_FLOP_PER_PAIR = 32  # executed: v_mfma_f32_32x32x16_f16 = 2*32*32*16 flop per 1024 pairs
 REF_OPTI_GPU_LOOP_FPS = 9.36368  # reference README.md:108 (GTX 1050, cow_ref/cow_tr1)
 
 
@@ -90,7 +92,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--nn", choices=["certified", "fp64"], default="certified")
-    ap.add_argument("--variant", choices=["auto", "valu", "mfma"], default="auto")
+    ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
     args = ap.parse_args()
@@ -118,11 +120,15 @@ def main():
     else:
         ctx = icp_amd.Context(local, nn_mode)
 
-    variant = {"auto": icp_amd.VARIANT_AUTO, "valu": icp_amd.VARIANT_VALU, "mfma": icp_amd.VARIANT_MFMA}[args.variant]
+    variant = {"auto": icp_amd.VARIANT_AUTO, "valu": icp_amd.VARIANT_VALU, "mfma": icp_amd.VARIANT_MFMA,
+               "mfma16": icp_amd.VARIANT_MFMA16}[args.variant]
     ctx.set_nn_variant(variant)
     m, p = icp_amd.synthetic_pair(args.n, seed=42)
     b, c = icp_amd.shard_range(args.n, rank, world)
-    uses_mfma = args.nn == "certified" and (args.variant == "mfma" or (args.variant == "auto" and c >= 65536 and args.n >= 65536))
+    big = c >= 65536 and args.n >= 65536
+    level1 = None if args.nn != "certified" else (
+        "mfma16" if args.variant == "mfma16" or (args.variant == "auto" and big) else
+        ("mfma" if args.variant == "mfma" else None))
     ctx.set_model(m)
     ctx.set_scene(p[b:b + c], np_total=args.n)
 
@@ -141,7 +147,13 @@ def main():
         dt = float(t.item())
 
     nn_avg_ms = st["nn_ms"] / max(st["nn_launches"], 1)
-    flops = FLOP_PER_PAIR * c * args.n
+    pairs = c * args.n
+    algo_tflops = FLOP_PER_PAIR * pairs / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
+    if level1 == "mfma16":
+        # the kernel runs on the f16 matrix cores: executed MFMA flop vs the dense f16 peak
+        flops, peak, achieved = MFMA16_FLOP_PER_PAIR * pairs, PEAK_F16_MFMA_TFLOPS, None
+    else:
+        flops, peak, achieved = FLOP_PER_PAIR * pairs, PEAK_FP32_TFLOPS, None
     achieved = flops / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
 
     if rank == 0:
@@ -162,14 +174,19 @@ def main():
                        "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
                        "parallelism": f"scene-sharded x{world}, model replicated, RCCL all-reduce of 18 fp64 sums/iter"},
             "roofline": {"bound": "mfma",
-                         "compute_unit": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)" if uses_mfma
-                         else ("VALU fp64" if args.nn == "fp64" else "VALU fp32 direct form (peak = f32 MFMA peak)"),
-                         "kernel": "nn_mfma_kernel" if uses_mfma else ("nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel"),
+                         "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + 2 VALU/pair min tracking",
+                                          "mfma": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)"}.get(
+                             level1, "VALU fp64" if args.nn == "fp64" else "VALU fp32 direct form (peak = f32 MFMA peak)"),
+                         "kernel": {"mfma16": "nn_mfma16_kernel", "mfma": "nn_mfma_kernel"}.get(
+                             level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel"),
                          "achieved": achieved,
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                         "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None,
                          "avg_launch_ms": nn_avg_ms, "flop_per_launch": flops,
-                         "flop_definition": "8 flop per (query, model) pair"},
+                         "flop_definition": ("executed f16 MFMA flop: 32 per (query, model) pair (K = 16 slots, 14 used)"
+                                             if level1 == "mfma16" else "8 flop per (query, model) pair"),
+                         "algorithmic_tflops_8flop_per_pair": algo_tflops,
+                         "pairs_per_s": pairs / (nn_avg_ms * 1e-3) if nn_avg_ms > 0 else 0.0},
             "mfma_uncertified_per_iter": st["level1_queued"] / max(st["iterations"], 1),
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,

@@ -45,13 +45,16 @@ extern "C" {
 #define ICP_NN_FP64 1      /* fp64 brute force (reference-faithful cross-check)           */
 
 /* Filter used by ICP_NN_CERTIFIED (results identical; speed differs):
- * VALU: direct-form fp32 distances on the vector ALUs (8 VALU ops per pair);
- * MFMA: expanded form |m|^2 - 2 p.m on v_mfma_f32_16x16x4_f32 (256 pairs per instruction),
- *       uncertified queries cascade to the VALU filter, then to fp64;
- * AUTO: MFMA when both clouds have >= 65536 points, else VALU. */
+ * VALU:   direct-form fp32 distances on the vector ALUs (8 VALU ops per pair);
+ * MFMA:   expanded form |m|^2 - 2 p.m on v_mfma_f32_16x16x4_f32 (256 pairs / instruction);
+ * MFMA16: the same form on v_mfma_f32_32x32x16_f16 with hi/lo f16 splits (1024 pairs /
+ *         instruction, co-executes with the VALU);
+ * MFMA and MFMA16 send uncertified queries to the VALU filter, then to fp64.
+ * AUTO:   MFMA16 when both clouds have >= 65536 points, else VALU. */
 #define ICP_NN_VARIANT_AUTO 0
 #define ICP_NN_VARIANT_VALU 1
 #define ICP_NN_VARIANT_MFMA 2
+#define ICP_NN_VARIANT_MFMA16 3
 
 typedef struct icp_ctx icp_ctx;
 

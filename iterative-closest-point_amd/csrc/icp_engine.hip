@@ -48,7 +48,10 @@ struct icp_ctx {
     float4 *m32 = nullptr;   // centred fp32 model, padded to nm_pad with far points
     float4 *mperm = nullptr; // same, (mm, x, y, z) permuted for the MFMA operands
     float *mm = nullptr;     // |m~|^2 rounded to fp32 (the MFMA's k = 0 operand)
-    size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0;
+    char *mimg16 = nullptr;  // f16 split image for the 32x32x16 f16 MFMA (1 KiB / 32 points)
+    float *mms16 = nullptr;  // |b_s|^2 (scaled) per model point, fp32
+    double scale16 = 1.0;    // power of two: max |b_s| in [2^11, 2^12)
+    size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0, mimg16_cap = 0, mms16_cap = 0;
     int nn_variant = ICP_NN_VARIANT_AUTO;
     int level1_queued = 0; // queries the last MFMA pass could not certify
     double c[3] = {0, 0, 0}; // centring point = model centroid
@@ -211,11 +214,13 @@ int ensure_queue(icp_ctx *ctx, size_t n)
 
 // The MFMA filter pays off once both clouds are large (its uncertified queries cost a
 // host round trip to size the second-level launch).
-bool use_mfma(const icp_ctx *ctx, size_t n)
+// level-1 filter of a certified search: 0 = none (VALU filter only), 1 = f32 MFMA, 2 = f16 MFMA
+int level1_kind(const icp_ctx *ctx, size_t n)
 {
-    if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return true;
-    if (ctx->nn_variant == ICP_NN_VARIANT_VALU) return false;
-    return n >= 65536 && ctx->nm >= 65536;
+    if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return 1;
+    if (ctx->nn_variant == ICP_NN_VARIANT_MFMA16) return 2;
+    if (ctx->nn_variant == ICP_NN_VARIANT_VALU) return 0;
+    return (n >= 65536 && ctx->nm >= 65536) ? 2 : 0;
 }
 
 // NN search of the n queries in q against the resident model -> ctx->idx[0..n).
@@ -237,9 +242,9 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
         LAUNCHCHK("nn_fp64");
-    } else if (use_mfma(ctx, n)) {
+    } else if (const int l1 = level1_kind(ctx, n)) {
         // level 1: MFMA expanded-form filter over every query
-        const NNPlan pl = plan_nn_mfma(n, ctx->nm_pad);
+        const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad) : plan_nn_mfma(n, ctx->nm_pad);
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap,
                  (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int))));
         float *pb = (float *)ctx->part;
@@ -249,10 +254,18 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
         HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 2, ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
-        launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        if (l1 == 2)
+            launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, ctx->mimg16, (int)ctx->nm_pad, pl,
+                             pb, ps, pi, ctx->st);
+        else
+            launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
-        launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
-                                ctx->amb_count + 1, ctx->amb1, ctx->st);
+        if (l1 == 2)
+            launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16,
+                                      ctx->mms16, ctx->idx, ctx->amb_count + 1, ctx->amb1, ctx->st);
+        else
+            launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
+                                    ctx->amb_count + 1, ctx->amb1, ctx->st);
         LAUNCHCHK("nn_mfma");
         HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
@@ -260,20 +273,7 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         ctx->level1_queued = c1;
         if (c1 > 0) {
             // level 2: direct-form fp32 filter on the uncertified queries only
-            const NNPlan p2 = plan_nn32((size_t)c1, ctx->nm_pad);
-            NNPlan p2l = p2;
-            p2l.q_per_lane = 1;
-            const size_t per_block = kBlock;
-            p2l.qblocks = (int)(((size_t)c1 + per_block - 1) / per_block);
-            {
-                const int tiles = (int)(ctx->nm_pad / kTile32);
-                int splits = (2048 + p2l.qblocks - 1) / p2l.qblocks;
-                if (splits > tiles) splits = tiles;
-                if (splits < 1) splits = 1;
-                const int tps = (tiles + splits - 1) / splits;
-                p2l.chunk = tps * kTile32;
-                p2l.splits = (tiles + tps - 1) / tps;
-            }
+            const NNPlan p2l = plan_nn32_list((size_t)c1, ctx->nm_pad);
             TRY(grow(ctx, (char **)&ctx->part2, &ctx->part2_cap,
                      (size_t)p2l.splits * c1 * (2 * sizeof(float) + sizeof(int))));
             float *qb = (float *)ctx->part2;
@@ -289,6 +289,7 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
                               ctx->st);
         }
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
+        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
         LAUNCHCHK("nn_mfma levels 2-3");
     } else {
         const NNPlan pl = plan_nn32(n, ctx->nm_pad);
@@ -309,18 +310,23 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx,
                           ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
+        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
         LAUNCHCHK("nn_certified");
     }
     return ICP_OK;
 }
 
-// after the stream has been synchronised: fold the NN events into the stats
+// after the stream has been synchronised: fold the NN events and queue sizes into the stats
 void account_nn(icp_ctx *ctx, size_t n)
 {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->stats.nn_ms += ms;
     ctx->stats.nn_launches += 1;
     ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
+    if (ctx->nn_mode == ICP_NN_CERTIFIED && n) {
+        ctx->stats.ambiguous += ctx->h_amb[0];
+        if (level1_kind(ctx, n)) ctx->stats.level1_queued += ctx->level1_queued;
+    }
 }
 
 // Sum `count` device doubles over the ranks: RCCL on the context stream, or the caller's
@@ -466,7 +472,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
     free_cloud(ctx->Y);
     free_cloud(ctx->qa);
     free_cloud(ctx->qb);
-    for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, ctx->part2,
+    for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
+                    (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
                     (void *)ctx->sums, (void *)ctx->stage})
@@ -483,7 +490,7 @@ const char *icp_last_error(const icp_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int icp_set_nn_variant(icp_ctx *ctx, int variant)
 {
-    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_MFMA) return ICP_E_ARG;
+    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_MFMA16) return ICP_E_ARG;
     ctx->nn_variant = variant;
     return ICP_OK;
 }
@@ -542,7 +549,18 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     TRY(grow(ctx, &ctx->mm, &ctx->mm_cap, nm_pad));
     HIPCHK(hipMemcpyAsync(ctx->mperm, hp.data(), sizeof(float) * 4 * nm_pad, hipMemcpyHostToDevice, ctx->st));
     HIPCHK(hipMemcpyAsync(ctx->mm, hmm.data(), sizeof(float) * nm_pad, hipMemcpyHostToDevice, ctx->st));
+    // f16 split image: scale S = 2^e with max |m - c| * S in [2^11, 2^12)
+    double rm64 = 0.0;
+    for (size_t j = 0; j < nm; ++j)
+        for (int k = 0; k < 3; ++k) rm64 = std::fmax(rm64, std::fabs(m_xyz[3 * j + k] - ctx->c[k]));
+    ctx->scale16 = rm64 > 0.0 ? std::ldexp(1.0, (int)std::floor(std::log2(4096.0 / rm64))) : 1.0;
+    while (rm64 * ctx->scale16 >= 4096.0) ctx->scale16 *= 0.5;
     TRY(upload_cloud(ctx, ctx->model, m_xyz, nm, false));
+    TRY(grow(ctx, &ctx->mimg16, &ctx->mimg16_cap, nm_pad * 32));
+    TRY(grow(ctx, &ctx->mms16, &ctx->mms16_cap, nm_pad));
+    launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, (int)nm_pad, ctx->c,
+                          ctx->scale16, ctx->mimg16, ctx->mms16, ctx->st);
+    LAUNCHCHK("build_mimage16");
     HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->nm = nm;
     ctx->nm_pad = nm_pad;
@@ -594,8 +612,6 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     icp_result r{};
     r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55)
     r.R[0] = r.R[4] = r.R[8] = 1.0;
-    long long amb = 0;
-
     for (int it = 0; it < max_iter; ++it) {
         // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
         TRY(nn_search(ctx, P, n));
@@ -614,14 +630,8 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         TRY(allreduce(ctx, ctx->sums + kSumS, 11));
         HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * kSumErr, hipMemcpyDeviceToHost,
                               ctx->st));
-        if (ctx->nn_mode == ICP_NN_CERTIFIED)
-            HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
         account_nn(ctx, n);
-        if (ctx->nn_mode == ICP_NN_CERTIFIED) {
-            amb += ctx->h_amb[0];
-            ctx->stats.level1_queued += use_mfma(ctx, n) ? ctx->level1_queued : 0;
-        }
 
         // 4. host Horn solve (gpu.cc:106-146)
         const double *h = ctx->h_sums;
@@ -656,7 +666,6 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             break;
         }
     }
-    ctx->stats.ambiguous += amb;
     ctx->stats.iter_ms +=
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
     if (res) *res = r;

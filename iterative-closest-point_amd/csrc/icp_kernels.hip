@@ -29,6 +29,7 @@
 #include "icp_kernels.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace icp {
 
@@ -65,13 +66,22 @@ __device__ double cert_window(float b32, float4 p, double rm)
     return (bp + f(X)) * (1.0 + 1e-12);
 }
 
-// v_min_f32 without the canonicalising v_max hipcc puts in front of fminf on MFMA
-// results (one per operand; the values here are never NaN / denormal-sensitive)
-__device__ __forceinline__ float min_nocanon(float a, float b)
+// Running-minimum helpers for MFMA results.  Plain fminf: this file is built with IEEE
+// mode off and no-NaN semantics (Makefile: -mno-amdgpu-ieee -fno-honor-nans), so hipcc
+// emits bare v_min_f32 / v_min3_f32 (no canonicalising v_max per operand) AND pads the
+// MFMA-result -> VALU-read hazard itself.  (Inline asm readers of MFMA results are NOT
+// padded by hipcc: 12 wait states are required after an 8-pass MFMA, guide §5.7.)
+__device__ __forceinline__ float min_nocanon(float a, float b) { return fminf(a, b); }
+
+// minimum of the 16 accumulator values of a 32x32 MFMA
+template <class V> __device__ __forceinline__ float min16_nocanon(const V &d)
 {
-    float r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
+    const float a = fminf(fminf(d[0], d[1]), d[2]);
+    const float b = fminf(fminf(d[3], d[4]), d[5]);
+    const float c = fminf(fminf(d[6], d[7]), d[8]);
+    const float e = fminf(fminf(d[9], d[10]), d[11]);
+    const float f = fminf(fminf(d[12], d[13]), d[14]);
+    return fminf(fminf(fminf(a, b), c), fminf(fminf(e, f), d[15]));
 }
 
 // Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
@@ -173,21 +183,31 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
         for (int k = tid; k < kTile32; k += kBlock) tile[k] = m32[t0 + k];
         __syncthreads();
         for (int sb = 0; sb < kTile32; sb += kSub) {
-            float prev[Q];
+            // pass 1: sub-block minimum only (v_min3: half an op per pair)
+            float tmin[Q];
 #pragma unroll
-            for (int q = 0; q < Q; ++q) prev[q] = best[q];
+            for (int q = 0; q < Q; ++q) tmin[q] = INFINITY;
 #pragma unroll 8
             for (int k = 0; k < kSub; ++k) {
                 const float4 m = tile[sb + k];
 #pragma unroll
-                for (int q = 0; q < Q; ++q) {
-                    const float d = d32(px[q], py[q], pz[q], m);
-                    second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d);
-                    best[q] = __builtin_fminf(best[q], d);
+                for (int q = 0; q < Q; ++q) tmin[q] = fminf(tmin[q], d32(px[q], py[q], pz[q], m));
+            }
+            // pass 2 (per query slot q, wave-uniform) only if some lane's (best, second) can
+            // change (tmin < second); the distances are recomputed bit-identically
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                if (__any(tmin[q] < second[q])) {
+                    const float prev = best[q];
+#pragma unroll 8
+                    for (int k = 0; k < kSub; ++k) {
+                        const float d = d32(px[q], py[q], pz[q], tile[sb + k]);
+                        second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d);
+                        best[q] = fminf(best[q], d);
+                    }
+                    bsub[q] = best[q] < prev ? (t0 + sb) : bsub[q];
                 }
             }
-#pragma unroll
-            for (int q = 0; q < Q; ++q) bsub[q] = best[q] < prev[q] ? (t0 + sb) : bsub[q];
         }
     }
 
@@ -363,6 +383,297 @@ __global__ __launch_bounds__(kBlock) void nn_mfma_kernel(
             part_second[o] = s2;
             part_idx[o] = id;
         }
+    }
+}
+
+// ---- NN: f16 split-precision MFMA filter ---------------------------------------------
+// v_mfma_f32_32x32x16_f16 evaluates G_s = |b_s|^2 - 2 a_s.b_s for 32 model points x 32
+// queries, where a_s = S (p - c), b_s = S (m - c) (fp64 centred, S = 2^e puts the model's
+// max |coordinate| in [2^11, 2^12)).  Every coordinate is split into two f16 (hi, lo =
+// f16(x - hi)); the 16 K-slots carry all four hi/lo products of each axis (x4 x 3 = 12) and a
+// hi/lo split of |b_s|^2 / 2^12 times 2^12 (2), i.e. 14 exact f16 x f16 products summed in
+// fp32.  These matrix cores co-execute with the VALU (unlike the f32-input MFMA), so the
+// 2 VALU / value of min/med3 tracking is the bound.  Lane l (i = l & 31, h = l >> 5):
+// A = model image half8 [blk*64 + l]; B = this lane's 8 query slots; D reg r = row
+// (r&3) + 8(r>>2) + 4h of the 32-point block, column = query i.  The argmin index is
+// recovered by re-running the (deterministic) MFMA on each lane's winning block.
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void split_f16(double x, _Float16 &hi, _Float16 &lo)
+{
+    hi = (_Float16)x;
+    lo = (_Float16)(x - (double)hi);
+}
+
+// query-side operand of lane half h for the (clamped) scaled query a
+__device__ __forceinline__ half8_t query_frag(const double a[3], int h)
+{
+    _Float16 xh, xl, yh, yl, zh, zl;
+    split_f16(a[0], xh, xl);
+    split_f16(a[1], yh, yl);
+    split_f16(a[2], zh, zl);
+    const _Float16 m2 = (_Float16)-2.0f;
+    half8_t b;
+    if (h == 0) {
+        b[0] = m2 * xh; b[1] = m2 * xh; b[2] = m2 * xl; b[3] = m2 * yh;
+        b[4] = m2 * yh; b[5] = m2 * yl; b[6] = m2 * zh; b[7] = m2 * zh;
+    } else {
+        b[0] = m2 * zl; b[1] = (_Float16)4096.0f; b[2] = (_Float16)4096.0f; b[3] = m2 * xl;
+        b[4] = m2 * yl; b[5] = m2 * zl; b[6] = (_Float16)0.0f; b[7] = (_Float16)0.0f;
+    }
+    return b;
+}
+
+constexpr double kF16QueryClamp = 32000.0;
+constexpr int kTile16 = 512; // model points per LDS tile of the f16 filter (16 KiB), x2 buffers
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int kVmcnt0 = 0x0F70;                   // vmcnt(0)
+constexpr int kVmcntDma = 0x0F70 | (512 / 32 / 4); // vmcnt(4): one tile's DMA may stay in flight
+constexpr int kLgkmcnt0 = 0xC07F;                 // lgkmcnt(0) // |a_s| beyond this: operand clamped, not certified
+
+template <int QG, int NS>
+__global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, double cx, double cy, double cz, double scale, const half8_t *__restrict__ mimg,
+    int nm_pad, int chunk, float *__restrict__ part_best, float *__restrict__ part_second,
+    int *__restrict__ part_idx)
+{
+    // NS independent (best, second, block) trackers per query group, each over 16/NS of
+    // the 16 result registers: shorter min/med3 dependency chains, merged at the end.
+    // two 512-point tiles (16 KiB each): the next tile streams in by LDS-DMA
+    // (global_load_lds_dwordx4, one 1-KiB block per wave-instruction) while this one is used
+    __shared__ half8_t tiles[2][kTile16 * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm_pad);
+    const int qbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
+    constexpr int RPS = 16 / NS; // result registers per tracker
+    constexpr int kBlocksPerTile = kTile16 / 32;            // 16
+    constexpr int kDmaPerWave = kBlocksPerTile / 4;         // 4 wave-instructions per tile
+
+    half8_t bq[QG];
+    float best[QG][NS], second[QG][NS];
+    int bblk[QG][NS];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int j = qbase + q * 32;
+        double a[3] = {0.0, 0.0, 0.0};
+        if (j < np) {
+            a[0] = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[1] = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[2] = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+        }
+        bq[q] = query_frag(a, h);
+#pragma unroll
+        for (int t = 0; t < NS; ++t) {
+            best[q][t] = INFINITY;
+            second[q][t] = INFINITY;
+            bblk[q][t] = m0 >> 5;
+        }
+    }
+    const f32x16_t zero = {};
+
+    auto issue_tile = [&](int tpt, int buf) { // wave w fetches blocks w, w+4, w+8, w+12
+#pragma unroll
+        for (int i = 0; i < kDmaPerWave; ++i) {
+            const int blk = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((const void *)(mimg + ((size_t)(tpt >> 5) + blk) * 64 + lane),
+                                             (__attribute__((address_space(3))) void *)&tiles[buf][blk * 64],
+                                             16, 0, 0);
+        }
+    };
+    issue_tile(m0, 0);
+    int it = 0;
+    for (int t0 = m0; t0 < m1; t0 += kTile16, ++it) {
+        const int cur = it & 1;
+        if (t0 + kTile16 < m1) {
+            issue_tile(t0 + kTile16, cur ^ 1);
+            __builtin_amdgcn_s_waitcnt(kVmcntDma); // this wave's DMA of `cur` has landed
+        } else {
+            __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        }
+        __builtin_amdgcn_s_barrier(); // ... and every other wave's
+        const half8_t *tile = tiles[cur];
+        half8_t a_next = tile[lane];
+        for (int b = 0; b < kBlocksPerTile; ++b) {
+            const half8_t a8 = a_next;
+            if (b + 1 < kBlocksPerTile) a_next = tile[(b + 1) * 64 + lane]; // LDS prefetch
+            // all QG MFMAs first (independent), then their minima, then ONE wave-uniform
+            // branch: a branch per MFMA would serialise MFMA -> result -> branch -> MFMA.
+            f32x16_t d[QG];
+#pragma unroll
+            for (int q = 0; q < QG; ++q) d[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+            // A block can change (best, second) only if its minimum is < second
+            // (d >= second  =>  med3(best, second, d) = second and min(best, d) = best): the
+            // 32-op update runs only when some lane needs it, which after the running
+            // minima settle is a few percent of blocks.
+            bool need[QG];
+            bool any_need = false;
+#pragma unroll
+            for (int q = 0; q < QG; ++q) {
+                float s_min = second[q][0];
+#pragma unroll
+                for (int t = 1; t < NS; ++t) s_min = fmaxf(s_min, second[q][t]);
+                need[q] = min16_nocanon(d[q]) < s_min;
+                any_need |= need[q];
+            }
+            if (__any(any_need)) {
+#pragma unroll
+                for (int q = 0; q < QG; ++q) {
+                    if (!__any(need[q])) continue;
+#pragma unroll
+                    for (int t = 0; t < NS; ++t) {
+                        const float prev = best[q][t];
+#pragma unroll
+                        for (int r = t * RPS; r < (t + 1) * RPS; ++r) {
+                            second[q][t] = __builtin_amdgcn_fmed3f(best[q][t], second[q][t], d[q][r]);
+                            best[q][t] = min_nocanon(best[q][t], d[q][r]);
+                        }
+                        bblk[q][t] = best[q][t] < prev ? ((t0 >> 5) + b) : bblk[q][t];
+                    }
+                }
+            }
+        }
+        // every wave is done reading `cur` before the next iteration's DMA overwrites it
+        __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+        __builtin_amdgcn_s_barrier();
+    }
+
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        // merge the NS trackers of this lane (ties: keep the lower tracker; a tie makes
+        // second == best, i.e. uncertified, so which block is kept does not matter)
+        float b = best[q][0], s2 = second[q][0];
+        int blk = bblk[q][0];
+#pragma unroll
+        for (int t = 1; t < NS; ++t) {
+            if (best[q][t] < b) {
+                s2 = fminf(b, second[q][t]);
+                b = best[q][t];
+                blk = bblk[q][t];
+            } else {
+                s2 = fminf(s2, best[q][t]);
+                if (best[q][t] == b) blk = min(blk, bblk[q][t]);
+            }
+        }
+        // Index recovery: re-run the MFMA on every distinct winning block of the wave (the
+        // MFMA is deterministic: same operands -> same bits); lowest row with d == best.
+        int found = -1;
+        bool done = false;
+        for (int guard = 0; guard < 64; ++guard) {
+            const unsigned long long pend = __ballot(!done);
+            if (pend == 0ull) break;
+            const int lead = __ffsll((long long)pend) - 1;
+            const int rb = __shfl(blk, lead, 64);
+            const half8_t a8 = mimg[(size_t)rb * 64 + lane];
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+            if (!done && blk == rb) {
+#pragma unroll
+                for (int r = 15; r >= 0; --r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    found = (d[r] == b) ? rb * 32 + row : found;
+                }
+                done = true;
+            }
+        }
+        int id = found;
+        {
+            const float ob = __shfl_xor(b, 32, 64), os = __shfl_xor(s2, 32, 64);
+            const int oi = __shfl_xor(id, 32, 64);
+            if (ob < b) {
+                s2 = fminf(b, os);
+                b = ob;
+                id = oi;
+            } else {
+                s2 = fminf(s2, ob);
+                if (ob == b && oi >= 0 && (id < 0 || oi < id)) id = oi;
+            }
+        }
+        const int j = qbase + q * 32;
+        if (h == 0 && j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = b;
+            part_second[o] = s2;
+            part_idx[o] = id;
+        }
+    }
+}
+
+// Certificate of the f16 filter, in scaled units (a_s, b_s), u = 2^-24, A = |a_s|:
+//   |G^ - G| <= delta(R) = 21u R^2 + 52u A R + 2e-3   for |b_s| <= R
+// (fp32 accumulation of 14 exact products in any order: 14u (R^2 + 2AR) with slack;
+//  hi/lo representation error 2^-22 per coordinate and per |b|^2: 4u R^2 + 16u A R, with
+//  slack; f16 subnormal floors: 2e-3).  Then as for the f32 filter:
+//   Db = b + delta(Rb) + A^2 (1+4u),  Rc = A (1+2u) + sqrt(Db (1+2^-40)),
+//   T = b + delta(Rb) + delta(Rc) + 2^-48 Db;  second > T => unique candidate.
+__global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
+    const float *__restrict__ part_best, const float *__restrict__ part_second,
+    const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
+    const double *__restrict__ py, const double *__restrict__ pz, int np, double cx, double cy,
+    double cz, double scale, const float *__restrict__ mms, int *__restrict__ idx, int *amb_count,
+    int *amb_list)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    float b, s2;
+    int id;
+    merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    const double ax = (px[j] - cx) * scale, ay = (py[j] - cy) * scale, az = (pz[j] - cz) * scale;
+    bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
+              fabs(az) <= kF16QueryClamp;
+    if (ok) {
+        const double u = 0x1.0p-24;
+        const double a2 = ax * ax + ay * ay + az * az;
+        const double A = sqrt(a2);
+        auto delta = [&](double R) { return 21.0 * u * R * R + 52.0 * u * A * R + 2e-3; };
+        const double db = delta(sqrt((double)mms[id]) * (1.0 + 0x1.0p-20));
+        const double Db = fmax((double)b + db + a2 * (1.0 + 4.0 * u), 0.0);
+        const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
+        double T = (double)b + db + delta(Rc) + 0x1.0p-48 * Db;
+        T += fabs(T) * 1e-12 + 1e-300;
+        ok = (double)s2 > T;
+    }
+    if (ok) {
+        idx[j] = id;
+    } else {
+        const int slot = atomicAdd(amb_count, 1);
+        amb_list[slot] = j;
+    }
+}
+
+// model image for the f16 filter (see nn_mfma16_kernel); padding points get G ~ 2.7e8
+__global__ __launch_bounds__(kBlock) void build_mimage16_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
+    int nm, int nm_pad, double cx, double cy, double cz, double scale, half8_t *__restrict__ img,
+    float *__restrict__ mms)
+{
+    for (int P = blockIdx.x * kBlock + threadIdx.x; P < nm_pad; P += gridDim.x * kBlock) {
+        half8_t lo8 = {}, hi8 = {};
+        float mmv = 0.f;
+        if (P < nm) {
+            const double b0 = (mx[P] - cx) * scale, b1 = (my[P] - cy) * scale, b2 = (mz[P] - cz) * scale;
+            const double mm = b0 * b0 + b1 * b1 + b2 * b2;
+            _Float16 xh, xl, yh, yl, zh, zl, mh, ml;
+            split_f16(b0, xh, xl);
+            split_f16(b1, yh, yl);
+            split_f16(b2, zh, zl);
+            split_f16(mm / 4096.0, mh, ml);
+            lo8[0] = xh; lo8[1] = xl; lo8[2] = xh; lo8[3] = yh;
+            lo8[4] = yl; lo8[5] = yh; lo8[6] = zh; lo8[7] = zl;
+            hi8[0] = zh; hi8[1] = mh; hi8[2] = ml; hi8[3] = xl;
+            hi8[4] = yl; hi8[5] = zl;
+            mmv = (float)mm;
+        } else {
+            hi8[1] = (_Float16)65504.0f;
+            mmv = 1.0e30f;
+        }
+        const int blk = P >> 5, i = P & 31;
+        img[(size_t)blk * 64 + i] = lo8;      // lane half h = 0
+        img[(size_t)blk * 64 + 32 + i] = hi8; // lane half h = 1
+        mms[P] = mmv;
     }
 }
 
@@ -737,6 +1048,9 @@ static NNPlan make_plan(size_t np, size_t nm, int tile, int q_small, int q_large
 }
 
 NNPlan plan_nn32(size_t np, size_t nm_pad) { return make_plan(np, nm_pad, kTile32, 1, 4, 262144); }
+// second-level (list) search: register-block 4 queries per lane as soon as there are enough
+// to keep >= 2048 workgroups busy through model splits
+NNPlan plan_nn32_list(size_t count, size_t nm_pad) { return make_plan(count, nm_pad, kTile32, 1, 4, 8192); }
 NNPlan plan_nn64(size_t np, size_t nm) { return make_plan(np, nm, kTile64, 1, 2, 262144); }
 
 void launch_nn_filter(const float4 *p32, const int *list, int nslots, const float4 *m32, int nm_pad,
@@ -744,7 +1058,10 @@ void launch_nn_filter(const float4 *p32, const int *list, int nslots, const floa
                       hipStream_t st)
 {
     dim3 grid(pl.qblocks, pl.splits);
-    if (list) {
+    if (list && pl.q_per_lane == 4) {
+        nn_filter_kernel<4, true><<<grid, kBlock, 0, st>>>(p32, list, nslots, m32, nm_pad, pl.chunk,
+                                                           part_best, part_second, part_idx);
+    } else if (list) {
         nn_filter_kernel<1, true><<<grid, kBlock, 0, st>>>(p32, list, nslots, m32, nm_pad, pl.chunk,
                                                            part_best, part_second, part_idx);
     } else if (pl.q_per_lane == 4) {
@@ -794,6 +1111,71 @@ void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, 
     dim3 grid(pl.qblocks, pl.splits);
     nn_mfma_kernel<kMfmaQG><<<grid, kBlock, 0, st>>>(p32, np, mperm, nm_pad, pl.chunk, part_best,
                                                      part_second, part_idx);
+}
+
+static int mfma16_cfg()
+{
+    // tuning knob for experiments: ICP_MFMA16_CFG = 21 | 22 | 41 | 42 (QG, NS)
+    static int cfg = [] {
+        const char *e = getenv("ICP_MFMA16_CFG");
+        const int v = e ? atoi(e) : 0;
+        return (v == 21 || v == 22 || v == 41 || v == 42 || v == 24) ? v : 41;
+    }();
+    return cfg;
+}
+
+NNPlan plan_nn_mfma16(size_t np, size_t nm_pad)
+{
+    NNPlan pl;
+    pl.q_per_lane = mfma16_cfg() / 10;
+    const size_t per_block = (size_t)4 * pl.q_per_lane * 32;
+    pl.qblocks = (int)((np + per_block - 1) / per_block);
+    if (pl.qblocks < 1) pl.qblocks = 1;
+    const int tiles = (int)((nm_pad + kTile32 - 1) / kTile32);
+    int splits = (2048 + pl.qblocks - 1) / pl.qblocks;
+    if (splits > tiles) splits = tiles;
+    if (splits < 1) splits = 1;
+    const int tps = (tiles + splits - 1) / splits;
+    pl.chunk = tps * kTile32;
+    pl.splits = (tiles + tps - 1) / tps;
+    return pl;
+}
+
+void launch_build_mimage16(const double *mx, const double *my, const double *mz, int nm, int nm_pad,
+                           const double c[3], double scale, void *img, float *mms, hipStream_t st)
+{
+    build_mimage16_kernel<<<grid_for(nm_pad), kBlock, 0, st>>>(mx, my, mz, nm, nm_pad, c[0], c[1], c[2],
+                                                               scale, (half8_t *)img, mms);
+}
+
+void launch_nn_mfma16(const double *px, const double *py, const double *pz, int np, const double c[3],
+                      double scale, const void *img, int nm_pad, const NNPlan &pl, float *part_best,
+                      float *part_second, int *part_idx, hipStream_t st)
+{
+    dim3 grid(pl.qblocks, pl.splits);
+    const half8_t *im = (const half8_t *)img;
+#define LAUNCH16(QG, NS)                                                                         \
+    nn_mfma16_kernel<QG, NS><<<grid, kBlock, 0, st>>>(px, py, pz, np, c[0], c[1], c[2], scale, im,  \
+                                                      nm_pad, pl.chunk, part_best, part_second,    \
+                                                      part_idx)
+    switch (mfma16_cfg()) {
+    case 21: LAUNCH16(2, 1); break;
+    case 42: LAUNCH16(4, 2); break;
+    case 24: LAUNCH16(2, 4); break;
+    case 22: LAUNCH16(2, 2); break;
+    default: LAUNCH16(4, 1); break;
+    }
+#undef LAUNCH16
+}
+
+void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
+                               int splits, const double *px, const double *py, const double *pz,
+                               int np, const double c[3], double scale, const float *mms, int *idx,
+                               int *amb_count, int *amb_list, hipStream_t st)
+{
+    nn_finalize_mfma16_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
+        part_best, part_second, part_idx, splits, px, py, pz, np, c[0], c[1], c[2], scale, mms, idx,
+        amb_count, amb_list);
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,

@@ -44,6 +44,7 @@ NN_FP64 = 1
 VARIANT_AUTO = 0
 VARIANT_VALU = 1
 VARIANT_MFMA = 2
+VARIANT_MFMA16 = 3
 
 # every function include/icp_capi.h declares (checked by tests/test_capi.py)
 EXPORTED = [

@@ -21,8 +21,8 @@ GOLD = os.path.join(HERE, "golden")
 RNG = np.random.default_rng(99)
 # (nn_mode, filter variant): certified with the VALU filter, certified with the MFMA filter
 # (+ VALU second level + fp64), fp64 brute force
-MODES = ["valu", "mfma", "fp64"]
-_MODE_ARGS = {"valu": (0, 1), "mfma": (0, 2), "fp64": (1, 0)}
+MODES = ["valu", "mfma", "mfma16", "fp64"]
+_MODE_ARGS = {"valu": (0, 1), "mfma": (0, 2), "mfma16": (0, 3), "fp64": (1, 0)}
 
 
 @pytest.fixture(scope="module")
@@ -107,7 +107,7 @@ def test_nn_exact_ties_and_duplicates(amd, ctxs, oracle, mode):
     np.testing.assert_array_equal(idx, ref)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_nn_certificate_sends_ties_to_resolution(amd, variant):
     with amd.Context(0, 0) as ctx:
         ctx.set_nn_variant(variant)
@@ -138,18 +138,20 @@ def test_nn_certified_equals_fp64_at_1m(amd, ctxs, oracle):
         _, out[mode] = ctxs[mode].closest_matrix(p)
     np.testing.assert_array_equal(out["valu"], out["fp64"])
     np.testing.assert_array_equal(out["mfma"], out["fp64"])
+    np.testing.assert_array_equal(out["mfma16"], out["fp64"])
     sel = RNG.choice(p.shape[0], size=96, replace=False)
     _, ref = oracle.closest(p[sel], m)
     np.testing.assert_array_equal(out["fp64"][sel], ref)
 
 
-def test_mfma_rescan_matches_mfma_bits(amd):
-    # the MFMA filter recovers its argmin by recomputing G with a VALU fma chain; if the
-    # MFMA's rounding ever differed, those queries would all fall back to level 2.  On
-    # random data essentially every query must be certified at level 1 or 2.
+@pytest.mark.parametrize("variant", [2, 3])
+def test_mfma_level1_certifies_most_queries(amd, variant):
+    # the MFMA filters recover their argmin by recomputing G (f32: VALU fma chain, f16:
+    # re-running the MFMA); if those bits ever differed, the queries would all fall back to
+    # level 2.  On random data almost every query must be settled at level 1 or 2.
     m, p = amd.synthetic_pair(1 << 17, seed=3)
     with amd.Context(0, 0) as ctx:
-        ctx.set_nn_variant(amd.VARIANT_MFMA)
+        ctx.set_nn_variant(variant)
         ctx.set_model(m)
         ctx.set_scene(p, np_total=p.shape[0])
         ctx.set_allow_unequal(True)
@@ -199,7 +201,7 @@ def test_icp_synthetic_fixed_iterations(amd, golden_traces):
 def test_modes_bitwise_identical(amd):
     m, p = load(amd, "horse_ref"), load(amd, "horse_tr1")
     a = run_engine(amd, "valu", m, p, 6, -1.0)
-    for mode in ("mfma", "fp64"):
+    for mode in ("mfma", "mfma16", "fp64"):
         b = run_engine(amd, mode, m, p, 6, -1.0)
         np.testing.assert_array_equal(a[1], b[1])
         np.testing.assert_array_equal(a[2], b[2])

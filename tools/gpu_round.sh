@@ -32,21 +32,26 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_mfma) run bench_mfma 300 python bench.py --variant mfma --no-cpu-baseline --no-cow ;;
+    bench_mfma16) run bench_mfma16 300 python bench.py --variant mfma16 --no-cpu-baseline --no-cow ;;
     bench_valu) run bench_valu 300 python bench.py --variant valu --no-cpu-baseline --no-cow ;;
     bench_fp64) run bench_fp64 300 python bench.py --nn fp64 --steps 5 --warmup 1 --no-cpu-baseline --no-cow ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
                python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cow ;;
+    profv) for v in ${PROFV:-mfma16 valu}; do
+               run rocprof_$v 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$v" -o bench -- \
+                   python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cow --variant $v; done ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc1" -o fetch -- \
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc2" -o write -- \
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow ;;
-    sq)    for v in mfma valu; do
+    sq)    for v in ${SQV:-mfma valu}; do
                run sq1_$v 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE \
                    --output-format csv -d "$OUT/sq1_$v" -o sq -- python3 tools/nn_probe.py --variant $v --reps 1
-               run sq2_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INST_CYCLES_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE \
+               run sq2_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INST_CYCLES_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE \
                    --output-format csv -d "$OUT/sq2_$v" -o sq -- python3 tools/nn_probe.py --variant $v --reps 1
            done ;;
-    probe) for v in mfma valu; do run probe_$v 300 python3 tools/nn_probe.py --variant $v; done ;;
+    probe) for v in mfma16 mfma valu; do run probe_$v 300 python3 tools/nn_probe.py --variant $v; done ;;
+    cfg16) for c in 21 22 24 41 42; do ICP_MFMA16_CFG=$c run probe16_$c 300 python3 tools/nn_probe.py --variant mfma16; done ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
     *) echo "unknown step $s" ;;

@@ -15,13 +15,13 @@ import icp_amd  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", default="mfma", choices=["valu", "mfma", "fp64"])
+    ap.add_argument("--variant", default="mfma", choices=["valu", "mfma", "mfma16", "fp64"])
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     mode = icp_amd.NN_FP64 if a.variant == "fp64" else icp_amd.NN_CERTIFIED
     with icp_amd.Context(0, mode) as ctx:
-        ctx.set_nn_variant({"valu": 1, "mfma": 2, "fp64": 0}[a.variant])
+        ctx.set_nn_variant({"valu": 1, "mfma": 2, "mfma16": 3, "fp64": 0}[a.variant])
         m, p = icp_amd.synthetic_pair(a.n, seed=42)
         ctx.set_model(m)
         ctx.closest_matrix(p)
@@ -32,6 +32,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.reps
         st = ctx.stats()
     ms = st["nn_ms"] / max(st["nn_launches"], 1)
+    print(f"level1 queued {st['level1_queued'] / max(st['nn_launches'], 1):.0f}, fp64 {st['ambiguous']}")
     print(f"{a.variant}: wall {dt * 1e3:.2f} ms/search, filter kernel {ms:.2f} ms, "
           f"{8.0 * a.n * a.n / (ms * 1e-3) / 1e12:.1f} TF(8 flop/pair)")
 
