@@ -73,6 +73,7 @@ typedef struct icp_stats {
     long long nn_pairs;    /* sum over searches of np_local * nm                        */
     long long ambiguous;   /* queries the fp32 certificate sent to fp64 resolution      */
     long long level1_queued; /* queries the MFMA certificate sent to the VALU filter     */
+    long long level1_unrecovered; /* ... of which the MFMA filter proposed no candidate      */
     double iter_ms;        /* host wall time inside icp_run                             */
     long long iterations;  /* iterations executed by icp_run                            */
 } icp_stats;

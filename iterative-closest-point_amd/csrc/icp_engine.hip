@@ -71,8 +71,9 @@ struct icp_ctx {
     size_t idx_cap = 0;
     void *part = nullptr, *part2 = nullptr;
     size_t part_cap = 0, part2_cap = 0;
-    int *amb1 = nullptr; // queue of the MFMA certificate
-    size_t amb1_cap = 0;
+    int *amb1 = nullptr;           // queue of the MFMA certificate
+    float *amb1_seed = nullptr;    // ... and each queued query's level-2 seed
+    size_t amb1_cap = 0, amb1_seed_cap = 0;
     int *amb_count = nullptr, *amb_list = nullptr;
     double *amb_T = nullptr;
     size_t amb_cap = 0;
@@ -252,7 +253,9 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         int *pi = (int *)(ps + (size_t)pl.splits * n);
         TRY(ensure_queue(ctx, n));
         TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
-        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 2, ctx->st));
+        TRY(grow(ctx, &ctx->amb1_seed, &ctx->amb1_seed_cap, n));
+        // amb_count: [0] level-2 -> fp64 queue, [2] level-1 queue, [3] level-1 without candidate
+        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
         if (l1 == 2)
             launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, ctx->mimg16, (int)ctx->nm_pad, pl,
@@ -262,14 +265,17 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16,
-                                      ctx->mms16, ctx->idx, ctx->amb_count + 1, ctx->amb1, ctx->st);
+                                      ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed,
+                                      q.f, ctx->m32, ctx->rm, ctx->st);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
-                                    ctx->amb_count + 1, ctx->amb1, ctx->st);
+                                    ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed, ctx->m32, ctx->rm,
+                                    ctx->st);
         LAUNCHCHK("nn_mfma");
-        HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipMemcpyAsync(ctx->h_amb + 2, ctx->amb_count + 2, sizeof(int) * 2, hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
-        const int c1 = ctx->h_amb[1];
+        const int c1 = ctx->h_amb[2];
+        ctx->stats.level1_unrecovered += ctx->h_amb[3];
         ctx->level1_queued = c1;
         if (c1 > 0) {
             // level 2: direct-form fp32 filter on the uncertified queries only
@@ -279,7 +285,8 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
             float *qb = (float *)ctx->part2;
             float *qs = qb + (size_t)p2l.splits * c1;
             int *qi = (int *)(qs + (size_t)p2l.splits * c1);
-            launch_nn_filter(q.f, ctx->amb1, c1, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi, ctx->st);
+            launch_nn_filter(q.f, ctx->amb1, ctx->amb1_seed, c1, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi,
+                             ctx->st);
             CertParams cp{ctx->rm};
             launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->amb1, c1, cp, ctx->idx, ctx->amb_count,
                                ctx->amb_list, ctx->amb_T, ctx->st);
@@ -301,7 +308,7 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         TRY(ensure_queue(ctx, n));
         HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int), ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
-        launch_nn_filter(q.f, nullptr, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        launch_nn_filter(q.f, nullptr, nullptr, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
         CertParams cp{ctx->rm};
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, nullptr, (int)n, cp, ctx->idx, ctx->amb_count,
@@ -472,7 +479,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     free_cloud(ctx->Y);
     free_cloud(ctx->qa);
     free_cloud(ctx->qb);
-    for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
+    for (void *p : {(void *)ctx->amb1_seed, (void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,

@@ -35,9 +35,10 @@ NNPlan plan_nn32_list(size_t count, size_t nm_pad);
 
 // fp32 direct-form filter: partial (best, second, argbest) per (split, slot); slot s is
 // query s, or query list[s] when list != nullptr.
-void launch_nn_filter(const float4 *p32, const int *list, int nslots, const float4 *m32, int nm_pad,
-                      const NNPlan &plan, float *part_best, float *part_second, int *part_idx,
-                      hipStream_t st);
+// seed (list mode, nullable): initial `second` per slot from the level-1 candidate
+void launch_nn_filter(const float4 *p32, const int *list, const float *seed, int nslots,
+                      const float4 *m32, int nm_pad, const NNPlan &plan, float *part_best,
+                      float *part_second, int *part_idx, hipStream_t st);
 // merge splits, certify, write idx for certified queries, queue the rest (with window T).
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
                         int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
@@ -50,7 +51,8 @@ void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, 
                     float *part_best, float *part_second, int *part_idx, hipStream_t st);
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
                              int splits, const float4 *p32, int np, const float *mm, int *idx,
-                             int *amb_count, int *amb_list, hipStream_t st);
+                             int *amb_count, int *amb_list, float *amb_seed, const float4 *m32,
+                             double rm, hipStream_t st);
 // f16 split-precision MFMA filter (v_mfma_f32_32x32x16_f16): model image (1 KiB per 32
 // points) built once per model; uncertified queries appended to amb_list.
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad);
@@ -62,7 +64,8 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, const double c[3], double scale, const float *mms, int *idx,
-                               int *amb_count, int *amb_list, hipStream_t st);
+                               int *amb_count, int *amb_list, float *amb_seed, const float4 *p32,
+                               const float4 *m32, double rm, hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,

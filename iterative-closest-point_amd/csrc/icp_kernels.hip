@@ -29,7 +29,11 @@
 #include "icp_kernels.h"
 
 #include <cmath>
+#include <cstdio>
+#include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 namespace icp {
 
@@ -82,6 +86,16 @@ template <class V> __device__ __forceinline__ float min16_nocanon(const V &d)
     const float e = fminf(fminf(d[9], d[10]), d[11]);
     const float f = fminf(fminf(d[12], d[13]), d[14]);
     return fminf(fminf(fminf(a, b), c), fminf(fminf(e, f), d[15]));
+}
+
+// Level-2 seed for a query proposed m_hint by level 1: X = T(D32(m_hint)) (+ slack).  The
+// final window T(best) <= X since best <= D32(m_hint) and T is increasing, so a `second`
+// capped at X is conservative (second > T still implies uniqueness).
+__device__ float seed_from_hint(float4 p, const float4 *__restrict__ m32, int hint, double rm)
+{
+    if (hint < 0) return INFINITY;
+    const double X = cert_window(d32(p.x, p.y, p.z, m32[hint]), p, rm);
+    return (float)(X * (1.0 + 0x1.0p-20)) * (1.0f + 0x1.0p-20f);
 }
 
 // Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
@@ -151,9 +165,9 @@ __global__ __launch_bounds__(kBlock) void make_f32_kernel(const double *__restri
 // ds_read_b96 feeds 64*Q pairs).  Per pair: 3 v_sub + v_mul + 2 v_fma + v_min + v_med3.
 template <int Q, bool LIST>
 __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
-    const float4 *__restrict__ p32, const int *__restrict__ list, int nslots,
-    const float4 *__restrict__ m32, int nm_pad, int chunk, float *__restrict__ part_best,
-    float *__restrict__ part_second, int *__restrict__ part_idx)
+    const float4 *__restrict__ p32, const int *__restrict__ list, const float *__restrict__ seed,
+    int nslots, const float4 *__restrict__ m32, int nm_pad, int chunk,
+    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx)
 {
     __shared__ float4 tile[kTile32];
     const int tid = threadIdx.x;
@@ -175,6 +189,9 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
         best[q] = INFINITY;
         second[q] = INFINITY;
         bsub[q] = m0;
+        // `second` starts at the level-1 seed X (seed_from_hint): points with D32 >= X can
+        // neither be the answer nor rescue the certificate, so almost every block is skipped
+        if (LIST && seed && s < nslots) second[q] = seed[s];
     }
 
     for (int t0 = m0; t0 < m1; t0 += kTile32) {
@@ -215,10 +232,12 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         int found = bsub[q];
-#pragma unroll
-        for (int k = kSub - 1; k >= 0; --k) {
-            const float d = d32(px[q], py[q], pz[q], m32[bsub[q] + k]);
-            found = (d == best[q]) ? bsub[q] + k : found;
+        if (best[q] < INFINITY) { // (seeded list searches: most splits find nothing)
+#pragma unroll 8 // (a full unroll keeps 32 loads = 96 VGPRs in flight: occupancy /2)
+            for (int k = kSub - 1; k >= 0; --k) {
+                const float d = d32(px[q], py[q], pz[q], m32[bsub[q] + k]);
+                found = (d == best[q]) ? bsub[q] + k : found;
+            }
         }
         const int s = sbase + q * kBlock;
         if (s < nslots) {
@@ -603,10 +622,18 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
 }
 
 // Certificate of the f16 filter, in scaled units (a_s, b_s), u = 2^-24, A = |a_s|:
-//   |G^ - G| <= delta(R) = 21u R^2 + 52u A R + 2e-3   for |b_s| <= R
-// (fp32 accumulation of 14 exact products in any order: 14u (R^2 + 2AR) with slack;
-//  hi/lo representation error 2^-22 per coordinate and per |b|^2: 4u R^2 + 16u A R, with
-//  slack; f16 subnormal floors: 2e-3).  Then as for the f32 filter:
+//   |G^ - G| <= delta(R) = 26u R^2 + 60u A R + 4u (A + R) + 1e-3   for |b_s| <= R.
+// Accumulation (measured on gfx950 by tools/mfma_probe.hip): the MFMA sums
+// the K-slots in two passes (0-7, then 8-15 plus the carried fp32 partial); within a pass
+// every exact product is truncated toward zero to a multiple of 2^(E-24), E = the largest
+// term's exponent, and the pass sum is rounded to fp32.  Error <= u (n_terms + carries +
+// passes) sum|p|; budgeted for up to four passes: (14 + 3 + 4) u sum|p| <= 21u (R^2 + 2AR)
+// (1 + 2^-9).  A subnormal f16 operand is aligned as if its exponent were -14, which can
+// raise E to at most -14 + 15 + 1 = 2 (operands < 2^16): <= 16 x 2^-22 absolute.
+// Representation: hi/lo split error 2^-22 |x| per coordinate and for |b|^2: 4u R^2 + 16u A R;
+// a subnormal lo part adds 2^-25 absolute per coordinate (x2 on the query side):
+// 2^-24 sum_i (|a_i| + |b_i|) <= 2u (A + R); 4096 x 2^-25 for |b|^2/4096.  The constant
+// 1e-3 covers the absolute terms (1.3e-4).  Then as for the f32 filter:
 //   Db = b + delta(Rb) + A^2 (1+4u),  Rc = A (1+2u) + sqrt(Db (1+2^-40)),
 //   T = b + delta(Rb) + delta(Rc) + 2^-48 Db;  second > T => unique candidate.
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
@@ -614,7 +641,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int np, double cx, double cy,
     double cz, double scale, const float *__restrict__ mms, int *__restrict__ idx, int *amb_count,
-    int *amb_list)
+    int *amb_list, float *amb_seed, const float4 *__restrict__ p32, const float4 *__restrict__ m32,
+    double rm)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -628,7 +656,9 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         const double u = 0x1.0p-24;
         const double a2 = ax * ax + ay * ay + az * az;
         const double A = sqrt(a2);
-        auto delta = [&](double R) { return 21.0 * u * R * R + 52.0 * u * A * R + 2e-3; };
+        auto delta = [&](double R) {
+            return 26.0 * u * R * R + 60.0 * u * A * R + 4.0 * u * (A + R) + 1e-3;
+        };
         const double db = delta(sqrt((double)mms[id]) * (1.0 + 0x1.0p-20));
         const double Db = fmax((double)b + db + a2 * (1.0 + 4.0 * u), 0.0);
         const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
@@ -641,6 +671,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     } else {
         const int slot = atomicAdd(amb_count, 1);
         amb_list[slot] = j;
+        amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
+        if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
 
@@ -686,7 +718,8 @@ __global__ __launch_bounds__(kBlock) void build_mimage16_kernel(
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
-    const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list)
+    const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list,
+    float *amb_seed, const float4 *__restrict__ m32, double rm)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -712,6 +745,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     } else {
         const int slot = atomicAdd(amb_count, 1);
         amb_list[slot] = j;
+        amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
+        if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
 
@@ -1029,48 +1064,101 @@ void launch_make_f32(const double *x, const double *y, const double *z, size_t n
     make_f32_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, cx, cy, cz, f);
 }
 
-static NNPlan make_plan(size_t np, size_t nm, int tile, int q_small, int q_large, size_t large_np)
+// Workgroups the whole chip keeps resident for `kernel` (occupancy API x CU count), cached.
+static int resident_wgs(const void *kernel)
+{
+    static std::mutex mu;
+    static std::map<const void *, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(kernel);
+    if (it != cache.end()) return it->second;
+    int dev = 0, cus = 256, per_cu = 4;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu < 1)
+            per_cu = 4;
+    }
+    const int r = std::max(1, cus * per_cu);
+    cache[kernel] = r;
+    return r;
+}
+
+// Split the model axis so the grid fills whole rounds of resident workgroups: a grid of
+// 1.35 rounds runs its second round at a third of the chip.  Smallest split count with
+// >= 90% round efficiency and at least one full round, else the most efficient one.
+static void choose_splits(NNPlan &pl, int tiles, int tile, int cap)
+{
+    int best_tps = tiles, best_s = 1;
+    double best_eff = -1.0;
+    for (int s = 1; s <= tiles; ++s) {
+        const int tps = (tiles + s - 1) / s;
+        const int real_s = (tiles + tps - 1) / tps;
+        if (real_s != s) continue;
+        const long wgs = (long)pl.qblocks * real_s;
+        const long rounds = (wgs + cap - 1) / cap;
+        const double eff = (double)wgs / (double)(rounds * cap);
+        if (wgs >= cap && eff >= 0.9) {
+            best_tps = tps;
+            best_s = real_s;
+            break;
+        }
+        if (eff > best_eff + 1e-9) {
+            best_eff = eff;
+            best_tps = tps;
+            best_s = real_s;
+        }
+    }
+    pl.chunk = best_tps * tile;
+    pl.splits = best_s;
+}
+
+static NNPlan make_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel)
 {
     NNPlan pl;
-    pl.q_per_lane = np >= large_np ? q_large : q_small;
-    const size_t per_block = (size_t)kBlock * pl.q_per_lane;
+    pl.q_per_lane = q;
+    const size_t per_block = (size_t)queries_per_lane_block;
     pl.qblocks = (int)((np + per_block - 1) / per_block);
     if (pl.qblocks < 1) pl.qblocks = 1;
     const int tiles = (int)((nm + tile - 1) / tile);
-    // aim for >= 2048 workgroups (8 per CU) so small scenes still fill the chip
-    int splits = (2048 + pl.qblocks - 1) / pl.qblocks;
-    if (splits > tiles) splits = tiles;
-    if (splits < 1) splits = 1;
-    const int tiles_per_split = (tiles + splits - 1) / splits;
-    pl.chunk = tiles_per_split * tile;
-    pl.splits = (tiles + tiles_per_split - 1) / tiles_per_split;
+    const int cap = resident_wgs(kernel);
+    choose_splits(pl, tiles, tile, cap);
+    if (getenv("ICP_DEBUG_PLAN"))
+        fprintf(stderr, "[plan] np=%zu nm=%zu q=%d qblocks=%d splits=%d chunk=%d resident=%d wgs=%ld\n", np, nm,
+                pl.q_per_lane, pl.qblocks, pl.splits, pl.chunk, cap, (long)pl.qblocks * pl.splits);
     return pl;
 }
 
-NNPlan plan_nn32(size_t np, size_t nm_pad) { return make_plan(np, nm_pad, kTile32, 1, 4, 262144); }
-// second-level (list) search: register-block 4 queries per lane as soon as there are enough
-// to keep >= 2048 workgroups busy through model splits
-NNPlan plan_nn32_list(size_t count, size_t nm_pad) { return make_plan(count, nm_pad, kTile32, 1, 4, 8192); }
-NNPlan plan_nn64(size_t np, size_t nm) { return make_plan(np, nm, kTile64, 1, 2, 262144); }
+NNPlan plan_nn32(size_t np, size_t nm_pad)
+{
+    return np >= 262144 ? make_plan(np, nm_pad, kTile32, 4, 4 * kBlock, (const void *)nn_filter_kernel<4, false>)
+                        : make_plan(np, nm_pad, kTile32, 1, kBlock, (const void *)nn_filter_kernel<1, false>);
+}
+// second-level (list) search: register-block 4 queries per lane once there are enough to
+// keep the chip busy through model splits
+NNPlan plan_nn32_list(size_t count, size_t nm_pad)
+{
+    return count >= 8192 ? make_plan(count, nm_pad, kTile32, 4, 4 * kBlock, (const void *)nn_filter_kernel<4, true>)
+                         : make_plan(count, nm_pad, kTile32, 1, kBlock, (const void *)nn_filter_kernel<1, true>);
+}
+NNPlan plan_nn64(size_t np, size_t nm)
+{
+    return np >= 262144 ? make_plan(np, nm, kTile64, 2, 2 * kBlock, (const void *)nn_fp64_kernel<2>)
+                        : make_plan(np, nm, kTile64, 1, kBlock, (const void *)nn_fp64_kernel<1>);
+}
 
-void launch_nn_filter(const float4 *p32, const int *list, int nslots, const float4 *m32, int nm_pad,
-                      const NNPlan &pl, float *part_best, float *part_second, int *part_idx,
-                      hipStream_t st)
+void launch_nn_filter(const float4 *p32, const int *list, const float *seed, int nslots,
+                      const float4 *m32, int nm_pad, const NNPlan &pl, float *part_best,
+                      float *part_second, int *part_idx, hipStream_t st)
 {
     dim3 grid(pl.qblocks, pl.splits);
-    if (list && pl.q_per_lane == 4) {
-        nn_filter_kernel<4, true><<<grid, kBlock, 0, st>>>(p32, list, nslots, m32, nm_pad, pl.chunk,
-                                                           part_best, part_second, part_idx);
-    } else if (list) {
-        nn_filter_kernel<1, true><<<grid, kBlock, 0, st>>>(p32, list, nslots, m32, nm_pad, pl.chunk,
-                                                           part_best, part_second, part_idx);
-    } else if (pl.q_per_lane == 4) {
-        nn_filter_kernel<4, false><<<grid, kBlock, 0, st>>>(p32, nullptr, nslots, m32, nm_pad,
-                                                            pl.chunk, part_best, part_second, part_idx);
-    } else {
-        nn_filter_kernel<1, false><<<grid, kBlock, 0, st>>>(p32, nullptr, nslots, m32, nm_pad,
-                                                            pl.chunk, part_best, part_second, part_idx);
-    }
+#define LAUNCH_F(Q, L)                                                                          \
+    nn_filter_kernel<Q, L><<<grid, kBlock, 0, st>>>(p32, list, seed, nslots, m32, nm_pad, pl.chunk, \
+                                                    part_best, part_second, part_idx)
+    if (list && pl.q_per_lane == 4) LAUNCH_F(4, true);
+    else if (list) LAUNCH_F(1, true);
+    else if (pl.q_per_lane == 4) LAUNCH_F(4, false);
+    else LAUNCH_F(1, false);
+#undef LAUNCH_F
 }
 
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
@@ -1090,19 +1178,7 @@ void launch_nn_finalize(const float *part_best, const float *part_second, const 
 
 NNPlan plan_nn_mfma(size_t np, size_t nm_pad)
 {
-    NNPlan pl;
-    pl.q_per_lane = kMfmaQG;
-    const size_t per_block = (size_t)4 * kMfmaQG * 16;
-    pl.qblocks = (int)((np + per_block - 1) / per_block);
-    if (pl.qblocks < 1) pl.qblocks = 1;
-    const int tiles = (int)((nm_pad + kTile32 - 1) / kTile32);
-    int splits = (2048 + pl.qblocks - 1) / pl.qblocks;
-    if (splits > tiles) splits = tiles;
-    if (splits < 1) splits = 1;
-    const int tps = (tiles + splits - 1) / splits;
-    pl.chunk = tps * kTile32;
-    pl.splits = (tiles + tps - 1) / tps;
-    return pl;
+    return make_plan(np, nm_pad, kTile32, kMfmaQG, 4 * kMfmaQG * 16, (const void *)nn_mfma_kernel<kMfmaQG>);
 }
 
 void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, const NNPlan &pl,
@@ -1124,21 +1200,21 @@ static int mfma16_cfg()
     return cfg;
 }
 
+static const void *mfma16_kernel_ptr()
+{
+    switch (mfma16_cfg()) {
+    case 21: return (const void *)nn_mfma16_kernel<2, 1>;
+    case 42: return (const void *)nn_mfma16_kernel<4, 2>;
+    case 24: return (const void *)nn_mfma16_kernel<2, 4>;
+    case 22: return (const void *)nn_mfma16_kernel<2, 2>;
+    default: return (const void *)nn_mfma16_kernel<4, 1>;
+    }
+}
+
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad)
 {
-    NNPlan pl;
-    pl.q_per_lane = mfma16_cfg() / 10;
-    const size_t per_block = (size_t)4 * pl.q_per_lane * 32;
-    pl.qblocks = (int)((np + per_block - 1) / per_block);
-    if (pl.qblocks < 1) pl.qblocks = 1;
-    const int tiles = (int)((nm_pad + kTile32 - 1) / kTile32);
-    int splits = (2048 + pl.qblocks - 1) / pl.qblocks;
-    if (splits > tiles) splits = tiles;
-    if (splits < 1) splits = 1;
-    const int tps = (tiles + splits - 1) / splits;
-    pl.chunk = tps * kTile32;
-    pl.splits = (tiles + tps - 1) / tps;
-    return pl;
+    const int qg = mfma16_cfg() / 10;
+    return make_plan(np, nm_pad, kTile32, qg, 4 * qg * 32, mfma16_kernel_ptr());
 }
 
 void launch_build_mimage16(const double *mx, const double *my, const double *mz, int nm, int nm_pad,
@@ -1171,19 +1247,22 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, const double c[3], double scale, const float *mms, int *idx,
-                               int *amb_count, int *amb_list, hipStream_t st)
+                               int *amb_count, int *amb_list, float *amb_seed, const float4 *p32,
+                               const float4 *m32, double rm, hipStream_t st)
 {
     nn_finalize_mfma16_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
         part_best, part_second, part_idx, splits, px, py, pz, np, c[0], c[1], c[2], scale, mms, idx,
-        amb_count, amb_list);
+        amb_count, amb_list, amb_seed, p32, m32, rm);
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
                              int splits, const float4 *p32, int np, const float *mm, int *idx,
-                             int *amb_count, int *amb_list, hipStream_t st)
+                             int *amb_count, int *amb_list, float *amb_seed, const float4 *m32,
+                             double rm, hipStream_t st)
 {
     nn_finalize_mfma_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list);
+        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list, amb_seed, m32,
+        rm);
 }
 
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,

@@ -32,7 +32,8 @@ def main():
         dt = (time.perf_counter() - t0) / a.reps
         st = ctx.stats()
     ms = st["nn_ms"] / max(st["nn_launches"], 1)
-    print(f"level1 queued {st['level1_queued'] / max(st['nn_launches'], 1):.0f}, fp64 {st['ambiguous']}")
+    print(f"level1 queued {st['level1_queued'] / max(st['nn_launches'], 1):.0f} "
+          f"(no candidate {st['level1_unrecovered'] / max(st['nn_launches'], 1):.0f}), fp64 {st['ambiguous']}")
     print(f"{a.variant}: wall {dt * 1e3:.2f} ms/search, filter kernel {ms:.2f} ms, "
           f"{8.0 * a.n * a.n / (ms * 1e-3) / 1e12:.1f} TF(8 flop/pair)")
 
