@@ -13,8 +13,10 @@ sums are all-reduced with RCCL inside libicp_hip.so; total work is fixed => "str
 
 Timed region: K iterations of icp_run on clouds already resident in HBM, bracketed by a
 barrier + device synchronisation on both sides; ms_per_step = max over ranks.
-roofline: the O(N*M) NN filter kernel, 8 flop/pair (3 sub + 1 mul + 2 fma), timed with HIP
-events on the engine's stream, against the 157.3 TF fp32 peak (VALU == f32 MFMA rate).
+roofline: the level-1 O(N*M) NN filter kernel, timed with HIP events on the engine's stream.
+For the f16 MFMA filter (default at C4): executed MFMA flop (32 per pair) against the 2.5 PF
+dense f16 peak; for the fp32 filters: 8 flop/pair against 157.3 TF.  traffic: HBM bytes per
+launch from the committed rocprofv3 PMC summary (profiles/*_pmc_traffic.json).
 cpu_baseline: the oracle (C restatement of src/cpu.cc, 1 core) on rank 0: NN on a
 4096-query sample against the full model, scaled by N/4096, + the O(N) steps in full.
 """
@@ -38,6 +40,21 @@ PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF den
 FLOP_PER_PAIR = 8          # SURVEY.md §8d (algorithmic: 3 sub + 1 mul + 2 fma)
 MFMA16_FLOP_PER_PAIR = 32  # executed: v_mfma_f32_32x32x16_f16 = 2*32*32*16 flop per 1024 pairs
 REF_OPTI_GPU_LOOP_FPS = 9.36368  # reference README.md:108 (GTX 1050, cow_ref/cow_tr1)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950 correction)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            k = json.load(open(path))["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(m, p, sample=4096, seed=0):
@@ -155,6 +172,12 @@ def main():
     else:
         flops, peak, achieved = FLOP_PER_PAIR * pairs, PEAK_FP32_TFLOPS, None
     achieved = flops / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
+    kernel = {"mfma16": "nn_mfma16_kernel", "mfma": "nn_mfma_kernel"}.get(
+        level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
+    traffic, traffic_src = pmc_traffic(kernel) if world == 1 and args.n == 1 << 20 else (None, None)
+    dtype = {"mfma16": "f16 hi/lo-split MFMA filter (fp32 accumulate); fp64 certificate, resolve and reductions",
+             "mfma": "f32 MFMA filter; fp64 certificate, resolve and reductions"}.get(
+        level1, "f64" if args.nn == "fp64" else "f32 VALU filter; fp64 certificate, resolve and reductions")
 
     if rank == 0:
         out = {
@@ -168,7 +191,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32 NN filter + f64 certificate/reductions",
+            "dtype": dtype,
             "data": "synthetic (mt19937_64 seed 42, uniform [-1,1]^3; scene = 5deg rotation + translation)",
             "config": {"workload": f"C4 synthetic {args.n}-pt model vs rigid-transformed copy, fixed iterations",
                        "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
@@ -177,11 +200,11 @@ def main():
                          "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + 2 VALU/pair min tracking",
                                           "mfma": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)"}.get(
                              level1, "VALU fp64" if args.nn == "fp64" else "VALU fp32 direct form (peak = f32 MFMA peak)"),
-                         "kernel": {"mfma16": "nn_mfma16_kernel", "mfma": "nn_mfma_kernel"}.get(
-                             level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel"),
+                         "kernel": kernel,
                          "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
+                         "frac": achieved / peak, "traffic": traffic,
+                         "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
                          "avg_launch_ms": nn_avg_ms, "flop_per_launch": flops,
                          "flop_definition": ("executed f16 MFMA flop: 32 per (query, model) pair (K = 16 slots, 14 used)"
                                              if level1 == "mfma16" else "8 flop per (query, model) pair"),
