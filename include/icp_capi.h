@@ -76,6 +76,7 @@ typedef struct icp_stats {
     long long level1_unrecovered; /* ... of which the MFMA filter proposed no candidate      */
     double iter_ms;        /* host wall time inside icp_run                             */
     long long iterations;  /* iterations executed by icp_run                            */
+    long long grid_fallback; /* near ties the grid resolver handed back to brute force     */
 } icp_stats;
 
 /* ---- context ------------------------------------------------------------ */

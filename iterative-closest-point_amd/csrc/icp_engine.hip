@@ -77,6 +77,16 @@ struct icp_ctx {
     int *amb_count = nullptr, *amb_list = nullptr;
     double *amb_T = nullptr;
     size_t amb_cap = 0;
+    // exact grid resolver (icp_grid.hip): model grid + the queues around it
+    GridParams grid{};
+    int *g_cid = nullptr, *g_count = nullptr, *g_start = nullptr, *g_bsum = nullptr, *g_fill = nullptr;
+    double4 *g_pts = nullptr;
+    size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
+    int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
+    int *fb_list = nullptr;                           // queries the grid hands back
+    float *fb_seed = nullptr;
+    double *fb_T = nullptr;
+    size_t amb1_hint_cap = 0, amb_hint_cap = 0, fb_list_cap = 0, fb_seed_cap = 0, fb_T_cap = 0;
 
     // reductions
     double *partials = nullptr;
@@ -224,6 +234,19 @@ int level1_kind(const icp_ctx *ctx, size_t n)
     return (n >= 65536 && ctx->nm >= 65536) ? 2 : 0;
 }
 
+GridView grid_view(const icp_ctx *ctx)
+{
+    GridView gv{};
+    gv.pts = ctx->g_pts;
+    gv.start = ctx->g_start;
+    for (int a = 0; a < 3; ++a) {
+        gv.g[a] = ctx->grid.g[a];
+        gv.lo[a] = ctx->grid.lo[a];
+    }
+    gv.inv_h = ctx->grid.inv_h;
+    return gv;
+}
+
 // NN search of the n queries in q against the resident model -> ctx->idx[0..n).
 // Timed with HIP events on the context stream (ev[0]..ev[1] = the O(N*M) kernel).
 int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
@@ -254,7 +277,11 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         TRY(ensure_queue(ctx, n));
         TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
         TRY(grow(ctx, &ctx->amb1_seed, &ctx->amb1_seed_cap, n));
-        // amb_count: [0] level-2 -> fp64 queue, [2] level-1 queue, [3] level-1 without candidate
+        TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
+        TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
+        TRY(grow(ctx, &ctx->fb_seed, &ctx->fb_seed_cap, n));
+        // amb_count: [0] level-2 -> fp64 queue, [1] grid -> level-2 fallback, [2] level-1 queue,
+        // [3] level-1 queries without a candidate
         HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
         if (l1 == 2)
@@ -266,33 +293,39 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16,
                                       ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed,
-                                      q.f, ctx->m32, ctx->rm, ctx->st);
+                                      ctx->amb1_hint, q.f, ctx->m32, ctx->rm, ctx->st);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
-                                    ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed, ctx->m32, ctx->rm,
-                                    ctx->st);
+                                    ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed, ctx->amb1_hint, ctx->m32,
+                                    ctx->rm, ctx->st);
+        // exact resolution of the near ties through the model grid, around each candidate
+        launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z,
+                               ctx->model.x, ctx->model.y, ctx->model.z, grid_view(ctx), kGridBudget,
+                               ctx->idx, ctx->amb_count + 1, ctx->fb_list, ctx->amb1_seed, ctx->fb_seed,
+                               nullptr, nullptr, ctx->st);
         LAUNCHCHK("nn_mfma");
-        HIPCHK(hipMemcpyAsync(ctx->h_amb + 2, ctx->amb_count + 2, sizeof(int) * 2, hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int) * 3, hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
-        const int c1 = ctx->h_amb[2];
+        const int c1 = ctx->h_amb[2], cfb = ctx->h_amb[1];
         ctx->stats.level1_unrecovered += ctx->h_amb[3];
+        ctx->stats.grid_fallback += cfb;
         ctx->level1_queued = c1;
-        if (c1 > 0) {
-            // level 2: direct-form fp32 filter on the uncertified queries only
-            const NNPlan p2l = plan_nn32_list((size_t)c1, ctx->nm_pad);
+        if (cfb > 0) {
+            // level 2: direct-form fp32 filter on what the grid handed back
+            const NNPlan p2l = plan_nn32_list((size_t)cfb, ctx->nm_pad);
             TRY(grow(ctx, (char **)&ctx->part2, &ctx->part2_cap,
-                     (size_t)p2l.splits * c1 * (2 * sizeof(float) + sizeof(int))));
+                     (size_t)p2l.splits * cfb * (2 * sizeof(float) + sizeof(int))));
             float *qb = (float *)ctx->part2;
-            float *qs = qb + (size_t)p2l.splits * c1;
-            int *qi = (int *)(qs + (size_t)p2l.splits * c1);
-            launch_nn_filter(q.f, ctx->amb1, ctx->amb1_seed, c1, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi,
+            float *qs = qb + (size_t)p2l.splits * cfb;
+            int *qi = (int *)(qs + (size_t)p2l.splits * cfb);
+            launch_nn_filter(q.f, ctx->fb_list, ctx->fb_seed, cfb, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi,
                              ctx->st);
             CertParams cp{ctx->rm};
-            launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->amb1, c1, cp, ctx->idx, ctx->amb_count,
-                               ctx->amb_list, ctx->amb_T, ctx->st);
+            launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->fb_list, cfb, cp, ctx->idx, ctx->amb_count,
+                               ctx->amb_list, ctx->amb_T, nullptr, ctx->st);
             // level 3: exact fp64 on the candidates of what is still open
             launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, c1, ctx->idx,
+                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, cfb, ctx->idx,
                               ctx->st);
         }
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
@@ -306,18 +339,26 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         float *ps = pb + (size_t)pl.splits * n;
         int *pi = (int *)(ps + (size_t)pl.splits * n);
         TRY(ensure_queue(ctx, n));
-        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int), ctx->st));
+        TRY(grow(ctx, &ctx->amb_hint, &ctx->amb_hint_cap, n));
+        TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
+        TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
+        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 2, ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
         launch_nn_filter(q.f, nullptr, nullptr, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
         CertParams cp{ctx->rm};
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, nullptr, (int)n, cp, ctx->idx, ctx->amb_count,
-                           ctx->amb_list, ctx->amb_T, ctx->st);
-        launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                           ctx->amb_list, ctx->amb_T, ctx->amb_hint, ctx->st);
+        // near ties: exact through the model grid; what it cannot take, fp64 brute force
+        launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z,
+                               ctx->model.x, ctx->model.y, ctx->model.z, grid_view(ctx), kGridBudget,
+                               ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr, nullptr, ctx->amb_T,
+                               ctx->fb_T, ctx->st);
+        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx,
                           ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
-        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int) * 2, hipMemcpyDeviceToHost, ctx->st));
         LAUNCHCHK("nn_certified");
     }
     return ICP_OK;
@@ -333,6 +374,7 @@ void account_nn(icp_ctx *ctx, size_t n)
     if (ctx->nn_mode == ICP_NN_CERTIFIED && n) {
         ctx->stats.ambiguous += ctx->h_amb[0];
         if (level1_kind(ctx, n)) ctx->stats.level1_queued += ctx->level1_queued;
+        else ctx->stats.grid_fallback += ctx->h_amb[1];
     }
 }
 
@@ -483,7 +525,10 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
-                    (void *)ctx->sums, (void *)ctx->stage})
+                    (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
+                    (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
+                    (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
+                    (void *)ctx->fb_seed, (void *)ctx->fb_T})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -568,6 +613,18 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, (int)nm_pad, ctx->c,
                           ctx->scale16, ctx->mimg16, ctx->mms16, ctx->st);
     LAUNCHCHK("build_mimage16");
+    // uniform grid over the fp64 model for the exact resolver
+    ctx->grid = grid_params(m_xyz, nm);
+    const long long ncell = grid_cells(ctx->grid);
+    TRY(grow(ctx, &ctx->g_cid, &ctx->g_cid_cap, nm));
+    TRY(grow(ctx, &ctx->g_count, &ctx->g_count_cap, (size_t)ncell + 1));
+    TRY(grow(ctx, &ctx->g_start, &ctx->g_start_cap, (size_t)ncell + 1));
+    TRY(grow(ctx, &ctx->g_bsum, &ctx->g_bsum_cap, grid_scan_blocks(ncell + 1)));
+    TRY(grow(ctx, &ctx->g_fill, &ctx->g_fill_cap, (size_t)ncell));
+    TRY(grow(ctx, &ctx->g_pts, &ctx->g_pts_cap, nm));
+    launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_cid, ctx->g_count,
+                      ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->st);
+    LAUNCHCHK("grid_build");
     HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->nm = nm;
     ctx->nm_pad = nm_pad;

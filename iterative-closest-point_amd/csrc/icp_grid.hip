@@ -1,0 +1,257 @@
+// icp_grid.hip — uniform-grid exact resolver for the certified NN search.
+//
+// The brute-force filters (icp_kernels.hip) settle ~92% of queries at C4 with their
+// certificate; the rest are near ties.  For those, each filter also knows a candidate m_h
+// (its winner), and the exact answer (fp64 first minimum of D64, the reference's rule:
+// compute.cu:112-117,137 / cpu.cc:17-22) lies among the model points with D64 <= r2 =
+// D64(q, m_h).  This file finds them through a uniform grid over the model, built once per
+// icp_set_model, instead of re-scanning all M points.
+//
+// Why the box is complete.  cell(x) = clamp(floor((x - lo) * inv_h), 0, g - 1), evaluated
+// in fp64 for the model points when the grid is built and for the box bounds here, is
+// monotone non-decreasing in x (fp subtraction and multiplication by a positive constant
+// are monotone; so are floor and clamp).  Any m with D64(q, m) <= r2 has, per axis,
+// |q_a - m_a| <= sqrt(r2) (1 + 3u) (D64 >= fl(dx^2) >= dx^2 (1 - u), |q - m| <= |dx|/(1 - u),
+// u = 2^-53).  The bounds L = q_a - (R + s), U = q_a + (R + s) with R = fl(sqrt(r2)) and
+// s = (|q_a| + R) 2^-44 therefore satisfy L <= m_a <= U even after their own rounding, so
+// cell(L) <= cell(m_a) <= cell(U): m lies in the scanned box.  Within it the lexicographic
+// (D64, index) minimum is the first minimum.  No geometric assumption about the cloud is
+// made; a box larger than `budget` cells is handed back to the brute-force levels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "icp_kernels.h"
+
+namespace icp {
+namespace {
+
+__device__ __forceinline__ double d64g(double px, double py, double pz, double mx, double my,
+                                       double mz)
+{
+    const double dx = px - mx;
+    const double dy = py - my;
+    const double dz = pz - mz;
+    return (dx * dx + dy * dy) + dz * dz; // cpu.cc:17-19 order, no FMA (-ffp-contract=off)
+}
+
+__device__ __forceinline__ int cell1(double x, double lo, double inv_h, int g)
+{
+    const double t = (x - lo) * inv_h;
+    if (!(t > 0.0)) return 0;
+    if (t >= (double)(g - 1)) return g - 1;
+    return (int)t;
+}
+
+__global__ __launch_bounds__(kBlock) void grid_count_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
+    int nm, GridView gv, int *__restrict__ cid, int *__restrict__ count)
+{
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < nm; i += gridDim.x * kBlock) {
+        const int cx = cell1(mx[i], gv.lo[0], gv.inv_h, gv.g[0]);
+        const int cy = cell1(my[i], gv.lo[1], gv.inv_h, gv.g[1]);
+        const int cz = cell1(mz[i], gv.lo[2], gv.inv_h, gv.g[2]);
+        const int c = (cz * gv.g[1] + cy) * gv.g[0] + cx;
+        cid[i] = c;
+        atomicAdd(count + c, 1);
+    }
+}
+
+// exclusive scan, 4096 ints per block: local scan + block totals
+constexpr int kScanThreads = 1024, kScanPer = 4, kScanChunk = kScanThreads * kScanPer;
+
+__global__ __launch_bounds__(kScanThreads) void scan_local_kernel(const int *__restrict__ in, int n,
+                                                                  int *__restrict__ out,
+                                                                  int *__restrict__ bsum)
+{
+    __shared__ int sh[kScanThreads];
+    const int base = blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+    int v[kScanPer], s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        v[k] = base + k < n ? in[base + k] : 0;
+        s += v[k];
+    }
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < kScanThreads; off <<= 1) { // Hillis-Steele inclusive scan
+        const int t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += t;
+        __syncthreads();
+    }
+    int run = sh[threadIdx.x] - s; // exclusive prefix of this thread within the block
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == kScanThreads - 1) bsum[blockIdx.x] = sh[threadIdx.x];
+}
+
+__global__ void scan_blocks_kernel(int *bsum, int nb) // one thread: nb <= a few thousand
+{
+    int run = 0;
+    for (int b = 0; b < nb; ++b) {
+        const int t = bsum[b];
+        bsum[b] = run;
+        run += t;
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_add_kernel(int *__restrict__ out, int n,
+                                                                const int *__restrict__ bsum)
+{
+    const int add = bsum[blockIdx.x];
+    const int base = blockIdx.x * kScanChunk;
+    for (int k = threadIdx.x; k < kScanChunk && base + k < n; k += kScanThreads) out[base + k] += add;
+}
+
+__global__ __launch_bounds__(kBlock) void grid_scatter_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
+    int nm, const int *__restrict__ cid, const int *__restrict__ start, int *__restrict__ fill,
+    double4 *__restrict__ pts)
+{
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < nm; i += gridDim.x * kBlock) {
+        const int c = cid[i];
+        const int pos = start[c] + atomicAdd(fill + c, 1); // order within a cell is irrelevant
+        pts[pos] = make_double4(mx[i], my[i], mz[i], (double)i);
+    }
+}
+
+// One thread per queued query (grid-stride over *count).
+__global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
+    const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
+    GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
+    const float *__restrict__ seed_in, float *__restrict__ seed_out,
+    const double *__restrict__ T_in, double *__restrict__ T_out)
+{
+    const int count = *count_ptr;
+    for (int t = blockIdx.x * kBlock + threadIdx.x; t < count; t += gridDim.x * kBlock) {
+        const int j = list[t];
+        const int h = hint[t];
+        bool ok = h >= 0;
+        int c0[3] = {0, 0, 0}, c1[3] = {-1, -1, -1};
+        double q[3] = {px[j], py[j], pz[j]};
+        double best = 0.0;
+        int bi = h;
+        if (ok) {
+            best = d64g(q[0], q[1], q[2], mx[h], my[h], mz[h]);
+            const double R = sqrt(best);
+            long long cells = 1;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double s = (fabs(q[a]) + R) * 0x1.0p-44;
+                c0[a] = cell1(q[a] - (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
+                c1[a] = cell1(q[a] + (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
+                cells *= (long long)(c1[a] - c0[a] + 1);
+            }
+            ok = cells <= budget;
+        }
+        if (ok) {
+            for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                    const int row = (cz * gv.g[1] + cy) * gv.g[0];
+                    const int k1 = gv.start[row + c1[0] + 1];
+                    for (int k = gv.start[row + c0[0]]; k < k1; ++k) { // one x-run of cells
+                        const double4 m = gv.pts[k];
+                        const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
+                        const int mi = (int)m.w;
+                        if (d < best || (d == best && mi < bi)) {
+                            best = d;
+                            bi = mi;
+                        }
+                    }
+                }
+            idx[j] = bi;
+        } else {
+            const int slot = atomicAdd(fb_count, 1);
+            fb_list[slot] = j;
+            if (seed_in) seed_out[slot] = seed_in[t];
+            if (T_in) T_out[slot] = T_in[t];
+        }
+    }
+}
+
+} // namespace
+
+GridParams grid_params(const double *m_xyz, size_t nm)
+{
+    GridParams p{};
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t j = 0; j < nm; ++j)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], m_xyz[3 * j + a]);
+            hi[a] = std::max(hi[a], m_xyz[3 * j + a]);
+        }
+    double ext[3], emax = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        ext[a] = hi[a] - lo[a];
+        emax = std::max(emax, ext[a]);
+        p.lo[a] = lo[a];
+    }
+    if (!(emax > 0.0) || !std::isfinite(emax)) { // one point (or all equal): a single cell
+        p.g[0] = p.g[1] = p.g[2] = 1;
+        p.inv_h = 1.0;
+        return p;
+    }
+    // ~2 model points per cell of the bounding box (flat axes count as 1e-3 of the largest)
+    double vol = 1.0;
+    for (int a = 0; a < 3; ++a) vol *= std::max(ext[a], emax * 1e-3);
+    double h = std::cbrt(vol * 2.0 / (double)std::max<size_t>(nm, 1));
+    auto dims = [&](double hh, int g[3]) {
+        long long tot = 1;
+        for (int a = 0; a < 3; ++a) {
+            g[a] = (int)std::min<double>(std::floor(ext[a] / hh) + 1.0, 1 << 12);
+            tot *= g[a];
+        }
+        return tot;
+    };
+    while (dims(h, p.g) > kGridMaxCells) h *= 1.25;
+    p.inv_h = 1.0 / h;
+    return p;
+}
+
+long long grid_cells(const GridParams &p) { return (long long)p.g[0] * p.g[1] * p.g[2]; }
+
+size_t grid_scan_blocks(long long n) { return (size_t)((n + kScanChunk - 1) / kScanChunk); }
+
+void launch_grid_build(const double *mx, const double *my, const double *mz, int nm,
+                       const GridParams &p, int *cid, int *count, int *start, int *bsum, int *fill,
+                       double4 *pts, hipStream_t st)
+{
+    const long long ncell = grid_cells(p);
+    GridView gv{};
+    for (int a = 0; a < 3; ++a) {
+        gv.g[a] = p.g[a];
+        gv.lo[a] = p.lo[a];
+    }
+    gv.inv_h = p.inv_h;
+    const int blocks = std::max(1, std::min((nm + kBlock - 1) / kBlock, 4096));
+    (void)hipMemsetAsync(count, 0, sizeof(int) * (ncell + 1), st);
+    (void)hipMemsetAsync(fill, 0, sizeof(int) * ncell, st);
+    grid_count_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, gv, cid, count);
+    const int n = (int)(ncell + 1);
+    const int nb = (int)grid_scan_blocks(n);
+    scan_local_kernel<<<nb, kScanThreads, 0, st>>>(count, n, start, bsum);
+    scan_blocks_kernel<<<1, 1, 0, st>>>(bsum, nb);
+    scan_add_kernel<<<nb, kScanThreads, 0, st>>>(start, n, bsum);
+    grid_scatter_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, cid, start, fill, pts);
+}
+
+void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
+                            const double *px, const double *py, const double *pz, const double *mx,
+                            const double *my, const double *mz, const GridView &gv, int budget,
+                            int *idx, int *fb_count, int *fb_list, const float *seed_in,
+                            float *seed_out, const double *T_in, double *T_out, hipStream_t st)
+{
+    const int blocks = std::max(1, std::min((max_items + kBlock - 1) / kBlock, 2048));
+    nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, mx, my, mz, gv,
+                                                      budget, idx, fb_count, fb_list, seed_in, seed_out,
+                                                      T_in, T_out);
+}
+
+} // namespace icp

@@ -40,9 +40,11 @@ void launch_nn_filter(const float4 *p32, const int *list, const float *seed, int
                       const float4 *m32, int nm_pad, const NNPlan &plan, float *part_best,
                       float *part_second, int *part_idx, hipStream_t st);
 // merge splits, certify, write idx for certified queries, queue the rest (with window T).
+// amb_hint (nullable): the queued query's fp32 winner, the grid resolver's candidate
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
                         int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
-                        int *idx, int *amb_count, int *amb_list, double *amb_T, hipStream_t st);
+                        int *idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint,
+                        hipStream_t st);
 // MFMA expanded-form filter (G = |m|^2 - 2 p.m) and its certificate; uncertified queries
 // are appended to amb_list (no window: they go through the direct-form filter next).
 constexpr int kMfmaQG = 4; // 16-query groups per wave
@@ -51,8 +53,8 @@ void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, 
                     float *part_best, float *part_second, int *part_idx, hipStream_t st);
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
                              int splits, const float4 *p32, int np, const float *mm, int *idx,
-                             int *amb_count, int *amb_list, float *amb_seed, const float4 *m32,
-                             double rm, hipStream_t st);
+                             int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
+                             const float4 *m32, double rm, hipStream_t st);
 // f16 split-precision MFMA filter (v_mfma_f32_32x32x16_f16): model image (1 KiB per 32
 // points) built once per model; uncertified queries appended to amb_list.
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad);
@@ -64,8 +66,8 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, const double c[3], double scale, const float *mms, int *idx,
-                               int *amb_count, int *amb_list, float *amb_seed, const float4 *p32,
-                               const float4 *m32, double rm, hipStream_t st);
+                               int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
+                               const float4 *p32, const float4 *m32, double rm, hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
@@ -77,6 +79,37 @@ void launch_nn_fp64(const double *px, const double *py, const double *pz, int np
                     const NNPlan &plan, double *part_best, int *part_idx, hipStream_t st);
 void launch_nn_finalize64(const double *part_best, const int *part_idx, int splits, int np,
                           int *idx, hipStream_t st);
+
+// ---- uniform grid over the model: exact resolver of queued queries (icp_grid.hip) ---
+constexpr long long kGridMaxCells = 1LL << 24;
+constexpr int kGridBudget = 1024; // cells per query box; larger boxes go back to brute force
+struct GridParams {
+    int g[3];
+    double lo[3];
+    double inv_h;
+};
+struct GridView {
+    const double4 *pts; // model points sorted by cell: (x, y, z, original index)
+    const int *start;   // ncells + 1 offsets into pts
+    int g[3];
+    double lo[3];
+    double inv_h;
+};
+GridParams grid_params(const double *m_xyz, size_t nm); // host: bounding box, ~2 points/cell
+long long grid_cells(const GridParams &p);
+size_t grid_scan_blocks(long long n);
+// cid[nm], count/start[ncells + 1], bsum[grid_scan_blocks(ncells + 1)], fill[ncells], pts[nm]
+void launch_grid_build(const double *mx, const double *my, const double *mz, int nm,
+                       const GridParams &p, int *cid, int *count, int *start, int *bsum, int *fill,
+                       double4 *pts, hipStream_t st);
+// For queued query list[t] (t < *count_ptr) with candidate hint[t]: exact fp64 first minimum
+// over the grid box that must contain every point at least as close as the candidate ->
+// idx; hint < 0 or a box over `budget` cells -> appended to fb_list (with its seed / T).
+void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
+                            const double *px, const double *py, const double *pz, const double *mx,
+                            const double *my, const double *mz, const GridView &gv, int budget,
+                            int *idx, int *fb_count, int *fb_list, const float *seed_in,
+                            float *seed_out, const double *T_in, double *T_out, hipStream_t st);
 
 // ---- streaming reductions (deterministic two-stage, fp64) --------------------------
 int red_blocks(size_t n);

@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32,
     const int *__restrict__ list, int nslots, double rm, int *__restrict__ idx, int *amb_count,
-    int *amb_list, double *amb_T)
+    int *amb_list, double *amb_T, int *amb_hint)
 {
     const int s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= nslots) return;
@@ -291,6 +291,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
         const int slot = atomicAdd(amb_count, 1);
         amb_list[slot] = j;
         amb_T[slot] = T;
+        if (amb_hint) amb_hint[slot] = id;
     }
 }
 
@@ -641,8 +642,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int np, double cx, double cy,
     double cz, double scale, const float *__restrict__ mms, int *__restrict__ idx, int *amb_count,
-    int *amb_list, float *amb_seed, const float4 *__restrict__ p32, const float4 *__restrict__ m32,
-    double rm)
+    int *amb_list, float *amb_seed, int *amb_hint, const float4 *__restrict__ p32,
+    const float4 *__restrict__ m32, double rm)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -672,6 +673,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         const int slot = atomicAdd(amb_count, 1);
         amb_list[slot] = j;
         amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
+        amb_hint[slot] = id;                                  // the grid resolver's candidate
         if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
     const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list,
-    float *amb_seed, const float4 *__restrict__ m32, double rm)
+    float *amb_seed, int *amb_hint, const float4 *__restrict__ m32, double rm)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -746,6 +748,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
         const int slot = atomicAdd(amb_count, 1);
         amb_list[slot] = j;
         amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
+        amb_hint[slot] = id;                                  // the grid resolver's candidate
         if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
@@ -1163,17 +1166,18 @@ void launch_nn_filter(const float4 *p32, const int *list, const float *seed, int
 
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
                         int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
-                        int *idx, int *amb_count, int *amb_list, double *amb_T, hipStream_t st)
+                        int *idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint,
+                        hipStream_t st)
 {
     const int grid = (nslots + kBlock - 1) / kBlock;
     if (list)
         nn_finalize_kernel<true><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32,
                                                           list, nslots, cp.rm, idx, amb_count,
-                                                          amb_list, amb_T);
+                                                          amb_list, amb_T, amb_hint);
     else
         nn_finalize_kernel<false><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits,
                                                            p32, nullptr, nslots, cp.rm, idx,
-                                                           amb_count, amb_list, amb_T);
+                                                           amb_count, amb_list, amb_T, amb_hint);
 }
 
 NNPlan plan_nn_mfma(size_t np, size_t nm_pad)
@@ -1247,22 +1251,22 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, const double c[3], double scale, const float *mms, int *idx,
-                               int *amb_count, int *amb_list, float *amb_seed, const float4 *p32,
-                               const float4 *m32, double rm, hipStream_t st)
+                               int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
+                               const float4 *p32, const float4 *m32, double rm, hipStream_t st)
 {
     nn_finalize_mfma16_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
         part_best, part_second, part_idx, splits, px, py, pz, np, c[0], c[1], c[2], scale, mms, idx,
-        amb_count, amb_list, amb_seed, p32, m32, rm);
+        amb_count, amb_list, amb_seed, amb_hint, p32, m32, rm);
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
                              int splits, const float4 *p32, int np, const float *mm, int *idx,
-                             int *amb_count, int *amb_list, float *amb_seed, const float4 *m32,
-                             double rm, hipStream_t st)
+                             int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
+                             const float4 *m32, double rm, hipStream_t st)
 {
     nn_finalize_mfma_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list, amb_seed, m32,
-        rm);
+        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list, amb_seed,
+        amb_hint, m32, rm);
 }
 
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,

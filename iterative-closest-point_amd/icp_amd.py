@@ -71,7 +71,8 @@ class Result(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("nn_ms", C.c_double), ("nn_launches", C.c_longlong), ("nn_pairs", C.c_longlong),
-                ("ambiguous", C.c_longlong), ("level1_queued", C.c_longlong), ("level1_unrecovered", C.c_longlong), ("iter_ms", C.c_double), ("iterations", C.c_longlong)]
+                ("ambiguous", C.c_longlong), ("level1_queued", C.c_longlong), ("level1_unrecovered", C.c_longlong), ("iter_ms", C.c_double), ("iterations", C.c_longlong),
+                ("grid_fallback", C.c_longlong)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)

@@ -1,0 +1,98 @@
+"""The grid resolver (icp_grid.hip): exact fp64 first-minimum for the certificate's near ties.
+
+Every certified variant hands its uncertified queries, with its fp32 winner as candidate, to
+the uniform-grid resolver; boxes over the cell budget go back to the brute-force levels.
+Indices must equal the oracle's (src/cpu.cc rule on squared fp64 distances, lowest index on
+ties) bit for bit, whatever the shape of the model's bounding box.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RNG = np.random.default_rng(2024)
+CERTIFIED = {"valu": 1, "mfma": 2, "mfma16": 3}
+
+
+@pytest.fixture(scope="module")
+def amd(icp_lib):
+    if icp_lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    return icp_lib
+
+
+def search(amd, variant, m, p):
+    with amd.Context(0, amd.NN_CERTIFIED) as ctx:
+        ctx.set_nn_variant(CERTIFIED[variant])
+        ctx.set_model(m)
+        ctx.reset_stats()
+        _, idx = ctx.closest_matrix(p)
+        return idx, ctx.stats()
+
+
+def integer_lattice(n):
+    g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij"), -1)
+    return g.reshape(-1, 3).astype(np.float64)
+
+
+@pytest.mark.parametrize("variant", list(CERTIFIED))
+def test_grid_flat_model(amd, oracle, variant):
+    # all model points in the plane z = 0.25 (flat bounding box) on a half-integer lattice:
+    # many exactly equidistant candidates
+    xy = RNG.integers(0, 80, size=(6000, 2)) * 0.5
+    m = np.column_stack([xy, np.full(len(xy), 0.25)])
+    p = np.column_stack([RNG.integers(0, 160, size=(3000, 2)) * 0.25, RNG.uniform(-1, 1, 3000)])
+    idx, _ = search(amd, variant, m, p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+
+
+@pytest.mark.parametrize("variant", list(CERTIFIED))
+def test_grid_line_and_identical_points(amd, oracle, variant):
+    t = RNG.integers(0, 400, size=5000) * 0.125
+    m = np.column_stack([t, 2.0 * t, -t])              # a line: two degenerate axes
+    p = np.column_stack([t[:2000] + 0.0625, 2.0 * t[:2000], -t[:2000]]) + RNG.normal(scale=1e-3, size=(2000, 3))
+    idx, _ = search(amd, variant, m, p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+    same = np.tile([[1.5, -2.0, 3.0]], (777, 1))       # one point repeated: index 0 always
+    idx, _ = search(amd, variant, same, RNG.normal(size=(300, 3)))
+    assert (idx == 0).all()
+
+
+@pytest.mark.parametrize("variant", list(CERTIFIED))
+def test_grid_clustered_model(amd, oracle, variant):
+    # two dense clusters 1e3 apart plus sparse outliers: most cells empty, a few crowded
+    a = RNG.normal(scale=0.01, size=(20000, 3))
+    b = RNG.normal(scale=0.01, size=(20000, 3)) + 1000.0
+    o = RNG.uniform(-50, 1050, size=(200, 3))
+    m = np.round(np.concatenate([a, b, o]) * 4096) / 4096   # coarse values: many ties
+    p = np.round(np.concatenate([a[:3000] + 0.003, b[:3000] - 0.002, o[:100] + 1.0]) * 4096) / 4096
+    idx, _ = search(amd, variant, m, p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+
+
+@pytest.mark.parametrize("variant", list(CERTIFIED))
+def test_grid_ties_over_budget_fall_back_to_brute_force(amd, oracle, variant):
+    # hollow 60^3 lattice cube (faces only) and queries near its centre, tied between points
+    # of several faces: the candidate ball spans the whole grid (> budget cells), so these
+    # queries go back to the brute-force levels; queries near the faces stay in the grid
+    g = integer_lattice(60)
+    m = g[(g == 0).any(1) | (g == 59).any(1)]
+    k = 48
+    centre = np.column_stack([np.full(k, 29.5), np.full(k, 29.5), 29.5 + RNG.integers(-3, 4, k)])
+    near = np.column_stack([np.full(k, 0.5), RNG.integers(1, 58, k) + 0.5, RNG.integers(1, 58, k) + 0.5])
+    p = np.concatenate([centre, near])
+    idx, st = search(amd, variant, m, p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+    assert st["grid_fallback"] > 0, st
+
+
+def test_grid_takes_the_near_ties_at_c4(amd):
+    # at the bench configuration the grid must settle (almost) all level-1 leftovers
+    m, p = amd.synthetic_pair(1 << 18, seed=7)
+    idx, st = search(amd, "mfma16", m, p)
+    assert st["level1_queued"] > 0, st
+    assert st["grid_fallback"] <= max(16, st["level1_queued"] // 1000), st
