@@ -82,6 +82,9 @@ struct icp_ctx {
     int *g_cid = nullptr, *g_count = nullptr, *g_start = nullptr, *g_bsum = nullptr, *g_fill = nullptr;
     double4 *g_pts = nullptr;
     size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
+    unsigned *seed16 = nullptr; // seeded f16 filter: per-query shift (icp_run iterations >= 2)
+    size_t seed16_cap = 0;
+    bool seeds_valid = false;   // idx holds the previous search over the resident scene
     int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
     int *fb_list = nullptr;                           // queries the grid hands back
     float *fb_seed = nullptr;
@@ -249,7 +252,8 @@ GridView grid_view(const icp_ctx *ctx)
 
 // NN search of the n queries in q against the resident model -> ctx->idx[0..n).
 // Timed with HIP events on the context stream (ev[0]..ev[1] = the O(N*M) kernel).
-int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
+// seeded: ctx->idx holds a previous correspondence of each of these n queries (icp_run)
+int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     if (!n) return ICP_OK;
@@ -268,7 +272,14 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         LAUNCHCHK("nn_fp64");
     } else if (const int l1 = level1_kind(ctx, n)) {
         // level 1: MFMA expanded-form filter over every query
-        const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad) : plan_nn_mfma(n, ctx->nm_pad);
+        const bool sd = seeded && l1 == 2;
+        const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd) : plan_nn_mfma(n, ctx->nm_pad);
+        if (sd) {
+            TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
+            launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, ctx->c,
+                               ctx->scale16, ctx->seed16, ctx->st);
+        }
+        const unsigned *seeds = sd ? ctx->seed16 : nullptr;
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap,
                  (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int))));
         float *pb = (float *)ctx->part;
@@ -285,14 +296,14 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
         HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
         HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
         if (l1 == 2)
-            launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, ctx->mimg16, (int)ctx->nm_pad, pl,
-                             pb, ps, pi, ctx->st);
+            launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, seeds, ctx->mimg16, (int)ctx->nm_pad,
+                             pl, pb, ps, pi, ctx->st);
         else
             launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
         if (l1 == 2)
-            launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16,
-                                      ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed,
+            launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
+                                      ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed,
                                       ctx->amb1_hint, q.f, ctx->m32, ctx->rm, ctx->st);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
@@ -528,7 +539,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
-                    (void *)ctx->fb_seed, (void *)ctx->fb_T})
+                    (void *)ctx->fb_seed, (void *)ctx->fb_T, (void *)ctx->seed16})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -629,6 +640,7 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     ctx->nm = nm;
     ctx->nm_pad = nm_pad;
     ctx->has_model = true;
+    ctx->seeds_valid = false;
     // the scene's fp32 copy depends on c: refresh it
     if (ctx->has_scene && ctx->scene.n) {
         launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1],
@@ -650,6 +662,7 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->np_total = np_total;
     ctx->has_scene = true;
+    ctx->seeds_valid = false;
     return ICP_OK;
 }
 
@@ -678,7 +691,8 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     r.R[0] = r.R[4] = r.R[8] = 1.0;
     for (int it = 0; it < max_iter; ++it) {
         // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
-        TRY(nn_search(ctx, P, n));
+        TRY(nn_search(ctx, P, n, ctx->seeds_valid));
+        ctx->seeds_valid = true; // idx now pairs every point of the resident scene
         // 2. centroids (gpu.cc:98-99): sum p, sum y   [+ RCCL all-reduce, 6 doubles]
         const int nb = red_blocks(n);
         launch_gather_moments(ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, P.x, P.y, P.z,
@@ -744,6 +758,7 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
     TRY(check_ready(ctx, false));
     if (!p_xyz && np) return ICP_E_ARG;
     TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
+    ctx->seeds_valid = false; // idx is about to hold other queries' correspondences
     TRY(nn_search(ctx, ctx->qa, np));
     if (np && y_xyz_out) {
         TRY(grow_cloud(ctx, ctx->qb, np, false));

@@ -57,17 +57,22 @@ void launch_nn_finalize_mfma(const float *part_best, const float *part_second, c
                              const float4 *m32, double rm, hipStream_t st);
 // f16 split-precision MFMA filter (v_mfma_f32_32x32x16_f16): model image (1 KiB per 32
 // points) built once per model; uncertified queries appended to amb_list.
-NNPlan plan_nn_mfma16(size_t np, size_t nm_pad);
+NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded);
+// seeds of the seeded filter from the previous correspondences (packed f16 of -s0 / 2^14)
+void launch_mfma16_seed(const double *px, const double *py, const double *pz, int np, const int *prev,
+                        const double *mx, const double *my, const double *mz, const double c[3], double scale,
+                        unsigned *seed16, hipStream_t st);
 void launch_build_mimage16(const double *mx, const double *my, const double *mz, int nm, int nm_pad,
                            const double c[3], double scale, void *img, float *mms, hipStream_t st);
+// seed16 == nullptr: unseeded filter
 void launch_nn_mfma16(const double *px, const double *py, const double *pz, int np, const double c[3],
-                      double scale, const void *img, int nm_pad, const NNPlan &plan, float *part_best,
-                      float *part_second, int *part_idx, hipStream_t st);
+                      double scale, const unsigned *seed16, const void *img, int nm_pad, const NNPlan &plan,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st);
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
-                               int np, const double c[3], double scale, const float *mms, int *idx,
-                               int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
-                               const float4 *p32, const float4 *m32, double rm, hipStream_t st);
+                               int np, int nm, const double c[3], double scale, const unsigned *seed16,
+                               const float *mms, int *idx, int *amb_count, int *amb_list, float *amb_seed,
+                               int *amb_hint, const float4 *p32, const float4 *m32, double rm, hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,

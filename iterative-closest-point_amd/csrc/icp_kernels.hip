@@ -426,8 +426,9 @@ __device__ __forceinline__ void split_f16(double x, _Float16 &hi, _Float16 &lo)
     lo = (_Float16)(x - (double)hi);
 }
 
-// query-side operand of lane half h for the (clamped) scaled query a
-__device__ __forceinline__ half8_t query_frag(const double a[3], int h)
+// query-side operand of lane half h for the (clamped) scaled query a; `seed` = packed f16
+// (hi | lo << 16) of -s0 / 2^14 for the seeded filter (slots 14, 15; model side = 2^14), else 0
+__device__ __forceinline__ half8_t query_frag(const double a[3], int h, unsigned seed)
 {
     _Float16 xh, xl, yh, yl, zh, zl;
     split_f16(a[0], xh, xl);
@@ -440,9 +441,19 @@ __device__ __forceinline__ half8_t query_frag(const double a[3], int h)
         b[4] = m2 * yh; b[5] = m2 * yl; b[6] = m2 * zh; b[7] = m2 * zh;
     } else {
         b[0] = m2 * zl; b[1] = (_Float16)4096.0f; b[2] = (_Float16)4096.0f; b[3] = m2 * xl;
-        b[4] = m2 * yl; b[5] = m2 * zl; b[6] = (_Float16)0.0f; b[7] = (_Float16)0.0f;
+        b[4] = m2 * yl; b[5] = m2 * zl;
+        b[6] = __builtin_bit_cast(_Float16, (unsigned short)(seed & 0xffffu));
+        b[7] = __builtin_bit_cast(_Float16, (unsigned short)(seed >> 16));
     }
     return b;
+}
+
+// s0' = the shift the seeded filter applies (exact in fp64): -(hi + lo) * 2^14 of the operand
+__device__ __forceinline__ double seed_shift(unsigned seed)
+{
+    const double hi = (double)__builtin_bit_cast(_Float16, (unsigned short)(seed & 0xffffu));
+    const double lo = (double)__builtin_bit_cast(_Float16, (unsigned short)(seed >> 16));
+    return -(hi + lo) * 16384.0;
 }
 
 constexpr double kF16QueryClamp = 32000.0;
@@ -452,15 +463,33 @@ constexpr int kVmcnt0 = 0x0F70;                   // vmcnt(0)
 constexpr int kVmcntDma = 0x0F70 | (512 / 32 / 4); // vmcnt(4): one tile's DMA may stay in flight
 constexpr int kLgkmcnt0 = 0xC07F;                 // lgkmcnt(0) // |a_s| beyond this: operand clamped, not certified
 
-template <int QG, int NS>
-__global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
-    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
-    int np, double cx, double cy, double cz, double scale, const half8_t *__restrict__ mimg,
-    int nm_pad, int chunk, float *__restrict__ part_best, float *__restrict__ part_second,
-    int *__restrict__ part_idx)
+// min over the 16 result registers of one MFMA (v_min3 tree, no canonicalisation)
+__device__ __forceinline__ float min16v(const f32x16_t &d)
 {
-    // NS independent (best, second, block) trackers per query group, each over 16/NS of
-    // the 16 result registers: shorter min/med3 dependency chains, merged at the end.
+    const float a = fminf(fminf(d[0], d[1]), d[2]), b = fminf(fminf(d[3], d[4]), d[5]);
+    const float c = fminf(fminf(d[6], d[7]), d[8]), e = fminf(fminf(d[9], d[10]), d[11]);
+    const float f = fminf(fminf(d[12], d[13]), d[14]);
+    return fminf(fminf(fminf(a, b), c), fminf(fminf(e, f), d[15]));
+}
+
+// Unseeded (SEEDED = false): values G^ = |b_s|^2 - 2 a_s.b_s; each lane tracks (best, second)
+// per query group from +inf and a block is examined in full only if its minimum is below
+// `second` (d >= second changes neither).
+// Seeded (SEEDED = true, ICP iterations after the first): the query operand also carries
+// -s0 in slots 14/15 (model side 2^14), s0 = an fp64 upper bound of the query's G just above
+// its previous correspondence's, so the MFMA returns D^ = G^ - s0' and every query's
+// interesting values are < 0.  best / second start at 0 ("nothing below s0'") and the skip
+// test is ONE v_min3 tree over all QG x 16 values against max_q second[q] (<= 0): ~8 VALU per
+// MFMA, and the update path runs only for the few points just around each query's minimum.
+// (A barrier-free variant in which every wave streams the image into registers itself ran
+// 5% slower at C4; the 4 waves of a workgroup share each 512-point LDS tile instead.)
+template <int QG, bool SEEDED>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void nn_mfma16_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
+    const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
+    float *__restrict__ part_second, int *__restrict__ part_idx)
+{
     // two 512-point tiles (16 KiB each): the next tile streams in by LDS-DMA
     // (global_load_lds_dwordx4, one 1-KiB block per wave-instruction) while this one is used
     __shared__ half8_t tiles[2][kTile16 * 2];
@@ -470,30 +499,30 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
     const int m0 = split * chunk;
     const int m1 = min(m0 + chunk, nm_pad);
     const int qbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
-    constexpr int RPS = 16 / NS; // result registers per tracker
     constexpr int kBlocksPerTile = kTile16 / 32;            // 16
     constexpr int kDmaPerWave = kBlocksPerTile / 4;         // 4 wave-instructions per tile
+    constexpr float kStart = SEEDED ? 0.0f : INFINITY;
 
     half8_t bq[QG];
-    float best[QG][NS], second[QG][NS];
-    int bblk[QG][NS];
+    float best[QG], second[QG];
+    int bblk[QG];
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
         const int j = qbase + q * 32;
         double a[3] = {0.0, 0.0, 0.0};
+        unsigned sd = 0u;
         if (j < np) {
             a[0] = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
             a[1] = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
             a[2] = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+            if (SEEDED) sd = seed16[j];
         }
-        bq[q] = query_frag(a, h);
-#pragma unroll
-        for (int t = 0; t < NS; ++t) {
-            best[q][t] = INFINITY;
-            second[q][t] = INFINITY;
-            bblk[q][t] = m0 >> 5;
-        }
+        bq[q] = query_frag(a, h, sd);
+        best[q] = kStart;
+        second[q] = kStart;
+        bblk[q] = m0 >> 5;
     }
+    float s_max = kStart; // SEEDED: max_q second[q]
     const f32x16_t zero = {};
 
     auto issue_tile = [&](int tpt, int buf) { // wave w fetches blocks w, w+4, w+8, w+12
@@ -505,6 +534,43 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
                                              16, 0, 0);
         }
     };
+    auto update = [&](const f32x16_t (&d)[QG], int blk_id) {
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            if (!__any(min16v(d[q]) < second[q])) continue;
+            const float prev = best[q];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d[q][r]);
+                best[q] = min_nocanon(best[q], d[q][r]);
+            }
+            bblk[q] = best[q] < prev ? blk_id : bblk[q];
+        }
+        if (SEEDED) {
+            s_max = second[0];
+#pragma unroll
+            for (int q = 1; q < QG; ++q) s_max = fmaxf(s_max, second[q]);
+        }
+    };
+    auto process = [&](const half8_t &a8, int blk_id) {
+        // all QG MFMAs first (independent), then their minima, then ONE wave-uniform branch
+        f32x16_t d[QG];
+#pragma unroll
+        for (int q = 0; q < QG; ++q) d[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+        bool need;
+        if (SEEDED) {
+            float m = min16v(d[0]);
+#pragma unroll
+            for (int q = 1; q < QG; ++q) m = fminf(m, min16v(d[q]));
+            need = m < s_max;
+        } else {
+            need = false;
+#pragma unroll
+            for (int q = 0; q < QG; ++q) need |= min16v(d[q]) < second[q];
+        }
+        if (__any(need)) update(d, blk_id);
+    };
+
     issue_tile(m0, 0);
     int it = 0;
     for (int t0 = m0; t0 < m1; t0 += kTile16, ++it) {
@@ -517,45 +583,14 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
         }
         __builtin_amdgcn_s_barrier(); // ... and every other wave's
         const half8_t *tile = tiles[cur];
-        half8_t a_next = tile[lane];
-        for (int b = 0; b < kBlocksPerTile; ++b) {
-            const half8_t a8 = a_next;
-            if (b + 1 < kBlocksPerTile) a_next = tile[(b + 1) * 64 + lane]; // LDS prefetch
-            // all QG MFMAs first (independent), then their minima, then ONE wave-uniform
-            // branch: a branch per MFMA would serialise MFMA -> result -> branch -> MFMA.
-            f32x16_t d[QG];
-#pragma unroll
-            for (int q = 0; q < QG; ++q) d[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
-            // A block can change (best, second) only if its minimum is < second
-            // (d >= second  =>  med3(best, second, d) = second and min(best, d) = best): the
-            // 32-op update runs only when some lane needs it, which after the running
-            // minima settle is a few percent of blocks.
-            bool need[QG];
-            bool any_need = false;
-#pragma unroll
-            for (int q = 0; q < QG; ++q) {
-                float s_min = second[q][0];
-#pragma unroll
-                for (int t = 1; t < NS; ++t) s_min = fmaxf(s_min, second[q][t]);
-                need[q] = min16_nocanon(d[q]) < s_min;
-                any_need |= need[q];
-            }
-            if (__any(any_need)) {
-#pragma unroll
-                for (int q = 0; q < QG; ++q) {
-                    if (!__any(need[q])) continue;
-#pragma unroll
-                    for (int t = 0; t < NS; ++t) {
-                        const float prev = best[q][t];
-#pragma unroll
-                        for (int r = t * RPS; r < (t + 1) * RPS; ++r) {
-                            second[q][t] = __builtin_amdgcn_fmed3f(best[q][t], second[q][t], d[q][r]);
-                            best[q][t] = min_nocanon(best[q][t], d[q][r]);
-                        }
-                        bblk[q][t] = best[q][t] < prev ? ((t0 >> 5) + b) : bblk[q][t];
-                    }
-                }
-            }
+        const int blk0 = t0 >> 5;
+        // two blocks per step with ping-pong operand registers (no copies)
+        half8_t a0 = tile[lane], a1;
+        for (int b = 0; b < kBlocksPerTile; b += 2) {
+            a1 = tile[(b + 1) * 64 + lane];
+            process(a0, blk0 + b);
+            if (b + 2 < kBlocksPerTile) a0 = tile[(b + 2) * 64 + lane];
+            process(a1, blk0 + b + 1);
         }
         // every wave is done reading `cur` before the next iteration's DMA overwrites it
         __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
@@ -564,25 +599,13 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
 
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
-        // merge the NS trackers of this lane (ties: keep the lower tracker; a tie makes
-        // second == best, i.e. uncertified, so which block is kept does not matter)
-        float b = best[q][0], s2 = second[q][0];
-        int blk = bblk[q][0];
-#pragma unroll
-        for (int t = 1; t < NS; ++t) {
-            if (best[q][t] < b) {
-                s2 = fminf(b, second[q][t]);
-                b = best[q][t];
-                blk = bblk[q][t];
-            } else {
-                s2 = fminf(s2, best[q][t]);
-                if (best[q][t] == b) blk = min(blk, bblk[q][t]);
-            }
-        }
+        const float b = best[q];
+        const float s2 = second[q];
+        const int blk = bblk[q];
         // Index recovery: re-run the MFMA on every distinct winning block of the wave (the
         // MFMA is deterministic: same operands -> same bits); lowest row with d == best.
         int found = -1;
-        bool done = false;
+        bool done = !(b < kStart); // seeded and nothing below s0': no candidate
         for (int guard = 0; guard < 64; ++guard) {
             const unsigned long long pend = __ballot(!done);
             if (pend == 0ull) break;
@@ -599,27 +622,233 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
                 done = true;
             }
         }
+        float bb = b, ss = s2;
         int id = found;
         {
-            const float ob = __shfl_xor(b, 32, 64), os = __shfl_xor(s2, 32, 64);
+            const float ob = __shfl_xor(bb, 32, 64), os = __shfl_xor(ss, 32, 64);
             const int oi = __shfl_xor(id, 32, 64);
-            if (ob < b) {
-                s2 = fminf(b, os);
-                b = ob;
+            if (ob < bb) {
+                ss = fminf(bb, os);
+                bb = ob;
                 id = oi;
             } else {
-                s2 = fminf(s2, ob);
-                if (ob == b && oi >= 0 && (id < 0 || oi < id)) id = oi;
+                ss = fminf(ss, ob);
+                if (ob == bb && oi >= 0 && (id < 0 || oi < id)) id = oi;
             }
         }
         const int j = qbase + q * 32;
         if (h == 0 && j < np) {
             const size_t o = (size_t)split * np + j;
-            part_best[o] = b;
-            part_second[o] = s2;
+            part_best[o] = bb;
+            part_second[o] = ss;
             part_idx[o] = id;
         }
     }
+}
+
+// Software-pipelined f16 filter (QG = 4 query groups per wave, LDS tiles as above): the next
+// block's first MFMA is issued before the current block's last min tree and branch, so each
+// MFMA is followed by the 8-op tree of the result issued one step earlier (ready by then) and
+// the per-block branch never waits on a result in flight.  d0 alternates between two register
+// sets (loop unrolled by 2 blocks); the per-group minima t_q are reused by the update.
+// Same values, same tracking, same outputs as nn_mfma16_kernel<4, SEEDED, false>.
+template <bool SEEDED>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_mfma16p_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
+    const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
+    float *__restrict__ part_second, int *__restrict__ part_idx)
+{
+    constexpr int QG = 4;
+    __shared__ half8_t tiles[2][kTile16 * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm_pad);
+    const int qbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
+    constexpr int kBlocksPerTile = kTile16 / 32;
+    constexpr int kDmaPerWave = kBlocksPerTile / 4;
+    constexpr float kStart = SEEDED ? 0.0f : INFINITY;
+
+    half8_t bq[QG];
+    float best[QG], second[QG];
+    int bblk[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int j = qbase + q * 32;
+        double a[3] = {0.0, 0.0, 0.0};
+        unsigned sd = 0u;
+        if (j < np) {
+            a[0] = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[1] = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[2] = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+            if (SEEDED) sd = seed16[j];
+        }
+        bq[q] = query_frag(a, h, sd);
+        best[q] = kStart;
+        second[q] = kStart;
+        bblk[q] = m0 >> 5;
+    }
+    float s_max = kStart;
+    const f32x16_t zero = {};
+
+    auto issue_tile = [&](int tpt, int buf) {
+#pragma unroll
+        for (int i = 0; i < kDmaPerWave; ++i) {
+            const int blk = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((const void *)(mimg + ((size_t)(tpt >> 5) + blk) * 64 + lane),
+                                             (__attribute__((address_space(3))) void *)&tiles[buf][blk * 64],
+                                             16, 0, 0);
+        }
+    };
+    auto upd1 = [&](int q, const f32x16_t &d, int blk_id) {
+        const float prev = best[q];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d[r]);
+            best[q] = min_nocanon(best[q], d[r]);
+        }
+        bblk[q] = best[q] < prev ? blk_id : bblk[q];
+    };
+    // one block: d0 holds its q0 result (issued one step earlier); issues the next block's
+    // q0 MFMA into dn
+    auto step = [&](const half8_t &a8, const half8_t &an, f32x16_t &d0, f32x16_t &dn, int blk_id) {
+        const f32x16_t d1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[1], zero, 0, 0, 0);
+        const float t0 = min16v(d0);
+        const f32x16_t d2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[2], zero, 0, 0, 0);
+        const float t1 = min16v(d1);
+        const f32x16_t d3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[3], zero, 0, 0, 0);
+        const float t2 = min16v(d2);
+        dn = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bq[0], zero, 0, 0, 0);
+        const float t3 = min16v(d3);
+        bool need;
+        if (SEEDED) {
+            need = fminf(fminf(t0, t1), fminf(t2, t3)) < s_max;
+        } else {
+            need = (t0 < second[0]) | (t1 < second[1]) | (t2 < second[2]) | (t3 < second[3]);
+        }
+        // issue order: MFMA d1 | tree d0 | MFMA d2 | tree d1 | MFMA d3 | tree d2 | MFMA dn | tree d3
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (__any(need)) {
+            if (__any(t0 < second[0])) upd1(0, d0, blk_id);
+            if (__any(t1 < second[1])) upd1(1, d1, blk_id);
+            if (__any(t2 < second[2])) upd1(2, d2, blk_id);
+            if (__any(t3 < second[3])) upd1(3, d3, blk_id);
+            if (SEEDED) s_max = fmaxf(fmaxf(second[0], second[1]), fmaxf(second[2], second[3]));
+        }
+    };
+
+    issue_tile(m0, 0);
+    int it = 0;
+    for (int t0 = m0; t0 < m1; t0 += kTile16, ++it) {
+        const int cur = it & 1;
+        if (t0 + kTile16 < m1) {
+            issue_tile(t0 + kTile16, cur ^ 1);
+            __builtin_amdgcn_s_waitcnt(kVmcntDma);
+        } else {
+            __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        }
+        __builtin_amdgcn_s_barrier();
+        const half8_t *tile = tiles[cur];
+        const int blk0 = t0 >> 5;
+        half8_t a0 = tile[lane], a1 = tile[64 + lane];
+        f32x16_t dA = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[0], zero, 0, 0, 0), dB;
+        for (int b = 0; b < kBlocksPerTile; b += 2) {
+            // block b (q0 in dA) issues block b+1's q0 into dB; block b+1 issues b+2's into dA
+            step(a0, a1, dA, dB, blk0 + b);
+            a0 = tile[min(b + 2, kBlocksPerTile - 1) * 64 + lane]; // last step: a dummy, dropped
+            step(a1, a0, dB, dA, blk0 + b + 1);
+            a1 = tile[min(b + 3, kBlocksPerTile - 1) * 64 + lane];
+        }
+        __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+        __builtin_amdgcn_s_barrier();
+    }
+
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const float b = best[q];
+        const float s2 = second[q];
+        const int blk = bblk[q];
+        int found = -1;
+        bool done = !(b < kStart);
+        for (int guard = 0; guard < 64; ++guard) {
+            const unsigned long long pend = __ballot(!done);
+            if (pend == 0ull) break;
+            const int lead = __ffsll((long long)pend) - 1;
+            const int rb = __shfl(blk, lead, 64);
+            const half8_t a8 = mimg[(size_t)rb * 64 + lane];
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+            if (!done && blk == rb) {
+#pragma unroll
+                for (int r = 15; r >= 0; --r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    found = (d[r] == b) ? rb * 32 + row : found;
+                }
+                done = true;
+            }
+        }
+        float bb = b, ss = s2;
+        int id = found;
+        {
+            const float ob = __shfl_xor(bb, 32, 64), os = __shfl_xor(ss, 32, 64);
+            const int oi = __shfl_xor(id, 32, 64);
+            if (ob < bb) {
+                ss = fminf(bb, os);
+                bb = ob;
+                id = oi;
+            } else {
+                ss = fminf(ss, ob);
+                if (ob == bb && oi >= 0 && (id < 0 || oi < id)) id = oi;
+            }
+        }
+        const int j = qbase + q * 32;
+        if (h == 0 && j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = bb;
+            part_second[o] = ss;
+            part_idx[o] = id;
+        }
+    }
+}
+
+// Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
+// s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see
+// nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
+__global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, const int *__restrict__ prev, const double *__restrict__ mx, const double *__restrict__ my,
+    const double *__restrict__ mz, double cx, double cy, double cz, double scale,
+    unsigned *__restrict__ seed16)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    const int k = prev[j];
+    const double a0 = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double a1 = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double a2 = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double b0 = (mx[k] - cx) * scale, b1 = (my[k] - cy) * scale, b2 = (mz[k] - cz) * scale;
+    const double bb = b0 * b0 + b1 * b1 + b2 * b2;
+    const double G = bb - 2.0 * (a0 * b0 + a1 * b1 + a2 * b2);
+    const double u = 0x1.0p-24;
+    const double A = sqrt(a0 * a0 + a1 * a1 + a2 * a2), R = sqrt(bb);
+    const double span = R * R + 2.0 * A * R;
+    const double ds = 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * (fabs(G) + 1e-3 * span) +
+                      4.0 * u * (A + R) + 1e-3;
+    double s0 = G + 4.0 * ds + 1.0;
+    s0 += fabs(s0) * 0x1.0p-20;
+    const double x = fmin(fmax(-s0 / 16384.0, -65000.0), 65000.0);
+    const _Float16 hi = (_Float16)x;
+    const _Float16 lo = (_Float16)(x - (double)hi);
+    seed16[j] = (unsigned)__builtin_bit_cast(unsigned short, hi) |
+                ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
 }
 
 // Certificate of the f16 filter, in scaled units (a_s, b_s), u = 2^-24, A = |a_s|:
@@ -637,19 +866,27 @@ __global__ __launch_bounds__(kBlock) void nn_mfma16_kernel(
 // 1e-3 covers the absolute terms (1.3e-4).  Then as for the f32 filter:
 //   Db = b + delta(Rb) + A^2 (1+4u),  Rc = A (1+2u) + sqrt(Db (1+2^-40)),
 //   T = b + delta(Rb) + delta(Rc) + 2^-48 Db;  second > T => unique candidate.
+// Seeded filter: it returns D^ = computed (G - s0') with best/second capped at 0; in G terms
+// b = b_D + s0', second >= s2_D + s0' (values never tracked are >= s0').  Two more exact
+// products (the shift) enter the accumulation: (16 + 3 + 4) u sum|p| with sum|p| including
+// |s0'|, so delta_s(R) = 28u R^2 + 64u A R + 24u |s0'| + 4u (A + R) + 1e-3.  Any s0' keeps
+// the test sound; a poor one only queues the query.
+template <bool SEEDED>
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
-    const double *__restrict__ py, const double *__restrict__ pz, int np, double cx, double cy,
-    double cz, double scale, const float *__restrict__ mms, int *__restrict__ idx, int *amb_count,
-    int *amb_list, float *amb_seed, int *amb_hint, const float4 *__restrict__ p32,
-    const float4 *__restrict__ m32, double rm)
+    const double *__restrict__ py, const double *__restrict__ pz, int np, int nm, double cx,
+    double cy, double cz, double scale, const unsigned *__restrict__ seed16,
+    const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list,
+    float *amb_seed, int *amb_hint, const float4 *__restrict__ p32, const float4 *__restrict__ m32,
+    double rm)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
     float b, s2;
     int id;
     merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
     const double ax = (px[j] - cx) * scale, ay = (py[j] - cy) * scale, az = (pz[j] - cz) * scale;
     bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
               fabs(az) <= kF16QueryClamp;
@@ -657,15 +894,19 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         const double u = 0x1.0p-24;
         const double a2 = ax * ax + ay * ay + az * az;
         const double A = sqrt(a2);
+        const double sh = SEEDED ? seed_shift(seed16[j]) : 0.0;
         auto delta = [&](double R) {
-            return 26.0 * u * R * R + 60.0 * u * A * R + 4.0 * u * (A + R) + 1e-3;
+            return SEEDED ? 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * fabs(sh) + 4.0 * u * (A + R) + 1e-3
+                          : 26.0 * u * R * R + 60.0 * u * A * R + 4.0 * u * (A + R) + 1e-3;
         };
+        // shift back to G (fp64 sums of an fp32 and an exact value: relative 2^-53)
+        const double bg = (double)b + sh, sg = (double)s2 + sh;
         const double db = delta(sqrt((double)mms[id]) * (1.0 + 0x1.0p-20));
-        const double Db = fmax((double)b + db + a2 * (1.0 + 4.0 * u), 0.0);
+        const double Db = fmax(bg + db + a2 * (1.0 + 4.0 * u), 0.0);
         const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
-        double T = (double)b + db + delta(Rc) + 0x1.0p-48 * Db;
-        T += fabs(T) * 1e-12 + 1e-300;
-        ok = (double)s2 > T;
+        double T = bg + db + delta(Rc) + 0x1.0p-48 * Db;
+        T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
+        ok = sg > T;
     }
     if (ok) {
         idx[j] = id;
@@ -698,10 +939,12 @@ __global__ __launch_bounds__(kBlock) void build_mimage16_kernel(
             lo8[0] = xh; lo8[1] = xl; lo8[2] = xh; lo8[3] = yh;
             lo8[4] = yl; lo8[5] = yh; lo8[6] = zh; lo8[7] = zl;
             hi8[0] = zh; hi8[1] = mh; hi8[2] = ml; hi8[3] = xl;
-            hi8[4] = yl; hi8[5] = zl;
+            hi8[4] = yl; hi8[5] = zl; hi8[6] = (_Float16)16384.0f; hi8[7] = (_Float16)16384.0f;
             mmv = (float)mm;
         } else {
             hi8[1] = (_Float16)65504.0f;
+            hi8[6] = (_Float16)16384.0f; // the seeded filter's shift applies to padding too
+            hi8[7] = (_Float16)16384.0f;
             mmv = 1.0e30f;
         }
         const int blk = P >> 5, i = P & 31;
@@ -1193,32 +1436,51 @@ void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, 
                                                      part_second, part_idx);
 }
 
-static int mfma16_cfg()
+static int mfma16_qg()
 {
-    // tuning knob for experiments: ICP_MFMA16_CFG = 21 | 22 | 41 | 42 (QG, NS)
-    static int cfg = [] {
-        const char *e = getenv("ICP_MFMA16_CFG");
-        const int v = e ? atoi(e) : 0;
-        return (v == 21 || v == 22 || v == 41 || v == 42 || v == 24) ? v : 41;
+    // tuning knob for experiments: ICP_MFMA16_QG = 2 | 4 (32-query groups per wave)
+    static int qg = [] {
+        const char *e = getenv("ICP_MFMA16_QG");
+        return (e && atoi(e) == 2) ? 2 : 4;
     }();
-    return cfg;
+    return qg;
 }
 
-static const void *mfma16_kernel_ptr()
+// Seeded searches use the software-pipelined kernel (4% faster at C4); unseeded ones the
+// plain kernel (the pipelined one is 5% slower there: its update branch fires often).
+// Knob for experiments: ICP_MFMA16_KERNEL = plain | pipe (both searches), ICP_MFMA16_QG = 2.
+static int mfma16_kernel_choice(bool seeded) // 0 plain, 1 pipelined
 {
-    switch (mfma16_cfg()) {
-    case 21: return (const void *)nn_mfma16_kernel<2, 1>;
-    case 42: return (const void *)nn_mfma16_kernel<4, 2>;
-    case 24: return (const void *)nn_mfma16_kernel<2, 4>;
-    case 22: return (const void *)nn_mfma16_kernel<2, 2>;
-    default: return (const void *)nn_mfma16_kernel<4, 1>;
-    }
+    static int forced = [] {
+        const char *e = getenv("ICP_MFMA16_KERNEL");
+        if (!e) return -1;
+        return std::string(e) == "pipe" ? 1 : (std::string(e) == "plain" ? 0 : -1);
+    }();
+    if (mfma16_qg() != 4) return 0;
+    return forced >= 0 ? forced : (seeded ? 1 : 0);
 }
 
-NNPlan plan_nn_mfma16(size_t np, size_t nm_pad)
+static const void *mfma16_kernel_ptr(bool seeded)
 {
-    const int qg = mfma16_cfg() / 10;
-    return make_plan(np, nm_pad, kTile32, qg, 4 * qg * 32, mfma16_kernel_ptr());
+    if (mfma16_kernel_choice(seeded))
+        return seeded ? (const void *)nn_mfma16p_kernel<true> : (const void *)nn_mfma16p_kernel<false>;
+    if (mfma16_qg() == 2)
+        return seeded ? (const void *)nn_mfma16_kernel<2, true> : (const void *)nn_mfma16_kernel<2, false>;
+    return seeded ? (const void *)nn_mfma16_kernel<4, true> : (const void *)nn_mfma16_kernel<4, false>;
+}
+
+NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded)
+{
+    const int qg = mfma16_qg();
+    return make_plan(np, nm_pad, kTile32, qg, 4 * qg * 32, mfma16_kernel_ptr(seeded));
+}
+
+void launch_mfma16_seed(const double *px, const double *py, const double *pz, int np, const int *prev,
+                        const double *mx, const double *my, const double *mz, const double c[3], double scale,
+                        unsigned *seed16, hipStream_t st)
+{
+    mfma16_seed_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(px, py, pz, np, prev, mx, my, mz, c[0],
+                                                                       c[1], c[2], scale, seed16);
 }
 
 void launch_build_mimage16(const double *mx, const double *my, const double *mz, int nm, int nm_pad,
@@ -1229,34 +1491,40 @@ void launch_build_mimage16(const double *mx, const double *my, const double *mz,
 }
 
 void launch_nn_mfma16(const double *px, const double *py, const double *pz, int np, const double c[3],
-                      double scale, const void *img, int nm_pad, const NNPlan &pl, float *part_best,
-                      float *part_second, int *part_idx, hipStream_t st)
+                      double scale, const unsigned *seed16, const void *img, int nm_pad, const NNPlan &pl,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st)
 {
     dim3 grid(pl.qblocks, pl.splits);
     const half8_t *im = (const half8_t *)img;
-#define LAUNCH16(QG, NS)                                                                         \
-    nn_mfma16_kernel<QG, NS><<<grid, kBlock, 0, st>>>(px, py, pz, np, c[0], c[1], c[2], scale, im,  \
-                                                      nm_pad, pl.chunk, part_best, part_second,    \
-                                                      part_idx)
-    switch (mfma16_cfg()) {
-    case 21: LAUNCH16(2, 1); break;
-    case 42: LAUNCH16(4, 2); break;
-    case 24: LAUNCH16(2, 4); break;
-    case 22: LAUNCH16(2, 2); break;
-    default: LAUNCH16(4, 1); break;
+#define LAUNCH16(K)                                                                               \
+    K<<<grid, kBlock, 0, st>>>(px, py, pz, np, c[0], c[1], c[2], scale, seed16, im, nm_pad, pl.chunk, \
+                               part_best, part_second, part_idx)
+    const bool sd = seed16 != nullptr;
+    if (mfma16_kernel_choice(sd)) {
+        if (sd) LAUNCH16(nn_mfma16p_kernel<true>); else LAUNCH16(nn_mfma16p_kernel<false>);
+    } else if (mfma16_qg() == 2) {
+        if (sd) LAUNCH16((nn_mfma16_kernel<2, true>)); else LAUNCH16((nn_mfma16_kernel<2, false>));
+    } else {
+        if (sd) LAUNCH16((nn_mfma16_kernel<4, true>)); else LAUNCH16((nn_mfma16_kernel<4, false>));
     }
 #undef LAUNCH16
 }
 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
-                               int np, const double c[3], double scale, const float *mms, int *idx,
-                               int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
-                               const float4 *p32, const float4 *m32, double rm, hipStream_t st)
+                               int np, int nm, const double c[3], double scale, const unsigned *seed16,
+                               const float *mms, int *idx, int *amb_count, int *amb_list, float *amb_seed,
+                               int *amb_hint, const float4 *p32, const float4 *m32, double rm, hipStream_t st)
 {
-    nn_finalize_mfma16_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-        part_best, part_second, part_idx, splits, px, py, pz, np, c[0], c[1], c[2], scale, mms, idx,
-        amb_count, amb_list, amb_seed, amb_hint, p32, m32, rm);
+    const int grid = (np + kBlock - 1) / kBlock;
+    if (seed16)
+        nn_finalize_mfma16_kernel<true><<<grid, kBlock, 0, st>>>(
+            part_best, part_second, part_idx, splits, px, py, pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,
+            idx, amb_count, amb_list, amb_seed, amb_hint, p32, m32, rm);
+    else
+        nn_finalize_mfma16_kernel<false><<<grid, kBlock, 0, st>>>(
+            part_best, part_second, part_idx, splits, px, py, pz, np, nm, c[0], c[1], c[2], scale, nullptr, mms,
+            idx, amb_count, amb_list, amb_seed, amb_hint, p32, m32, rm);
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,

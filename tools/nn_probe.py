@@ -18,12 +18,29 @@ def main():
     ap.add_argument("--variant", default="mfma", choices=["valu", "mfma", "mfma16", "fp64"])
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--icp", type=int, default=0,
+                    help="run this many ICP iterations instead (iterations >= 2 use the seeded filter)")
     a = ap.parse_args()
     mode = icp_amd.NN_FP64 if a.variant == "fp64" else icp_amd.NN_CERTIFIED
     with icp_amd.Context(0, mode) as ctx:
         ctx.set_nn_variant({"valu": 1, "mfma": 2, "mfma16": 3, "fp64": 0}[a.variant])
         m, p = icp_amd.synthetic_pair(a.n, seed=42)
         ctx.set_model(m)
+        if a.icp:
+            ctx.set_scene(p, np_total=a.n)
+            ctx.reset_stats()
+            t0 = time.perf_counter()
+            per = []
+            for _ in range(a.icp):  # one iteration per call: the scene (and the seeds) carry over
+                ctx.reset_stats()
+                _, errs = ctx.run(1, -1.0)
+                st = ctx.stats()
+                per.append((st["nn_ms"], st["level1_queued"], float(errs[0])))
+            dt = (time.perf_counter() - t0) / a.icp
+            for i, (ms, qd, e) in enumerate(per):
+                print(f"  it {i:2d}: filter {ms:7.2f} ms  queued {qd:7d}  err {e:.4e}")
+            print(f"icp: {dt * 1e3:.2f} ms/iteration, filter {sum(x[0] for x in per) / a.icp:.2f} ms avg")
+            return
         ctx.closest_matrix(p)
         ctx.reset_stats()
         t0 = time.perf_counter()
