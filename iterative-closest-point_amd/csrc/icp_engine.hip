@@ -82,6 +82,8 @@ struct icp_ctx {
     int *g_cid = nullptr, *g_count = nullptr, *g_start = nullptr, *g_bsum = nullptr, *g_fill = nullptr;
     double4 *g_pts = nullptr;
     size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
+    double4 *m4 = nullptr;      // model as (x, y, z, 0) doubles: one read per random gather
+    size_t m4_cap = 0;
     unsigned *seed16 = nullptr; // seeded f16 filter: per-query shift (icp_run iterations >= 2)
     size_t seed16_cap = 0;
     bool seeds_valid = false;   // idx holds the previous search over the resident scene
@@ -276,8 +278,8 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
         const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd) : plan_nn_mfma(n, ctx->nm_pad);
         if (sd) {
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
-            launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, ctx->c,
-                               ctx->scale16, ctx->seed16, ctx->st);
+            launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->m4, ctx->c, ctx->scale16, ctx->seed16,
+                               ctx->st);
         }
         const unsigned *seeds = sd ? ctx->seed16 : nullptr;
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap,
@@ -310,8 +312,8 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
                                     ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed, ctx->amb1_hint, ctx->m32,
                                     ctx->rm, ctx->st);
         // exact resolution of the near ties through the model grid, around each candidate
-        launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z,
-                               ctx->model.x, ctx->model.y, ctx->model.z, grid_view(ctx), kGridBudget,
+        launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
+                               grid_view(ctx), kGridBudget,
                                ctx->idx, ctx->amb_count + 1, ctx->fb_list, ctx->amb1_seed, ctx->fb_seed,
                                nullptr, nullptr, ctx->st);
         LAUNCHCHK("nn_mfma");
@@ -361,8 +363,8 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, nullptr, (int)n, cp, ctx->idx, ctx->amb_count,
                            ctx->amb_list, ctx->amb_T, ctx->amb_hint, ctx->st);
         // near ties: exact through the model grid; what it cannot take, fp64 brute force
-        launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z,
-                               ctx->model.x, ctx->model.y, ctx->model.z, grid_view(ctx), kGridBudget,
+        launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z, ctx->m4,
+                               grid_view(ctx), kGridBudget,
                                ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr, nullptr, ctx->amb_T,
                                ctx->fb_T, ctx->st);
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
@@ -539,7 +541,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
-                    (void *)ctx->fb_seed, (void *)ctx->fb_T, (void *)ctx->seed16})
+                    (void *)ctx->fb_seed, (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -624,6 +626,8 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, (int)nm_pad, ctx->c,
                           ctx->scale16, ctx->mimg16, ctx->mms16, ctx->st);
     LAUNCHCHK("build_mimage16");
+    TRY(grow(ctx, &ctx->m4, &ctx->m4_cap, nm));
+    launch_make_aos4(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->m4, ctx->st);
     // uniform grid over the fp64 model for the exact resolver
     ctx->grid = grid_params(m_xyz, nm);
     const long long ncell = grid_cells(ctx->grid);
@@ -695,7 +699,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         ctx->seeds_valid = true; // idx now pairs every point of the resident scene
         // 2. centroids (gpu.cc:98-99): sum p, sum y   [+ RCCL all-reduce, 6 doubles]
         const int nb = red_blocks(n);
-        launch_gather_moments(ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, P.x, P.y, P.z,
+        launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z,
                               (int)n, Y.x, Y.y, Y.z, ctx->partials, ctx->st);
         launch_reduce(ctx->partials, nb, 6, ctx->sums + kSumP, ctx->st);
         LAUNCHCHK("moments");
@@ -762,7 +766,7 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
     TRY(nn_search(ctx, ctx->qa, np));
     if (np && y_xyz_out) {
         TRY(grow_cloud(ctx, ctx->qb, np, false));
-        launch_gather_moments(ctx->idx, ctx->model.x, ctx->model.y, ctx->model.z, ctx->qa.x,
+        launch_gather_moments(ctx->idx, ctx->m4, ctx->qa.x,
                               ctx->qa.y, ctx->qa.z, (int)np, ctx->qb.x, ctx->qb.y, ctx->qb.z,
                               ctx->partials, ctx->st);
         LAUNCHCHK("gather");

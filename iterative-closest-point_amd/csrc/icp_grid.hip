@@ -124,8 +124,7 @@ __global__ __launch_bounds__(kBlock) void grid_scatter_kernel(
 __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
-    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
-    GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
+    const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
     const float *__restrict__ seed_in, float *__restrict__ seed_out,
     const double *__restrict__ T_in, double *__restrict__ T_out)
 {
@@ -139,7 +138,8 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
         double best = 0.0;
         int bi = h;
         if (ok) {
-            best = d64g(q[0], q[1], q[2], mx[h], my[h], mz[h]);
+            const double4 mh = m4[h];
+            best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
             const double R = sqrt(best);
             long long cells = 1;
 #pragma unroll
@@ -167,8 +167,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
                     }
                 }
             idx[j] = bi;
-        } else {
-            const int slot = atomicAdd(fb_count, 1);
+        }
+        const int slot = wave_append(fb_count, !ok);
+        if (!ok) {
             fb_list[slot] = j;
             if (seed_in) seed_out[slot] = seed_in[t];
             if (T_in) T_out[slot] = T_in[t];
@@ -243,13 +244,13 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 }
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
-                            const double *px, const double *py, const double *pz, const double *mx,
-                            const double *my, const double *mz, const GridView &gv, int budget,
+                            const double *px, const double *py, const double *pz, const double4 *m4,
+                            const GridView &gv, int budget,
                             int *idx, int *fb_count, int *fb_list, const float *seed_in,
                             float *seed_out, const double *T_in, double *T_out, hipStream_t st)
 {
     const int blocks = std::max(1, std::min((max_items + kBlock - 1) / kBlock, 2048));
-    nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, mx, my, mz, gv,
+    nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv,
                                                       budget, idx, fb_count, fb_list, seed_in, seed_out,
                                                       T_in, T_out);
 }

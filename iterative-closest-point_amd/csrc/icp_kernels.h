@@ -7,6 +7,22 @@
 
 namespace icp {
 
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// Append to a device queue with ONE atomic per wave: returns this lane's slot if `pred`.
+// Lanes that exited earlier simply do not take part (ballot over the active lanes).
+__device__ __forceinline__ int wave_append(int *counter, bool pred)
+{
+    const unsigned long long mask = __ballot(pred);
+    if (mask == 0ull) return -1;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, __popcll(mask));
+    base = __shfl(base, leader, 64);
+    return pred ? base + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
+}
+#endif
+
 // Parameters of the fp32 certificate (see icp_kernels.hip, "certified NN").
 struct CertParams {
     double rm; // max |coordinate| of the centred fp32 model (real points only)
@@ -60,8 +76,7 @@ void launch_nn_finalize_mfma(const float *part_best, const float *part_second, c
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded);
 // seeds of the seeded filter from the previous correspondences (packed f16 of -s0 / 2^14)
 void launch_mfma16_seed(const double *px, const double *py, const double *pz, int np, const int *prev,
-                        const double *mx, const double *my, const double *mz, const double c[3], double scale,
-                        unsigned *seed16, hipStream_t st);
+                        const double4 *m4, const double c[3], double scale, unsigned *seed16, hipStream_t st);
 void launch_build_mimage16(const double *mx, const double *my, const double *mz, int nm, int nm_pad,
                            const double c[3], double scale, void *img, float *mms, hipStream_t st);
 // seed16 == nullptr: unseeded filter
@@ -111,17 +126,20 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 // over the grid box that must contain every point at least as close as the candidate ->
 // idx; hint < 0 or a box over `budget` cells -> appended to fb_list (with its seed / T).
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
-                            const double *px, const double *py, const double *pz, const double *mx,
-                            const double *my, const double *mz, const GridView &gv, int budget,
+                            const double *px, const double *py, const double *pz, const double4 *m4,
+                            const GridView &gv, int budget,
                             int *idx, int *fb_count, int *fb_list, const float *seed_in,
                             float *seed_out, const double *T_in, double *T_out, hipStream_t st);
 
 // ---- streaming reductions (deterministic two-stage, fp64) --------------------------
 int red_blocks(size_t n);
 // y = m[idx]; partial [sum p (3), sum y (3)]
-void launch_gather_moments(const int *idx, const double *mx, const double *my, const double *mz,
-                           const double *px, const double *py, const double *pz, int n,
-                           double *yx, double *yy, double *yz, double *partials, hipStream_t st);
+// m4: the model as (x, y, z, 0) double4 (one 32-byte read per gathered point)
+void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
+                           const double *pz, int n, double *yx, double *yy, double *yz,
+                           double *partials, hipStream_t st);
+void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4,
+                      hipStream_t st);
 // partial [sum p (3)] of one cloud
 void launch_sum3(const double *x, const double *y, const double *z, int n, double *partials,
                  hipStream_t st);

@@ -285,10 +285,10 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     int id;
     merge_splits(part_best, part_second, part_idx, splits, nslots, s, b, s2, id);
     const double T = cert_window(b, p32[j], rm);
-    if ((double)s2 > T) {
-        idx[j] = id; // unique candidate => exact fp64 first-min
-    } else {
-        const int slot = atomicAdd(amb_count, 1);
+    const bool ok = (double)s2 > T;
+    if (ok) idx[j] = id; // unique candidate => exact fp64 first-min
+    const int slot = wave_append(amb_count, !ok);
+    if (!ok) {
         amb_list[slot] = j;
         amb_T[slot] = T;
         if (amb_hint) amb_hint[slot] = id;
@@ -824,9 +824,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
 // nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
 __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
-    int np, const int *__restrict__ prev, const double *__restrict__ mx, const double *__restrict__ my,
-    const double *__restrict__ mz, double cx, double cy, double cz, double scale,
-    unsigned *__restrict__ seed16)
+    int np, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx, double cy,
+    double cz, double scale, unsigned *__restrict__ seed16)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -834,7 +833,8 @@ __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
     const double a0 = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
     const double a1 = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
     const double a2 = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double b0 = (mx[k] - cx) * scale, b1 = (my[k] - cy) * scale, b2 = (mz[k] - cz) * scale;
+    const double4 m = m4[k];
+    const double b0 = (m.x - cx) * scale, b1 = (m.y - cy) * scale, b2 = (m.z - cz) * scale;
     const double bb = b0 * b0 + b1 * b1 + b2 * b2;
     const double G = bb - 2.0 * (a0 * b0 + a1 * b1 + a2 * b2);
     const double u = 0x1.0p-24;
@@ -908,10 +908,9 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
         ok = sg > T;
     }
-    if (ok) {
-        idx[j] = id;
-    } else {
-        const int slot = atomicAdd(amb_count, 1);
+    if (ok) idx[j] = id;
+    const int slot = wave_append(amb_count, !ok);
+    if (!ok) {
         amb_list[slot] = j;
         amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
         amb_hint[slot] = id;                                  // the grid resolver's candidate
@@ -985,10 +984,9 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
         T += fabs(T) * 1e-12 + 1e-300;
         ok = (double)s2 > T;
     }
-    if (ok) {
-        idx[j] = id;
-    } else {
-        const int slot = atomicAdd(amb_count, 1);
+    if (ok) idx[j] = id;
+    const int slot = wave_append(amb_count, !ok);
+    if (!ok) {
         amb_list[slot] = j;
         amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
         amb_hint[slot] = id;                                  // the grid resolver's candidate
@@ -1145,15 +1143,14 @@ __global__ __launch_bounds__(kBlock) void nn_finalize64_kernel(const double *__r
 // ---- streaming reductions ----------------------------------------------------------
 
 __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
-    const int *__restrict__ idx, const double *__restrict__ mx, const double *__restrict__ my,
-    const double *__restrict__ mz, const double *__restrict__ px, const double *__restrict__ py,
-    const double *__restrict__ pz, int n, double *__restrict__ yx, double *__restrict__ yy,
-    double *__restrict__ yz, double *__restrict__ partials)
+    const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
+    const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
+    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials)
 {
     double a[6] = {0, 0, 0, 0, 0, 0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const int k = idx[i];
-        const double y0 = mx[k], y1 = my[k], y2 = mz[k];
+        const double4 m = m4[idx[i]];
+        const double y0 = m.x, y1 = m.y, y2 = m.z;
         yx[i] = y0;
         yy[i] = y1;
         yz[i] = y2;
@@ -1476,11 +1473,10 @@ NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded)
 }
 
 void launch_mfma16_seed(const double *px, const double *py, const double *pz, int np, const int *prev,
-                        const double *mx, const double *my, const double *mz, const double c[3], double scale,
-                        unsigned *seed16, hipStream_t st)
+                        const double4 *m4, const double c[3], double scale, unsigned *seed16, hipStream_t st)
 {
-    mfma16_seed_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(px, py, pz, np, prev, mx, my, mz, c[0],
-                                                                       c[1], c[2], scale, seed16);
+    mfma16_seed_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(px, py, pz, np, prev, m4, c[0], c[1],
+                                                                       c[2], scale, seed16);
 }
 
 void launch_build_mimage16(const double *mx, const double *my, const double *mz, int nm, int nm_pad,
@@ -1570,12 +1566,25 @@ void launch_nn_finalize64(const double *part_best, const int *part_idx, int spli
 
 int red_blocks(size_t n) { return grid_for(n, kRedMaxBlocks); }
 
-void launch_gather_moments(const int *idx, const double *mx, const double *my, const double *mz,
-                           const double *px, const double *py, const double *pz, int n,
-                           double *yx, double *yy, double *yz, double *partials, hipStream_t st)
+void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
+                           const double *pz, int n, double *yx, double *yy, double *yz,
+                           double *partials, hipStream_t st)
 {
-    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, mx, my, mz, px, py, pz, n, yx, yy,
-                                                             yz, partials);
+    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials);
+}
+
+__global__ __launch_bounds__(kBlock) void make_aos4_kernel(const double *__restrict__ x,
+                                                           const double *__restrict__ y,
+                                                           const double *__restrict__ z, int n,
+                                                           double4 *__restrict__ m4)
+{
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+        m4[i] = make_double4(x[i], y[i], z[i], 0.0);
+}
+
+void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4, hipStream_t st)
+{
+    make_aos4_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, m4);
 }
 
 void launch_sum3(const double *x, const double *y, const double *z, int n, double *partials,
