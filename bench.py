@@ -40,6 +40,15 @@ PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF den
 FLOP_PER_PAIR = 8          # SURVEY.md §8d (algorithmic: 3 sub + 1 mul + 2 fma)
 MFMA16_FLOP_PER_PAIR = 32  # executed: v_mfma_f32_32x32x16_f16 = 2*32*32*16 flop per 1024 pairs
 REF_OPTI_GPU_LOOP_FPS = 9.36368  # reference README.md:108 (GTX 1050, cow_ref/cow_tr1)
+# the reference's published google-benchmark times, ms per iteration (README.md:95-108;
+# GTX 1050 / i7-4790 1 thread, cow_ref vs cow_tr1; *_loop = one complete registration)
+REF_README_MS = {
+    "cpu_closest_matrix": 8726, "naive_gpu_closest_matrix": 2935, "opti_gpu_closest_matrix": 7.46,
+    "cpu_find_alignment": 14.9, "gpu_find_alignment": 5.52, "cpu_compute_centroid": 1.33,
+    "gpu_compute_centroid": 2.38, "cpu_err_compute": 8.44, "gpu_err_compute": 1.16,
+    "cpu_err_compute_alignment": 8.54, "gpu_err_compute_alignment": 1.75, "cpu_loop": 61276,
+    "naive_gpu_loop": 18240, "opti_gpu_loop": 107,
+}
 
 
 def pmc_traffic(kernel):
@@ -83,6 +92,59 @@ def cpu_baseline(m, p, sample=4096, seed=0):
             "seconds_per_iteration": per_iter}
 
 
+def _cow_paths():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import datasets
+    return datasets.path("cow_ref"), datasets.path("cow_tr1")
+
+
+def reference_cases_gpu(min_time=0.3):
+    """The reference's 8 GPU benchmark cases (src/bench.cc:391-445) through
+    iterative-closest-point_amd/build/icp-bench, on the bundled cow pair."""
+    import subprocess
+    ref, scene = _cow_paths()
+    exe = os.path.join(ROOT, "iterative-closest-point_amd", "build", "icp-bench")
+    r = subprocess.run([exe, "--ref", ref, "--scene", scene, "--min-time", str(min_time), "--json"],
+                       capture_output=True, text=True, timeout=600, check=True)
+    cases = json.loads(r.stdout.strip().splitlines()[-1])["cases"]
+    return {k: {"ms": v["ms"], "frame_rate": v["frame_rate"], "reference_ms": REF_README_MS.get(k),
+                "speedup_vs_reference": (REF_README_MS[k] / v["ms"]) if k in REF_README_MS else None}
+            for k, v in cases.items()}
+
+
+def reference_cases_cpu(reps=3):
+    """The reference's 6 CPU cases on this host with the oracle (the C restatement of
+    src/cpu.cc, 1 core); cpu_compute_centroid is numpy (Eigen's rowwise mean + colwise -)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O
+    m, p = (O.load_matrix(x) for x in _cow_paths())
+    y, _ = O.closest(p, m, O.NN_CPU_SQRT)
+    al = O.find_alignment(p, y)
+    R = np.array(al.R).reshape(3, 3)
+
+    def t(f, n=reps):
+        f()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            f()
+        return (time.perf_counter() - t0) * 1e3 / n
+
+    def centroid():
+        for a in (p, y):
+            _ = a - a.mean(axis=0)
+
+    ms = {
+        "cpu_closest_matrix": t(lambda: O.closest(p, m, O.NN_CPU_SQRT), 1),
+        "cpu_find_alignment": t(lambda: O.find_alignment(p, y)),
+        "cpu_compute_centroid": t(centroid),
+        "cpu_err_compute": t(lambda: O.err_compute(p, y, al.s, R, al.t)),
+        "cpu_err_compute_alignment": t(lambda: O.err_compute_alignment(p, y, al.s, R, al.t)),
+        "cpu_loop": t(lambda: O.icp(m, p, 20, 1e-5, O.NN_CPU_SQRT), 1),
+    }
+    return {k: {"ms": v, "reference_ms": REF_README_MS[k], "speedup_vs_reference": REF_README_MS[k] / v}
+            for k, v in ms.items()}
+
+
 def cow_frame_rate(device, reps=20):
     """Reference headline: opti_gpu_loop frame_rate = complete cow registrations/s."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -112,6 +174,7 @@ def main():
     ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
+    ap.add_argument("--no-cases", action="store_true", help="skip the reference's 14 benchmark cases")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -216,8 +279,12 @@ def main():
         }
         if world == 1 and not args.no_cow:
             out["cow_frame_rate"] = cow_frame_rate(local)
+        if world == 1 and not args.no_cases:
+            out["reference_cases"] = reference_cases_gpu()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(m, p)
+            if not args.no_cases:
+                out["cpu_baseline"]["reference_cases_cpu"] = reference_cases_cpu()
             out["gpu_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -387,6 +387,32 @@ class ICP:
         self.s, self.r, self.t = s, R, t
         return e
 
+    def compute_y_naive(self):
+        """gpu.cc:6-15: one NN search per scene point (compute_distance_w_naive)."""
+        Y = np.empty_like(self.new_p)
+        for j in range(self.new_p.shape[0]):
+            Y[j] = self.m[compute_distance_w_naive(self.m, self.new_p[j], self._ctx)]
+        return Y
+
+    def find_corresponding_naive(self):
+        """gpu.cc:17-49: the per-point loop; err = (find_alignment + transform residual)/np,
+        stop after the iteration whose err < threshold.  Same results as the opti loop."""
+        if self.p.shape[0] != self.m.shape[0] and not self.allow_unequal:
+            raise ICPError(ICP_E_SIZE_MISMATCH, "Point sets need to have the same number of points.")
+        if self.p.shape[0] < 4:
+            raise ICPError(ICP_E_TOO_FEW_POINTS, "Need at least 4 point pairs")
+        errs = []
+        for _ in range(self.max_iter):
+            Y = self.compute_y_naive()
+            err = self.find_alignment(Y)
+            e2, self.new_p = self._ctx.err_compute(Y, self.new_p, True, self.s * self.r, self.t)
+            err = (err + e2) / self.p.shape[0]
+            errs.append(err)
+            if err < self.threshold:
+                break
+        self.errors = np.array(errs)
+        return len(errs)
+
 
 _default_ctx: Context | None = None
 
@@ -397,6 +423,13 @@ def _ctx_for_model(m) -> Context:
         _default_ctx = Context()
     _default_ctx.set_model(m)
     return _default_ctx
+
+
+def compute_distance_w_naive(m, pi, ctx: Context | None = None) -> int:
+    """compute.cu:279-308: index of the first nearest model point of one query point."""
+    c = ctx if ctx is not None else _ctx_for_model(m)
+    _, idx = c.closest_matrix(np.asarray(pi, dtype=np.float64).reshape(1, 3))
+    return int(idx[0])
 
 
 def compute_Y_w_opti(m, p):

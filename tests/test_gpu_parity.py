@@ -265,3 +265,18 @@ def test_reference_shaped_icp_class(amd, golden_traces):
     assert res.iterations == 7 and res.converged
     np.testing.assert_allclose(icp.errors, golden_traces["cow_tr1"]["err"], rtol=1e-9)
     np.testing.assert_allclose(icp.new_p, m, atol=1e-5)
+
+
+def test_naive_path_matches_opti_and_oracle(amd, golden_traces):
+    # GPU::ICP::find_corresponding_naive (gpu.cc:17-49): one NN call per point; the same
+    # NN rule as the batched search, so the same 7-iteration trajectory on cow
+    m, p = load(amd, "cow_ref"), load(amd, "cow_tr1")
+    icp = amd.ICP(m, p, 20)
+    it = icp.find_corresponding_naive()
+    assert it == 7
+    np.testing.assert_allclose(icp.errors, golden_traces["cow_tr1"]["err"], rtol=1e-9)
+    np.testing.assert_allclose(icp.new_p, m, atol=1e-5)
+    sel = RNG.choice(p.shape[0], size=64, replace=False)
+    _, ref = amd.compute_Y_w_opti(m, p)
+    for j in sel:
+        assert amd.compute_distance_w_naive(m, p[j]) == ref[j]
