@@ -145,6 +145,23 @@ def reference_cases_cpu(reps=3):
             for k, v in ms.items()}
 
 
+def csv_io(m):
+    """load.cc:3-97 at C4 size: write the model (ostream %g rows) and load it back
+    (sscanf %lf rows) with the product's parallel exact parser / formatter."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        f = os.path.join(d, "cloud.txt")
+        t0 = time.perf_counter()
+        icp_amd.write_matrix(f, m)
+        tw = time.perf_counter() - t0
+        size = os.path.getsize(f)
+        t0 = time.perf_counter()
+        back = icp_amd.load_matrix(f)
+        tl = time.perf_counter() - t0
+    return {"rows": int(m.shape[0]), "bytes": size, "write_s": tw, "load_s": tl,
+            "load_mb_per_s": size / tl / 1e6, "roundtrip_rows": int(back.shape[0])}
+
+
 def cow_frame_rate(device, reps=20):
     """Reference headline: opti_gpu_loop frame_rate = complete cow registrations/s."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -281,6 +298,7 @@ def main():
             out["cow_frame_rate"] = cow_frame_rate(local)
         if world == 1 and not args.no_cases:
             out["reference_cases"] = reference_cases_gpu()
+            out["csv_io"] = csv_io(m)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(m, p)
             if not args.no_cases:

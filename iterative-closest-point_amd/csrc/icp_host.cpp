@@ -6,11 +6,15 @@
 // (max_element_index), src/load.cc:3-97 (I/O).
 #include "icp_internal.h"
 
+#include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
+#include <thread>
 #include <vector>
 
 namespace icp {
@@ -122,22 +126,111 @@ void shard_range(size_t n, int rank, int world, size_t *begin, size_t *count)
     *count = base + (r < rem ? 1 : 0);
 }
 
-// ---- CSV I/O (src/load.cc) ---------------------------------------------------
-// Row parse = sscanf(line, "%lf,%lf,%lf") (load.cc:27): %lf skips leading whitespace
-// and converts with strtod; each ',' must follow its number directly; fields that do
-// not parse stay 0 (load.cc:26).
-static void parse_row(char *s, double out[3])
+// ---- CSV point-cloud I/O (src/load.cc:3-97) ---------------------------------------------
+// Row semantics of load.cc:26-27: sscanf(line, "%lf,%lf,%lf") into zero-initialised x, y, z.
+// glibc's %lf is greedier than strtod: it consumes "1e" or "1e+" (an exponent marker with no
+// digits) and converts the consumed text, so "1e,2,3" is (1, 2, 3).  Rows the fast path
+// below does not fully cover go through that very call.
+static void parse_row_sscanf(const char *line, double out[3])
 {
-    for (int k = 0; k < 3; ++k) {
-        char *e = nullptr;
-        const double v = std::strtod(s, &e);
-        if (e == s) return;
-        out[k] = v;
-        if (k < 2) {
-            if (*e != ',') return;
-            s = e + 1;
+    double x = 0., y = 0., z = 0.;
+    std::sscanf(line, "%lf,%lf,%lf", &x, &y, &z);
+    out[0] = x;
+    out[1] = y;
+    out[2] = z;
+}
+
+// Clinger's exact fast path: [-]digits[.digits][(e|E)[+-]digits] with a decimal mantissa
+// m <= 2^53 and |exponent| <= 22 is m * 10^e (or m / 10^-e): one correctly rounded operation
+// on exact operands, i.e. the same double strtod (and so %lf) returns.  Anything else
+// (whitespace, '+', hex, inf/nan, long mantissas, huge exponents, a bare exponent marker)
+// -> false, and the row goes through sscanf.
+static bool parse_number_fast(const char *s, const char *end, double &v, const char *&stop)
+{
+    static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    const char *p = s;
+    bool neg = false;
+    if (p < end && *p == '-') {
+        neg = true;
+        ++p;
+    }
+    uint64_t m = 0;
+    int exp10 = 0;
+    bool any = false;
+    const uint64_t kMax = (uint64_t)1 << 53;
+    const char *int_start = p;
+    while (p < end && *p >= '0' && *p <= '9') {
+        m = m * 10 + (uint64_t)(*p - '0');
+        if (m > kMax) return false;
+        ++p;
+        any = true;
+    }
+    if (p < end && (*p == 'x' || *p == 'X') && p - int_start == 1 && *int_start == '0') return false; // hex
+    if (p < end && *p == '.') {
+        ++p;
+        while (p < end && *p >= '0' && *p <= '9') {
+            m = m * 10 + (uint64_t)(*p - '0');
+            if (m > kMax) return false;
+            --exp10;
+            ++p;
+            any = true;
         }
     }
+    if (!any) return false;
+    if (p < end && (*p == 'e' || *p == 'E')) {
+        const char *q = p + 1;
+        bool eneg = false;
+        if (q < end && (*q == '+' || *q == '-')) {
+            eneg = *q == '-';
+            ++q;
+        }
+        if (!(q < end && *q >= '0' && *q <= '9')) return false; // "1e", "1e+": sscanf's own rule
+        {
+            int ex = 0;
+            while (q < end && *q >= '0' && *q <= '9') {
+                if (ex > 10000) return false;
+                ex = ex * 10 + (*q - '0');
+                ++q;
+            }
+            exp10 += eneg ? -ex : ex;
+            p = q;
+        }
+    }
+    if (exp10 < -22 || exp10 > 22) return false;
+    const double dm = (double)m; // exact: m <= 2^53
+    v = exp10 >= 0 ? dm * kPow10[exp10] : dm / kPow10[-exp10];
+    if (neg) v = -v;
+    stop = p;
+    return true;
+}
+
+// one row [s, end) (end = its '\n' or the end of the file)
+static void parse_row(const char *s, const char *end, double out[3])
+{
+    double v[3] = {0, 0, 0};
+    const char *p = s;
+    for (int k = 0; k < 3; ++k) {
+        const char *e = nullptr;
+        if (!parse_number_fast(p, end, v[k], e)) { // any other form: the reference's own call
+            const std::string line(s, (size_t)(end - s));
+            parse_row_sscanf(line.c_str(), out);
+            return;
+        }
+        out[k] = v[k];
+        if (k < 2) {
+            if (e >= end || *e != ',') return;
+            p = e + 1;
+        }
+    }
+}
+
+static unsigned io_threads(size_t bytes)
+{
+    unsigned t = std::thread::hardware_concurrency();
+    if (const char *e = std::getenv("ICP_IO_THREADS")) t = (unsigned)std::atoi(e);
+    t = std::max(1u, std::min(t, 16u));
+    return (unsigned)std::max<size_t>(1, std::min<size_t>(t, bytes / (1 << 20) + 1)); // >= 1 MiB each
 }
 
 int load_matrix(const char *path, std::vector<double> &xyz, size_t *n_out)
@@ -151,34 +244,79 @@ int load_matrix(const char *path, std::vector<double> &xyz, size_t *n_out)
     const size_t got = sz > 0 ? std::fread(buf.data(), 1, (size_t)sz, f) : 0;
     std::fclose(f);
     buf[got] = '\0';
+    const char *base = buf.data(), *end = base + got;
+    // chunks at arbitrary byte offsets; a '\n' at offset q starts row (#'\n' before q), the
+    // header being line 0 (load.cc:21)
+    const unsigned T = io_threads(got);
+    std::vector<size_t> cut(T + 1), nl(T + 1, 0);
+    for (unsigned t = 0; t <= T; ++t) cut[t] = got * t / T;
+    auto count = [&](unsigned t) {
+        size_t c = 0;
+        for (const char *p = base + cut[t], *e = base + cut[t + 1];
+             (p = (const char *)std::memchr(p, '\n', (size_t)(e - p))) != nullptr; ++p)
+            ++c;
+        nl[t + 1] = c;
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < T; ++t) pool.emplace_back(count, t);
+    count(0);
+    for (auto &th : pool) th.join();
+    pool.clear();
+    for (unsigned t = 0; t < T; ++t) nl[t + 1] += nl[t];
     // load.cc:15-17: getline() count minus the header
-    size_t lines = 0;
-    for (size_t i = 0; i < got; ++i) lines += buf[i] == '\n';
-    if (got && buf[got - 1] != '\n') ++lines;
+    const size_t lines = nl[T] + ((got && buf[got - 1] != '\n') ? 1 : 0);
     const size_t n = lines > 0 ? lines - 1 : 0;
     xyz.assign(3 * n, 0.0);
-    char *cur = buf.data(), *end = buf.data() + got;
-    char *nl = (char *)std::memchr(cur, '\n', (size_t)(end - cur));
-    cur = nl ? nl + 1 : end; // load.cc:21: skip the header line
-    for (size_t i = 0; i < n; ++i) {
-        char *le = cur < end ? (char *)std::memchr(cur, '\n', (size_t)(end - cur)) : nullptr;
-        if (le) *le = '\0';
-        parse_row(cur, &xyz[3 * i]);
-        cur = le ? le + 1 : end;
-    }
+    auto parse = [&](unsigned t) {
+        size_t row = nl[t];
+        for (const char *p = base + cut[t], *e = base + cut[t + 1];
+             (p = (const char *)std::memchr(p, '\n', (size_t)(e - p))) != nullptr; ++p, ++row) {
+            if (row >= n) break;
+            const char *s = p + 1;
+            const char *le = (const char *)std::memchr(s, '\n', (size_t)(end - s));
+            parse_row(s, le ? le : end, &xyz[3 * row]);
+        }
+    };
+    for (unsigned t = 1; t < T; ++t) pool.emplace_back(parse, t);
+    parse(0);
+    for (auto &th : pool) th.join();
     *n_out = n;
     return ICP_OK;
 }
 
+// load.cc:68-81: header, then `os << x << ',' << y << ',' << z << std::endl` with the default
+// stream format (precision 6, %g).  Rows are formatted in parallel, written in order.
 int write_matrix(const char *path, const double *xyz, size_t n)
 {
     FILE *f = std::fopen(path, "wb");
     if (!f) return ICP_E_IO;
-    std::fputs("Points_0,Points_1,Points_2\n", f); // load.cc:73
-    for (size_t j = 0; j < n; ++j)                 // ostream default: %g, precision 6
-        std::fprintf(f, "%g,%g,%g\n", xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2]);
-    std::fclose(f);
-    return ICP_OK;
+    std::fputs("Points_0,Points_1,Points_2\n", f);
+    const unsigned T = io_threads(n * 40);
+    std::vector<std::string> part(T);
+    auto fmt = [&](unsigned t) {
+        const size_t j0 = n * t / T, j1 = n * (t + 1) / T;
+        std::string &o = part[t];
+        o.reserve((j1 - j0) * 40);
+        char line[128];
+        for (size_t j = j0; j < j1; ++j) {
+            // std::to_chars(general, 6) is specified as printf("%.6g") in the C locale (the
+            // stream default); Ryu-based, and without glibc printf's shared state
+            char *c = line;
+            for (int k = 0; k < 3; ++k) {
+                c = std::to_chars(c, line + sizeof(line), xyz[3 * j + k], std::chars_format::general, 6).ptr;
+                *c++ = k < 2 ? ',' : '\n';
+            }
+            o.append(line, (size_t)(c - line));
+        }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < T; ++t) pool.emplace_back(fmt, t);
+    fmt(0);
+    for (auto &th : pool) th.join();
+    bool ok = true;
+    for (const auto &o : part) ok = ok && std::fwrite(o.data(), 1, o.size(), f) == o.size();
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? ICP_OK : ICP_E_IO;
 }
 
 void synthetic_pair(uint64_t seed, size_t n, double angle_deg, const double axis_in[3],

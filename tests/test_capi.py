@@ -109,6 +109,67 @@ def test_load_matrix_edge_cases(icp_lib, oracle, tmp_path):
         icp_lib.load_matrix(str(tmp_path / "missing.txt"))
 
 
+def _fuzz_token(rng):
+    """A number spelled one of the ways a CSV row may carry it (decimal, exponent, long
+    mantissa, hex, inf/nan, padding, signs) or junk."""
+    v = rng.normal() * 10.0 ** rng.integers(-30, 30)
+    k = rng.integers(0, 16)
+    if k < 6:
+        return f"{v:.{rng.integers(1, 18)}g}"
+    if k == 6:
+        return repr(v)
+    if k == 7:
+        return f"{v:.{rng.integers(0, 25)}f}"
+    if k == 8:
+        return float(v).hex()
+    if k == 9:
+        return str(rng.choice(["inf", "-inf", "nan", "Infinity", "-0", "0", "-0.0", "1e400", "-1e-400",
+                               "4.9e-324", "2.2250738585072014e-308", "9007199254740993", "1e22", "1e23"]))
+    if k == 10:
+        return " " * int(rng.integers(1, 3)) + f"{v:.6g}"
+    if k == 11:
+        return "+" + f"{abs(v):.8g}"
+    if k == 12:
+        return str(rng.integers(-10**6, 10**6)) + "." + "0" * int(rng.integers(0, 30)) + str(rng.integers(0, 10**6))
+    if k == 13:
+        return f"{v:.5e}".replace("e", "E")
+    if k == 14:
+        return str(rng.choice(["", "-", ".", "1e", "1e+", "abc", "0x", "00x1", ".5", "-.5", "5.", "1.5e+0x"]))
+    return "0" * int(rng.integers(1, 5)) + f"{abs(v):.7g}"
+
+
+def test_load_matrix_fuzz_bitwise_equals_sscanf(icp_lib, oracle, tmp_path):
+    # the oracle parses with sscanf("%lf,%lf,%lf") (load.cc:27); the product's parser takes an
+    # exact fast path for plain decimals and strtod for the rest: bit-identical either way
+    rng = np.random.default_rng(5)
+    rows = []
+    for _ in range(4000):
+        toks = [_fuzz_token(rng) for _ in range(int(rng.integers(0, 5)))]
+        sep = str(rng.choice([",", ",", ",", ", ", ";"]))
+        rows.append(sep.join(toks) + str(rng.choice(["", "", "\r"])))
+    f = tmp_path / "fuzz.txt"
+    f.write_bytes(("Points_0,Points_1,Points_2\n" + "\n".join(rows) + "\n").encode())
+    a, b = icp_lib.load_matrix(str(f)), oracle.load_matrix(str(f))
+    assert a.shape == b.shape
+    np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def test_load_matrix_multithreaded_large(icp_lib, oracle, tmp_path):
+    # > 1 MiB per thread: the chunked parallel path, rows split across chunk boundaries
+    x = RNG.normal(size=(300000, 3)) * 10.0 ** RNG.integers(-5, 5, size=(300000, 1))
+    f = tmp_path / "big.txt"
+    with open(f, "w") as fh:
+        fh.write("Points_0,Points_1,Points_2\n")
+        fh.writelines(f"{a:.17g},{b:.9g},{c!r}\n" for a, b, c in x)
+    a, b = icp_lib.load_matrix(str(f)), oracle.load_matrix(str(f))
+    assert a.shape == (300000, 3)
+    np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64))
+    out1, out2 = tmp_path / "o1.txt", tmp_path / "o2.txt"
+    icp_lib.write_matrix(str(out1), a)
+    oracle.lib().oracle_write_matrix(str(out2).encode(), oracle._dp(np.ascontiguousarray(a)), a.shape[0])
+    assert out1.read_bytes() == out2.read_bytes()
+
+
 def test_write_matrix_byte_identical(icp_lib, oracle, tmp_path):
     x = np.concatenate([RNG.normal(size=(100, 3)) * 10.0 ** RNG.integers(-8, 8, size=(100, 1)),
                         [[0.0, -0.0, 1e300]]])
