@@ -27,8 +27,9 @@ def per_kernel(path, counter):
 
 
 def short(name):
-    """Kernel name without namespace, arguments or template arguments; the level-2 list
-    variant of nn_filter_kernel is tagged "<list>"."""
+    """Kernel name without namespace or arguments.  Tags: "<list>" for the level-2 list
+    variant of nn_filter_kernel, "<seeded>" for the seeded f16 filters."""
+    full = name
     n = name.replace("void ", "").replace("icp::(anonymous namespace)::", "")
     if n.startswith("_ZN3icp12_GLOBAL__N_1"):  # mangled: _ZN3icp12_GLOBAL__N_1<len><name>...
         rest = n[len("_ZN3icp12_GLOBAL__N_1"):]
@@ -37,7 +38,11 @@ def short(name):
     base = n.split("(")[0]
     tmpl = base[base.find("<"):] if "<" in base else ""
     base = base.split("<")[0]
-    return base + ("<list>" if "true" in tmpl else "")
+    if base == "nn_filter_kernel" and "true" in tmpl:
+        return base + "<list>"
+    if base.startswith("nn_mfma16") and ("<true" in tmpl or "true>" in tmpl or "Lb1E" in full):
+        return base + "<seeded>"
+    return base
 
 
 def main():
