@@ -145,6 +145,24 @@ def reference_cases_cpu(reps=3):
             for k, v in ms.items()}
 
 
+def grid_nn_rate(device, m, p, steps, warmup=3):
+    """the same C4 iterations with ICP_NN_VARIANT_GRID (exact fp64 search
+    on the model grid, no brute-force filter).  Reported beside the headline, not as it."""
+    with icp_amd.Context(device) as ctx:
+        ctx.set_nn_variant(icp_amd.VARIANT_GRID)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        ctx.run(warmup, -1.0)
+        ctx.reset_stats()
+        t0 = time.perf_counter()
+        _, errs = ctx.run(steps, -1.0)
+        dt = time.perf_counter() - t0
+        st = ctx.stats()
+    return {"iterations_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps,
+            "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1), "brute_force_fallbacks": st["grid_fallback"],
+            "final_err": float(errs[-1]), "kernel": "nn_grid_search_kernel"}
+
+
 def csv_io(m):
     """load.cc:3-97 at C4 size: write the model (ostream %g rows) and load it back
     (sscanf %lf rows) with the product's parallel exact parser / formatter."""
@@ -188,7 +206,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--nn", choices=["certified", "fp64"], default="certified")
-    ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16"], default="auto")
+    ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16", "grid"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
     ap.add_argument("--no-cases", action="store_true", help="skip the reference's 14 benchmark cases")
@@ -218,7 +236,7 @@ def main():
         ctx = icp_amd.Context(local, nn_mode)
 
     variant = {"auto": icp_amd.VARIANT_AUTO, "valu": icp_amd.VARIANT_VALU, "mfma": icp_amd.VARIANT_MFMA,
-               "mfma16": icp_amd.VARIANT_MFMA16}[args.variant]
+               "mfma16": icp_amd.VARIANT_MFMA16, "grid": icp_amd.VARIANT_GRID}[args.variant]
     ctx.set_nn_variant(variant)
     m, p = icp_amd.synthetic_pair(args.n, seed=42)
     b, c = icp_amd.shard_range(args.n, rank, world)
@@ -255,6 +273,8 @@ def main():
     # timed iterations are seeded (the first icp_run iteration after set_scene is warm-up)
     kernel = {"mfma16": "nn_mfma16p_kernel<seeded>", "mfma": "nn_mfma_kernel"}.get(
         level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
+    if args.variant == "grid":
+        kernel = "nn_grid_search_kernel"
     traffic, traffic_src = pmc_traffic(kernel) if world == 1 and args.n == 1 << 20 else (None, None)
     dtype = {"mfma16": "f16 hi/lo-split MFMA filter (fp32 accumulate); fp64 certificate, resolve and reductions",
              "mfma": "f32 MFMA filter; fp64 certificate, resolve and reductions"}.get(
@@ -295,11 +315,24 @@ def main():
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
         }
+        if args.variant == "grid":
+            # no brute-force filter: the grid search streams queries and the model points
+            # near each one; algorithmic bytes = 24 (query) + 4 (index) per query + the
+            # model's 32-byte grid records once
+            gbytes = 28.0 * c + 32.0 * args.n
+            ach = gbytes / (nn_avg_ms * 1e-3) / 1e9 if nn_avg_ms > 0 else 0.0
+            out["roofline"] = {"bound": "hbm", "kernel": kernel, "achieved": ach, "peak": 8000.0,
+                               "unit": "GB/s", "frac": ach / 8000.0, "traffic": None,
+                               "avg_launch_ms": nn_avg_ms, "bytes_per_launch": gbytes,
+                               "note": "latency-bound gather search; compulsory bytes only"}
+            out["dtype"] = "f64"
         if world == 1 and not args.no_cow:
             out["cow_frame_rate"] = cow_frame_rate(local)
         if world == 1 and not args.no_cases:
             out["reference_cases"] = reference_cases_gpu()
             out["csv_io"] = csv_io(m)
+            if args.variant != "grid" and args.nn == "certified":
+                out["grid_nn"] = grid_nn_rate(local, m, p, args.steps)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(m, p)
             if not args.no_cases:

@@ -49,12 +49,17 @@ extern "C" {
  * MFMA:   expanded form |m|^2 - 2 p.m on v_mfma_f32_16x16x4_f32 (256 pairs / instruction);
  * MFMA16: the same form on v_mfma_f32_32x32x16_f16 with hi/lo f16 splits (1024 pairs /
  *         instruction, co-executes with the VALU);
- * MFMA and MFMA16 send uncertified queries to the VALU filter, then to fp64.
+ * All filters send uncertified queries to an exact fp64 search on a uniform model grid,
+ * then (boxes over budget) to the VALU filter and fp64 brute force.
+ * GRID:   no brute-force filter: exact fp64 search on the model grid for every query
+ *         (same first-minimum rule, same results); O(N) instead of
+ *         O(N*M) for clouds whose nearest neighbours are local.
  * AUTO:   MFMA16 when both clouds have >= 65536 points, else VALU. */
 #define ICP_NN_VARIANT_AUTO 0
 #define ICP_NN_VARIANT_VALU 1
 #define ICP_NN_VARIANT_MFMA 2
 #define ICP_NN_VARIANT_MFMA16 3
+#define ICP_NN_VARIANT_GRID 4
 
 typedef struct icp_ctx icp_ctx;
 

@@ -235,7 +235,7 @@ int level1_kind(const icp_ctx *ctx, size_t n)
 {
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return 1;
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA16) return 2;
-    if (ctx->nn_variant == ICP_NN_VARIANT_VALU) return 0;
+    if (ctx->nn_variant == ICP_NN_VARIANT_VALU || ctx->nn_variant == ICP_NN_VARIANT_GRID) return 0;
     return (n >= 65536 && ctx->nm >= 65536) ? 2 : 0;
 }
 
@@ -272,6 +272,39 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
         launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
         HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
         LAUNCHCHK("nn_fp64");
+    } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
+        // exact grid search for every query; over-budget boxes -> VALU list filter -> fp64
+        TRY(ensure_queue(ctx, n));
+        TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
+        TRY(grow(ctx, &ctx->fb_seed, &ctx->fb_seed_cap, n));
+        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
+        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1,
+                              ctx->fb_list, ctx->fb_seed, ctx->st);
+        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        LAUNCHCHK("nn_grid_search");
+        HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        const int cfb = ctx->h_amb[1];
+        ctx->stats.grid_fallback += cfb;
+        if (cfb > 0) {
+            const NNPlan p2l = plan_nn32_list((size_t)cfb, ctx->nm_pad);
+            TRY(grow(ctx, (char **)&ctx->part2, &ctx->part2_cap,
+                     (size_t)p2l.splits * cfb * (2 * sizeof(float) + sizeof(int))));
+            float *qb = (float *)ctx->part2;
+            float *qs = qb + (size_t)p2l.splits * cfb;
+            int *qi = (int *)(qs + (size_t)p2l.splits * cfb);
+            launch_nn_filter(q.f, ctx->fb_list, ctx->fb_seed, cfb, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi,
+                             ctx->st);
+            CertParams cp{ctx->rm};
+            launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->fb_list, cfb, cp, ctx->idx, ctx->amb_count,
+                               ctx->amb_list, ctx->amb_T, nullptr, ctx->st);
+            launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, cfb, ctx->idx, ctx->st);
+        }
+        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
+        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        LAUNCHCHK("nn_grid fallback");
     } else if (const int l1 = level1_kind(ctx, n)) {
         // level 1: MFMA expanded-form filter over every query
         const bool sd = seeded && l1 == 2;
@@ -387,7 +420,7 @@ void account_nn(icp_ctx *ctx, size_t n)
     if (ctx->nn_mode == ICP_NN_CERTIFIED && n) {
         ctx->stats.ambiguous += ctx->h_amb[0];
         if (level1_kind(ctx, n)) ctx->stats.level1_queued += ctx->level1_queued;
-        else ctx->stats.grid_fallback += ctx->h_amb[1];
+        else if (ctx->nn_variant != ICP_NN_VARIANT_GRID) ctx->stats.grid_fallback += ctx->h_amb[1];
     }
 }
 
@@ -555,7 +588,7 @@ const char *icp_last_error(const icp_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int icp_set_nn_variant(icp_ctx *ctx, int variant)
 {
-    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_MFMA16) return ICP_E_ARG;
+    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_GRID) return ICP_E_ARG;
     ctx->nn_variant = variant;
     return ICP_OK;
 }

@@ -177,6 +177,94 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     }
 }
 
+// Exact grid NN for every query (ICP_NN_VARIANT_GRID).  Candidate: the (D64, index) best of
+// the smallest cube of cells around the query's (clamped) cell that holds a point; then the
+// complete box around that candidate, exactly as in nn_grid_resolve_kernel.  Either step
+// over `budget` cells -> the query goes to the brute-force levels (seed +inf).
+__global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
+    int np, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
+    float *__restrict__ fb_seed)
+{
+    for (int j = blockIdx.x * kBlock + threadIdx.x; j < np; j += gridDim.x * kBlock) {
+        const double q[3] = {px[j], py[j], pz[j]};
+        int c[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) c[a] = cell1(q[a], gv.lo[a], gv.inv_h, gv.g[a]);
+        double best = INFINITY;
+        int bi = -1;
+        bool ok = true;
+        // 1) rings: cube [c - r, c + r] (clamped) until it holds a point
+        for (int r = 0; bi < 0; ++r) {
+            int c0[3], c1[3];
+            long long cells = 1;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                c0[a] = max(c[a] - r, 0);
+                c1[a] = min(c[a] + r, gv.g[a] - 1);
+                cells *= (long long)(c1[a] - c0[a] + 1);
+            }
+            if (cells > budget) {
+                ok = false;
+                break;
+            }
+            for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                    const int row = (cz * gv.g[1] + cy) * gv.g[0];
+                    const int k1 = gv.start[row + c1[0] + 1];
+                    for (int k = gv.start[row + c0[0]]; k < k1; ++k) {
+                        const double4 m = gv.pts[k];
+                        const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
+                        const int mi = (int)m.w;
+                        if (d < best || (d == best && mi < bi)) {
+                            best = d;
+                            bi = mi;
+                        }
+                    }
+                }
+            if (c0[0] == 0 && c0[1] == 0 && c0[2] == 0 && c1[0] == gv.g[0] - 1 && c1[1] == gv.g[1] - 1 &&
+                c1[2] == gv.g[2] - 1)
+                break; // the whole grid (bi >= 0 unless the model is empty)
+        }
+        // 2) the complete box around the candidate (see the header)
+        if (ok && bi >= 0) {
+            const double R = sqrt(best);
+            int c0[3], c1[3];
+            long long cells = 1;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const double s = (fabs(q[a]) + R) * 0x1.0p-44;
+                c0[a] = cell1(q[a] - (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
+                c1[a] = cell1(q[a] + (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
+                cells *= (long long)(c1[a] - c0[a] + 1);
+            }
+            ok = cells <= budget;
+            if (ok)
+                for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                    for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                        const int row = (cz * gv.g[1] + cy) * gv.g[0];
+                        const int k1 = gv.start[row + c1[0] + 1];
+                        for (int k = gv.start[row + c0[0]]; k < k1; ++k) {
+                            const double4 m = gv.pts[k];
+                            const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
+                            const int mi = (int)m.w;
+                            if (d < best || (d == best && mi < bi)) {
+                                best = d;
+                                bi = mi;
+                            }
+                        }
+                    }
+        }
+        ok = ok && bi >= 0;
+        if (ok) idx[j] = bi;
+        const int slot = wave_append(fb_count, !ok);
+        if (!ok) {
+            fb_list[slot] = j;
+            fb_seed[slot] = INFINITY;
+        }
+    }
+}
+
 } // namespace
 
 GridParams grid_params(const double *m_xyz, size_t nm)
@@ -241,6 +329,13 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
     scan_blocks_kernel<<<1, 1, 0, st>>>(bsum, nb);
     scan_add_kernel<<<nb, kScanThreads, 0, st>>>(start, n, bsum);
     grid_scatter_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, cid, start, fill, pts);
+}
+
+void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
+                           int budget, int *idx, int *fb_count, int *fb_list, float *fb_seed, hipStream_t st)
+{
+    const int blocks = std::max(1, std::min((np + kBlock - 1) / kBlock, 8192));
+    nn_grid_search_kernel<<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_seed);
 }
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,

@@ -131,6 +131,11 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             int *idx, int *fb_count, int *fb_list, const float *seed_in,
                             float *seed_out, const double *T_in, double *T_out, hipStream_t st);
 
+// Exact grid NN of all np queries (ICP_NN_VARIANT_GRID): idx, or fb_list (+ fb_seed = +inf)
+// for the queries whose ring or box would exceed `budget` cells.
+void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
+                           int budget, int *idx, int *fb_count, int *fb_list, float *fb_seed, hipStream_t st);
+
 // ---- streaming reductions (deterministic two-stage, fp64) --------------------------
 int red_blocks(size_t n);
 // y = m[idx]; partial [sum p (3), sum y (3)]

@@ -45,6 +45,7 @@ VARIANT_AUTO = 0
 VARIANT_VALU = 1
 VARIANT_MFMA = 2
 VARIANT_MFMA16 = 3
+VARIANT_GRID = 4  # exact grid NN for every query
 
 # every function include/icp_capi.h declares (checked by tests/test_capi.py)
 EXPORTED = [

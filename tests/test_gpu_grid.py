@@ -11,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 RNG = np.random.default_rng(2024)
-CERTIFIED = {"valu": 1, "mfma": 2, "mfma16": 3}
+CERTIFIED = {"valu": 1, "mfma": 2, "mfma16": 3, "grid": 4}
 
 
 @pytest.fixture(scope="module")
@@ -96,3 +96,13 @@ def test_grid_takes_the_near_ties_at_c4(amd):
     idx, st = search(amd, "mfma16", m, p)
     assert st["level1_queued"] > 0, st
     assert st["grid_fallback"] <= max(16, st["level1_queued"] // 1000), st
+
+
+def test_grid_variant_at_c4_matches_fp64_and_rarely_falls_back(amd):
+    m, p = amd.synthetic_pair(1 << 18, seed=11)
+    idx, st = search(amd, "grid", m, p)
+    with amd.Context(0, amd.NN_FP64) as ctx:
+        ctx.set_model(m)
+        _, ref = ctx.closest_matrix(p)
+    np.testing.assert_array_equal(idx, ref)
+    assert st["grid_fallback"] <= 16, st
