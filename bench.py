@@ -221,6 +221,10 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")  # control plane only; the data path is RCCL in the engine
     import torch
+    # one GPU per rank; fewer GPUs than ranks happens only in the gloo rehearsal
+    ndev = icp_amd.device_count()
+    if ndev > 0 and local >= ndev:
+        local = local % ndev
 
     def barrier_sync():
         if dist is not None:
@@ -228,7 +232,15 @@ def main():
         torch.cuda.synchronize(local)
 
     nn_mode = icp_amd.NN_CERTIFIED if args.nn == "certified" else icp_amd.NN_FP64
-    if world > 1:
+    if world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1":
+        # rehearsal of the multi-rank flow where RCCL cannot run (several ranks on one GPU):
+        # the engine's sums go through gloo instead; timing and results are otherwise the same
+        def host_allreduce(buf):
+            t = torch.from_numpy(buf.copy())
+            dist.all_reduce(t)
+            buf[:] = t.numpy()
+        ctx = icp_amd.Context(local, nn_mode, rank, world, host_allreduce=host_allreduce)
+    elif world > 1:
         obj = [icp_amd.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx = icp_amd.Context(local, nn_mode, rank, world, obj[0])
@@ -296,7 +308,9 @@ def main():
             "data": "synthetic (mt19937_64 seed 42, uniform [-1,1]^3; scene = 5deg rotation + translation)",
             "config": {"workload": f"C4 synthetic {args.n}-pt model vs rigid-transformed copy, fixed iterations",
                        "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
-                       "parallelism": f"scene-sharded x{world}, model replicated, RCCL all-reduce of 18 fp64 sums/iter"},
+                       "parallelism": f"scene-sharded x{world}, model replicated, "
+                                      + ("gloo host all-reduce (rehearsal)" if os.environ.get("ICP_BENCH_HOST_REDUCE") == "1" and world > 1
+                                         else "RCCL all-reduce") + " of 18 fp64 sums/iter"},
             "roofline": {"bound": "mfma",
                          "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + 2 VALU/pair min tracking",
                                           "mfma": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)"}.get(
