@@ -5,7 +5,7 @@
 // which here is the oracle (test infrastructure): bench.py times those in its cpu_baseline
 // leg.
 //
-//   icp-bench [--ref PATH] [--scene PATH] [--min-time SECONDS] [--json] [--cold]
+//   icp-bench [--ref PATH] [--scene PATH] [--min-time SECONDS] [--json] [--cold] [--only NAME]
 //
 // Inputs follow the reference's parameter functions (bench.cc:241-389), quirks included:
 //  * gpu_find_alignment, gpu_err_compute*: Y = Matrix::Zero (bench.cc:270-276, 378-388);
@@ -60,8 +60,11 @@ struct Result {
 };
 
 // google-benchmark style: run until min_time has elapsed (at least one timed iteration)
+std::string g_only; // --only: run just this case
+
 Result run_case(const std::string &name, double min_time, const std::function<void()> &body)
 {
+    if (!g_only.empty() && name != g_only) return {name, 0.0, 0};
     body(); // warm-up (first-launch costs)
     long it = 0;
     const auto t0 = std::chrono::steady_clock::now();
@@ -81,6 +84,7 @@ int main(int argc, char **argv)
     std::string ref = "data_students/cow_ref.txt", scene = "data_students/cow_tr1.txt";
     double min_time = 0.5;
     bool json = false, cold = false;
+    std::string only;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         if (a == "--ref" && i + 1 < argc) ref = argv[++i];
@@ -88,11 +92,13 @@ int main(int argc, char **argv)
         else if (a == "--min-time" && i + 1 < argc) min_time = std::atof(argv[++i]);
         else if (a == "--json") json = true;
         else if (a == "--cold") cold = true;
+        else if (a == "--only" && i + 1 < argc) only = argv[++i];
         else {
             std::fprintf(stderr, "usage: icp-bench [--ref PATH] [--scene PATH] [--min-time S] [--json] [--cold]\n");
             return 2;
         }
     }
+    g_only = only;
     Cloud m, p;
     if (!load(ref.c_str(), m) || !load(scene.c_str(), p)) {
         std::fprintf(stderr, "[icp-bench] cannot read %s / %s\n", ref.c_str(), scene.c_str());
@@ -176,14 +182,19 @@ int main(int argc, char **argv)
     if (json) {
         std::printf("{\"ref\": \"%s\", \"scene\": \"%s\", \"opti_iterations\": %d, \"naive_iterations\": %d, \"cases\": {",
                     ref.c_str(), scene.c_str(), res.iterations, naive_iters);
-        for (size_t i = 0; i < out.size(); ++i)
-            std::printf("%s\"%s\": {\"ms\": %.6g, \"iterations\": %ld, \"frame_rate\": %.6g}", i ? ", " : "",
+        bool first = true;
+        for (size_t i = 0; i < out.size(); ++i) {
+            if (!out[i].iterations) continue;
+            std::printf("%s\"%s\": {\"ms\": %.6g, \"iterations\": %ld, \"frame_rate\": %.6g}", first ? "" : ", ",
                         out[i].name.c_str(), out[i].ms, out[i].iterations, 1e3 / out[i].ms);
+            first = false;
+        }
         std::printf("}}\n");
     } else {
         std::printf("%-40s %14s %12s %s\n", "Benchmark", "Time", "Iterations", "UserCounters...");
         for (const auto &r : out)
-            std::printf("%-40s %11.4g ms %12ld frame_rate=%.6g/s\n", (r.name + "/real_time").c_str(), r.ms,
+            if (r.iterations)
+                std::printf("%-40s %11.4g ms %12ld frame_rate=%.6g/s\n", (r.name + "/real_time").c_str(), r.ms,
                         r.iterations, 1e3 / r.ms);
     }
     return 0;

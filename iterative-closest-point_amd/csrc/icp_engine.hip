@@ -13,12 +13,14 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "icp_horn.h"
 #include "icp_kernels.h"
 
 using namespace icp;
@@ -53,7 +55,6 @@ struct icp_ctx {
     double scale16 = 1.0;    // power of two: max |b_s| in [2^11, 2^12)
     size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0, mimg16_cap = 0, mms16_cap = 0;
     int nn_variant = ICP_NN_VARIANT_AUTO;
-    int level1_queued = 0; // queries the last MFMA pass could not certify
     double c[3] = {0, 0, 0}; // centring point = model centroid
     double rm = 0.0;         // max |centred fp32 model coordinate|
     bool has_model = false;
@@ -82,6 +83,13 @@ struct icp_ctx {
     int *g_cid = nullptr, *g_count = nullptr, *g_start = nullptr, *g_bsum = nullptr, *g_fill = nullptr;
     double4 *g_pts = nullptr;
     size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
+    IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
+    size_t iter_state_cap = 0;
+    IterState *h_iter = nullptr;     // pinned copy
+    int *h_flags = nullptr;          // pinned (done, iter) per in-flight iteration
+    double *err_trace_dev = nullptr;
+    size_t err_trace_cap = 0;
+    std::vector<hipEvent_t> iter_ev; // per-iteration (begin, end) of the O(N*M) kernel
     double4 *m4 = nullptr;      // model as (x, y, z, 0) doubles: one read per random gather
     size_t m4_cap = 0;
     unsigned *seed16 = nullptr; // seeded f16 filter: per-query shift (icp_run iterations >= 2)
@@ -252,59 +260,40 @@ GridView grid_view(const icp_ctx *ctx)
     return gv;
 }
 
-// NN search of the n queries in q against the resident model -> ctx->idx[0..n).
-// Timed with HIP events on the context stream (ev[0]..ev[1] = the O(N*M) kernel).
-// seeded: ctx->idx holds a previous correspondence of each of these n queries (icp_run)
-int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
+// Launches the complete NN search of the n queries in q against the resident model ->
+// ctx->idx, with no host synchronisation: every level is sized on the device.  Queue sizes:
+// amb_count [0] queue of the VALU certificate, [1] grid -> fp64 brute-force fallback,
+// [2] level-1 (MFMA) queue, [3] level-1 queries without a candidate.  ev0..ev1 brackets the
+// O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
+int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     if (!n) return ICP_OK;
+    TRY(ensure_queue(ctx, n));
+    HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
     if (ctx->nn_mode == ICP_NN_FP64) {
         const NNPlan pl = plan_nn64(n, ctx->nm);
         const size_t need = (size_t)pl.splits * n * (sizeof(double) + sizeof(int));
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap, need));
         double *pb = (double *)ctx->part;
         int *pi = (int *)(pb + (size_t)pl.splits * n);
-        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_fp64(q.x, q.y, q.z, (int)n, ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm,
                        pl, pb, pi, ctx->st);
-        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
-        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
         LAUNCHCHK("nn_fp64");
     } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
-        // exact grid search for every query; over-budget boxes -> VALU list filter -> fp64
-        TRY(ensure_queue(ctx, n));
+        // exact grid search for every query; over-budget boxes -> fp64 brute force per query
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
-        TRY(grow(ctx, &ctx->fb_seed, &ctx->fb_seed_cap, n));
-        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
-        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
+        HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1,
-                              ctx->fb_list, ctx->fb_seed, ctx->st);
-        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+                              ctx->fb_list, ctx->fb_T, ctx->st);
+        HIPCHK(hipEventRecord(ev1, ctx->st));
+        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_grid_search");
-        HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-        HIPCHK(hipStreamSynchronize(ctx->st));
-        const int cfb = ctx->h_amb[1];
-        ctx->stats.grid_fallback += cfb;
-        if (cfb > 0) {
-            const NNPlan p2l = plan_nn32_list((size_t)cfb, ctx->nm_pad);
-            TRY(grow(ctx, (char **)&ctx->part2, &ctx->part2_cap,
-                     (size_t)p2l.splits * cfb * (2 * sizeof(float) + sizeof(int))));
-            float *qb = (float *)ctx->part2;
-            float *qs = qb + (size_t)p2l.splits * cfb;
-            int *qi = (int *)(qs + (size_t)p2l.splits * cfb);
-            launch_nn_filter(q.f, ctx->fb_list, ctx->fb_seed, cfb, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi,
-                             ctx->st);
-            CertParams cp{ctx->rm};
-            launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->fb_list, cfb, cp, ctx->idx, ctx->amb_count,
-                               ctx->amb_list, ctx->amb_T, nullptr, ctx->st);
-            launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, cfb, ctx->idx, ctx->st);
-        }
-        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
-        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-        LAUNCHCHK("nn_grid fallback");
     } else if (const int l1 = level1_kind(ctx, n)) {
         // level 1: MFMA expanded-form filter over every query
         const bool sd = seeded && l1 == 2;
@@ -320,63 +309,33 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
         float *pb = (float *)ctx->part;
         float *ps = pb + (size_t)pl.splits * n;
         int *pi = (int *)(ps + (size_t)pl.splits * n);
-        TRY(ensure_queue(ctx, n));
         TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
         TRY(grow(ctx, &ctx->amb1_seed, &ctx->amb1_seed_cap, n));
         TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
-        TRY(grow(ctx, &ctx->fb_seed, &ctx->fb_seed_cap, n));
-        // amb_count: [0] level-2 -> fp64 queue, [1] grid -> level-2 fallback, [2] level-1 queue,
-        // [3] level-1 queries without a candidate
-        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
-        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
+        HIPCHK(hipEventRecord(ev0, ctx->st));
         if (l1 == 2)
             launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, seeds, ctx->mimg16, (int)ctx->nm_pad,
                              pl, pb, ps, pi, ctx->st);
         else
             launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
-        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        HIPCHK(hipEventRecord(ev1, ctx->st));
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
-                                      ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed,
-                                      ctx->amb1_hint, q.f, ctx->m32, ctx->rm, ctx->st);
+                                      ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
+                                      ctx->amb1_seed, ctx->amb1_hint, q.f, ctx->m32, ctx->rm, ctx->st);
         else
-            launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx,
-                                    ctx->amb_count + 2, ctx->amb1, ctx->amb1_seed, ctx->amb1_hint, ctx->m32,
-                                    ctx->rm, ctx->st);
-        // exact resolution of the near ties through the model grid, around each candidate
+            launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx, ctx->amb_count + 2,
+                                    ctx->amb1, ctx->amb1_seed, ctx->amb1_hint, ctx->m32, ctx->rm, ctx->st);
+        // exact resolution of the near ties through the model grid, around each candidate;
+        // what it cannot take (none at C4): fp64 over every model point, one workgroup each
         launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
-                               grid_view(ctx), kGridBudget,
-                               ctx->idx, ctx->amb_count + 1, ctx->fb_list, ctx->amb1_seed, ctx->fb_seed,
-                               nullptr, nullptr, ctx->st);
+                               grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
+                               nullptr, nullptr, ctx->fb_T, ctx->st);
+        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_mfma");
-        HIPCHK(hipMemcpyAsync(ctx->h_amb + 1, ctx->amb_count + 1, sizeof(int) * 3, hipMemcpyDeviceToHost, ctx->st));
-        HIPCHK(hipStreamSynchronize(ctx->st));
-        const int c1 = ctx->h_amb[2], cfb = ctx->h_amb[1];
-        ctx->stats.level1_unrecovered += ctx->h_amb[3];
-        ctx->stats.grid_fallback += cfb;
-        ctx->level1_queued = c1;
-        if (cfb > 0) {
-            // level 2: direct-form fp32 filter on what the grid handed back
-            const NNPlan p2l = plan_nn32_list((size_t)cfb, ctx->nm_pad);
-            TRY(grow(ctx, (char **)&ctx->part2, &ctx->part2_cap,
-                     (size_t)p2l.splits * cfb * (2 * sizeof(float) + sizeof(int))));
-            float *qb = (float *)ctx->part2;
-            float *qs = qb + (size_t)p2l.splits * cfb;
-            int *qi = (int *)(qs + (size_t)p2l.splits * cfb);
-            launch_nn_filter(q.f, ctx->fb_list, ctx->fb_seed, cfb, ctx->m32, (int)ctx->nm_pad, p2l, qb, qs, qi,
-                             ctx->st);
-            CertParams cp{ctx->rm};
-            launch_nn_finalize(qb, qs, qi, p2l.splits, q.f, ctx->fb_list, cfb, cp, ctx->idx, ctx->amb_count,
-                               ctx->amb_list, ctx->amb_T, nullptr, ctx->st);
-            // level 3: exact fp64 on the candidates of what is still open
-            launch_nn_resolve(ctx->amb_count, ctx->amb_list, ctx->amb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, cfb, ctx->idx,
-                              ctx->st);
-        }
-        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
-        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-        LAUNCHCHK("nn_mfma levels 2-3");
     } else {
         const NNPlan pl = plan_nn32(n, ctx->nm_pad);
         const size_t need = (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int));
@@ -384,33 +343,44 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded = false)
         float *pb = (float *)ctx->part;
         float *ps = pb + (size_t)pl.splits * n;
         int *pi = (int *)(ps + (size_t)pl.splits * n);
-        TRY(ensure_queue(ctx, n));
         TRY(grow(ctx, &ctx->amb_hint, &ctx->amb_hint_cap, n));
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
-        HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 2, ctx->st));
-        HIPCHK(hipEventRecord(ctx->ev[0], ctx->st));
+        HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_filter(q.f, nullptr, nullptr, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
-        HIPCHK(hipEventRecord(ctx->ev[1], ctx->st));
+        HIPCHK(hipEventRecord(ev1, ctx->st));
         CertParams cp{ctx->rm};
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, nullptr, (int)n, cp, ctx->idx, ctx->amb_count,
                            ctx->amb_list, ctx->amb_T, ctx->amb_hint, ctx->st);
         // near ties: exact through the model grid; what it cannot take, fp64 brute force
+        // (sized on the device: no host round trip on this path)
         launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z, ctx->m4,
-                               grid_view(ctx), kGridBudget,
-                               ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr, nullptr, ctx->amb_T,
-                               ctx->fb_T, ctx->st);
+                               grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
+                               nullptr, ctx->amb_T, ctx->fb_T, ctx->st);
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx,
-                          ctx->st);
-        HIPCHK(hipEventRecord(ctx->ev[2], ctx->st));
-        HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int) * 2, hipMemcpyDeviceToHost, ctx->st));
+                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_certified");
     }
     return ICP_OK;
 }
 
-// after the stream has been synchronised: fold the NN events and queue sizes into the stats
+// queue sizes of the last search -> pinned h_amb (the caller synchronises)
+int nn_counts_to_host(icp_ctx *ctx)
+{
+    HIPCHK(hipMemcpyAsync(ctx->h_amb, ctx->amb_count, sizeof(int) * 4, hipMemcpyDeviceToHost, ctx->st));
+    return ICP_OK;
+}
+
+// NN search for the per-operation surface: queues the counts to h_amb; the caller
+// synchronises, then calls account_nn.
+int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
+{
+    TRY(nn_search_begin(ctx, q, n, false, ctx->ev[0], ctx->ev[1]));
+    return n ? nn_counts_to_host(ctx) : ICP_OK;
+}
+
+// after the stream has been synchronised (h_amb holds the last search's final counts): fold
+// the NN events and queue sizes into the stats
 void account_nn(icp_ctx *ctx, size_t n)
 {
     float ms = 0.f;
@@ -419,8 +389,9 @@ void account_nn(icp_ctx *ctx, size_t n)
     ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
     if (ctx->nn_mode == ICP_NN_CERTIFIED && n) {
         ctx->stats.ambiguous += ctx->h_amb[0];
-        if (level1_kind(ctx, n)) ctx->stats.level1_queued += ctx->level1_queued;
-        else if (ctx->nn_variant != ICP_NN_VARIANT_GRID) ctx->stats.grid_fallback += ctx->h_amb[1];
+        ctx->stats.grid_fallback += ctx->h_amb[1];
+        ctx->stats.level1_queued += ctx->h_amb[2];
+        ctx->stats.level1_unrecovered += ctx->h_amb[3];
     }
 }
 
@@ -574,10 +545,14 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
-                    (void *)ctx->fb_seed, (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4})
+                    (void *)ctx->fb_seed, (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
+                    (void *)ctx->iter_state, (void *)ctx->err_trace_dev})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
+    if (ctx->h_iter) (void)hipHostFree(ctx->h_iter);
+    if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+    for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -711,6 +686,31 @@ int icp_get_scene(icp_ctx *ctx, double *p_xyz_out)
     return download_cloud(ctx, ctx->scene, ctx->scene.n, p_xyz_out);
 }
 
+// moments of one iteration, all on the device: Y = m[idx]; sum p, sum y [all-reduce 6];
+// centred S, d_caps, sp around the all-reduced centroids [all-reduce 11]
+static int moments_phase(icp_ctx *ctx, size_t n)
+{
+    const DevCloud &P = ctx->scene, &Y = ctx->Y;
+    const int nb = red_blocks(n);
+    launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, ctx->partials, ctx->st);
+    launch_reduce(ctx->partials, nb, 6, ctx->sums + kSumP, ctx->st);
+    LAUNCHCHK("moments");
+    TRY(allreduce(ctx, ctx->sums + kSumP, 6));
+    launch_centred_moments(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, ctx->sums, (double)ctx->np_total, ctx->partials,
+                           ctx->st);
+    launch_reduce(ctx->partials, nb, 11, ctx->sums + kSumS, ctx->st);
+    LAUNCHCHK("centred_moments");
+    return allreduce(ctx, ctx->sums + kSumS, 11);
+}
+
+// The loop of GPU::ICP::find_corresponding_opti (gpu.cc:52-83), device-resident: every
+// iteration is enqueued without waiting on the previous one -- NN search, moments and their
+// all-reduces, the Horn solve (horn_step, the host's own code), transform + residual and its
+// all-reduce, the error test (err_step).  The host runs one iteration ahead: it enqueues
+// iteration i+1, then waits for iteration i's completion event and its (done, iter) flag.
+// After the iteration whose err < threshold the device flag freezes the state (the one
+// iteration already enqueued behind it changes nothing), which is exactly where the
+// reference's loop breaks (gpu.cc:79-80).
 int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res)
 {
     TRY(check_ready(ctx, true));
@@ -723,63 +723,83 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     const size_t n = ctx->scene.n;
     const double N = (double)ctx->np_total;
     DevCloud &P = ctx->scene, &Y = ctx->Y;
+    constexpr int kAhead = 1, kRing = 4; // iterations in flight beyond the one waited on
+    TRY(grow(ctx, &ctx->iter_state, &ctx->iter_state_cap, 1));
+    if (!ctx->h_iter) HIPCHK(hipHostMalloc((void **)&ctx->h_iter, sizeof(IterState), hipHostMallocDefault));
+    if (!ctx->h_flags) HIPCHK(hipHostMalloc((void **)&ctx->h_flags, sizeof(int) * 2 * kRing, hipHostMallocDefault));
+    TRY(grow(ctx, &ctx->err_trace_dev, &ctx->err_trace_cap, (size_t)(max_iter > 0 ? max_iter : 1)));
+    while (ctx->iter_ev.size() < 3 * (size_t)kRing) { // (nn begin, nn end, iteration done) per slot
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        ctx->iter_ev.push_back(e);
+    }
+    HIPCHK(hipMemsetAsync(ctx->iter_state, 0, sizeof(IterState), ctx->st));
+    IterState *sd = ctx->iter_state;
+    int enqueued = 0, waited = 0, recorded = 0;
+    bool stop = false;
+    while (!stop && waited < max_iter) {
+        if (enqueued < max_iter && enqueued - waited <= kAhead) {
+            const int slot = enqueued % kRing;
+            // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
+            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]));
+            ctx->seeds_valid = true; // idx pairs every point of the resident scene
+            launch_count_step(ctx->amb_count, sd, ctx->st);
+            // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142)
+            TRY(moments_phase(ctx, n));
+            // 4. Horn solve (gpu.cc:106-146) on the device
+            launch_horn_step(ctx->sums, N, ctx->c, sd, ctx->st);
+            // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
+            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f, ctx->partials,
+                                     ctx->st);
+            launch_reduce(ctx->partials, red_blocks(n), 1, ctx->sums + kSumErr, ctx->st);
+            LAUNCHCHK("transform_err");
+            TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
+            // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
+            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->st);
+            LAUNCHCHK("err_step");
+            HIPCHK(hipMemcpyAsync(ctx->h_flags + 2 * slot, &sd->done, sizeof(int) * 2, hipMemcpyDeviceToHost,
+                                  ctx->st)); // (done, iter)
+            HIPCHK(hipEventRecord(ctx->iter_ev[3 * slot + 2], ctx->st));
+            ++enqueued;
+            continue;
+        }
+        const int slot = waited % kRing;
+        HIPCHK(hipEventSynchronize(ctx->iter_ev[3 * slot + 2]));
+        ++waited;
+        const int done = ctx->h_flags[2 * slot], iters = ctx->h_flags[2 * slot + 1];
+        if (iters > recorded) { // this iteration counted: its NN kernel time
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess)
+                ctx->stats.nn_ms += ms;
+            ctx->stats.nn_launches += 1;
+            ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
+            recorded = iters;
+        }
+        stop = done != 0;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->h_iter, sd, sizeof(IterState), hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    const IterState &hs = *ctx->h_iter;
     icp_result r{};
-    r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55)
+    r.iterations = hs.iter;
+    r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55) when no iteration ran
     r.R[0] = r.R[4] = r.R[8] = 1.0;
-    for (int it = 0; it < max_iter; ++it) {
-        // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
-        TRY(nn_search(ctx, P, n, ctx->seeds_valid));
-        ctx->seeds_valid = true; // idx now pairs every point of the resident scene
-        // 2. centroids (gpu.cc:98-99): sum p, sum y   [+ RCCL all-reduce, 6 doubles]
-        const int nb = red_blocks(n);
-        launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z,
-                              (int)n, Y.x, Y.y, Y.z, ctx->partials, ctx->st);
-        launch_reduce(ctx->partials, nb, 6, ctx->sums + kSumP, ctx->st);
-        LAUNCHCHK("moments");
-        TRY(allreduce(ctx, ctx->sums + kSumP, 6));
-        // 3. centred cross-covariance + norms (gpu.cc:101-104, :142) [+ all-reduce, 11]
-        launch_centred_moments(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, ctx->sums, N, ctx->partials,
-                               ctx->st);
-        launch_reduce(ctx->partials, nb, 11, ctx->sums + kSumS, ctx->st);
-        LAUNCHCHK("centred_moments");
-        TRY(allreduce(ctx, ctx->sums + kSumS, 11));
-        HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * kSumErr, hipMemcpyDeviceToHost,
-                              ctx->st));
-        HIPCHK(hipStreamSynchronize(ctx->st));
-        account_nn(ctx, n);
-
-        // 4. host Horn solve (gpu.cc:106-146)
-        const double *h = ctx->h_sums;
-        const double mu_p[3] = {h[kSumP] / N, h[kSumP + 1] / N, h[kSumP + 2] / N};
-        const double mu_y[3] = {h[kSumY] / N, h[kSumY + 1] / N, h[kSumY + 2] / N};
-        horn_solve(h + kSumS, mu_p, mu_y, h[kSumDcaps], h[kSumSp], &r.s, r.R, r.t);
-
-        // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2.
-        //    find_alignment's own residual (gpu.cc:148) is the identical sum, so
-        //    err = (e + e) / np exactly.
-        Xform xf;
-        for (int k = 0; k < 9; ++k) xf.sR[k] = r.s * r.R[k];
-        for (int k = 0; k < 3; ++k) {
-            xf.t[k] = r.t[k];
-            xf.c[k] = ctx->c[k];
-        }
-        launch_transform_err(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, xf, 1, P.f, ctx->partials, ctx->st);
-        launch_reduce(ctx->partials, nb, 1, ctx->sums + kSumErr, ctx->st);
-        LAUNCHCHK("transform_err");
-        TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
-        HIPCHK(hipMemcpyAsync(ctx->h_sums + kSumErr, ctx->sums + kSumErr, sizeof(double),
-                              hipMemcpyDeviceToHost, ctx->st));
-        HIPCHK(hipStreamSynchronize(ctx->st));
-        const double e = ctx->h_sums[kSumErr];
-        const double err = (e + e) / N; // gpu.cc:71-76
-        if (err_trace) err_trace[it] = err;
-        r.err = err;
-        r.iterations = it + 1;
-        ctx->stats.iterations += 1;
-        if (err < threshold) { // gpu.cc:79-80
-            r.converged = 1;
-            break;
-        }
+    if (hs.iter > 0) {
+        std::vector<double> tr((size_t)hs.iter);
+        HIPCHK(hipMemcpy(tr.data(), ctx->err_trace_dev, sizeof(double) * tr.size(), hipMemcpyDeviceToHost));
+        if (err_trace) std::memcpy(err_trace, tr.data(), sizeof(double) * tr.size());
+        r.err = tr.back();
+        r.converged = r.err < threshold ? 1 : 0;
+        r.s = hs.srt[0];
+        for (int k = 0; k < 9; ++k) r.R[k] = hs.srt[1 + k];
+        for (int k = 0; k < 3; ++k) r.t[k] = hs.srt[10 + k];
+    }
+    ctx->stats.iterations += hs.iter;
+    if (ctx->nn_mode == ICP_NN_CERTIFIED) {
+        ctx->stats.ambiguous += hs.nn_counts[0];
+        ctx->stats.grid_fallback += hs.nn_counts[1];
+        ctx->stats.level1_queued += hs.nn_counts[2];
+        ctx->stats.level1_unrecovered += hs.nn_counts[3];
     }
     ctx->stats.iter_ms +=
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();

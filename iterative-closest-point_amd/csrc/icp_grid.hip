@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
         if (!ok) {
             fb_list[slot] = j;
             if (seed_in) seed_out[slot] = seed_in[t];
-            if (T_in) T_out[slot] = T_in[t];
+            if (T_out) T_out[slot] = T_in ? T_in[t] : INFINITY; // +inf: every model point
         }
     }
 }
@@ -180,11 +180,11 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
 // Exact grid NN for every query (ICP_NN_VARIANT_GRID).  Candidate: the (D64, index) best of
 // the smallest cube of cells around the query's (clamped) cell that holds a point; then the
 // complete box around that candidate, exactly as in nn_grid_resolve_kernel.  Either step
-// over `budget` cells -> the query goes to the brute-force levels (seed +inf).
+// over `budget` cells -> the query goes to the fp64 brute force (window T = +inf).
 __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
     int np, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
-    float *__restrict__ fb_seed)
+    double *__restrict__ fb_T)
 {
     for (int j = blockIdx.x * kBlock + threadIdx.x; j < np; j += gridDim.x * kBlock) {
         const double q[3] = {px[j], py[j], pz[j]};
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
         const int slot = wave_append(fb_count, !ok);
         if (!ok) {
             fb_list[slot] = j;
-            fb_seed[slot] = INFINITY;
+            fb_T[slot] = INFINITY; // exact fp64 over every model point (nn_resolve_kernel)
         }
     }
 }
@@ -332,10 +332,10 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 }
 
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
-                           int budget, int *idx, int *fb_count, int *fb_list, float *fb_seed, hipStream_t st)
+                           int budget, int *idx, int *fb_count, int *fb_list, double *fb_T, hipStream_t st)
 {
     const int blocks = std::max(1, std::min((np + kBlock - 1) / kBlock, 8192));
-    nn_grid_search_kernel<<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_seed);
+    nn_grid_search_kernel<<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
 }
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,

@@ -10,9 +10,6 @@
 namespace icp {
 
 // ---- host-only (icp_host.cpp) ------------------------------------------------
-void largest_eigvec_sym4(const double N[16], double q[4], double evals[4]);
-void horn_solve(const double S[9], const double mu_p[3], const double mu_y[3], double d_caps,
-                double sp, double *s, double R[9], double t[3]);
 void shard_range(size_t n, int rank, int world, size_t *begin, size_t *count);
 int load_matrix(const char *path, std::vector<double> &xyz, size_t *n_out);
 int write_matrix(const char *path, const double *xyz, size_t n);

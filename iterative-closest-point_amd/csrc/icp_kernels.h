@@ -124,17 +124,18 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
                        double4 *pts, hipStream_t st);
 // For queued query list[t] (t < *count_ptr) with candidate hint[t]: exact fp64 first minimum
 // over the grid box that must contain every point at least as close as the candidate ->
-// idx; hint < 0 or a box over `budget` cells -> appended to fb_list (with its seed / T).
+// idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its seed (if
+// seed_in) and its window T_in, or T = +inf without T_in (if T_out).
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget,
                             int *idx, int *fb_count, int *fb_list, const float *seed_in,
                             float *seed_out, const double *T_in, double *T_out, hipStream_t st);
 
-// Exact grid NN of all np queries (ICP_NN_VARIANT_GRID): idx, or fb_list (+ fb_seed = +inf)
+// Exact grid NN of all np queries (ICP_NN_VARIANT_GRID): idx, or fb_list (+ fb_T = +inf)
 // for the queries whose ring or box would exceed `budget` cells.
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
-                           int budget, int *idx, int *fb_count, int *fb_list, float *fb_seed, hipStream_t st);
+                           int budget, int *idx, int *fb_count, int *fb_list, double *fb_T, hipStream_t st);
 
 // ---- streaming reductions (deterministic two-stage, fp64) --------------------------
 int red_blocks(size_t n);
@@ -143,6 +144,8 @@ int red_blocks(size_t n);
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
                            double *partials, hipStream_t st);
+// *out = (double)*cnt (a device count joining an all-reduced vector of sums)
+void launch_count_to_double(const int *cnt, double *out, hipStream_t st);
 void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4,
                       hipStream_t st);
 // partial [sum p (3)] of one cloud
@@ -168,6 +171,30 @@ struct Xform {
 void launch_transform_err(double *px, double *py, double *pz, const double *yx, const double *yy,
                           const double *yz, int n, Xform xf, int write_p, float4 *p32,
                           double *partials, hipStream_t st);
+// same, the transform read from device memory (the device Horn solve); a no-op once *done
+void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
+                              const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
+                              double *partials, hipStream_t st);
+
+// ---- device-resident ICP iteration (icp_iter.hip) -----------------------------------
+// Per-run device state: done flag, iterations recorded, error trace, last (s, R, t),
+// the transform for launch_transform_err_dev, NN queue-size totals.
+struct IterState {
+    int done;          // the loop has converged: later iterations change nothing
+    int iter;          // iterations recorded in err_trace
+    double srt[13];    // s, R (row-major), t of the last applied iteration
+    Xform xf;          // s R, t, c for the transform kernel
+    long long nn_counts[4]; // sums of amb_count[0..3] over the recorded searches
+};
+// (1 thread) Horn solve from the reduced sums (icp_horn.h), unless done
+void launch_horn_step(const double *sums, double n_total, const double c[3], IterState *st_dev, hipStream_t st);
+// (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold
+// or iter == max_iter
+void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
+                     IterState *st_dev, hipStream_t st);
+// (1 thread) nn_counts += amb_count[0..3], unless done
+void launch_count_step(const int *amb_count, IterState *st_dev, hipStream_t st);
+
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);
 

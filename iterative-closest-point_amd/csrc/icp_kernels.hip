@@ -1235,8 +1235,20 @@ __global__ __launch_bounds__(kBlock) void norms_kernel(
 __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
-    int n, Xform xf, int write_p, float4 *__restrict__ p32, double *__restrict__ partials)
+    int n, Xform xfv, const Xform *__restrict__ xfd, const int *__restrict__ done, int write_p,
+    float4 *__restrict__ p32, double *__restrict__ partials)
 {
+    // xfd / done (device-resident loop): the transform comes from the device Horn solve, and
+    // nothing is applied once the loop has converged.  One load per workgroup, via LDS.
+    __shared__ Xform sxf;
+    __shared__ int sdone;
+    if (threadIdx.x == 0) {
+        sdone = done ? *done : 0;
+        sxf = xfd ? *xfd : xfv;
+    }
+    __syncthreads();
+    if (sdone) return;
+    const Xform xf = sxf;
     double a[1] = {0.0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const double p0 = px[i], p1 = py[i], p2 = pz[i];
@@ -1582,6 +1594,16 @@ __global__ __launch_bounds__(kBlock) void make_aos4_kernel(const double *__restr
         m4[i] = make_double4(x[i], y[i], z[i], 0.0);
 }
 
+__global__ void count_to_double_kernel(const int *__restrict__ cnt, double *__restrict__ out)
+{
+    *out = (double)*cnt;
+}
+
+void launch_count_to_double(const int *cnt, double *out, hipStream_t st)
+{
+    count_to_double_kernel<<<1, 1, 0, st>>>(cnt, out);
+}
+
 void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4, hipStream_t st)
 {
     make_aos4_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, m4);
@@ -1618,7 +1640,15 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                           const double *yz, int n, Xform xf, int write_p, float4 *p32,
                           double *partials, hipStream_t st)
 {
-    transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, write_p,
+    transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
+                                                            write_p, p32, partials);
+}
+
+void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
+                              const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
+                              double *partials, hipStream_t st)
+{
+    transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done, 1,
                                                             p32, partials);
 }
 

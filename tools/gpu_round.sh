@@ -55,6 +55,10 @@ for s in $STEPS; do
     test16plain) ICP_MFMA16_KERNEL=plain run pytest_gpu_plain 900 python -m pytest tests -m gpu -q -rf -k "mfma16 or grid or sharded" ;;
     dist2) ICP_BENCH_HOST_REDUCE=1 run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 10 --warmup 2 ;;
+    profcow) COW=$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_ref"), datasets.path("cow_tr1"))')
+           set -- $COW
+           run rocprof_cow 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_cow" -o cow -- \
+               ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.3 --only opti_gpu_loop ;;
     sqseed) run sqs1 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE \
                 --output-format csv -d "$OUT/sqs1" -o sq -- python3 tools/nn_probe.py --variant mfma16 --icp 4 &&
             run sqs2 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE \
