@@ -73,8 +73,7 @@ struct icp_ctx {
     void *part = nullptr, *part2 = nullptr;
     size_t part_cap = 0, part2_cap = 0;
     int *amb1 = nullptr;           // queue of the MFMA certificate
-    float *amb1_seed = nullptr;    // ... and each queued query's level-2 seed
-    size_t amb1_cap = 0, amb1_seed_cap = 0;
+    size_t amb1_cap = 0;
     int *amb_count = nullptr, *amb_list = nullptr;
     double *amb_T = nullptr;
     size_t amb_cap = 0;
@@ -97,13 +96,13 @@ struct icp_ctx {
     bool seeds_valid = false;   // idx holds the previous search over the resident scene
     int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
     int *fb_list = nullptr;                           // queries the grid hands back
-    float *fb_seed = nullptr;
     double *fb_T = nullptr;
-    size_t amb1_hint_cap = 0, amb_hint_cap = 0, fb_list_cap = 0, fb_seed_cap = 0, fb_T_cap = 0;
+    size_t amb1_hint_cap = 0, amb_hint_cap = 0, fb_list_cap = 0, fb_T_cap = 0;
 
     // reductions
     double *partials = nullptr;
     double *sums = nullptr;
+    unsigned *red_counter = nullptr; // last-workgroup reductions of the loop kernels (3 words)
     double *h_sums = nullptr; // pinned
     int *h_amb = nullptr;     // pinned
     double *stage = nullptr;
@@ -214,6 +213,8 @@ int ensure_reduction_space(icp_ctx *ctx)
     if (ctx->partials) return ICP_OK;
     HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocks * 12));
     HIPCHK(hipMalloc((void **)&ctx->sums, sizeof(double) * 32));
+    HIPCHK(hipMalloc((void **)&ctx->red_counter, sizeof(unsigned) * 4));
+    HIPCHK(hipMemset(ctx->red_counter, 0, sizeof(unsigned) * 4));
     HIPCHK(hipHostMalloc((void **)&ctx->h_sums, sizeof(double) * 32, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));
     return ICP_OK;
@@ -265,12 +266,14 @@ GridView grid_view(const icp_ctx *ctx)
 // amb_count [0] queue of the VALU certificate, [1] grid -> fp64 brute-force fallback,
 // [2] level-1 (MFMA) queue, [3] level-1 queries without a candidate.  ev0..ev1 brackets the
 // O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
-int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1)
+// zero_counts = false: amb_count is already zero (icp_run: err_step clears it)
+int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
+                    bool zero_counts = true)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     if (!n) return ICP_OK;
     TRY(ensure_queue(ctx, n));
-    HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
+    if (zero_counts) HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
     if (ctx->nn_mode == ICP_NN_FP64) {
         const NNPlan pl = plan_nn64(n, ctx->nm);
         const size_t need = (size_t)pl.splits * n * (sizeof(double) + sizeof(int));
@@ -310,7 +313,6 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         float *ps = pb + (size_t)pl.splits * n;
         int *pi = (int *)(ps + (size_t)pl.splits * n);
         TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
-        TRY(grow(ctx, &ctx->amb1_seed, &ctx->amb1_seed_cap, n));
         TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
@@ -324,15 +326,15 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
-                                      ctx->amb1_seed, ctx->amb1_hint, q.f, ctx->m32, ctx->rm, ctx->st);
+                                      ctx->amb1_hint, ctx->st);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx, ctx->amb_count + 2,
-                                    ctx->amb1, ctx->amb1_seed, ctx->amb1_hint, ctx->m32, ctx->rm, ctx->st);
+                                    ctx->amb1, ctx->amb1_hint, ctx->st);
         // exact resolution of the near ties through the model grid, around each candidate;
         // what it cannot take (none at C4): fp64 over every model point, one workgroup each
         launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                                grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
-                               nullptr, nullptr, ctx->fb_T, ctx->st);
+                               ctx->fb_T, ctx->st);
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_mfma");
@@ -347,16 +349,16 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         HIPCHK(hipEventRecord(ev0, ctx->st));
-        launch_nn_filter(q.f, nullptr, nullptr, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         HIPCHK(hipEventRecord(ev1, ctx->st));
         CertParams cp{ctx->rm};
-        launch_nn_finalize(pb, ps, pi, pl.splits, q.f, nullptr, (int)n, cp, ctx->idx, ctx->amb_count,
-                           ctx->amb_list, ctx->amb_T, ctx->amb_hint, ctx->st);
+        launch_nn_finalize(pb, ps, pi, pl.splits, q.f, (int)n, cp, ctx->idx, ctx->amb_count, ctx->amb_list,
+                           ctx->amb_T, ctx->amb_hint, ctx->st);
         // near ties: exact through the model grid; what it cannot take, fp64 brute force
         // (sized on the device: no host round trip on this path)
         launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z, ctx->m4,
-                               grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
-                               nullptr, ctx->amb_T, ctx->fb_T, ctx->st);
+                               grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list,
+                               ctx->amb_T, ctx->fb_T, ctx->st);
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_certified");
@@ -538,14 +540,14 @@ void icp_ctx_destroy(icp_ctx *ctx)
     free_cloud(ctx->Y);
     free_cloud(ctx->qa);
     free_cloud(ctx->qb);
-    for (void *p : {(void *)ctx->amb1_seed, (void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
+    for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
-                    (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
+                    (void *)ctx->sums, (void *)ctx->red_counter, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
-                    (void *)ctx->fb_seed, (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
+                    (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
@@ -741,21 +743,21 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         if (enqueued < max_iter && enqueued - waited <= kAhead) {
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
-            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]));
+            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1],
+                                enqueued == 0));
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
-            launch_count_step(ctx->amb_count, sd, ctx->st);
             // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142)
             TRY(moments_phase(ctx, n));
             // 4. Horn solve (gpu.cc:106-146) on the device
             launch_horn_step(ctx->sums, N, ctx->c, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
             launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f, ctx->partials,
-                                     ctx->st);
+                                     nullptr, nullptr, ctx->st);
             launch_reduce(ctx->partials, red_blocks(n), 1, ctx->sums + kSumErr, ctx->st);
             LAUNCHCHK("transform_err");
             TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
-            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->st);
+            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, ctx->amb_count, sd, ctx->st);
             LAUNCHCHK("err_step");
             HIPCHK(hipMemcpyAsync(ctx->h_flags + 2 * slot, &sd->done, sizeof(int) * 2, hipMemcpyDeviceToHost,
                                   ctx->st)); // (done, iter)

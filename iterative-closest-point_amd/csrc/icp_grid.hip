@@ -124,9 +124,8 @@ __global__ __launch_bounds__(kBlock) void grid_scatter_kernel(
 __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
-    const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
-    const float *__restrict__ seed_in, float *__restrict__ seed_out,
-    const double *__restrict__ T_in, double *__restrict__ T_out)
+    const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count,
+    int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out)
 {
     const int count = *count_ptr;
     for (int t = blockIdx.x * kBlock + threadIdx.x; t < count; t += gridDim.x * kBlock) {
@@ -171,8 +170,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
         const int slot = wave_append(fb_count, !ok);
         if (!ok) {
             fb_list[slot] = j;
-            if (seed_in) seed_out[slot] = seed_in[t];
-            if (T_out) T_out[slot] = T_in ? T_in[t] : INFINITY; // +inf: every model point
+            T_out[slot] = T_in ? T_in[t] : INFINITY; // +inf: every model point
         }
     }
 }
@@ -340,14 +338,12 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
-                            const GridView &gv, int budget,
-                            int *idx, int *fb_count, int *fb_list, const float *seed_in,
-                            float *seed_out, const double *T_in, double *T_out, hipStream_t st)
+                            const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
+                            const double *T_in, double *T_out, hipStream_t st)
 {
     const int blocks = std::max(1, std::min((max_items + kBlock - 1) / kBlock, 2048));
-    nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv,
-                                                      budget, idx, fb_count, fb_list, seed_in, seed_out,
-                                                      T_in, T_out);
+    nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
+                                                      fb_count, fb_list, T_in, T_out);
 }
 
 } // namespace icp

@@ -19,6 +19,7 @@ void synthetic_pair(uint64_t seed, size_t n, double angle_deg, const double axis
 // ---- NN kernel geometry (icp_kernels.hip) -----------------------------------------
 constexpr int kBlock = 256;   // threads per workgroup (4 waves of 64)
 constexpr int kTile32 = 1024; // model points per LDS tile, fp32 filter (16 KiB)
+constexpr int kTileSmall = 128; // ... for small models (more model splits per search)
 constexpr int kTile64 = 512;  // model points per LDS tile, fp64 path (16 KiB)
 constexpr int kSub = 32;      // sub-block granularity of the running-argmin bookkeeping
 constexpr int kRedMaxBlocks = 1024; // max workgroups of a streaming reduction pass

@@ -44,23 +44,19 @@ struct NNPlan {
     int qblocks;    // workgroups along the query axis
     int splits;     // workgroups along the model axis
     int chunk;      // model points per split (multiple of the tile)
+    int tile = 0;   // LDS tile of the VALU filter when not the default (kTileSmall)
 };
 NNPlan plan_nn32(size_t np, size_t nm_pad);
 NNPlan plan_nn64(size_t np, size_t nm_pad);
-NNPlan plan_nn32_list(size_t count, size_t nm_pad);
 
-// fp32 direct-form filter: partial (best, second, argbest) per (split, slot); slot s is
-// query s, or query list[s] when list != nullptr.
-// seed (list mode, nullable): initial `second` per slot from the level-1 candidate
-void launch_nn_filter(const float4 *p32, const int *list, const float *seed, int nslots,
-                      const float4 *m32, int nm_pad, const NNPlan &plan, float *part_best,
-                      float *part_second, int *part_idx, hipStream_t st);
-// merge splits, certify, write idx for certified queries, queue the rest (with window T).
-// amb_hint (nullable): the queued query's fp32 winner, the grid resolver's candidate
+// fp32 direct-form filter: partial (best, second, argbest) per (split, query)
+void launch_nn_filter(const float4 *p32, int nslots, const float4 *m32, int nm_pad, const NNPlan &plan,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st);
+// merge splits, certify, write idx for certified queries, queue the rest (window T, and the
+// fp32 winner in amb_hint: the grid resolver's candidate).
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
-                        int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
-                        int *idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint,
-                        hipStream_t st);
+                        int splits, const float4 *p32, int nslots, CertParams cp, int *idx, int *amb_count,
+                        int *amb_list, double *amb_T, int *amb_hint, hipStream_t st);
 // MFMA expanded-form filter (G = |m|^2 - 2 p.m) and its certificate; uncertified queries
 // are appended to amb_list (no window: they go through the direct-form filter next).
 constexpr int kMfmaQG = 4; // 16-query groups per wave
@@ -69,8 +65,7 @@ void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, 
                     float *part_best, float *part_second, int *part_idx, hipStream_t st);
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
                              int splits, const float4 *p32, int np, const float *mm, int *idx,
-                             int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
-                             const float4 *m32, double rm, hipStream_t st);
+                             int *amb_count, int *amb_list, int *amb_hint, hipStream_t st);
 // f16 split-precision MFMA filter (v_mfma_f32_32x32x16_f16): model image (1 KiB per 32
 // points) built once per model; uncertified queries appended to amb_list.
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded);
@@ -86,8 +81,8 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
-                               const float *mms, int *idx, int *amb_count, int *amb_list, float *amb_seed,
-                               int *amb_hint, const float4 *p32, const float4 *m32, double rm, hipStream_t st);
+                               const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
+                               hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
@@ -124,13 +119,12 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
                        double4 *pts, hipStream_t st);
 // For queued query list[t] (t < *count_ptr) with candidate hint[t]: exact fp64 first minimum
 // over the grid box that must contain every point at least as close as the candidate ->
-// idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its seed (if
-// seed_in) and its window T_in, or T = +inf without T_in (if T_out).
+// idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its window T_in[t]
+// (T = +inf without T_in: every model point) for nn_resolve.
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
-                            const GridView &gv, int budget,
-                            int *idx, int *fb_count, int *fb_list, const float *seed_in,
-                            float *seed_out, const double *T_in, double *T_out, hipStream_t st);
+                            const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
+                            const double *T_in, double *T_out, hipStream_t st);
 
 // Exact grid NN of all np queries (ICP_NN_VARIANT_GRID): idx, or fb_list (+ fb_T = +inf)
 // for the queries whose ring or box would exceed `budget` cells.
@@ -141,9 +135,11 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 int red_blocks(size_t n);
 // y = m[idx]; partial [sum p (3), sum y (3)]
 // m4: the model as (x, y, z, 0) double4 (one 32-byte read per gathered point)
+// counter / out (optional): fold the partials into out[0..K) in the kernel (last workgroup)
+// instead of a following launch_reduce; counter = a zeroed device word per call site
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
-                           double *partials, hipStream_t st);
+                           double *partials, hipStream_t st, unsigned *counter = nullptr, double *out = nullptr);
 // *out = (double)*cnt (a device count joining an all-reduced vector of sums)
 void launch_count_to_double(const int *cnt, double *out, hipStream_t st);
 void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4,
@@ -155,7 +151,7 @@ void launch_sum3(const double *x, const double *y, const double *z, int n, doubl
 void launch_centred_moments(const double *px, const double *py, const double *pz,
                             const double *yx, const double *yy, const double *yz, int n,
                             const double *sums, double n_total, double *partials,
-                            hipStream_t st);
+                            hipStream_t st, unsigned *counter = nullptr, double *out = nullptr);
 // p' = p - mu in place (substract_col)
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
                      hipStream_t st);
@@ -174,7 +170,7 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, hipStream_t st);
+                              double *partials, unsigned *counter, double *out, hipStream_t st);
 
 // ---- device-resident ICP iteration (icp_iter.hip) -----------------------------------
 // Per-run device state: done flag, iterations recorded, error trace, last (s, R, t),
@@ -189,11 +185,9 @@ struct IterState {
 // (1 thread) Horn solve from the reduced sums (icp_horn.h), unless done
 void launch_horn_step(const double *sums, double n_total, const double c[3], IterState *st_dev, hipStream_t st);
 // (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold
-// or iter == max_iter
+// or iter == max_iter; nn_counts += amb_count[0..3] (unless done), then amb_count = 0
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
-                     IterState *st_dev, hipStream_t st);
-// (1 thread) nn_counts += amb_count[0..3], unless done
-void launch_count_step(const int *amb_count, IterState *st_dev, hipStream_t st);
+                     int *amb_count, IterState *st_dev, hipStream_t st);
 
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);

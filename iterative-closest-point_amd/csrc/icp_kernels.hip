@@ -88,16 +88,6 @@ template <class V> __device__ __forceinline__ float min16_nocanon(const V &d)
     return fminf(fminf(fminf(a, b), c), fminf(fminf(e, f), d[15]));
 }
 
-// Level-2 seed for a query proposed m_hint by level 1: X = T(D32(m_hint)) (+ slack).  The
-// final window T(best) <= X since best <= D32(m_hint) and T is increasing, so a `second`
-// capped at X is conservative (second > T still implies uniqueness).
-__device__ float seed_from_hint(float4 p, const float4 *__restrict__ m32, int hint, double rm)
-{
-    if (hint < 0) return INFINITY;
-    const double X = cert_window(d32(p.x, p.y, p.z, m32[hint]), p, rm);
-    return (float)(X * (1.0 + 0x1.0p-20)) * (1.0f + 0x1.0p-20f);
-}
-
 // Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
 // out[k].  Fixed shuffle tree + fixed LDS order: deterministic.
 template <int K>
@@ -117,6 +107,38 @@ __device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
         const int k = threadIdx.x;
         out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
     }
+}
+
+// The workgroup that finishes last folds every workgroup's K partials into out[0..K) in
+// reduce_kernel's fixed order (so the sums are bitwise those of the two-launch version),
+// then re-arms the counter.  counter == nullptr: nothing (a separate reduce_kernel follows).
+template <int K>
+__device__ __forceinline__ void last_block_reduce(const double *partials, unsigned *counter, double *out)
+{
+    if (!counter) return;
+    __shared__ unsigned ticket;
+    __shared__ double shr[kBlock];
+    __threadfence(); // this workgroup's partials are visible before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) ticket = atomicAdd(counter, 1u);
+    __syncthreads();
+    if (ticket != gridDim.x - 1) return;
+    __threadfence();
+    const volatile double *vp = partials; // written by other workgroups: read past L1
+    const int nblocks = (int)gridDim.x;
+    for (int k = 0; k < K; ++k) {
+        double a = 0.0;
+        for (int b = threadIdx.x; b < nblocks; b += kBlock) a += vp[(size_t)b * K + k];
+        shr[threadIdx.x] = a;
+        __syncthreads();
+        for (int st = kBlock / 2; st > 0; st >>= 1) {
+            if (threadIdx.x < st) shr[threadIdx.x] += shr[threadIdx.x + st];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[k] = shr[0];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *counter = 0u;
 }
 
 // ---- layout ------------------------------------------------------------------------
@@ -158,18 +180,19 @@ __global__ __launch_bounds__(kBlock) void make_f32_kernel(const double *__restri
 }
 
 // ---- NN: fp32 filter ----------------------------------------------------------------
-// grid = (qblocks, splits).  Lane owns Q query slots (s = blockIdx.x*256*Q + q*256 + tid);
-// slot s is query s, or query list[s] when LIST (second-level filter of the queries the
-// MFMA certificate could not settle).  The workgroup streams its model chunk through a
-// 1024-point LDS tile; every lane reads the same model point (LDS broadcast: one
-// ds_read_b96 feeds 64*Q pairs).  Per pair: 3 v_sub + v_mul + 2 v_fma + v_min + v_med3.
-template <int Q, bool LIST>
+// grid = (qblocks, splits).  Lane owns Q queries (s = blockIdx.x*256*Q + q*256 + tid).  The
+// workgroup streams its model chunk through a 1024-point LDS tile; every lane reads the
+// same model point (LDS broadcast: one ds_read_b96 feeds 64*Q pairs).  Per pair: 3 v_sub +
+// v_mul + 2 v_fma, then a v_min3 sub-block minimum; the med3/min update only for sub-blocks
+// whose minimum is below some lane's `second`.
+// TILE = 128 for small models (cow: 2,903 points): the model then splits into 24 chunks
+// instead of 3, so a small search still fills the chip.
+template <int Q, int TILE>
 __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
-    const float4 *__restrict__ p32, const int *__restrict__ list, const float *__restrict__ seed,
-    int nslots, const float4 *__restrict__ m32, int nm_pad, int chunk,
+    const float4 *__restrict__ p32, int nslots, const float4 *__restrict__ m32, int nm_pad, int chunk,
     float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx)
 {
-    __shared__ float4 tile[kTile32];
+    __shared__ float4 tile[TILE];
     const int tid = threadIdx.x;
     const int split = blockIdx.y;
     const int m0 = split * chunk;
@@ -182,24 +205,21 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
     for (int q = 0; q < Q; ++q) {
         const int s = sbase + q * kBlock;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (s < nslots) v = p32[LIST ? list[s] : s];
+        if (s < nslots) v = p32[s];
         px[q] = v.x;
         py[q] = v.y;
         pz[q] = v.z;
         best[q] = INFINITY;
         second[q] = INFINITY;
         bsub[q] = m0;
-        // `second` starts at the level-1 seed X (seed_from_hint): points with D32 >= X can
-        // neither be the answer nor rescue the certificate, so almost every block is skipped
-        if (LIST && seed && s < nslots) second[q] = seed[s];
     }
 
-    for (int t0 = m0; t0 < m1; t0 += kTile32) {
+    for (int t0 = m0; t0 < m1; t0 += TILE) {
         __syncthreads();
 #pragma unroll
-        for (int k = tid; k < kTile32; k += kBlock) tile[k] = m32[t0 + k];
+        for (int k = tid; k < TILE; k += kBlock) tile[k] = m32[t0 + k];
         __syncthreads();
-        for (int sb = 0; sb < kTile32; sb += kSub) {
+        for (int sb = 0; sb < TILE; sb += kSub) {
             // pass 1: sub-block minimum only (v_min3: half an op per pair)
             float tmin[Q];
 #pragma unroll
@@ -232,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         int found = bsub[q];
-        if (best[q] < INFINITY) { // (seeded list searches: most splits find nothing)
+        if (best[q] < INFINITY) {
 #pragma unroll 8 // (a full unroll keeps 32 loads = 96 VGPRs in flight: occupancy /2)
             for (int k = kSub - 1; k >= 0; --k) {
                 const float d = d32(px[q], py[q], pz[q], m32[bsub[q] + k]);
@@ -271,16 +291,14 @@ __device__ __forceinline__ void merge_splits(const float *__restrict__ part_best
     }
 }
 
-template <bool LIST>
 __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
-    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32,
-    const int *__restrict__ list, int nslots, double rm, int *__restrict__ idx, int *amb_count,
-    int *amb_list, double *amb_T, int *amb_hint)
+    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int nslots, double rm,
+    int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint)
 {
     const int s = blockIdx.x * kBlock + threadIdx.x;
     if (s >= nslots) return;
-    const int j = LIST ? list[s] : s;
+    const int j = s;
     float b, s2;
     int id;
     merge_splits(part_best, part_second, part_idx, splits, nslots, s, b, s2, id);
@@ -877,9 +895,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int np, int nm, double cx,
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
-    const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list,
-    float *amb_seed, int *amb_hint, const float4 *__restrict__ p32, const float4 *__restrict__ m32,
-    double rm)
+    const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -912,8 +928,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const int slot = wave_append(amb_count, !ok);
     if (!ok) {
         amb_list[slot] = j;
-        amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
-        amb_hint[slot] = id;                                  // the grid resolver's candidate
+        amb_hint[slot] = id; // the grid resolver's candidate
         if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
@@ -962,8 +977,7 @@ __global__ __launch_bounds__(kBlock) void build_mimage16_kernel(
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
-    const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list,
-    float *amb_seed, int *amb_hint, const float4 *__restrict__ m32, double rm)
+    const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
@@ -988,8 +1002,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     const int slot = wave_append(amb_count, !ok);
     if (!ok) {
         amb_list[slot] = j;
-        amb_seed[slot] = seed_from_hint(p32[j], m32, id, rm); // seeds the level-2 search
-        amb_hint[slot] = id;                                  // the grid resolver's candidate
+        amb_hint[slot] = id; // the grid resolver's candidate
         if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
@@ -1145,7 +1158,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize64_kernel(const double *__r
 __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
-    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials)
+    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials, unsigned *counter,
+    double *out)
 {
     double a[6] = {0, 0, 0, 0, 0, 0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
@@ -1162,6 +1176,7 @@ __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
         a[5] += y2;
     }
     block_sum_store<6>(a, partials + (size_t)blockIdx.x * 6);
+    last_block_reduce<6>(partials, counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__ x,
@@ -1181,7 +1196,8 @@ __global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__
 __global__ __launch_bounds__(kBlock) void centred_moments_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
-    int n, const double *__restrict__ sums, double n_total, double *__restrict__ partials)
+    int n, const double *__restrict__ sums, double n_total, double *__restrict__ partials, unsigned *counter,
+    double *out)
 {
     // mu = rowwise().mean() (gpu.cc:98-99), identical in every thread and on the host
     const double mpx = sums[kSumP] / n_total, mpy = sums[kSumP + 1] / n_total,
@@ -1207,6 +1223,7 @@ __global__ __launch_bounds__(kBlock) void centred_moments_kernel(
         a[10] += (p0 * p0 + p1 * p1) + p2 * p2; // y_p_norm sp     (compute.cu:438-439)
     }
     block_sum_store<11>(a, partials + (size_t)blockIdx.x * 11);
+    last_block_reduce<11>(partials, counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void subtract_kernel(double *x, double *y, double *z, int n,
@@ -1236,7 +1253,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
     int n, Xform xfv, const Xform *__restrict__ xfd, const int *__restrict__ done, int write_p,
-    float4 *__restrict__ p32, double *__restrict__ partials)
+    float4 *__restrict__ p32, double *__restrict__ partials, unsigned *counter, double *out)
 {
     // xfd / done (device-resident loop): the transform comes from the device Horn solve, and
     // nothing is applied once the loop has converged.  One load per workgroup, via LDS.
@@ -1268,6 +1285,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         }
     }
     block_sum_store<1>(a, partials + blockIdx.x);
+    last_block_reduce<1>(partials, counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict__ partials,
@@ -1385,15 +1403,15 @@ static NNPlan make_plan(size_t np, size_t nm, int tile, int q, int queries_per_l
 
 NNPlan plan_nn32(size_t np, size_t nm_pad)
 {
-    return np >= 262144 ? make_plan(np, nm_pad, kTile32, 4, 4 * kBlock, (const void *)nn_filter_kernel<4, false>)
-                        : make_plan(np, nm_pad, kTile32, 1, kBlock, (const void *)nn_filter_kernel<1, false>);
-}
-// second-level (list) search: register-block 4 queries per lane once there are enough to
-// keep the chip busy through model splits
-NNPlan plan_nn32_list(size_t count, size_t nm_pad)
-{
-    return count >= 8192 ? make_plan(count, nm_pad, kTile32, 4, 4 * kBlock, (const void *)nn_filter_kernel<4, true>)
-                         : make_plan(count, nm_pad, kTile32, 1, kBlock, (const void *)nn_filter_kernel<1, true>);
+    if (np >= 262144)
+        return make_plan(np, nm_pad, kTile32, 4, 4 * kBlock, (const void *)nn_filter_kernel<4, kTile32>);
+    NNPlan pl = make_plan(np, nm_pad, kTile32, 1, kBlock, (const void *)nn_filter_kernel<1, kTile32>);
+    const int cap = resident_wgs((const void *)nn_filter_kernel<1, kTile32>);
+    if ((long)pl.qblocks * pl.splits < cap / 2) { // too few workgroups: split the model finer
+        pl = make_plan(np, nm_pad, kTileSmall, 1, kBlock, (const void *)nn_filter_kernel<1, kTileSmall>);
+        pl.tile = kTileSmall;
+    }
+    return pl;
 }
 NNPlan plan_nn64(size_t np, size_t nm)
 {
@@ -1401,35 +1419,28 @@ NNPlan plan_nn64(size_t np, size_t nm)
                         : make_plan(np, nm, kTile64, 1, kBlock, (const void *)nn_fp64_kernel<1>);
 }
 
-void launch_nn_filter(const float4 *p32, const int *list, const float *seed, int nslots,
-                      const float4 *m32, int nm_pad, const NNPlan &pl, float *part_best,
-                      float *part_second, int *part_idx, hipStream_t st)
+void launch_nn_filter(const float4 *p32, int nslots, const float4 *m32, int nm_pad, const NNPlan &pl,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st)
 {
     dim3 grid(pl.qblocks, pl.splits);
-#define LAUNCH_F(Q, L)                                                                          \
-    nn_filter_kernel<Q, L><<<grid, kBlock, 0, st>>>(p32, list, seed, nslots, m32, nm_pad, pl.chunk, \
-                                                    part_best, part_second, part_idx)
-    if (list && pl.q_per_lane == 4) LAUNCH_F(4, true);
-    else if (list) LAUNCH_F(1, true);
-    else if (pl.q_per_lane == 4) LAUNCH_F(4, false);
-    else LAUNCH_F(1, false);
-#undef LAUNCH_F
+    if (pl.q_per_lane == 4)
+        nn_filter_kernel<4, kTile32><<<grid, kBlock, 0, st>>>(p32, nslots, m32, nm_pad, pl.chunk, part_best,
+                                                               part_second, part_idx);
+    else if (pl.tile == kTileSmall)
+        nn_filter_kernel<1, kTileSmall><<<grid, kBlock, 0, st>>>(p32, nslots, m32, nm_pad, pl.chunk, part_best,
+                                                                  part_second, part_idx);
+    else
+        nn_filter_kernel<1, kTile32><<<grid, kBlock, 0, st>>>(p32, nslots, m32, nm_pad, pl.chunk, part_best,
+                                                               part_second, part_idx);
 }
 
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
-                        int splits, const float4 *p32, const int *list, int nslots, CertParams cp,
-                        int *idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint,
-                        hipStream_t st)
+                        int splits, const float4 *p32, int nslots, CertParams cp, int *idx, int *amb_count,
+                        int *amb_list, double *amb_T, int *amb_hint, hipStream_t st)
 {
     const int grid = (nslots + kBlock - 1) / kBlock;
-    if (list)
-        nn_finalize_kernel<true><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32,
-                                                          list, nslots, cp.rm, idx, amb_count,
-                                                          amb_list, amb_T, amb_hint);
-    else
-        nn_finalize_kernel<false><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits,
-                                                           p32, nullptr, nslots, cp.rm, idx,
-                                                           amb_count, amb_list, amb_T, amb_hint);
+    nn_finalize_kernel<<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32, nslots, cp.rm, idx,
+                                                amb_count, amb_list, amb_T, amb_hint);
 }
 
 NNPlan plan_nn_mfma(size_t np, size_t nm_pad)
@@ -1521,28 +1532,26 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
-                               const float *mms, int *idx, int *amb_count, int *amb_list, float *amb_seed,
-                               int *amb_hint, const float4 *p32, const float4 *m32, double rm, hipStream_t st)
+                               const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
+                               hipStream_t st)
 {
     const int grid = (np + kBlock - 1) / kBlock;
     if (seed16)
         nn_finalize_mfma16_kernel<true><<<grid, kBlock, 0, st>>>(
             part_best, part_second, part_idx, splits, px, py, pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,
-            idx, amb_count, amb_list, amb_seed, amb_hint, p32, m32, rm);
+            idx, amb_count, amb_list, amb_hint);
     else
         nn_finalize_mfma16_kernel<false><<<grid, kBlock, 0, st>>>(
             part_best, part_second, part_idx, splits, px, py, pz, np, nm, c[0], c[1], c[2], scale, nullptr, mms,
-            idx, amb_count, amb_list, amb_seed, amb_hint, p32, m32, rm);
+            idx, amb_count, amb_list, amb_hint);
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
                              int splits, const float4 *p32, int np, const float *mm, int *idx,
-                             int *amb_count, int *amb_list, float *amb_seed, int *amb_hint,
-                             const float4 *m32, double rm, hipStream_t st)
+                             int *amb_count, int *amb_list, int *amb_hint, hipStream_t st)
 {
     nn_finalize_mfma_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list, amb_seed,
-        amb_hint, m32, rm);
+        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list, amb_hint);
 }
 
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
@@ -1580,9 +1589,10 @@ int red_blocks(size_t n) { return grid_for(n, kRedMaxBlocks); }
 
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
-                           double *partials, hipStream_t st)
+                           double *partials, hipStream_t st, unsigned *counter, double *out)
 {
-    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials);
+    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials,
+                                                            counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void make_aos4_kernel(const double *__restrict__ x,
@@ -1617,10 +1627,11 @@ void launch_sum3(const double *x, const double *y, const double *z, int n, doubl
 
 void launch_centred_moments(const double *px, const double *py, const double *pz,
                             const double *yx, const double *yy, const double *yz, int n,
-                            const double *sums, double n_total, double *partials, hipStream_t st)
+                            const double *sums, double n_total, double *partials, hipStream_t st,
+                            unsigned *counter, double *out)
 {
     centred_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, sums,
-                                                              n_total, partials);
+                                                              n_total, partials, counter, out);
 }
 
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
@@ -1641,15 +1652,15 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                           double *partials, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
-                                                            write_p, p32, partials);
+                                                            write_p, p32, partials, nullptr, nullptr);
 }
 
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, hipStream_t st)
+                              double *partials, unsigned *counter, double *out, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done, 1,
-                                                            p32, partials);
+                                                            p32, partials, counter, out);
 }
 
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st)
