@@ -102,7 +102,6 @@ struct icp_ctx {
     // reductions
     double *partials = nullptr;
     double *sums = nullptr;
-    unsigned *red_counter = nullptr; // last-workgroup reductions of the loop kernels (3 words)
     double *h_sums = nullptr; // pinned
     int *h_amb = nullptr;     // pinned
     double *stage = nullptr;
@@ -213,11 +212,17 @@ int ensure_reduction_space(icp_ctx *ctx)
     if (ctx->partials) return ICP_OK;
     HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocks * 12));
     HIPCHK(hipMalloc((void **)&ctx->sums, sizeof(double) * 32));
-    HIPCHK(hipMalloc((void **)&ctx->red_counter, sizeof(unsigned) * 4));
-    HIPCHK(hipMemset(ctx->red_counter, 0, sizeof(unsigned) * 4));
     HIPCHK(hipHostMalloc((void **)&ctx->h_sums, sizeof(double) * 32, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));
     return ICP_OK;
+}
+
+// A streaming reduction writes per-workgroup partials, then launch_reduce folds them; a
+// single-workgroup pass (small clouds) writes its K sums straight to `out` instead.
+double *red_target(icp_ctx *ctx, size_t n, double *out) { return red_blocks(n) == 1 ? out : ctx->partials; }
+void red_finish(icp_ctx *ctx, size_t n, int K, double *out)
+{
+    if (red_blocks(n) > 1) launch_reduce(ctx->partials, red_blocks(n), K, out, ctx->st);
 }
 
 // queue of queries the fp32 certificate could not settle (list + window T + counter)
@@ -544,7 +549,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
-                    (void *)ctx->sums, (void *)ctx->red_counter, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
+                    (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
@@ -693,14 +698,13 @@ int icp_get_scene(icp_ctx *ctx, double *p_xyz_out)
 static int moments_phase(icp_ctx *ctx, size_t n)
 {
     const DevCloud &P = ctx->scene, &Y = ctx->Y;
-    const int nb = red_blocks(n);
-    launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, nb, 6, ctx->sums + kSumP, ctx->st);
+    launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, red_target(ctx, n, ctx->sums + kSumP), ctx->st);
+    red_finish(ctx, n, 6, ctx->sums + kSumP);
     LAUNCHCHK("moments");
     TRY(allreduce(ctx, ctx->sums + kSumP, 6));
-    launch_centred_moments(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, ctx->sums, (double)ctx->np_total, ctx->partials,
+    launch_centred_moments(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, ctx->sums, (double)ctx->np_total, red_target(ctx, n, ctx->sums + kSumS),
                            ctx->st);
-    launch_reduce(ctx->partials, nb, 11, ctx->sums + kSumS, ctx->st);
+    red_finish(ctx, n, 11, ctx->sums + kSumS);
     LAUNCHCHK("centred_moments");
     return allreduce(ctx, ctx->sums + kSumS, 11);
 }
@@ -751,9 +755,9 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             // 4. Horn solve (gpu.cc:106-146) on the device
             launch_horn_step(ctx->sums, N, ctx->c, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
-            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f, ctx->partials,
-                                     nullptr, nullptr, ctx->st);
-            launch_reduce(ctx->partials, red_blocks(n), 1, ctx->sums + kSumErr, ctx->st);
+            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f, red_target(ctx, n, ctx->sums + kSumErr),
+                                     ctx->st);
+            red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
             TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
@@ -840,8 +844,8 @@ int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3]
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
     TRY(upload_cloud(ctx, ctx->qa, xyz, n, false));
-    launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, red_blocks(n), 3, ctx->sums, ctx->st);
+    launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, red_target(ctx, n, ctx->sums), ctx->st);
+    red_finish(ctx, n, 3, ctx->sums);
     LAUNCHCHK("sum3");
     HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -863,8 +867,8 @@ int icp_y_p_norm(icp_ctx *ctx, const double *y_xyz, const double *p_xyz, size_t 
     TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
     TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
     launch_norms(ctx->qa.x, ctx->qa.y, ctx->qa.z, ctx->qb.x, ctx->qb.y, ctx->qb.z, (int)n,
-                 ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, red_blocks(n), 2, ctx->sums, ctx->st);
+                 red_target(ctx, n, ctx->sums), ctx->st);
+    red_finish(ctx, n, 2, ctx->sums);
     LAUNCHCHK("norms");
     HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -886,8 +890,8 @@ int icp_err_compute(icp_ctx *ctx, const double *y_xyz, double *p_xyz, size_t n, 
     std::memcpy(xf.t, t, sizeof(xf.t));
     std::memcpy(xf.c, ctx->c, sizeof(xf.c));
     launch_transform_err(ctx->qb.x, ctx->qb.y, ctx->qb.z, ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, xf,
-                         in_place ? 1 : 0, nullptr, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, red_blocks(n), 1, ctx->sums, ctx->st);
+                         in_place ? 1 : 0, nullptr, red_target(ctx, n, ctx->sums), ctx->st);
+    red_finish(ctx, n, 1, ctx->sums);
     LAUNCHCHK("transform_err");
     HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -904,14 +908,13 @@ int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, s
     TRY(ensure_reduction_space(ctx));
     TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
     TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
-    const int nb = red_blocks(n);
-    launch_sum3(ctx->qb.x, ctx->qb.y, ctx->qb.z, (int)n, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, nb, 3, ctx->sums + kSumP, ctx->st);
-    launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, nb, 3, ctx->sums + kSumY, ctx->st);
+    launch_sum3(ctx->qb.x, ctx->qb.y, ctx->qb.z, (int)n, red_target(ctx, n, ctx->sums + kSumP), ctx->st);
+    red_finish(ctx, n, 3, ctx->sums + kSumP);
+    launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, red_target(ctx, n, ctx->sums + kSumY), ctx->st);
+    red_finish(ctx, n, 3, ctx->sums + kSumY);
     launch_centred_moments(ctx->qb.x, ctx->qb.y, ctx->qb.z, ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n,
-                           ctx->sums, (double)n, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, nb, 11, ctx->sums + kSumS, ctx->st);
+                           ctx->sums, (double)n, red_target(ctx, n, ctx->sums + kSumS), ctx->st);
+    red_finish(ctx, n, 11, ctx->sums + kSumS);
     LAUNCHCHK("find_alignment moments");
     HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * kSumErr, hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -927,8 +930,8 @@ int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, s
     std::memcpy(xf.t, t, sizeof(xf.t));
     std::memcpy(xf.c, ctx->c, sizeof(xf.c));
     launch_transform_err(ctx->qb.x, ctx->qb.y, ctx->qb.z, ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, xf,
-                         0, nullptr, ctx->partials, ctx->st);
-    launch_reduce(ctx->partials, nb, 1, ctx->sums + kSumErr, ctx->st);
+                         0, nullptr, red_target(ctx, n, ctx->sums + kSumErr), ctx->st);
+    red_finish(ctx, n, 1, ctx->sums + kSumErr);
     LAUNCHCHK("find_alignment err");
     HIPCHK(hipMemcpyAsync(ctx->h_sums + kSumErr, ctx->sums + kSumErr, sizeof(double),
                           hipMemcpyDeviceToHost, ctx->st));

@@ -135,11 +135,11 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 int red_blocks(size_t n);
 // y = m[idx]; partial [sum p (3), sum y (3)]
 // m4: the model as (x, y, z, 0) double4 (one 32-byte read per gathered point)
-// counter / out (optional): fold the partials into out[0..K) in the kernel (last workgroup)
-// instead of a following launch_reduce; counter = a zeroed device word per call site
+// partials: red_blocks(n) x K doubles, folded by launch_reduce; with red_blocks(n) == 1 the
+// single workgroup's K sums are final (the engine then passes the destination itself)
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
-                           double *partials, hipStream_t st, unsigned *counter = nullptr, double *out = nullptr);
+                           double *partials, hipStream_t st);
 // *out = (double)*cnt (a device count joining an all-reduced vector of sums)
 void launch_count_to_double(const int *cnt, double *out, hipStream_t st);
 void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4,
@@ -151,7 +151,7 @@ void launch_sum3(const double *x, const double *y, const double *z, int n, doubl
 void launch_centred_moments(const double *px, const double *py, const double *pz,
                             const double *yx, const double *yy, const double *yz, int n,
                             const double *sums, double n_total, double *partials,
-                            hipStream_t st, unsigned *counter = nullptr, double *out = nullptr);
+                            hipStream_t st);
 // p' = p - mu in place (substract_col)
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
                      hipStream_t st);
@@ -170,7 +170,7 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, unsigned *counter, double *out, hipStream_t st);
+                              double *partials, hipStream_t st);
 
 // ---- device-resident ICP iteration (icp_iter.hip) -----------------------------------
 // Per-run device state: done flag, iterations recorded, error trace, last (s, R, t),

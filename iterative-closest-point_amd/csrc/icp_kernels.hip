@@ -109,38 +109,6 @@ __device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
     }
 }
 
-// The workgroup that finishes last folds every workgroup's K partials into out[0..K) in
-// reduce_kernel's fixed order (so the sums are bitwise those of the two-launch version),
-// then re-arms the counter.  counter == nullptr: nothing (a separate reduce_kernel follows).
-template <int K>
-__device__ __forceinline__ void last_block_reduce(const double *partials, unsigned *counter, double *out)
-{
-    if (!counter) return;
-    __shared__ unsigned ticket;
-    __shared__ double shr[kBlock];
-    __threadfence(); // this workgroup's partials are visible before its ticket
-    __syncthreads();
-    if (threadIdx.x == 0) ticket = atomicAdd(counter, 1u);
-    __syncthreads();
-    if (ticket != gridDim.x - 1) return;
-    __threadfence();
-    const volatile double *vp = partials; // written by other workgroups: read past L1
-    const int nblocks = (int)gridDim.x;
-    for (int k = 0; k < K; ++k) {
-        double a = 0.0;
-        for (int b = threadIdx.x; b < nblocks; b += kBlock) a += vp[(size_t)b * K + k];
-        shr[threadIdx.x] = a;
-        __syncthreads();
-        for (int st = kBlock / 2; st > 0; st >>= 1) {
-            if (threadIdx.x < st) shr[threadIdx.x] += shr[threadIdx.x + st];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[k] = shr[0];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *counter = 0u;
-}
-
 // ---- layout ------------------------------------------------------------------------
 
 __global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const double *__restrict__ aos,
@@ -1158,8 +1126,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize64_kernel(const double *__r
 __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
-    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials, unsigned *counter,
-    double *out)
+    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials)
 {
     double a[6] = {0, 0, 0, 0, 0, 0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
@@ -1176,7 +1143,6 @@ __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
         a[5] += y2;
     }
     block_sum_store<6>(a, partials + (size_t)blockIdx.x * 6);
-    last_block_reduce<6>(partials, counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__ x,
@@ -1196,8 +1162,7 @@ __global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__
 __global__ __launch_bounds__(kBlock) void centred_moments_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
-    int n, const double *__restrict__ sums, double n_total, double *__restrict__ partials, unsigned *counter,
-    double *out)
+    int n, const double *__restrict__ sums, double n_total, double *__restrict__ partials)
 {
     // mu = rowwise().mean() (gpu.cc:98-99), identical in every thread and on the host
     const double mpx = sums[kSumP] / n_total, mpy = sums[kSumP + 1] / n_total,
@@ -1223,7 +1188,6 @@ __global__ __launch_bounds__(kBlock) void centred_moments_kernel(
         a[10] += (p0 * p0 + p1 * p1) + p2 * p2; // y_p_norm sp     (compute.cu:438-439)
     }
     block_sum_store<11>(a, partials + (size_t)blockIdx.x * 11);
-    last_block_reduce<11>(partials, counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void subtract_kernel(double *x, double *y, double *z, int n,
@@ -1253,7 +1217,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
     int n, Xform xfv, const Xform *__restrict__ xfd, const int *__restrict__ done, int write_p,
-    float4 *__restrict__ p32, double *__restrict__ partials, unsigned *counter, double *out)
+    float4 *__restrict__ p32, double *__restrict__ partials)
 {
     // xfd / done (device-resident loop): the transform comes from the device Horn solve, and
     // nothing is applied once the loop has converged.  One load per workgroup, via LDS.
@@ -1285,7 +1249,6 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         }
     }
     block_sum_store<1>(a, partials + blockIdx.x);
-    last_block_reduce<1>(partials, counter, out);
 }
 
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict__ partials,
@@ -1585,14 +1548,15 @@ void launch_nn_finalize64(const double *part_best, const int *part_idx, int spli
                                                                          splits, np, idx);
 }
 
-int red_blocks(size_t n) { return grid_for(n, kRedMaxBlocks); }
+// up to kRedSingle points one workgroup does the whole pass (and writes the final sums
+// itself, see the engine's red_target): a launch less per reduction for small clouds
+int red_blocks(size_t n) { return n <= (size_t)kRedSingle ? 1 : grid_for(n, kRedMaxBlocks); }
 
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
-                           double *partials, hipStream_t st, unsigned *counter, double *out)
+                           double *partials, hipStream_t st)
 {
-    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials,
-                                                            counter, out);
+    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials);
 }
 
 __global__ __launch_bounds__(kBlock) void make_aos4_kernel(const double *__restrict__ x,
@@ -1627,11 +1591,10 @@ void launch_sum3(const double *x, const double *y, const double *z, int n, doubl
 
 void launch_centred_moments(const double *px, const double *py, const double *pz,
                             const double *yx, const double *yy, const double *yz, int n,
-                            const double *sums, double n_total, double *partials, hipStream_t st,
-                            unsigned *counter, double *out)
+                            const double *sums, double n_total, double *partials, hipStream_t st)
 {
     centred_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, sums,
-                                                              n_total, partials, counter, out);
+                                                              n_total, partials);
 }
 
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
@@ -1652,15 +1615,15 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                           double *partials, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
-                                                            write_p, p32, partials, nullptr, nullptr);
+                                                            write_p, p32, partials);
 }
 
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, unsigned *counter, double *out, hipStream_t st)
+                              double *partials, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done, 1,
-                                                            p32, partials, counter, out);
+                                                            p32, partials);
 }
 
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st)
