@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <type_traits>
 
 namespace icp {
 
@@ -805,6 +806,401 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     }
 }
 
+// min3 trees over MFMA results (fminf pairs fold into v_min3_f32 under -fno-honor-nans)
+__device__ __forceinline__ float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+
+// 16 values -> 2 (7 v_min3)
+__device__ __forceinline__ void tree16(const f32x16_t &d, float &u, float &v)
+{
+    const float a = fmin3(d[0], d[1], d[2]), b = fmin3(d[3], d[4], d[5]), c = fmin3(d[6], d[7], d[8]);
+    const float e = fmin3(d[9], d[10], d[11]), f = fmin3(d[12], d[13], d[14]);
+    u = fmin3(a, b, c);
+    v = fmin3(e, f, d[15]);
+}
+
+// 16 values + the two carried (u, v) -> 2 (8 v_min3)
+__device__ __forceinline__ void tree18(const f32x16_t &d, float &u, float &v)
+{
+    const float a = fmin3(u, d[0], d[1]), b = fmin3(v, d[2], d[3]), c = fmin3(d[4], d[5], d[6]);
+    const float e = fmin3(d[7], d[8], d[9]), f = fmin3(d[10], d[11], d[12]), g = fmin3(d[13], d[14], d[15]);
+    u = fmin3(a, b, c);
+    v = fmin3(e, f, g);
+}
+
+// Unrolled f16 filter (QG = 4, LDS tiles as nn_mfma16_kernel), the default.  The loop is
+// issue-bound (every instruction costs the SIMD ~4 cycles, an MFMA 8, against the MFMA's 32),
+// so this variant strips the per-block instruction count:
+//  * ONE joint min3 tree over the block's 4 x 16 values, carried from MFMA to MFMA (31 v_min3
+//    + v_min + v_cmp = 33 VALU per block, against 4 x 8 per-group trees + 3 to combine them),
+//    tested against s_max = max_q second[q] -- a superset of the per-group tests, so the update
+//    (out of line, per group re-tested) tracks exactly what nn_mfma16p_kernel tracks;
+//  * the 16-block LDS tile fully unrolled: LDS offsets and block ids are immediates, no loop
+//    counter, address arithmetic or back-edge per block, and each tile's last block issues no
+//    dummy MFMA.
+// Same pipelining as nn_mfma16p_kernel (next block's q0 MFMA issued before the last tree).
+// Same values, same (best, second, block) tracking, same outputs.
+template <bool SEEDED>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_mfma16x_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
+    const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
+    float *__restrict__ part_second, int *__restrict__ part_idx)
+{
+    constexpr int QG = 4;
+    __shared__ half8_t tiles[2][kTile16 * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm_pad);
+    const int qbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
+    constexpr int kBlocksPerTile = kTile16 / 32;
+    constexpr int kDmaPerWave = kBlocksPerTile / 4;
+    constexpr float kStart = SEEDED ? 0.0f : INFINITY;
+
+    half8_t bq[QG];
+    float best[QG], second[QG];
+    int bblk[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int j = qbase + q * 32;
+        double a[3] = {0.0, 0.0, 0.0};
+        unsigned sd = 0u;
+        if (j < np) {
+            a[0] = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[1] = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[2] = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+            if (SEEDED) sd = seed16[j];
+        }
+        bq[q] = query_frag(a, h, sd);
+        best[q] = kStart;
+        second[q] = kStart;
+        bblk[q] = m0 >> 5;
+    }
+    float s_max = kStart; // max_q second[q]
+    const f32x16_t zero = {};
+
+    auto issue_tile = [&](int tpt, int buf) {
+#pragma unroll
+        for (int i = 0; i < kDmaPerWave; ++i) {
+            const int blk = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((const void *)(mimg + ((size_t)(tpt >> 5) + blk) * 64 + lane),
+                                             (__attribute__((address_space(3))) void *)&tiles[buf][blk * 64],
+                                             16, 0, 0);
+        }
+    };
+    auto upd1 = [&](int q, const f32x16_t &d, int blk_id) {
+        if (!__any(min16v(d) < second[q])) return;
+        const float prev = best[q];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d[r]);
+            best[q] = min_nocanon(best[q], d[r]);
+        }
+        bblk[q] = best[q] < prev ? blk_id : bblk[q];
+    };
+    // one block: d0, d1 = its q0, q1 results (issued one step earlier); issues the next
+    // block's q0, q1 MFMAs into dn0, dn1 unless LAST.  Every tree reads an MFMA issued >= 2
+    // MFMAs earlier, so no wait states (s_nop) are needed in front of it.
+    auto step = [&](const half8_t &a8, const half8_t &an, f32x16_t &d0, f32x16_t &d1, f32x16_t &dn0,
+                    f32x16_t &dn1, int blk_id, auto last_tag) {
+        constexpr bool LAST = decltype(last_tag)::value;
+        float u, v;
+        const f32x16_t d2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[2], zero, 0, 0, 0);
+        tree16(d0, u, v);
+        const f32x16_t d3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[3], zero, 0, 0, 0);
+        tree18(d1, u, v);
+        if (!LAST) dn0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bq[0], zero, 0, 0, 0);
+        tree18(d2, u, v);
+        if (!LAST) dn1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bq[1], zero, 0, 0, 0);
+        tree18(d3, u, v);
+        const bool need = fminf(u, v) < s_max;
+        // issue order: MFMA d2 | tree d0 | MFMA d3 | tree d1 | MFMA dn0 | tree d2 | MFMA dn1 | tree d3
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+        if (__builtin_expect(__any(need), 0)) {
+            upd1(0, d0, blk_id);
+            upd1(1, d1, blk_id);
+            upd1(2, d2, blk_id);
+            upd1(3, d3, blk_id);
+            s_max = fmaxf(fmaxf(second[0], second[1]), fmaxf(second[2], second[3]));
+        }
+    };
+    using More = std::integral_constant<bool, false>;
+    using Last = std::integral_constant<bool, true>;
+
+    issue_tile(m0, 0);
+    int it = 0;
+    for (int t0 = m0; t0 < m1; t0 += kTile16, ++it) {
+        const int cur = it & 1;
+        if (t0 + kTile16 < m1) {
+            issue_tile(t0 + kTile16, cur ^ 1);
+            __builtin_amdgcn_s_waitcnt(kVmcntDma);
+        } else {
+            __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        }
+        __builtin_amdgcn_s_barrier();
+        const half8_t *tile = tiles[cur];
+        const int blk0 = t0 >> 5;
+        half8_t a0 = tile[lane], a1 = tile[64 + lane];
+        f32x16_t dA0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[0], zero, 0, 0, 0);
+        f32x16_t dA1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[1], zero, 0, 0, 0), dB0, dB1;
+#pragma unroll
+        for (int b = 0; b < kBlocksPerTile - 2; b += 2) {
+            step(a0, a1, dA0, dA1, dB0, dB1, blk0 + b, More{});
+            a0 = tile[(b + 2) * 64 + lane];
+            step(a1, a0, dB0, dB1, dA0, dA1, blk0 + b + 1, More{});
+            a1 = tile[(b + 3) * 64 + lane];
+        }
+        step(a0, a1, dA0, dA1, dB0, dB1, blk0 + kBlocksPerTile - 2, More{});
+        step(a1, a0, dB0, dB1, dA0, dA1, blk0 + kBlocksPerTile - 1, Last{});
+        __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+        __builtin_amdgcn_s_barrier();
+    }
+
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const float b = best[q];
+        const float s2 = second[q];
+        const int blk = bblk[q];
+        int found = -1;
+        bool done = !(b < kStart);
+        for (int guard = 0; guard < 64; ++guard) {
+            const unsigned long long pend = __ballot(!done);
+            if (pend == 0ull) break;
+            const int lead = __ffsll((long long)pend) - 1;
+            const int rb = __shfl(blk, lead, 64);
+            const half8_t a8 = mimg[(size_t)rb * 64 + lane];
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+            if (!done && blk == rb) {
+#pragma unroll
+                for (int r = 15; r >= 0; --r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    found = (d[r] == b) ? rb * 32 + row : found;
+                }
+                done = true;
+            }
+        }
+        float bb = b, ss = s2;
+        int id = found;
+        {
+            const float ob = __shfl_xor(bb, 32, 64), os = __shfl_xor(ss, 32, 64);
+            const int oi = __shfl_xor(id, 32, 64);
+            if (ob < bb) {
+                ss = fminf(bb, os);
+                bb = ob;
+                id = oi;
+            } else {
+                ss = fminf(ss, ob);
+                if (ob == bb && oi >= 0 && (id < 0 || oi < id)) id = oi;
+            }
+        }
+        const int j = qbase + q * 32;
+        if (h == 0 && j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = bb;
+            part_second[o] = ss;
+            part_idx[o] = id;
+        }
+    }
+}
+
+// Seeded f16 filter with recompute-on-trigger (QG = 4 or 8 query groups per wave).  As
+// nn_mfma16x_kernel (joint carried min3 tree per block, unrolled tile, trees two MFMAs behind
+// their results), but a block's results die with its tree: when the block's test fires
+// (seeded: ~1% of blocks, the few points around each query's previous correspondence) the
+// update path re-issues the block's QG MFMAs (deterministic: same bits) and tracks each group
+// that has a value below its second.  With the results no longer held, a wave carries 8 query
+// groups (256 queries): the per-block LDS read, wait, compare and branch are spread over 8
+// MFMAs, and each workgroup's pass over the model serves twice the queries (half the L2->LDS
+// traffic per pair).  Same values, same tracking, same outputs as nn_mfma16p_kernel<true>.
+template <int QG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_mfma16r_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
+    const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
+    float *__restrict__ part_second, int *__restrict__ part_idx)
+{
+    static_assert(QG >= 4, "the pipeline issues two MFMAs ahead");
+    __shared__ half8_t tiles[2][kTile16 * 2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int split = blockIdx.y;
+    const int m0 = split * chunk;
+    const int m1 = min(m0 + chunk, nm_pad);
+    const int qbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
+    constexpr int kBlocksPerTile = kTile16 / 32;
+    constexpr int kDmaPerWave = kBlocksPerTile / 4;
+    constexpr float kStart = 0.0f; // seeded: "nothing below s0'"
+
+    half8_t bq[QG];
+    float best[QG], second[QG];
+    int bblk[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int j = qbase + q * 32;
+        double a[3] = {0.0, 0.0, 0.0};
+        unsigned sd = 0u;
+        if (j < np) {
+            a[0] = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[1] = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[2] = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+            sd = seed16[j];
+        }
+        bq[q] = query_frag(a, h, sd);
+        best[q] = kStart;
+        second[q] = kStart;
+        bblk[q] = m0 >> 5;
+    }
+    float s_max = kStart; // max_q second[q]
+    const f32x16_t zero = {};
+
+    auto issue_tile = [&](int tpt, int buf) {
+#pragma unroll
+        for (int i = 0; i < kDmaPerWave; ++i) {
+            const int blk = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((const void *)(mimg + ((size_t)(tpt >> 5) + blk) * 64 + lane),
+                                             (__attribute__((address_space(3))) void *)&tiles[buf][blk * 64],
+                                             16, 0, 0);
+        }
+    };
+    // the rare path: re-issue the block's MFMAs and track every group with a value below its second
+    auto update = [&](const half8_t &a8, int blk_id) {
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+            if (!__any(min16v(d) < second[q])) continue;
+            const float prev = best[q];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], d[r]);
+                best[q] = min_nocanon(best[q], d[r]);
+            }
+            bblk[q] = best[q] < prev ? blk_id : bblk[q];
+        }
+        float m = second[0];
+#pragma unroll
+        for (int q = 1; q < QG; ++q) m = fmaxf(m, second[q]);
+        s_max = m;
+    };
+    // one block: d0, d1 = its q0, q1 results (issued one step earlier); issues the next
+    // block's q0, q1 MFMAs into dn0, dn1 unless LAST
+    auto step = [&](const half8_t &a8, const half8_t &an, f32x16_t &d0, f32x16_t &d1, f32x16_t &dn0,
+                    f32x16_t &dn1, int blk_id, auto last_tag) {
+        constexpr bool LAST = decltype(last_tag)::value;
+        float u, v;
+        f32x16_t dm2 = d0, dm1 = d1; // results two and one MFMAs behind
+#pragma unroll
+        for (int k = 2; k < QG; ++k) {
+            const f32x16_t dk = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[k], zero, 0, 0, 0);
+            if (k == 2) tree16(dm2, u, v);
+            else tree18(dm2, u, v);
+            dm2 = dm1;
+            dm1 = dk;
+        }
+        if (!LAST) dn0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bq[0], zero, 0, 0, 0);
+        tree18(dm2, u, v);
+        if (!LAST) dn1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bq[1], zero, 0, 0, 0);
+        tree18(dm1, u, v);
+        const bool need = fminf(u, v) < s_max;
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+#pragma unroll
+        for (int k = 3; k < QG; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        }
+        if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+        if (__builtin_expect(__any(need), 0)) update(a8, blk_id);
+    };
+    using More = std::integral_constant<bool, false>;
+    using Last = std::integral_constant<bool, true>;
+
+    issue_tile(m0, 0);
+    int it = 0;
+    for (int t0 = m0; t0 < m1; t0 += kTile16, ++it) {
+        const int cur = it & 1;
+        if (t0 + kTile16 < m1) {
+            issue_tile(t0 + kTile16, cur ^ 1);
+            __builtin_amdgcn_s_waitcnt(kVmcntDma);
+        } else {
+            __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        }
+        __builtin_amdgcn_s_barrier();
+        const half8_t *tile = tiles[cur];
+        const int blk0 = t0 >> 5;
+        half8_t a0 = tile[lane], a1 = tile[64 + lane];
+        f32x16_t dA0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[0], zero, 0, 0, 0);
+        f32x16_t dA1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[1], zero, 0, 0, 0), dB0, dB1;
+#pragma unroll
+        for (int b = 0; b < kBlocksPerTile - 2; b += 2) {
+            step(a0, a1, dA0, dA1, dB0, dB1, blk0 + b, More{});
+            a0 = tile[(b + 2) * 64 + lane];
+            step(a1, a0, dB0, dB1, dA0, dA1, blk0 + b + 1, More{});
+            a1 = tile[(b + 3) * 64 + lane];
+        }
+        step(a0, a1, dA0, dA1, dB0, dB1, blk0 + kBlocksPerTile - 2, More{});
+        step(a1, a0, dB0, dB1, dA0, dA1, blk0 + kBlocksPerTile - 1, Last{});
+        __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+        __builtin_amdgcn_s_barrier();
+    }
+
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const float b = best[q];
+        const float s2 = second[q];
+        const int blk = bblk[q];
+        int found = -1;
+        bool done = !(b < kStart);
+        for (int guard = 0; guard < 64; ++guard) {
+            const unsigned long long pend = __ballot(!done);
+            if (pend == 0ull) break;
+            const int lead = __ffsll((long long)pend) - 1;
+            const int rb = __shfl(blk, lead, 64);
+            const half8_t a8 = mimg[(size_t)rb * 64 + lane];
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bq[q], zero, 0, 0, 0);
+            if (!done && blk == rb) {
+#pragma unroll
+                for (int r = 15; r >= 0; --r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    found = (d[r] == b) ? rb * 32 + row : found;
+                }
+                done = true;
+            }
+        }
+        float bb = b, ss = s2;
+        int id = found;
+        {
+            const float ob = __shfl_xor(bb, 32, 64), os = __shfl_xor(ss, 32, 64);
+            const int oi = __shfl_xor(id, 32, 64);
+            if (ob < bb) {
+                ss = fminf(bb, os);
+                bb = ob;
+                id = oi;
+            } else {
+                ss = fminf(ss, ob);
+                if (ob == bb && oi >= 0 && (id < 0 || oi < id)) id = oi;
+            }
+        }
+        const int j = qbase + q * 32;
+        if (h == 0 && j < np) {
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = bb;
+            part_second[o] = ss;
+            part_idx[o] = id;
+        }
+    }
+}
+
 // Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
 // s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see
 // nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
@@ -1429,24 +1825,40 @@ static int mfma16_qg()
     return qg;
 }
 
-// Seeded searches use the software-pipelined kernel (4% faster at C4); unseeded ones the
-// plain kernel (the pipelined one is 5% slower there: its update branch fires often).
-// Knob for experiments: ICP_MFMA16_KERNEL = plain | pipe (both searches), ICP_MFMA16_QG = 2.
-static int mfma16_kernel_choice(bool seeded) // 0 plain, 1 pipelined
+// Which f16 filter kernel runs.  Defaults: seeded searches (ICP iterations after the first)
+// nn_mfma16r_kernel<8>; unseeded ones (the first iteration, closest_matrix) the plain kernel,
+// whose per-group tests suit the frequent updates of a search that starts from +inf.
+// Knob for experiments: ICP_MFMA16_KERNEL = plain | pipe | unroll | r4 | r8 (the r kernels
+// are seeded-only; unseeded searches then use plain), ICP_MFMA16_QG = 2 (plain).
+enum { kK16Plain = 0, kK16Pipe, kK16Unroll, kK16R4, kK16R8 };
+static int mfma16_kernel_choice(bool seeded)
 {
     static int forced = [] {
         const char *e = getenv("ICP_MFMA16_KERNEL");
-        if (!e) return -1;
-        return std::string(e) == "pipe" ? 1 : (std::string(e) == "plain" ? 0 : -1);
+        const std::string v = e ? e : "";
+        if (v == "plain") return (int)kK16Plain;
+        if (v == "pipe") return (int)kK16Pipe;
+        if (v == "unroll") return (int)kK16Unroll;
+        if (v == "r4") return (int)kK16R4;
+        if (v == "r8") return (int)kK16R8;
+        return -1;
     }();
-    if (mfma16_qg() != 4) return 0;
-    return forced >= 0 ? forced : (seeded ? 1 : 0);
+    if (mfma16_qg() != 4) return kK16Plain;
+    if (forced >= 0) return (!seeded && forced >= kK16R4) ? (int)kK16Plain : forced;
+    return seeded ? (int)kK16R8 : (int)kK16Plain;
 }
+
+static int mfma16_groups(int kc) { return kc == kK16R8 ? 8 : (kc == kK16Plain ? mfma16_qg() : 4); }
 
 static const void *mfma16_kernel_ptr(bool seeded)
 {
-    if (mfma16_kernel_choice(seeded))
-        return seeded ? (const void *)nn_mfma16p_kernel<true> : (const void *)nn_mfma16p_kernel<false>;
+    switch (mfma16_kernel_choice(seeded)) {
+    case kK16R8: return (const void *)nn_mfma16r_kernel<8>;
+    case kK16R4: return (const void *)nn_mfma16r_kernel<4>;
+    case kK16Unroll: return seeded ? (const void *)nn_mfma16x_kernel<true> : (const void *)nn_mfma16x_kernel<false>;
+    case kK16Pipe: return seeded ? (const void *)nn_mfma16p_kernel<true> : (const void *)nn_mfma16p_kernel<false>;
+    default: break;
+    }
     if (mfma16_qg() == 2)
         return seeded ? (const void *)nn_mfma16_kernel<2, true> : (const void *)nn_mfma16_kernel<2, false>;
     return seeded ? (const void *)nn_mfma16_kernel<4, true> : (const void *)nn_mfma16_kernel<4, false>;
@@ -1454,8 +1866,8 @@ static const void *mfma16_kernel_ptr(bool seeded)
 
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded)
 {
-    const int qg = mfma16_qg();
-    return make_plan(np, nm_pad, kTile32, qg, 4 * qg * 32, mfma16_kernel_ptr(seeded));
+    const int g = mfma16_groups(mfma16_kernel_choice(seeded));
+    return make_plan(np, nm_pad, kTile32, g, 4 * g * 32, mfma16_kernel_ptr(seeded));
 }
 
 void launch_mfma16_seed(const double *px, const double *py, const double *pz, int np, const int *prev,
@@ -1482,12 +1894,21 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
     K<<<grid, kBlock, 0, st>>>(px, py, pz, np, c[0], c[1], c[2], scale, seed16, im, nm_pad, pl.chunk, \
                                part_best, part_second, part_idx)
     const bool sd = seed16 != nullptr;
-    if (mfma16_kernel_choice(sd)) {
+    switch (mfma16_kernel_choice(sd)) {
+    case kK16R8: LAUNCH16(nn_mfma16r_kernel<8>); break;
+    case kK16R4: LAUNCH16(nn_mfma16r_kernel<4>); break;
+    case kK16Unroll:
+        if (sd) LAUNCH16(nn_mfma16x_kernel<true>); else LAUNCH16(nn_mfma16x_kernel<false>);
+        break;
+    case kK16Pipe:
         if (sd) LAUNCH16(nn_mfma16p_kernel<true>); else LAUNCH16(nn_mfma16p_kernel<false>);
-    } else if (mfma16_qg() == 2) {
-        if (sd) LAUNCH16((nn_mfma16_kernel<2, true>)); else LAUNCH16((nn_mfma16_kernel<2, false>));
-    } else {
-        if (sd) LAUNCH16((nn_mfma16_kernel<4, true>)); else LAUNCH16((nn_mfma16_kernel<4, false>));
+        break;
+    default:
+        if (mfma16_qg() == 2) {
+            if (sd) LAUNCH16((nn_mfma16_kernel<2, true>)); else LAUNCH16((nn_mfma16_kernel<2, false>));
+        } else {
+            if (sd) LAUNCH16((nn_mfma16_kernel<4, true>)); else LAUNCH16((nn_mfma16_kernel<4, false>));
+        }
     }
 #undef LAUNCH16
 }

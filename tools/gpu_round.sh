@@ -51,7 +51,10 @@ for s in $STEPS; do
                    --output-format csv -d "$OUT/sq2_$v" -o sq -- python3 tools/nn_probe.py --variant $v --reps 1
            done ;;
     probe) for v in mfma16 mfma valu; do run probe_$v 300 python3 tools/nn_probe.py --variant $v; done ;;
-    abpipe) for ld in plain pipe; do ICP_MFMA16_KERNEL=$ld run abp_${ld} 300 python3 tools/nn_probe.py --variant mfma16 --icp 12; done ;;
+    abpipe) for ld in plain pipe unroll r4 r8; do ICP_MFMA16_KERNEL=$ld run abp_${ld} 300 python3 tools/nn_probe.py --variant mfma16 --icp 12; done ;;
+    test16k) for ld in ${K16:-unroll r4}; do
+               ICP_MFMA16_KERNEL=$ld run pytest_gpu_$ld 900 python -m pytest tests -m gpu -q -rf -k "mfma16 or grid or sharded or parity" || exit 1
+             done ;;
     test16plain) ICP_MFMA16_KERNEL=plain run pytest_gpu_plain 900 python -m pytest tests -m gpu -q -rf -k "mfma16 or grid or sharded" ;;
     dist2) ICP_BENCH_HOST_REDUCE=1 run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 10 --warmup 2 ;;
