@@ -283,7 +283,10 @@ def main():
         flops, peak, achieved = FLOP_PER_PAIR * pairs, PEAK_FP32_TFLOPS, None
     achieved = flops / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
     # timed iterations are seeded (the first icp_run iteration after set_scene is warm-up)
-    kernel = {"mfma16": "nn_mfma16p_kernel<seeded>", "mfma": "nn_mfma_kernel"}.get(
+    k16 = {"plain": "nn_mfma16_kernel<seeded>", "pipe": "nn_mfma16p_kernel<seeded>",
+           "unroll": "nn_mfma16x_kernel<seeded>", "r4": "nn_mfma16r_kernel<4>"}.get(
+        os.environ.get("ICP_MFMA16_KERNEL", ""), "nn_mfma16r_kernel<8>")
+    kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel"}.get(
         level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
     if args.variant == "grid":
         kernel = "nn_grid_search_kernel"
@@ -312,7 +315,7 @@ def main():
                                       + ("gloo host all-reduce (rehearsal)" if os.environ.get("ICP_BENCH_HOST_REDUCE") == "1" and world > 1
                                          else "RCCL all-reduce") + " of 18 fp64 sums/iter"},
             "roofline": {"bound": "mfma",
-                         "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + 2 VALU/pair min tracking",
+                         "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + joint v_min3 skip test (1 VALU per 2 pair values)",
                                           "mfma": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)"}.get(
                              level1, "VALU fp64" if args.nn == "fp64" else "VALU fp32 direct form (peak = f32 MFMA peak)"),
                          "kernel": kernel,

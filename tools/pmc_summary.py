@@ -40,6 +40,9 @@ def short(name):
     base = base.split("<")[0]
     if base == "nn_filter_kernel" and "true" in tmpl:
         return base + "<list>"
+    if base == "nn_mfma16r_kernel":  # seeded-only, template = query groups per wave
+        qg = tmpl.strip("<>") or ("8" if "ILi8E" in full else "4" if "ILi4E" in full else "?")
+        return f"{base}<{qg}>"
     if base.startswith("nn_mfma16") and ("<true" in tmpl or "true>" in tmpl or "Lb1E" in full):
         return base + "<seeded>"
     return base
