@@ -210,6 +210,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
     ap.add_argument("--no-cases", action="store_true", help="skip the reference's 14 benchmark cases")
+    ap.add_argument("--rccl", action="store_true",
+                    help="N=1: route the per-iteration sums through a 1-rank RCCL communicator, as N>1 does")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,6 +246,8 @@ def main():
         obj = [icp_amd.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx = icp_amd.Context(local, nn_mode, rank, world, obj[0])
+    elif args.rccl:
+        ctx = icp_amd.Context(local, nn_mode, 0, 1, icp_amd.rccl_unique_id())
     else:
         ctx = icp_amd.Context(local, nn_mode)
 
@@ -313,7 +317,8 @@ def main():
                        "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
                        "parallelism": f"scene-sharded x{world}, model replicated, "
                                       + ("gloo host all-reduce (rehearsal)" if os.environ.get("ICP_BENCH_HOST_REDUCE") == "1" and world > 1
-                                         else "RCCL all-reduce") + " of 18 fp64 sums/iter"},
+                                         else "RCCL all-reduce" if world > 1 or args.rccl else "no all-reduce (1 rank)")
+                                      + " of 18 fp64 sums/iter"},
             "roofline": {"bound": "mfma",
                          "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + joint v_min3 skip test (1 VALU per 2 pair values)",
                                           "mfma": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)"}.get(

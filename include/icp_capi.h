@@ -92,7 +92,9 @@ int icp_ctx_create(int device, int nn_mode, icp_ctx **out);
 /* One rank of a world_size-rank job (one process per GPU).  The scene is sharded,
  * the model replicated; per iteration the partial centroid / cross-covariance / error
  * sums are all-reduced with RCCL.  `rccl_id` = 128 bytes from icp_rccl_unique_id() on
- * rank 0, broadcast to all ranks by the caller. */
+ * rank 0, broadcast to all ranks by the caller.  With world_size 1 and a non-null id the
+ * context still creates a (1-rank) communicator and every sum goes through ncclAllReduce:
+ * the RCCL data path of a multi-GPU job, runnable on a single GPU. */
 int icp_ctx_create_dist(int device, int nn_mode, int rank, int world_size, const void *rccl_id,
                         icp_ctx **out);
 int icp_rccl_unique_id(void *out128);

@@ -406,11 +406,11 @@ void account_nn(icp_ctx *ctx, size_t n)
 // host all-reduce (device -> host, fn, host -> device).
 int allreduce(icp_ctx *ctx, double *buf, size_t count)
 {
-    if (ctx->world <= 1) return ICP_OK;
-    if (ctx->comm) {
+    if (ctx->comm) { // also a 1-rank communicator (icp_ctx_create_dist with world_size 1)
         RCCLCHK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, ctx->st));
         return ICP_OK;
     }
+    if (ctx->world <= 1) return ICP_OK;
     if (!ctx->host_reduce) return fail(ctx, ICP_E_ARG, "world_size > 1 without a communicator");
     double tmp[32];
     HIPCHK(hipMemcpyAsync(tmp, buf, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->st));
@@ -497,7 +497,7 @@ int icp_ctx_create_dist(int device, int nn_mode, int rank, int world_size, const
     ctx->rank = rank;
     ctx->world = world_size;
     int rc = ctx_init(ctx);
-    if (rc == ICP_OK && world_size > 1) {
+    if (rc == ICP_OK && rccl_id) { // world_size 1 + an id: a 1-rank communicator (exercises RCCL on one GPU)
         ncclUniqueId id;
         std::memcpy(&id, rccl_id, sizeof(id));
         ncclResult_t r = ncclCommInitRank(&ctx->comm, world_size, id, rank);

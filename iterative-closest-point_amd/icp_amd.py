@@ -245,7 +245,7 @@ class Context:
                     return 1
             self._cb = ALLREDUCE_FN(_cb)
             rc = L.icp_ctx_create_sharded(device, nn_mode, rank, world_size, self._cb, None, C.byref(h))
-        elif world_size > 1:
+        elif world_size > 1 or rccl_id is not None:
             rc = L.icp_ctx_create_dist(device, nn_mode, rank, world_size, rccl_id, C.byref(h))
         else:
             rc = L.icp_ctx_create(device, nn_mode, C.byref(h))

@@ -67,6 +67,9 @@ for s in $STEPS; do
             run sqs2 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE \
                 --output-format csv -d "$OUT/sqs2" -o sq -- python3 tools/nn_probe.py --variant mfma16 --icp 4 ;;
     cfg16) for c in 21 22 24 41 42; do ICP_MFMA16_CFG=$c run probe16_$c 300 python3 tools/nn_probe.py --variant mfma16; done ;;
+    shard) run shard_c4 600 python tools/shard_probe.py --worlds 1 2 4 8 &&
+           run shard_c5 600 python tools/shard_probe.py --n 8388608 --worlds 8 --steps 5 --warmup 2 ;;
+    testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
     *) echo "unknown step $s" ;;
