@@ -85,7 +85,9 @@ struct icp_ctx {
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
     IterState *h_iter = nullptr;     // pinned copy
-    int *h_flags = nullptr;          // pinned (done, iter) per in-flight iteration
+    int *h_flags = nullptr;          // mapped host (done, iter, ticket, -) per in-flight iteration
+    int *d_flags = nullptr;          // its device address (err_step writes it directly)
+    int flag_ticket = 0;             // last ticket handed to an iteration
     double *err_trace_dev = nullptr;
     size_t err_trace_cap = 0;
     std::vector<hipEvent_t> iter_ev; // per-iteration (begin, end) of the O(N*M) kernel
@@ -273,7 +275,7 @@ GridView grid_view(const icp_ctx *ctx)
 // O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
 // zero_counts = false: amb_count is already zero (icp_run: err_step clears it)
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
-                    bool zero_counts = true)
+                    bool zero_counts = true, bool seeds_ready = false)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     if (!n) return ICP_OK;
@@ -306,7 +308,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // level 1: MFMA expanded-form filter over every query
         const bool sd = seeded && l1 == 2;
         const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd) : plan_nn_mfma(n, ctx->nm_pad);
-        if (sd) {
+        if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
             launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->m4, ctx->c, ctx->scale16, ctx->seed16,
                                ctx->st);
@@ -454,7 +456,9 @@ static int ctx_init(icp_ctx *ctx)
         return fail(ctx, ICP_E_NO_DEVICE, "device ordinal out of range");
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking));
-    for (auto &e : ctx->ev) HIPCHK(hipEventCreate(&e));
+    // timing-only events: no system-scope fence (an L2 writeback + invalidate per record);
+    // data always reaches the host through a stream synchronisation or the mapped flags
+    for (auto &e : ctx->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     return ensure_reduction_space(ctx);
 }
 
@@ -709,6 +713,24 @@ static int moments_phase(icp_ctx *ctx, size_t n)
     return allreduce(ctx, ctx->sums + kSumS, 11);
 }
 
+// Spin until err_step has written `ticket` (system-scope release after (done, iter)).  No
+// event per iteration: an event marker costs the stream a ~6 us bubble.  If the stream
+// drains without the ticket (an earlier failure), report instead of spinning forever.
+static int wait_flag(icp_ctx *ctx, const int *flag, int ticket)
+{
+    for (unsigned spin = 1;; ++spin) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == ticket) return ICP_OK;
+        if ((spin & 1023u) == 0) {
+            const hipError_t q = hipStreamQuery(ctx->st);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == ticket) return ICP_OK;
+            if (q != hipSuccess) return fail(ctx, ICP_E_HIP, std::string("icp_run: ") + hipGetErrorString(q));
+            return fail(ctx, ICP_E_HIP, "icp_run: the stream drained without the iteration's flag");
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // The loop of GPU::ICP::find_corresponding_opti (gpu.cc:52-83), device-resident: every
 // iteration is enqueued without waiting on the previous one -- NN search, moments and their
 // all-reduces, the Horn solve (horn_step, the host's own code), transform + residual and its
@@ -732,11 +754,26 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     constexpr int kAhead = 1, kRing = 4; // iterations in flight beyond the one waited on
     TRY(grow(ctx, &ctx->iter_state, &ctx->iter_state_cap, 1));
     if (!ctx->h_iter) HIPCHK(hipHostMalloc((void **)&ctx->h_iter, sizeof(IterState), hipHostMallocDefault));
-    if (!ctx->h_flags) HIPCHK(hipHostMalloc((void **)&ctx->h_flags, sizeof(int) * 2 * kRing, hipHostMallocDefault));
+    if (!ctx->h_flags) {
+        HIPCHK(hipHostMalloc((void **)&ctx->h_flags, sizeof(int) * 4 * kRing,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(ctx->h_flags, 0, sizeof(int) * 4 * kRing);
+        HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_flags, ctx->h_flags, 0));
+    }
+    // seeded f16 searches: each transform writes the next search's seeds (no seed kernel)
+    const bool fuse_seeds = ctx->nn_mode == ICP_NN_CERTIFIED && level1_kind(ctx, n) == 2;
+    SeedArgs sa;
+    if (fuse_seeds) {
+        TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
+        sa.seed16 = ctx->seed16;
+        for (int a = 0; a < 3; ++a) sa.c[a] = ctx->c[a];
+        sa.scale = ctx->scale16;
+    }
+    int slot_ticket[kRing] = {};
     TRY(grow(ctx, &ctx->err_trace_dev, &ctx->err_trace_cap, (size_t)(max_iter > 0 ? max_iter : 1)));
     while (ctx->iter_ev.size() < 3 * (size_t)kRing) { // (nn begin, nn end, iteration done) per slot
         hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         ctx->iter_ev.push_back(e);
     }
     HIPCHK(hipMemsetAsync(ctx->iter_state, 0, sizeof(IterState), ctx->st));
@@ -748,31 +785,31 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1],
-                                enqueued == 0));
+                                enqueued == 0, fuse_seeds && enqueued > 0));
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
             // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142)
             TRY(moments_phase(ctx, n));
             // 4. Horn solve (gpu.cc:106-146) on the device
             launch_horn_step(ctx->sums, N, ctx->c, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
-            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f, red_target(ctx, n, ctx->sums + kSumErr),
-                                     ctx->st);
+            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f,
+                                     red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
             red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
             TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
-            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, ctx->amb_count, sd, ctx->st);
+            // (done, iter) straight into mapped host memory, then the slot's ticket
+            slot_ticket[slot] = ++ctx->flag_ticket;
+            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, ctx->amb_count, sd,
+                            ctx->d_flags + 4 * slot, slot_ticket[slot], ctx->st);
             LAUNCHCHK("err_step");
-            HIPCHK(hipMemcpyAsync(ctx->h_flags + 2 * slot, &sd->done, sizeof(int) * 2, hipMemcpyDeviceToHost,
-                                  ctx->st)); // (done, iter)
-            HIPCHK(hipEventRecord(ctx->iter_ev[3 * slot + 2], ctx->st));
             ++enqueued;
             continue;
         }
         const int slot = waited % kRing;
-        HIPCHK(hipEventSynchronize(ctx->iter_ev[3 * slot + 2]));
+        TRY(wait_flag(ctx, ctx->h_flags + 4 * slot + 2, slot_ticket[slot]));
         ++waited;
-        const int done = ctx->h_flags[2 * slot], iters = ctx->h_flags[2 * slot + 1];
+        const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
         if (iters > recorded) { // this iteration counted: its NN kernel time
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess)

@@ -120,7 +120,65 @@ __global__ __launch_bounds__(kBlock) void grid_scatter_kernel(
     }
 }
 
-// One thread per queued query (grid-stride over *count).
+// Lexicographic (D64, index) minimum, i.e. the first minimum (compute.cu:137 tie rule).
+__device__ __forceinline__ void lex_min(double &best, int &bi, double d, int mi)
+{
+    if (d < best || (d == best && (unsigned)mi < (unsigned)bi)) { // bi = -1 (none) compares as the largest
+        best = d;
+        bi = mi;
+    }
+}
+
+// Groups of kGroup lanes share one query: lane `sub` scans the x-runs (rows) sub, sub + G, ...
+// of the cell box [c0, c1], then the group folds its (D64, index) minima with xor shuffles.
+// One query's rows are independent, so the serial chain per lane is ~1/G of the box instead
+// of the whole box (the resolver is latency-bound: ~50-130 dependent loads per query).
+constexpr int kGroup = 16;
+
+__device__ __forceinline__ void scan_box(const double q[3], const int c0[3], const int c1[3], const GridView &gv,
+                                         int sub, double &best, int &bi)
+{
+    const int ny = c1[1] - c0[1] + 1;
+    const int nrows = ny * (c1[2] - c0[2] + 1);
+    for (int r = sub; r < nrows; r += kGroup) {
+        const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+        const int row = (cz * gv.g[1] + cy) * gv.g[0];
+        const int k1 = gv.start[row + c1[0] + 1];
+        for (int k = gv.start[row + c0[0]]; k < k1; ++k) { // one x-run of cells
+            const double4 m = gv.pts[k];
+            lex_min(best, bi, d64g(q[0], q[1], q[2], m.x, m.y, m.z), (int)m.w);
+        }
+    }
+}
+
+__device__ __forceinline__ void group_lex_min(double &best, int &bi)
+{
+#pragma unroll
+    for (int o = kGroup / 2; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(best, o, kGroup);
+        const int oi = __shfl_xor(bi, o, kGroup);
+        lex_min(best, bi, ob, oi);
+    }
+}
+
+// the cell box that must hold every m with D64(q, m) <= r2 (see the header); false if over budget
+__device__ __forceinline__ bool complete_box(const double q[3], double r2, const GridView &gv, int budget,
+                                             int c0[3], int c1[3])
+{
+    const double R = sqrt(r2);
+    long long cells = 1;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const double s = (fabs(q[a]) + R) * 0x1.0p-44;
+        c0[a] = cell1(q[a] - (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
+        c1[a] = cell1(q[a] + (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
+        cells *= (long long)(c1[a] - c0[a] + 1);
+    }
+    return cells <= budget;
+}
+
+// One kGroup-lane group per queued query (grid-stride over *count; the trip count is uniform
+// within a group, so a group is always entirely active).
 __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
@@ -128,63 +186,48 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out)
 {
     const int count = *count_ptr;
-    for (int t = blockIdx.x * kBlock + threadIdx.x; t < count; t += gridDim.x * kBlock) {
+    const int sub = threadIdx.x & (kGroup - 1);
+    const int groups = gridDim.x * (kBlock / kGroup);
+    for (int t = (blockIdx.x * kBlock + threadIdx.x) / kGroup; t < count; t += groups) {
         const int j = list[t];
         const int h = hint[t];
         bool ok = h >= 0;
-        int c0[3] = {0, 0, 0}, c1[3] = {-1, -1, -1};
-        double q[3] = {px[j], py[j], pz[j]};
+        int c0[3], c1[3];
+        const double q[3] = {px[j], py[j], pz[j]};
         double best = 0.0;
         int bi = h;
         if (ok) {
             const double4 mh = m4[h];
             best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
-            const double R = sqrt(best);
-            long long cells = 1;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const double s = (fabs(q[a]) + R) * 0x1.0p-44;
-                c0[a] = cell1(q[a] - (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
-                c1[a] = cell1(q[a] + (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
-                cells *= (long long)(c1[a] - c0[a] + 1);
-            }
-            ok = cells <= budget;
+            ok = complete_box(q, best, gv, budget, c0, c1);
         }
         if (ok) {
-            for (int cz = c0[2]; cz <= c1[2]; ++cz)
-                for (int cy = c0[1]; cy <= c1[1]; ++cy) {
-                    const int row = (cz * gv.g[1] + cy) * gv.g[0];
-                    const int k1 = gv.start[row + c1[0] + 1];
-                    for (int k = gv.start[row + c0[0]]; k < k1; ++k) { // one x-run of cells
-                        const double4 m = gv.pts[k];
-                        const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
-                        const int mi = (int)m.w;
-                        if (d < best || (d == best && mi < bi)) {
-                            best = d;
-                            bi = mi;
-                        }
-                    }
-                }
-            idx[j] = bi;
+            scan_box(q, c0, c1, gv, sub, best, bi);
+            group_lex_min(best, bi);
+            if (sub == 0) idx[j] = bi;
         }
-        const int slot = wave_append(fb_count, !ok);
-        if (!ok) {
+        const bool fb = !ok && sub == 0;
+        const int slot = wave_append(fb_count, fb);
+        if (fb) {
             fb_list[slot] = j;
             T_out[slot] = T_in ? T_in[t] : INFINITY; // +inf: every model point
         }
     }
 }
 
-// Exact grid NN for every query (ICP_NN_VARIANT_GRID).  Candidate: the (D64, index) best of
-// the smallest cube of cells around the query's (clamped) cell that holds a point; then the
-// complete box around that candidate, exactly as in nn_grid_resolve_kernel.  Either step
-// over `budget` cells -> the query goes to the fp64 brute force (window T = +inf).
+// Exact grid NN for every query (ICP_NN_VARIANT_GRID), one kGroup-lane group per query.
+// Candidate: the (D64, index) best of the smallest cube of cells around the query's
+// (clamped) cell that holds a point; then the complete box around that candidate, exactly
+// as in nn_grid_resolve_kernel.  Either step over `budget` cells -> the query goes to the
+// fp64 brute force (window T = +inf).
 __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
     int np, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
     double *__restrict__ fb_T)
 {
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < np; j += gridDim.x * kBlock) {
+    const int sub = threadIdx.x & (kGroup - 1);
+    const int groups = gridDim.x * (kBlock / kGroup);
+    for (int j = (blockIdx.x * kBlock + threadIdx.x) / kGroup; j < np; j += groups) {
         const double q[3] = {px[j], py[j], pz[j]};
         int c[3];
 #pragma unroll
@@ -192,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
         double best = INFINITY;
         int bi = -1;
         bool ok = true;
-        // 1) rings: cube [c - r, c + r] (clamped) until it holds a point
+        // 1) rings: cube [c - r, c + r] (clamped) until it holds a point (group-uniform decisions)
         for (int r = 0; bi < 0; ++r) {
             int c0[3], c1[3];
             long long cells = 1;
@@ -206,57 +249,26 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
                 ok = false;
                 break;
             }
-            for (int cz = c0[2]; cz <= c1[2]; ++cz)
-                for (int cy = c0[1]; cy <= c1[1]; ++cy) {
-                    const int row = (cz * gv.g[1] + cy) * gv.g[0];
-                    const int k1 = gv.start[row + c1[0] + 1];
-                    for (int k = gv.start[row + c0[0]]; k < k1; ++k) {
-                        const double4 m = gv.pts[k];
-                        const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
-                        const int mi = (int)m.w;
-                        if (d < best || (d == best && mi < bi)) {
-                            best = d;
-                            bi = mi;
-                        }
-                    }
-                }
+            scan_box(q, c0, c1, gv, sub, best, bi);
+            group_lex_min(best, bi);
             if (c0[0] == 0 && c0[1] == 0 && c0[2] == 0 && c1[0] == gv.g[0] - 1 && c1[1] == gv.g[1] - 1 &&
                 c1[2] == gv.g[2] - 1)
                 break; // the whole grid (bi >= 0 unless the model is empty)
         }
         // 2) the complete box around the candidate (see the header)
         if (ok && bi >= 0) {
-            const double R = sqrt(best);
             int c0[3], c1[3];
-            long long cells = 1;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                const double s = (fabs(q[a]) + R) * 0x1.0p-44;
-                c0[a] = cell1(q[a] - (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
-                c1[a] = cell1(q[a] + (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
-                cells *= (long long)(c1[a] - c0[a] + 1);
+            ok = complete_box(q, best, gv, budget, c0, c1);
+            if (ok) {
+                scan_box(q, c0, c1, gv, sub, best, bi);
+                group_lex_min(best, bi);
             }
-            ok = cells <= budget;
-            if (ok)
-                for (int cz = c0[2]; cz <= c1[2]; ++cz)
-                    for (int cy = c0[1]; cy <= c1[1]; ++cy) {
-                        const int row = (cz * gv.g[1] + cy) * gv.g[0];
-                        const int k1 = gv.start[row + c1[0] + 1];
-                        for (int k = gv.start[row + c0[0]]; k < k1; ++k) {
-                            const double4 m = gv.pts[k];
-                            const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
-                            const int mi = (int)m.w;
-                            if (d < best || (d == best && mi < bi)) {
-                                best = d;
-                                bi = mi;
-                            }
-                        }
-                    }
         }
         ok = ok && bi >= 0;
-        if (ok) idx[j] = bi;
-        const int slot = wave_append(fb_count, !ok);
-        if (!ok) {
+        if (ok && sub == 0) idx[j] = bi;
+        const bool fb = !ok && sub == 0;
+        const int slot = wave_append(fb_count, fb);
+        if (fb) {
             fb_list[slot] = j;
             fb_T[slot] = INFINITY; // exact fp64 over every model point (nn_resolve_kernel)
         }
@@ -332,7 +344,7 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, int *idx, int *fb_count, int *fb_list, double *fb_T, hipStream_t st)
 {
-    const int blocks = std::max(1, std::min((np + kBlock - 1) / kBlock, 8192));
+    const int blocks = std::max(1, std::min((np + kBlock / kGroup - 1) / (kBlock / kGroup), 16384));
     nn_grid_search_kernel<<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
 }
 
@@ -341,7 +353,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st)
 {
-    const int blocks = std::max(1, std::min((max_items + kBlock - 1) / kBlock, 2048));
+    const int blocks = std::max(1, std::min((max_items + kBlock / kGroup - 1) / (kBlock / kGroup), 4096));
     nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
                                                       fb_count, fb_list, T_in, T_out);
 }

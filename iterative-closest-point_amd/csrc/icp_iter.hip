@@ -34,19 +34,25 @@ __global__ void horn_step_kernel(const double *__restrict__ sums, double N, doub
 }
 
 __global__ void err_step_kernel(const double *__restrict__ sums, double N, double threshold, int max_iter,
-                                double *__restrict__ err_trace, int *__restrict__ cnt, IterState *__restrict__ s)
+                                double *__restrict__ err_trace, int *__restrict__ cnt, IterState *__restrict__ s,
+                                int *hflag, int ticket)
 {
     // the search's queue sizes: into the statistics, then zeroed for the next search (always:
     // the next search appends to these counters even after the loop has converged)
     const int c[4] = {cnt[0], cnt[1], cnt[2], cnt[3]};
     for (int k = 0; k < 4; ++k) cnt[k] = 0;
-    if (s->done) return;
-    for (int k = 0; k < 4; ++k) s->nn_counts[k] += c[k];
-    const double e = sums[kSumErr];
-    const double err = (e + e) / N; // gpu.cc:71-76: find_alignment's residual is the same sum
-    err_trace[s->iter] = err;
-    s->iter += 1;
-    if (err < threshold || s->iter >= max_iter) s->done = 1; // gpu.cc:79-80
+    if (!s->done) {
+        for (int k = 0; k < 4; ++k) s->nn_counts[k] += c[k];
+        const double e = sums[kSumErr];
+        const double err = (e + e) / N; // gpu.cc:71-76: find_alignment's residual is the same sum
+        err_trace[s->iter] = err;
+        s->iter += 1;
+        if (err < threshold || s->iter >= max_iter) s->done = 1; // gpu.cc:79-80
+    }
+    // (done, iter) to the host (mapped memory), then the ticket the host spins on
+    __hip_atomic_store(hflag, s->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hflag + 1, s->iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(hflag + 2, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 } // namespace
@@ -57,9 +63,10 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], Ite
 }
 
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
-                     int *amb_count, IterState *st_dev, hipStream_t st)
+                     int *amb_count, IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st)
 {
-    err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, amb_count, st_dev);
+    err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, amb_count, st_dev, hflag_dev,
+                                     ticket);
 }
 
 } // namespace icp

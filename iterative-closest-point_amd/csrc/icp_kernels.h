@@ -21,6 +21,36 @@ __device__ __forceinline__ int wave_append(int *counter, bool pred)
     base = __shfl(base, leader, 64);
     return pred ? base + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
 }
+
+// Append to a device queue with ONE atomic per workgroup (a same-address device atomic per
+// wave serialises: ~12 ns each, 16k of them at 1M queries).  Every thread of the kBlock-wide
+// workgroup must call it (no early exit).  Slots within the workgroup follow thread order.
+// Also adds the workgroup's count of `pred2` to *counter2 (statistics) if counter2 != nullptr.
+__device__ __forceinline__ int block_append(int *counter, bool pred, int *counter2 = nullptr, bool pred2 = false)
+{
+    __shared__ int s_cnt[kBlock / 64], s_cnt2[kBlock / 64], s_base;
+    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+    const unsigned long long mask = __ballot(pred);
+    const unsigned long long mask2 = __ballot(pred2);
+    if (lane == 0) {
+        s_cnt[wave] = __popcll(mask);
+        s_cnt2[wave] = __popcll(mask2);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0, tot2 = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const int c = s_cnt[w];
+            s_cnt[w] = tot;
+            tot += c;
+            tot2 += s_cnt2[w];
+        }
+        s_base = tot ? atomicAdd(counter, tot) : 0;
+        if (counter2 && tot2) atomicAdd(counter2, tot2);
+    }
+    __syncthreads();
+    return pred ? s_base + s_cnt[wave] + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
+}
 #endif
 
 // Parameters of the fp32 certificate (see icp_kernels.hip, "certified NN").
@@ -167,10 +197,17 @@ struct Xform {
 void launch_transform_err(double *px, double *py, double *pz, const double *yx, const double *yy,
                           const double *yz, int n, Xform xf, int write_p, float4 *p32,
                           double *partials, hipStream_t st);
+// seeds of the next seeded f16 search (mfma16_seed_kernel's values), written by the transform
+// when seed16 != nullptr; c / scale = the f16 image's centre and scale
+struct SeedArgs {
+    unsigned *seed16 = nullptr;
+    double c[3] = {0.0, 0.0, 0.0};
+    double scale = 1.0;
+};
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, hipStream_t st);
+                              double *partials, const SeedArgs &sa, hipStream_t st);
 
 // ---- device-resident ICP iteration (icp_iter.hip) -----------------------------------
 // Per-run device state: done flag, iterations recorded, error trace, last (s, R, t),
@@ -185,9 +222,10 @@ struct IterState {
 // (1 thread) Horn solve from the reduced sums (icp_horn.h), unless done
 void launch_horn_step(const double *sums, double n_total, const double c[3], IterState *st_dev, hipStream_t st);
 // (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold
-// or iter == max_iter; nn_counts += amb_count[0..3] (unless done), then amb_count = 0
+// or iter == max_iter; nn_counts += amb_count[0..3] (unless done), then amb_count = 0; finally
+// hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope, mapped host memory)
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
-                     int *amb_count, IterState *st_dev, hipStream_t st);
+                     int *amb_count, IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st);
 
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);

@@ -247,6 +247,7 @@ __device__ __forceinline__ void merge_splits(const float *__restrict__ part_best
     b = part_best[s];
     s2 = part_second[s];
     id = part_idx[s];
+#pragma unroll 4 // independent loads: four splits in flight (latency-bound at small n, many splits)
     for (int sp = 1; sp < splits; ++sp) {
         const size_t o = (size_t)sp * nslots + s;
         const float b2 = part_best[o], s22 = part_second[o];
@@ -265,16 +266,19 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int nslots, double rm,
     int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint)
 {
-    const int s = blockIdx.x * kBlock + threadIdx.x;
-    if (s >= nslots) return;
-    const int j = s;
-    float b, s2;
-    int id;
-    merge_splits(part_best, part_second, part_idx, splits, nslots, s, b, s2, id);
-    const double T = cert_window(b, p32[j], rm);
-    const bool ok = (double)s2 > T;
-    if (ok) idx[j] = id; // unique candidate => exact fp64 first-min
-    const int slot = wave_append(amb_count, !ok);
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = j < nslots; // no early exit: block_append is workgroup-wide
+    bool ok = true;
+    double T = 0.0;
+    int id = -1;
+    if (valid) {
+        float b, s2;
+        merge_splits(part_best, part_second, part_idx, splits, nslots, j, b, s2, id);
+        T = cert_window(b, p32[j], rm);
+        ok = (double)s2 > T;
+        if (ok) idx[j] = id; // unique candidate => exact fp64 first-min
+    }
+    const int slot = block_append(amb_count, !ok);
     if (!ok) {
         amb_list[slot] = j;
         amb_T[slot] = T;
@@ -1204,19 +1208,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
 // Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
 // s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see
 // nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
-__global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
-    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
-    int np, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx, double cy,
-    double cz, double scale, unsigned *__restrict__ seed16)
+// seed of query p (unscaled fp64) from a model point m: packed f16 (hi | lo << 16) of -s0 / 2^14
+__device__ __forceinline__ unsigned mfma16_seed_value(double p0, double p1, double p2, double m0, double m1,
+                                                      double m2, double cx, double cy, double cz, double scale)
 {
-    const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= np) return;
-    const int k = prev[j];
-    const double a0 = fmin(fmax((px[j] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double a1 = fmin(fmax((py[j] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double a2 = fmin(fmax((pz[j] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double4 m = m4[k];
-    const double b0 = (m.x - cx) * scale, b1 = (m.y - cy) * scale, b2 = (m.z - cz) * scale;
+    const double a0 = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double a1 = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double a2 = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double b0 = (m0 - cx) * scale, b1 = (m1 - cy) * scale, b2 = (m2 - cz) * scale;
     const double bb = b0 * b0 + b1 * b1 + b2 * b2;
     const double G = bb - 2.0 * (a0 * b0 + a1 * b1 + a2 * b2);
     const double u = 0x1.0p-24;
@@ -1229,8 +1228,18 @@ __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
     const double x = fmin(fmax(-s0 / 16384.0, -65000.0), 65000.0);
     const _Float16 hi = (_Float16)x;
     const _Float16 lo = (_Float16)(x - (double)hi);
-    seed16[j] = (unsigned)__builtin_bit_cast(unsigned short, hi) |
-                ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+    return (unsigned)__builtin_bit_cast(unsigned short, hi) | ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+}
+
+__global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    int np, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx, double cy,
+    double cz, double scale, unsigned *__restrict__ seed16)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= np) return;
+    const double4 m = m4[prev[j]];
+    seed16[j] = mfma16_seed_value(px[j], py[j], pz[j], m.x, m.y, m.z, cx, cy, cz, scale);
 }
 
 // Certificate of the f16 filter, in scaled units (a_s, b_s), u = 2^-24, A = |a_s|:
@@ -1262,19 +1271,20 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= np) return;
-    float b, s2;
-    int id;
-    merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    const bool valid = j < np; // no early exit: block_append is workgroup-wide
+    const int jj = valid ? j : 0;
+    float b = 0.0f, s2 = 0.0f;
+    int id = -1;
+    if (valid) merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
     if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
-    const double ax = (px[j] - cx) * scale, ay = (py[j] - cy) * scale, az = (pz[j] - cz) * scale;
+    const double ax = (px[jj] - cx) * scale, ay = (py[jj] - cy) * scale, az = (pz[jj] - cz) * scale;
     bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
               fabs(az) <= kF16QueryClamp;
     if (ok) {
         const double u = 0x1.0p-24;
         const double a2 = ax * ax + ay * ay + az * az;
         const double A = sqrt(a2);
-        const double sh = SEEDED ? seed_shift(seed16[j]) : 0.0;
+        const double sh = SEEDED ? seed_shift(seed16[jj]) : 0.0;
         auto delta = [&](double R) {
             return SEEDED ? 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * fabs(sh) + 4.0 * u * (A + R) + 1e-3
                           : 26.0 * u * R * R + 60.0 * u * A * R + 4.0 * u * (A + R) + 1e-3;
@@ -1288,12 +1298,13 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
         ok = sg > T;
     }
-    if (ok) idx[j] = id;
-    const int slot = wave_append(amb_count, !ok);
+    ok = ok || !valid;
+    if (ok && valid) idx[j] = id;
+    // queue + the statistic of queries without a level-1 candidate, one atomic each per workgroup
+    const int slot = block_append(amb_count, !ok, amb_count + 1, !ok && id < 0);
     if (!ok) {
         amb_list[slot] = j;
         amb_hint[slot] = id; // the grid resolver's candidate
-        if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
 
@@ -1344,10 +1355,10 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= np) return;
-    float b, s2;
-    int id;
-    merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    const bool valid = j < np; // no early exit: block_append is workgroup-wide
+    float b = 0.0f, s2 = 0.0f;
+    int id = -1;
+    if (valid) merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
     bool ok = id >= 0;
     if (ok) {
         const double u = 0x1.0p-24;
@@ -1362,12 +1373,13 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
         T += fabs(T) * 1e-12 + 1e-300;
         ok = (double)s2 > T;
     }
-    if (ok) idx[j] = id;
-    const int slot = wave_append(amb_count, !ok);
+    ok = ok || !valid;
+    if (ok && valid) idx[j] = id;
+    // queue + the statistic of queries without a level-1 candidate, one atomic each per workgroup
+    const int slot = block_append(amb_count, !ok, amb_count + 1, !ok && id < 0);
     if (!ok) {
         amb_list[slot] = j;
         amb_hint[slot] = id; // the grid resolver's candidate
-        if (id < 0) atomicAdd(amb_count + 1, 1); // no level-1 candidate (statistics)
     }
 }
 
@@ -1613,7 +1625,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
     int n, Xform xfv, const Xform *__restrict__ xfd, const int *__restrict__ done, int write_p,
-    float4 *__restrict__ p32, double *__restrict__ partials)
+    float4 *__restrict__ p32, double *__restrict__ partials, SeedArgs sa)
 {
     // xfd / done (device-resident loop): the transform comes from the device Horn solve, and
     // nothing is applied once the loop has converged.  One load per workgroup, via LDS.
@@ -1642,26 +1654,47 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
             if (p32)
                 p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]),
                                      (float)(q2 - xf.c[2]), 0.0f);
+            // the next seeded f16 search's seed: the new position against this iteration's
+            // correspondence (y = m[idx], exactly what mfma16_seed_kernel would gather)
+            if (sa.seed16)
+                sa.seed16[i] = mfma16_seed_value(q0, q1, q2, yx[i], yy[i], yz[i], sa.c[0], sa.c[1], sa.c[2],
+                                                 sa.scale);
         }
     }
     block_sum_store<1>(a, partials + blockIdx.x);
 }
 
-__global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict__ partials,
-                                                       int nblocks, int K, double *__restrict__ out)
+// out[k] = sum_b partials[b*K + k], one workgroup, fixed order (deterministic): thread t
+// accumulates the rows b = t, t + kBlock, ... (contiguous K-double rows: coalesced), then each
+// column is folded by a fixed xor-shuffle tree per wave and the 4 wave sums in wave order.
+template <int K>
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict__ partials, int nblocks,
+                                                       double *__restrict__ out)
 {
-    __shared__ double sh[kBlock];
+    __shared__ double sh[kBlock / 64][K];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += partials[(size_t)b * K + k];
+    }
+#pragma unroll
     for (int k = 0; k < K; ++k) {
-        double a = 0.0;
-        for (int b = threadIdx.x; b < nblocks; b += kBlock) a += partials[(size_t)b * K + k];
-        sh[threadIdx.x] = a;
-        __syncthreads();
-        for (int s = kBlock / 2; s > 0; s >>= 1) {
-            if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[k] = sh[0];
-        __syncthreads();
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        double r = sh[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
+        out[threadIdx.x] = r;
     }
 }
 
@@ -1718,8 +1751,20 @@ static int resident_wgs(const void *kernel)
 // Split the model axis so the grid fills whole rounds of resident workgroups: a grid of
 // 1.35 rounds runs its second round at a third of the chip.  Smallest split count with
 // >= 90% round efficiency and at least one full round, else the most efficient one.
+static int min_rounds()
+{
+    // experiment knob: ICP_NN_MIN_ROUNDS = k asks for >= k rounds of resident workgroups (a
+    // single round has no dynamic balancing: the slowest workgroup sets the kernel time)
+    static int r = [] {
+        const char *e = getenv("ICP_NN_MIN_ROUNDS");
+        return e ? std::max(1, atoi(e)) : 4;
+    }();
+    return r;
+}
+
 static void choose_splits(NNPlan &pl, int tiles, int tile, int cap)
 {
+    cap *= min_rounds();
     int best_tps = tiles, best_s = 1;
     double best_eff = -1.0;
     for (int s = 1; s <= tiles; ++s) {
@@ -2036,20 +2081,27 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                           double *partials, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
-                                                            write_p, p32, partials);
+                                                            write_p, p32, partials, SeedArgs{});
 }
 
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, hipStream_t st)
+                              double *partials, const SeedArgs &sa, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done, 1,
-                                                            p32, partials);
+                                                            p32, partials, sa);
 }
 
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st)
 {
-    reduce_kernel<<<1, kBlock, 0, st>>>(partials, nblocks, K, out);
+    switch (K) {
+#define RED_CASE(k) \
+    case k: reduce_kernel<k><<<1, kBlock, 0, st>>>(partials, nblocks, out); break;
+        RED_CASE(1) RED_CASE(2) RED_CASE(3) RED_CASE(4) RED_CASE(5) RED_CASE(6)
+        RED_CASE(7) RED_CASE(8) RED_CASE(9) RED_CASE(10) RED_CASE(11) RED_CASE(12)
+#undef RED_CASE
+    default: break; // K <= 12 (the partials buffer holds 12 per block)
+    }
 }
 
 } // namespace icp

@@ -69,6 +69,9 @@ for s in $STEPS; do
     cfg16) for c in 21 22 24 41 42; do ICP_MFMA16_CFG=$c run probe16_$c 300 python3 tools/nn_probe.py --variant mfma16; done ;;
     shard) run shard_c4 600 python tools/shard_probe.py --worlds 1 2 4 8 &&
            run shard_c5 600 python tools/shard_probe.py --n 8388608 --worlds 8 --steps 5 --warmup 2 ;;
+    profshard) run rocprof_shard8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_shard8" -o shard -- \
+               python3 tools/shard_probe.py --worlds 8 --steps 20 ;;
+    rounds) for r in 1 2 4 1 2 4; do ICP_NN_MIN_ROUNDS=$r ICP_DEBUG_PLAN=1 run rounds_$r 300 python tools/shard_probe.py --worlds 8 4 --steps 20 || exit 1; done ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
