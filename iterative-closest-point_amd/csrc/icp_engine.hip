@@ -212,7 +212,7 @@ int download_cloud(icp_ctx *ctx, const DevCloud &c, size_t n, double *xyz)
 int ensure_reduction_space(icp_ctx *ctx)
 {
     if (ctx->partials) return ICP_OK;
-    HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocks * 12));
+    HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocks * kRedMaxK));
     HIPCHK(hipMalloc((void **)&ctx->sums, sizeof(double) * 32));
     HIPCHK(hipHostMalloc((void **)&ctx->h_sums, sizeof(double) * 32, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));
@@ -287,20 +287,20 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap, need));
         double *pb = (double *)ctx->part;
         int *pi = (int *)(pb + (size_t)pl.splits * n);
-        HIPCHK(hipEventRecord(ev0, ctx->st));
+        if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_fp64(q.x, q.y, q.z, (int)n, ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm,
                        pl, pb, pi, ctx->st);
-        HIPCHK(hipEventRecord(ev1, ctx->st));
+        if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_fp64");
     } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
         // exact grid search for every query; over-budget boxes -> fp64 brute force per query
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
-        HIPCHK(hipEventRecord(ev0, ctx->st));
+        if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1,
                               ctx->fb_list, ctx->fb_T, ctx->st);
-        HIPCHK(hipEventRecord(ev1, ctx->st));
+        if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_grid_search");
@@ -323,13 +323,13 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
-        HIPCHK(hipEventRecord(ev0, ctx->st));
+        if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         if (l1 == 2)
             launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, seeds, ctx->mimg16, (int)ctx->nm_pad,
                              pl, pb, ps, pi, ctx->st);
         else
             launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
-        HIPCHK(hipEventRecord(ev1, ctx->st));
+        if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
@@ -355,9 +355,9 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->amb_hint, &ctx->amb_hint_cap, n));
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
-        HIPCHK(hipEventRecord(ev0, ctx->st));
+        if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
-        HIPCHK(hipEventRecord(ev1, ctx->st));
+        if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         CertParams cp{ctx->rm};
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, (int)n, cp, ctx->idx, ctx->amb_count, ctx->amb_list,
                            ctx->amb_T, ctx->amb_hint, ctx->st);
@@ -780,41 +780,76 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     IterState *sd = ctx->iter_state;
     int enqueued = 0, waited = 0, recorded = 0;
     bool stop = false;
+    // With an all-reduce (ranks > 1, or a 1-rank communicator) each iteration has ONE: the
+    // moments' 17 sums plus the previous iteration's residual e, whose err_step therefore runs
+    // one iteration late (before this iteration's Horn solve, so a converged state is still
+    // frozen at the same point).  Without one, err_step follows its own transform.
+    const bool lag = ctx->comm != nullptr || ctx->world > 1;
+    // the O(N*M) kernel is timed (two events) every timing_stride-th iteration
+    static const int timing_stride = [] {
+        const char *e = getenv("ICP_NN_TIMING_STRIDE");
+        return e ? std::max(1, atoi(e)) : 1;
+    }();
+    auto enqueue_err_step = [&](int it) -> int {
+        const int sl = it % kRing;
+        // (done, iter) straight into mapped host memory, then the slot's ticket
+        slot_ticket[sl] = ++ctx->flag_ticket;
+        launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->d_flags + 4 * sl,
+                        slot_ticket[sl], ctx->st);
+        LAUNCHCHK("err_step");
+        return ICP_OK;
+    };
     while (!stop && waited < max_iter) {
-        if (enqueued < max_iter && enqueued - waited <= kAhead) {
+        if (enqueued < max_iter && enqueued - waited <= kAhead + (lag ? 1 : 0)) {
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
-            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1],
-                                enqueued == 0, fuse_seeds && enqueued > 0));
+            const bool timed = enqueued % timing_stride == 0;
+            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[3 * slot] : nullptr,
+                                timed ? ctx->iter_ev[3 * slot + 1] : nullptr, enqueued == 0,
+                                fuse_seeds && enqueued > 0));
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
-            // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142)
-            TRY(moments_phase(ctx, n));
+            // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142): the first
+            // iteration two-pass (the reference's order); later ones in one pass around the shifts
+            // the previous Horn step left (its transformed centroid, its correspondence centroid)
+            if (enqueued == 0) {
+                TRY(moments_phase(ctx, n));
+            } else {
+                launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
+                                       red_target(ctx, n, ctx->sums), ctx->st);
+                red_finish(ctx, n, 17, ctx->sums);
+                LAUNCHCHK("shifted_moments");
+                if (lag) { // + the previous iteration's residual (sums[kSumErr], local until now)
+                    TRY(allreduce(ctx, ctx->sums, kNumSums));
+                    TRY(enqueue_err_step(enqueued - 1));
+                }
+            }
             // 4. Horn solve (gpu.cc:106-146) on the device
-            launch_horn_step(ctx->sums, N, ctx->c, sd, ctx->st);
+            launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
             launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f,
                                      red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
             red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
-            TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
-            // (done, iter) straight into mapped host memory, then the slot's ticket
-            slot_ticket[slot] = ++ctx->flag_ticket;
-            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, ctx->amb_count, sd,
-                            ctx->d_flags + 4 * slot, slot_ticket[slot], ctx->st);
-            LAUNCHCHK("err_step");
+            if (!lag) TRY(enqueue_err_step(enqueued));
             ++enqueued;
+            if (lag && enqueued == max_iter) { // the last residual has no next iteration to ride on
+                TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
+                TRY(enqueue_err_step(enqueued - 1));
+            }
             continue;
         }
         const int slot = waited % kRing;
         TRY(wait_flag(ctx, ctx->h_flags + 4 * slot + 2, slot_ticket[slot]));
         ++waited;
         const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
-        if (iters > recorded) { // this iteration counted: its NN kernel time
+        if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess)
+            if ((waited - 1) % timing_stride == 0 &&
+                hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess) {
                 ctx->stats.nn_ms += ms;
-            ctx->stats.nn_launches += 1;
+                ctx->stats.nn_launches += 1;
+            }
             ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
             recorded = iters;
         }

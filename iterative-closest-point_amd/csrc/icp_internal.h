@@ -24,6 +24,7 @@ constexpr int kTile64 = 512;  // model points per LDS tile, fp64 path (16 KiB)
 constexpr int kSub = 32;      // sub-block granularity of the running-argmin bookkeeping
 constexpr int kRedMaxBlocks = 1024; // max workgroups of a streaming reduction pass
 constexpr int kRedSingle = 4096;    // up to this many points: a single-workgroup pass
+constexpr int kRedMaxK = 17;        // max sums per workgroup of a streaming reduction pass
 
 // Slots of the per-iteration reduced-sum vector (device `sums`, fp64):
 //  [0..2]  sum p        [3..5]  sum y

@@ -12,13 +12,38 @@ namespace icp {
 namespace {
 
 __global__ void horn_step_kernel(const double *__restrict__ sums, double N, double c0, double c1, double c2,
-                                 IterState *__restrict__ s)
+                                 int shifted, int *__restrict__ cnt, IterState *__restrict__ s)
 {
+    // the search's queue sizes: into the statistics, then zeroed for the next search (always:
+    // the next search appends to these counters even after the loop has converged)
+    const int qc[4] = {cnt[0], cnt[1], cnt[2], cnt[3]};
+    for (int k = 0; k < 4; ++k) cnt[k] = 0;
     if (s->done) return;
-    const double mu_p[3] = {sums[kSumP] / N, sums[kSumP + 1] / N, sums[kSumP + 2] / N};
-    const double mu_y[3] = {sums[kSumY] / N, sums[kSumY + 1] / N, sums[kSumY + 2] / N};
+    for (int k = 0; k < 4; ++k) s->nn_counts[k] += qc[k];
+    double mu_p[3], mu_y[3], S[9], d_caps, sp;
+    if (!shifted) { // two-pass sums (moments_phase): Σp, Σy, then centred S, d_caps, sp
+        for (int k = 0; k < 3; ++k) {
+            mu_p[k] = sums[kSumP + k] / N; // rowwise().mean() (gpu.cc:98-99)
+            mu_y[k] = sums[kSumY + k] / N;
+        }
+        for (int k = 0; k < 9; ++k) S[k] = sums[kSumS + k];
+        d_caps = sums[kSumDcaps];
+        sp = sums[kSumSp];
+    } else { // one pass around (cp, cy): remove the shift
+        double dp[3], dy[3];
+        for (int k = 0; k < 3; ++k) {
+            dp[k] = sums[kSumP + k] / N;
+            dy[k] = sums[kSumY + k] / N;
+            mu_p[k] = s->shift_p[k] + dp[k];
+            mu_y[k] = s->shift_y[k] + dy[k];
+        }
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) S[3 * r + c] = sums[kSumS + 3 * r + c] - sums[kSumP + r] * dy[c];
+        d_caps = sums[kSumDcaps] - ((sums[kSumY] * dy[0] + sums[kSumY + 1] * dy[1]) + sums[kSumY + 2] * dy[2]);
+        sp = sums[kSumSp] - ((sums[kSumP] * dp[0] + sums[kSumP + 1] * dp[1]) + sums[kSumP + 2] * dp[2]);
+    }
     double sc, R[9], t[3];
-    horn_solve(sums + kSumS, mu_p, mu_y, sums[kSumDcaps], sums[kSumSp], &sc, R, t);
+    horn_solve(S, mu_p, mu_y, d_caps, sp, &sc, R, t);
     s->srt[0] = sc;
     for (int k = 0; k < 9; ++k) {
         s->srt[1 + k] = R[k];
@@ -31,18 +56,20 @@ __global__ void horn_step_kernel(const double *__restrict__ sums, double N, doub
     s->xf.c[0] = c0;
     s->xf.c[1] = c1;
     s->xf.c[2] = c2;
+    // the next iteration's shifts: the transformed scene's centroid (exactly sR mu_p + t in
+    // real arithmetic) and this iteration's correspondence centroid
+    double smu[3];
+    matvec3(s->xf.sR, mu_p, smu);
+    for (int k = 0; k < 3; ++k) {
+        s->shift_p[k] = smu[k] + t[k];
+        s->shift_y[k] = mu_y[k];
+    }
 }
 
 __global__ void err_step_kernel(const double *__restrict__ sums, double N, double threshold, int max_iter,
-                                double *__restrict__ err_trace, int *__restrict__ cnt, IterState *__restrict__ s,
-                                int *hflag, int ticket)
+                                double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag, int ticket)
 {
-    // the search's queue sizes: into the statistics, then zeroed for the next search (always:
-    // the next search appends to these counters even after the loop has converged)
-    const int c[4] = {cnt[0], cnt[1], cnt[2], cnt[3]};
-    for (int k = 0; k < 4; ++k) cnt[k] = 0;
     if (!s->done) {
-        for (int k = 0; k < 4; ++k) s->nn_counts[k] += c[k];
         const double e = sums[kSumErr];
         const double err = (e + e) / N; // gpu.cc:71-76: find_alignment's residual is the same sum
         err_trace[s->iter] = err;
@@ -57,16 +84,16 @@ __global__ void err_step_kernel(const double *__restrict__ sums, double N, doubl
 
 } // namespace
 
-void launch_horn_step(const double *sums, double n_total, const double c[3], IterState *st_dev, hipStream_t st)
+void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,
+                      IterState *st_dev, hipStream_t st)
 {
-    horn_step_kernel<<<1, 1, 0, st>>>(sums, n_total, c[0], c[1], c[2], st_dev);
+    horn_step_kernel<<<1, 1, 0, st>>>(sums, n_total, c[0], c[1], c[2], shifted, amb_count, st_dev);
 }
 
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
-                     int *amb_count, IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st)
+                     IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st)
 {
-    err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, amb_count, st_dev, hflag_dev,
-                                     ticket);
+    err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, st_dev, hflag_dev, ticket);
 }
 
 } // namespace icp

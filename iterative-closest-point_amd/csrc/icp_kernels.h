@@ -218,14 +218,26 @@ struct IterState {
     double srt[13];    // s, R (row-major), t of the last applied iteration
     Xform xf;          // s R, t, c for the transform kernel
     long long nn_counts[4]; // sums of amb_count[0..3] over the recorded searches
+    double shift_p[3]; // one-pass moments: the next iteration's shifts (~ its centroids)
+    double shift_y[3];
 };
-// (1 thread) Horn solve from the reduced sums (icp_horn.h), unless done
-void launch_horn_step(const double *sums, double n_total, const double c[3], IterState *st_dev, hipStream_t st);
+// One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
+// partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,
+// sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)
+void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
+                            const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
+                            double *partials, hipStream_t st);
+// (1 thread) NN queue sizes amb_count[0..3] -> nn_counts (unless done), then zeroed for the next
+// search; then, unless done, the Horn solve (icp_horn.h) from the reduced sums -- two-pass
+// sums (Σp, Σy, centred S, d_caps, sp) or, if shifted, launch_shifted_moments' -- and the
+// shifts of the next iteration: sR mu_p + t (the centroid of the transformed scene) and mu_y
+void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,
+                      IterState *st_dev, hipStream_t st);
 // (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold
-// or iter == max_iter; nn_counts += amb_count[0..3] (unless done), then amb_count = 0; finally
-// hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope, mapped host memory)
+// or iter == max_iter; finally hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope,
+// mapped host memory)
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
-                     int *amb_count, IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st);
+                     IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st);
 
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);

@@ -1553,6 +1553,47 @@ __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
     block_sum_store<6>(a, partials + (size_t)blockIdx.x * 6);
 }
 
+// one pass around shifts near the centroids: the centred sums follow as
+// S = sum (p - cp)(y - cy)^T - N dp dy^T etc. (horn_step), with N dp dy^T at rounding level
+__global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
+    const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
+    const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
+    double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st,
+    double *__restrict__ partials)
+{
+    const double cp0 = st->shift_p[0], cp1 = st->shift_p[1], cp2 = st->shift_p[2];
+    const double cy0 = st->shift_y[0], cy1 = st->shift_y[1], cy2 = st->shift_y[2];
+    double a[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) a[k] = 0.0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const double4 m = m4[idx[i]];
+        yx[i] = m.x;
+        yy[i] = m.y;
+        yz[i] = m.z;
+        const double p0 = px[i] - cp0, p1 = py[i] - cp1, p2 = pz[i] - cp2;
+        const double y0 = m.x - cy0, y1 = m.y - cy1, y2 = m.z - cy2;
+        a[0] += p0;
+        a[1] += p1;
+        a[2] += p2;
+        a[3] += y0;
+        a[4] += y1;
+        a[5] += y2;
+        a[6] += p0 * y0;
+        a[7] += p0 * y1;
+        a[8] += p0 * y2;
+        a[9] += p1 * y0;
+        a[10] += p1 * y1;
+        a[11] += p1 * y2;
+        a[12] += p2 * y0;
+        a[13] += p2 * y1;
+        a[14] += p2 * y2;
+        a[15] += (y0 * y0 + y1 * y1) + y2 * y2;
+        a[16] += (p0 * p0 + p1 * p1) + p2 * p2;
+    }
+    block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
+}
+
 __global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__ x,
                                                      const double *__restrict__ y,
                                                      const double *__restrict__ z, int n,
@@ -2018,6 +2059,13 @@ void launch_nn_finalize64(const double *part_best, const int *part_idx, int spli
 // itself, see the engine's red_target): a launch less per reduction for small clouds
 int red_blocks(size_t n) { return n <= (size_t)kRedSingle ? 1 : grid_for(n, kRedMaxBlocks); }
 
+void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
+                            const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
+                            double *partials, hipStream_t st)
+{
+    shifted_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, partials);
+}
+
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
                            double *partials, hipStream_t st)
@@ -2098,9 +2146,9 @@ void launch_reduce(const double *partials, int nblocks, int K, double *out, hipS
 #define RED_CASE(k) \
     case k: reduce_kernel<k><<<1, kBlock, 0, st>>>(partials, nblocks, out); break;
         RED_CASE(1) RED_CASE(2) RED_CASE(3) RED_CASE(4) RED_CASE(5) RED_CASE(6)
-        RED_CASE(7) RED_CASE(8) RED_CASE(9) RED_CASE(10) RED_CASE(11) RED_CASE(12)
+        RED_CASE(7) RED_CASE(8) RED_CASE(9) RED_CASE(10) RED_CASE(11) RED_CASE(12) RED_CASE(17)
 #undef RED_CASE
-    default: break; // K <= 12 (the partials buffer holds 12 per block)
+    default: break; // K <= 12 or 17 (the partials buffer holds kRedMaxK per block)
     }
 }
 

@@ -72,6 +72,12 @@ for s in $STEPS; do
     profshard) run rocprof_shard8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_shard8" -o shard -- \
                python3 tools/shard_probe.py --worlds 8 --steps 20 ;;
     rounds) for r in 1 2 4 1 2 4; do ICP_NN_MIN_ROUNDS=$r ICP_DEBUG_PLAN=1 run rounds_$r 300 python tools/shard_probe.py --worlds 8 4 --steps 20 || exit 1; done ;;
+    stride) for r in 1 1000 1 1000; do ICP_NN_TIMING_STRIDE=$r run stride_$r 300 python tools/shard_probe.py --worlds 8 1 --steps 20 || exit 1; cat $OUT/stride_$r.log >> $OUT/stride_all.log; done ;;
+    ab) # AB_REV=<rev built by tools/build_ab.sh>: alternate the working tree's library and that one
+        for k in 1 2; do
+            run ab_new_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1
+            ICP_AMD_LIB=iterative-closest-point_amd/build_ab/$AB_REV/libicp_hip.so run ab_old_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1
+        done ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
