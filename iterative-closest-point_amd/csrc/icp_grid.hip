@@ -133,14 +133,15 @@ __device__ __forceinline__ void lex_min(double &best, int &bi, double d, int mi)
 // of the cell box [c0, c1], then the group folds its (D64, index) minima with xor shuffles.
 // One query's rows are independent, so the serial chain per lane is ~1/G of the box instead
 // of the whole box (the resolver is latency-bound: ~50-130 dependent loads per query).
-constexpr int kGroup = 16;
+constexpr int kGroup = 16; // default lanes per query (the launchers pick G per size)
 
+template <int G = kGroup>
 __device__ __forceinline__ void scan_box(const double q[3], const int c0[3], const int c1[3], const GridView &gv,
                                          int sub, double &best, int &bi)
 {
     const int ny = c1[1] - c0[1] + 1;
     const int nrows = ny * (c1[2] - c0[2] + 1);
-    for (int r = sub; r < nrows; r += kGroup) {
+    for (int r = sub; r < nrows; r += G) {
         const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
         const int row = (cz * gv.g[1] + cy) * gv.g[0];
         const int k1 = gv.start[row + c1[0] + 1];
@@ -151,12 +152,12 @@ __device__ __forceinline__ void scan_box(const double q[3], const int c0[3], con
     }
 }
 
-__device__ __forceinline__ void group_lex_min(double &best, int &bi)
+template <int G = kGroup> __device__ __forceinline__ void group_lex_min(double &best, int &bi)
 {
 #pragma unroll
-    for (int o = kGroup / 2; o >= 1; o >>= 1) {
-        const double ob = __shfl_xor(best, o, kGroup);
-        const int oi = __shfl_xor(bi, o, kGroup);
+    for (int o = G / 2; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(best, o, G);
+        const int oi = __shfl_xor(bi, o, G);
         lex_min(best, bi, ob, oi);
     }
 }
@@ -177,8 +178,9 @@ __device__ __forceinline__ bool complete_box(const double q[3], double r2, const
     return cells <= budget;
 }
 
-// One kGroup-lane group per queued query (grid-stride over *count; the trip count is uniform
+// One G-lane group per queued query (grid-stride over *count; the trip count is uniform
 // within a group, so a group is always entirely active).
+template <int G>
 __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
@@ -186,9 +188,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out)
 {
     const int count = *count_ptr;
-    const int sub = threadIdx.x & (kGroup - 1);
-    const int groups = gridDim.x * (kBlock / kGroup);
-    for (int t = (blockIdx.x * kBlock + threadIdx.x) / kGroup; t < count; t += groups) {
+    const int sub = threadIdx.x & (G - 1);
+    const int groups = gridDim.x * (kBlock / G);
+    for (int t = (blockIdx.x * kBlock + threadIdx.x) / G; t < count; t += groups) {
         const int j = list[t];
         const int h = hint[t];
         bool ok = h >= 0;
@@ -202,8 +204,8 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
             ok = complete_box(q, best, gv, budget, c0, c1);
         }
         if (ok) {
-            scan_box(q, c0, c1, gv, sub, best, bi);
-            group_lex_min(best, bi);
+            scan_box<G>(q, c0, c1, gv, sub, best, bi);
+            group_lex_min<G>(best, bi);
             if (sub == 0) idx[j] = bi;
         }
         const bool fb = !ok && sub == 0;
@@ -220,14 +222,15 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
 // (clamped) cell that holds a point; then the complete box around that candidate, exactly
 // as in nn_grid_resolve_kernel.  Either step over `budget` cells -> the query goes to the
 // fp64 brute force (window T = +inf).
+template <int G>
 __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
     int np, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
     double *__restrict__ fb_T)
 {
-    const int sub = threadIdx.x & (kGroup - 1);
-    const int groups = gridDim.x * (kBlock / kGroup);
-    for (int j = (blockIdx.x * kBlock + threadIdx.x) / kGroup; j < np; j += groups) {
+    const int sub = threadIdx.x & (G - 1);
+    const int groups = gridDim.x * (kBlock / G);
+    for (int j = (blockIdx.x * kBlock + threadIdx.x) / G; j < np; j += groups) {
         const double q[3] = {px[j], py[j], pz[j]};
         int c[3];
 #pragma unroll
@@ -249,8 +252,8 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
                 ok = false;
                 break;
             }
-            scan_box(q, c0, c1, gv, sub, best, bi);
-            group_lex_min(best, bi);
+            scan_box<G>(q, c0, c1, gv, sub, best, bi);
+            group_lex_min<G>(best, bi);
             if (c0[0] == 0 && c0[1] == 0 && c0[2] == 0 && c1[0] == gv.g[0] - 1 && c1[1] == gv.g[1] - 1 &&
                 c1[2] == gv.g[2] - 1)
                 break; // the whole grid (bi >= 0 unless the model is empty)
@@ -260,8 +263,8 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
             int c0[3], c1[3];
             ok = complete_box(q, best, gv, budget, c0, c1);
             if (ok) {
-                scan_box(q, c0, c1, gv, sub, best, bi);
-                group_lex_min(best, bi);
+                scan_box<G>(q, c0, c1, gv, sub, best, bi);
+                group_lex_min<G>(best, bi);
             }
         }
         ok = ok && bi >= 0;
@@ -344,8 +347,22 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, int *idx, int *fb_count, int *fb_list, double *fb_T, hipStream_t st)
 {
-    const int blocks = std::max(1, std::min((np + kBlock / kGroup - 1) / (kBlock / kGroup), 16384));
-    nn_grid_search_kernel<<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
+    // lanes per query: many queries fill the chip one per lane; few (a shard, small clouds)
+    // share lanes to shorten each query's serial chain (measured at 2^20 and 2^17 queries: 4 lanes
+    // 0.35 / 0.066 ms, 1 lane 0.40 / 0.155, 16 lanes 0.445 / 0.068).  ICP_GRID_GROUP overrides (1|4|16).
+    static const int forced = [] {
+        const char *e = getenv("ICP_GRID_GROUP");
+        return e ? atoi(e) : 0;
+    }();
+    const int g = forced == 1 || forced == 4 || forced == 16 ? forced : (np >= (1 << 16) ? 4 : 16);
+    const int per_block = kBlock / g;
+    const int blocks = std::max(1, std::min((np + per_block - 1) / per_block, 16384));
+    if (g == 1)
+        nn_grid_search_kernel<1><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
+    else if (g == 4)
+        nn_grid_search_kernel<4><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
+    else
+        nn_grid_search_kernel<16><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
 }
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
@@ -353,9 +370,21 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st)
 {
-    const int blocks = std::max(1, std::min((max_items + kBlock / kGroup - 1) / (kBlock / kGroup), 4096));
-    nn_grid_resolve_kernel<<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
-                                                      fb_count, fb_list, T_in, T_out);
+    // 16 lanes per queued query (measured against 4 at C4 and at its 8-way shard: 16 is
+    // faster at both; the queue holds the hard near ties).  ICP_GRID_RGROUP overrides (4 | 16).
+    static const int forced = [] {
+        const char *e = getenv("ICP_GRID_RGROUP");
+        return e ? atoi(e) : 0;
+    }();
+    const int g = forced == 4 ? 4 : 16;
+    const int per_block = kBlock / g;
+    const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, 4096));
+    if (g == 4)
+        nn_grid_resolve_kernel<4><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
+                                                            fb_count, fb_list, T_in, T_out);
+    else
+        nn_grid_resolve_kernel<16><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget,
+                                                             idx, fb_count, fb_list, T_in, T_out);
 }
 
 } // namespace icp

@@ -78,6 +78,8 @@ for s in $STEPS; do
             run ab_new_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1
             ICP_AMD_LIB=iterative-closest-point_amd/build_ab/$AB_REV/libicp_hip.so run ab_old_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1
         done ;;
+    gridg) for g in 1 4 16 1 4 16; do ICP_GRID_GROUP=$g run gridg_$g 300 python tools/shard_probe.py --variant grid --worlds 1 8 --steps 30 || exit 1; cat $OUT/gridg_$g.log >> $OUT/gridg_all_$g.log; done ;;
+    gridr) for g in 4 16 4 16; do ICP_GRID_RGROUP=$g run gridr_$g 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1; cat $OUT/gridr_$g.log >> $OUT/gridr_all_$g.log; done ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;

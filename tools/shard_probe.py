@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-rccl", action="store_true")
+    ap.add_argument("--variant", choices=["auto", "grid"], default="auto")
     a = ap.parse_args()
     m, p = icp_amd.synthetic_pair(a.n, seed=42)
     rows = []
@@ -35,6 +36,8 @@ def main():
         b, c = icp_amd.shard_range(a.n, 0, w)
         uid = None if a.no_rccl else icp_amd.rccl_unique_id()
         with icp_amd.Context(0, icp_amd.NN_CERTIFIED, rank=0, world_size=1, rccl_id=uid) as ctx:
+            if a.variant == "grid":
+                ctx.set_nn_variant(icp_amd.VARIANT_GRID)
             ctx.set_model(m)
             ctx.set_scene(p[b:b + c], np_total=a.n)
             ctx.run(a.warmup, -1.0)
