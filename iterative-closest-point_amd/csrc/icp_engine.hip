@@ -216,6 +216,10 @@ int ensure_reduction_space(icp_ctx *ctx)
     HIPCHK(hipMalloc((void **)&ctx->sums, sizeof(double) * 32));
     HIPCHK(hipHostMalloc((void **)&ctx->h_sums, sizeof(double) * 32, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));
+    // NN queue counters: present even for an empty shard (horn_step folds and resets them
+    // every iteration, whether or not this rank searched anything)
+    HIPCHK(hipMalloc((void **)&ctx->amb_count, sizeof(int) * 4));
+    HIPCHK(hipMemset(ctx->amb_count, 0, sizeof(int) * 4));
     return ICP_OK;
 }
 
@@ -230,7 +234,6 @@ void red_finish(icp_ctx *ctx, size_t n, int K, double *out)
 // queue of queries the fp32 certificate could not settle (list + window T + counter)
 int ensure_queue(icp_ctx *ctx, size_t n)
 {
-    if (!ctx->amb_count) HIPCHK(hipMalloc((void **)&ctx->amb_count, sizeof(int) * 4));
     if (ctx->amb_cap >= n && ctx->amb_list) return ICP_OK;
     if (ctx->amb_list) HIPCHK(hipFree(ctx->amb_list));
     if (ctx->amb_T) HIPCHK(hipFree(ctx->amb_T));
@@ -273,7 +276,7 @@ GridView grid_view(const icp_ctx *ctx)
 // amb_count [0] queue of the VALU certificate, [1] grid -> fp64 brute-force fallback,
 // [2] level-1 (MFMA) queue, [3] level-1 queries without a candidate.  ev0..ev1 brackets the
 // O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
-// zero_counts = false: amb_count is already zero (icp_run: err_step clears it)
+// zero_counts = false: amb_count is already zero (icp_run: horn_step clears it)
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
                     bool zero_counts = true, bool seeds_ready = false)
 {
@@ -393,7 +396,8 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
 void account_nn(icp_ctx *ctx, size_t n)
 {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->stats.nn_ms += ms;
+    if (n && hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->stats.nn_ms += ms;
+    (void)hipGetLastError(); // (n == 0 records no events)
     ctx->stats.nn_launches += 1;
     ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
     if (ctx->nn_mode == ICP_NN_CERTIFIED && n) {
@@ -845,10 +849,13 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;
-            if ((waited - 1) % timing_stride == 0 &&
-                hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess) {
-                ctx->stats.nn_ms += ms;
-                ctx->stats.nn_launches += 1;
+            if (n && (waited - 1) % timing_stride == 0) { // (an empty shard records no events)
+                if (hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess) {
+                    ctx->stats.nn_ms += ms;
+                    ctx->stats.nn_launches += 1;
+                } else {
+                    (void)hipGetLastError(); // a failed query must not surface at the next launch check
+                }
             }
             ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
             recorded = iters;

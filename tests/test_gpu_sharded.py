@@ -126,3 +126,22 @@ def test_rccl_single_rank_communicator(icp_lib, name, n, iters):
     np.testing.assert_array_equal(errs, ref[1])
     np.testing.assert_array_equal(np.array(res.R), np.array(ref[0].R))
     np.testing.assert_array_equal(out, ref[2])
+
+
+def test_empty_shards(icp_lib):
+    """More ranks than points: ranks 6 and 7 of 8 hold no scene point.  Their moment,
+    residual and all-reduce contributions are zero; every rank still runs the same loop."""
+    amd = icp_lib
+    rng = np.random.default_rng(7)
+    m = rng.uniform(-1, 1, size=(6, 3))
+    ang = 0.1
+    R = np.array([[np.cos(ang), -np.sin(ang), 0], [np.sin(ang), np.cos(ang), 0], [0, 0, 1]])
+    p = m @ R.T + np.array([0.01, -0.02, 0.03]) + rng.normal(0.0, 0.01, size=(6, 3))  # no exact fit
+    ref = run_single(amd, m, p, 10, -1.0)
+    assert ref[1][-1] > 1e-8
+    out = run_sharded(amd, m, p, 8, 10, -1.0)
+    assert [o[2].shape[0] for o in out] == [1, 1, 1, 1, 1, 1, 0, 0]
+    for res, errs, _ in out:
+        np.testing.assert_array_equal(errs, out[0][1])
+    np.testing.assert_allclose(out[0][1], ref[1], rtol=1e-11)
+    np.testing.assert_allclose(np.concatenate([o[2] for o in out]), ref[2], atol=1e-12)
