@@ -85,6 +85,8 @@ struct icp_ctx {
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
     IterState *h_iter = nullptr;     // pinned copy
+    double *h_few = nullptr;         // mapped host staging of the few-query path: q (3 x kFewQueries),
+    double *d_few = nullptr;         //   y (3 x kFewQueries), idx (kFewQueries ints); device address
     int *h_flags = nullptr;          // mapped host (done, iter, ticket, -) per in-flight iteration
     int *d_flags = nullptr;          // its device address (err_step writes it directly)
     int flag_ticket = 0;             // last ticket handed to an iteration
@@ -567,6 +569,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
     if (ctx->h_iter) (void)hipHostFree(ctx->h_iter);
     if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+    if (ctx->h_few) (void)hipHostFree(ctx->h_few);
     for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
@@ -894,11 +897,40 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
 
 // ---- per-operation surface ------------------------------------------------------------
 
+// Few queries (the per-point API: compute_distance_w_naive, GPU::ICP::compute_y_naive): one
+// exact fp64 launch per call with mapped host I/O, instead of the certified cascade's ~10
+// launches and two pageable copies.  Same rule (first minimum of D64), same indices.  Taken
+// by the automatic variant choice (and the fp64 mode).
+constexpr size_t kFewQueries = 32;
+
+static int closest_few(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_xyz_out, int32_t *idx_out)
+{
+    if (!ctx->h_few) {
+        HIPCHK(hipHostMalloc((void **)&ctx->h_few, sizeof(double) * 7 * kFewQueries,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_few, ctx->h_few, 0));
+    }
+    double *hq = ctx->h_few, *hy = ctx->h_few + 3 * kFewQueries;
+    int *hi = (int *)(ctx->h_few + 6 * kFewQueries);
+    std::memcpy(hq, p_xyz, sizeof(double) * 3 * np);
+    launch_nn_exact_few(ctx->d_few, (int)np, ctx->m4, (int)ctx->nm, (int *)(ctx->d_few + 6 * kFewQueries),
+                        ctx->d_few + 3 * kFewQueries, ctx->st);
+    LAUNCHCHK("nn_exact_few");
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (y_xyz_out) std::memcpy(y_xyz_out, hy, sizeof(double) * 3 * np);
+    if (idx_out) std::memcpy(idx_out, hi, sizeof(int32_t) * np);
+    ctx->stats.nn_pairs += (long long)np * (long long)ctx->nm;
+    return ICP_OK;
+}
+
 int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_xyz_out,
                        int32_t *idx_out)
 {
     TRY(check_ready(ctx, false));
     if (!p_xyz && np) return ICP_E_ARG;
+    // (an explicitly chosen NN variant always runs its own cascade, as the tests of it expect)
+    if (np && np <= kFewQueries && (ctx->nn_variant == ICP_NN_VARIANT_AUTO || ctx->nn_mode == ICP_NN_FP64))
+        return closest_few(ctx, p_xyz, np, y_xyz_out, idx_out);
     TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
     ctx->seeds_valid = false; // idx is about to hold other queries' correspondences
     TRY(nn_search(ctx, ctx->qa, np));

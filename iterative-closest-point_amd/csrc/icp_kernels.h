@@ -239,6 +239,11 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], int
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                      IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st);
 
+// exact NN of nq (few) queries, one workgroup each: q_aos (3 x nq) in, idx and y = m[idx]
+// (3 x nq) out -- all three may be mapped host memory
+void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm, int *idx_out, double *y_aos,
+                         hipStream_t st);
+
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);
 

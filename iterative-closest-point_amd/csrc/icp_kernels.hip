@@ -1431,6 +1431,58 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
     }
 }
 
+// Exact NN of a few queries in ONE launch (the per-point API, compute_distance_w_naive):
+// one workgroup per query, fp64 D in the reference's order over every model point, the
+// lexicographic (D64, index) minimum = the first minimum.  Queries are read from, and
+// (idx, y = m[idx]) written to, mapped host memory: no copies around the launch.
+__global__ __launch_bounds__(kBlock) void nn_exact_few_kernel(const double *__restrict__ q_aos, int nq,
+                                                             const double4 *__restrict__ m4, int nm,
+                                                             int *__restrict__ idx_out, double *__restrict__ y_aos)
+{
+    __shared__ double shd[kBlock / 64];
+    __shared__ int shi[kBlock / 64];
+    const int j = blockIdx.x;
+    if (j >= nq) return;
+    const double qx = q_aos[3 * j], qy = q_aos[3 * j + 1], qz = q_aos[3 * j + 2];
+    double bd = INFINITY;
+    int bi = 0x7fffffff;
+    for (int k = threadIdx.x; k < nm; k += kBlock) {
+        const double4 m = m4[k];
+        const double e = d64(qx, qy, qz, m.x, m.y, m.z);
+        if (e < bd) { // k increases per thread: strict keeps the first
+            bd = e;
+            bi = k;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double od = __shfl_xor(bd, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (od < bd || (od == bd && oi < bi)) {
+            bd = od;
+            bi = oi;
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        shd[wave] = bd;
+        shi[wave] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w)
+            if (shd[w] < bd || (shd[w] == bd && shi[w] < bi)) {
+                bd = shd[w];
+                bi = shi[w];
+            }
+        idx_out[j] = bi;
+        const double4 m = m4[bi];
+        y_aos[3 * j] = m.x;
+        y_aos[3 * j + 1] = m.y;
+        y_aos[3 * j + 2] = m.z;
+    }
+}
+
 // ---- NN: fp64 brute force ------------------------------------------------------------
 struct D4 {
     double x, y, z, w;
@@ -2033,6 +2085,12 @@ void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *
     if (grid < 1) grid = 1;
     nn_resolve_kernel<<<grid, kBlock, 0, st>>>(amb_count, amb_list, amb_T, p32, px, py, pz, m32, mx,
                                                 my, mz, nm, idx);
+}
+
+void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm, int *idx_out, double *y_aos,
+                         hipStream_t st)
+{
+    nn_exact_few_kernel<<<nq, kBlock, 0, st>>>(q_aos, nq, m4, nm, idx_out, y_aos);
 }
 
 void launch_nn_fp64(const double *px, const double *py, const double *pz, int np, const double *mx,

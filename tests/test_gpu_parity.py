@@ -281,3 +281,17 @@ def test_naive_path_matches_opti_and_oracle(amd, golden_traces):
     _, ref = amd.compute_Y_w_opti(m, p)
     for j in sel:
         assert amd.compute_distance_w_naive(m, p[j]) == ref[j]
+
+
+@pytest.mark.parametrize("nq", [1, 7, 32, 33])
+def test_nn_few_queries_exact(amd, oracle, nq):
+    """<= 32 queries under the automatic variant take the one-launch exact path (the per-point
+    API); 33 take the certified cascade.  Both are the oracle's first minimum, ties included."""
+    m = np.floor(RNG.uniform(-4, 4, size=(3000, 3)))  # integer lattice points: many exact ties
+    p = np.floor(RNG.uniform(-4, 4, size=(nq, 3))) + 0.5
+    with amd.Context(0, amd.NN_CERTIFIED) as ctx:
+        ctx.set_model(m)
+        y, idx = ctx.closest_matrix(p)
+    _, ref = oracle.closest(p, m)
+    np.testing.assert_array_equal(idx, ref)
+    np.testing.assert_array_equal(y, m[ref])

@@ -80,6 +80,9 @@ for s in $STEPS; do
         done ;;
     gridg) for g in 1 4 16 1 4 16; do ICP_GRID_GROUP=$g run gridg_$g 300 python tools/shard_probe.py --variant grid --worlds 1 8 --steps 30 || exit 1; cat $OUT/gridg_$g.log >> $OUT/gridg_all_$g.log; done ;;
     gridr) for g in 4 16 4 16; do ICP_GRID_RGROUP=$g run gridr_$g 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1; cat $OUT/gridr_$g.log >> $OUT/gridr_all_$g.log; done ;;
+    cases) COW=$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_ref"), datasets.path("cow_tr1"))')
+           set -- $COW
+           run cases 300 ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.3 ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
