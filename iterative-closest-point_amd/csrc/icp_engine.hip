@@ -110,6 +110,11 @@ struct icp_ctx {
     int *h_amb = nullptr;     // pinned
     double *stage = nullptr;
     size_t stage_cap = 0;
+    // small host <-> device transfers: a mapped pinned buffer the conversion kernels read and
+    // write directly (no pageable-copy staging); bump-allocated, recycled after a sync
+    double *h_io = nullptr, *d_io = nullptr;
+    size_t io_cap = 0, io_off = 0;
+    bool io_pending = false; // a queued kernel may still read h_io
 
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     icp_stats stats{};
@@ -187,14 +192,47 @@ void free_cloud(DevCloud &c)
     c = DevCloud{};
 }
 
+// Clouds up to this many doubles (3 x 64k points, 1.5 MiB) move through the mapped buffer.
+constexpr size_t kMappedIo = 3 * 65536;
+
+// `count` (<= 2 x kMappedIo) doubles of the mapped buffer: host pointer (*h) and device pointer
+// (*d).  When the buffer is used up it is recycled from the start, after a sync if a kernel
+// may still read it.
+int io_take(icp_ctx *ctx, size_t count, double **h, double **d)
+{
+    if (ctx->io_off + count > ctx->io_cap) {
+        if (ctx->io_pending) HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        ctx->io_off = 0;
+        if (!ctx->h_io) {
+            ctx->io_cap = 2 * kMappedIo;
+            HIPCHK(hipHostMalloc((void **)&ctx->h_io, sizeof(double) * ctx->io_cap,
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_io, ctx->h_io, 0));
+        }
+    }
+    *h = ctx->h_io + ctx->io_off;
+    *d = ctx->d_io + ctx->io_off;
+    ctx->io_off += count;
+    return ICP_OK;
+}
+
 // host AoS (3 x n col-major) -> device SoA fp64 (+ centred fp32 copy)
 int upload_cloud(icp_ctx *ctx, DevCloud &c, const double *xyz, size_t n, bool make_f32)
 {
     TRY(grow_cloud(ctx, c, n, true));
     if (!n) return ICP_OK;
-    TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * n));
-    HIPCHK(hipMemcpyAsync(ctx->stage, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice, ctx->st));
-    launch_aos_to_soa(ctx->stage, n, c.x, c.y, c.z, ctx->st);
+    if (3 * n <= kMappedIo) { // small: the conversion kernel reads the host copy directly
+        double *h, *d;
+        TRY(io_take(ctx, 3 * n, &h, &d));
+        std::memcpy(h, xyz, sizeof(double) * 3 * n);
+        launch_aos_to_soa(d, n, c.x, c.y, c.z, ctx->st);
+        ctx->io_pending = true;
+    } else {
+        TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * n));
+        HIPCHK(hipMemcpyAsync(ctx->stage, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice, ctx->st));
+        launch_aos_to_soa(ctx->stage, n, c.x, c.y, c.z, ctx->st);
+    }
     if (make_f32) launch_make_f32(c.x, c.y, c.z, n, ctx->c[0], ctx->c[1], ctx->c[2], c.f, ctx->st);
     LAUNCHCHK("upload_cloud");
     return ICP_OK;
@@ -203,6 +241,16 @@ int upload_cloud(icp_ctx *ctx, DevCloud &c, const double *xyz, size_t n, bool ma
 int download_cloud(icp_ctx *ctx, const DevCloud &c, size_t n, double *xyz)
 {
     if (!n) return ICP_OK;
+    if (3 * n <= kMappedIo) { // small: the conversion kernel writes the host copy directly
+        double *h, *d;
+        TRY(io_take(ctx, 3 * n, &h, &d));
+        launch_soa_to_aos(c.x, c.y, c.z, n, d, ctx->st);
+        LAUNCHCHK("download_cloud");
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        std::memcpy(xyz, h, sizeof(double) * 3 * n);
+        return ICP_OK;
+    }
     TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * n));
     launch_soa_to_aos(c.x, c.y, c.z, n, ctx->stage, ctx->st);
     LAUNCHCHK("download_cloud");
@@ -570,6 +618,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->h_iter) (void)hipHostFree(ctx->h_iter);
     if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
     if (ctx->h_few) (void)hipHostFree(ctx->h_few);
+    if (ctx->h_io) (void)hipHostFree(ctx->h_io);
     for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
@@ -954,6 +1003,22 @@ int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3]
     if (!ctx || !mu || (!xyz && n) || n == 0) return ICP_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
+    if (3 * n <= kMappedIo) { // small: sum and centre straight from / into mapped host memory
+        double *hin, *din; // one region: input, then the centred output (<= the buffer's 2 x kMappedIo)
+        TRY(io_take(ctx, (centred_out ? 6 : 3) * n, &hin, &din));
+        double *hout = hin + 3 * n, *dout = din + 3 * n;
+        std::memcpy(hin, xyz, sizeof(double) * 3 * n);
+        launch_sum3(din, din + 1, din + 2, (int)n, red_target(ctx, n, ctx->sums), ctx->st, 3);
+        red_finish(ctx, n, 3, ctx->sums);
+        if (centred_out) launch_centre_aos(din, (int)n, ctx->sums, dout, ctx->st);
+        LAUNCHCHK("centroid");
+        HIPCHK(hipMemcpyAsync(ctx->h_sums, ctx->sums, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        for (int k = 0; k < 3; ++k) mu[k] = ctx->h_sums[k] / (double)n; // rowwise().mean()
+        if (centred_out) std::memcpy(centred_out, hout, sizeof(double) * 3 * n);
+        return ICP_OK;
+    }
     TRY(upload_cloud(ctx, ctx->qa, xyz, n, false));
     launch_sum3(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, red_target(ctx, n, ctx->sums), ctx->st);
     red_finish(ctx, n, 3, ctx->sums);

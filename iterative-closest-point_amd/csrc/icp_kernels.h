@@ -176,7 +176,9 @@ void launch_make_aos4(const double *x, const double *y, const double *z, int n, 
                       hipStream_t st);
 // partial [sum p (3)] of one cloud
 void launch_sum3(const double *x, const double *y, const double *z, int n, double *partials,
-                 hipStream_t st);
+                 hipStream_t st, int stride = 1);
+// out = in - sums[0..2] / n (AoS in and out; either may be mapped host memory)
+void launch_centre_aos(const double *in, int n, const double *sums, double *out, hipStream_t st);
 // partial [S (9), d_caps, sp] around mu = sums[kSumP..]/n_total, sums[kSumY..]/n_total
 void launch_centred_moments(const double *px, const double *py, const double *pz,
                             const double *yx, const double *yy, const double *yz, int n,

@@ -1646,18 +1646,33 @@ __global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
     block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
 }
 
+// stride 1: SoA rows; stride 3 with x, y, z = p, p + 1, p + 2: an AoS cloud (e.g. mapped host)
 __global__ __launch_bounds__(kBlock) void sum3_kernel(const double *__restrict__ x,
                                                      const double *__restrict__ y,
-                                                     const double *__restrict__ z, int n,
+                                                     const double *__restrict__ z, int n, int stride,
                                                      double *__restrict__ partials)
 {
     double a[3] = {0, 0, 0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        a[0] += x[i];
-        a[1] += y[i];
-        a[2] += z[i];
+        const size_t o = (size_t)i * stride;
+        a[0] += x[o];
+        a[1] += y[o];
+        a[2] += z[o];
     }
     block_sum_store<3>(a, partials + (size_t)blockIdx.x * 3);
+}
+
+// out = in - mu, AoS, mu = sums[0..2] / n_total (the host's division: the same mean bits)
+__global__ __launch_bounds__(kBlock) void centre_aos_kernel(const double *__restrict__ in, int n,
+                                                           const double *__restrict__ sums, double n_total,
+                                                           double *__restrict__ out)
+{
+    const double m0 = sums[0] / n_total, m1 = sums[1] / n_total, m2 = sums[2] / n_total;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        out[3 * (size_t)i] = in[3 * (size_t)i] - m0;
+        out[3 * (size_t)i + 1] = in[3 * (size_t)i + 1] - m1;
+        out[3 * (size_t)i + 2] = in[3 * (size_t)i + 2] - m2;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void centred_moments_kernel(
@@ -2156,9 +2171,14 @@ void launch_make_aos4(const double *x, const double *y, const double *z, int n, 
 }
 
 void launch_sum3(const double *x, const double *y, const double *z, int n, double *partials,
-                 hipStream_t st)
+                 hipStream_t st, int stride)
 {
-    sum3_kernel<<<red_blocks(n), kBlock, 0, st>>>(x, y, z, n, partials);
+    sum3_kernel<<<red_blocks(n), kBlock, 0, st>>>(x, y, z, n, stride, partials);
+}
+
+void launch_centre_aos(const double *in, int n, const double *sums, double *out, hipStream_t st)
+{
+    centre_aos_kernel<<<grid_for(n), kBlock, 0, st>>>(in, n, sums, (double)n, out);
 }
 
 void launch_centred_moments(const double *px, const double *py, const double *pz,
