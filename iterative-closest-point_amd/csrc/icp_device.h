@@ -1,0 +1,84 @@
+// icp_device.h — device helpers shared by the engine's kernel files (icp_kernels.hip,
+// icp_iter.hip): the workgroup sum, and the per-point arithmetic of the moment and transform
+// passes, so that the fused small-cloud iteration (icp_iter.hip) rounds exactly like the
+// separate kernels.  Compiled with -ffp-contract=off.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "icp_kernels.h"
+
+namespace icp {
+
+// Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
+// out[k].  Fixed shuffle tree + fixed LDS order: deterministic.
+template <int K>
+__device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
+{
+    __shared__ double sh[kBlock / 64][K];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += __shfl_down(a[k], off, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
+    }
+}
+
+// y_i = m[idx_i] (stored), then point i's terms of the one-pass moments around (cp, cy):
+// sum (p - cp), sum (y - cy), sum (p - cp)(y - cy)^T, sum ||y - cy||^2, sum ||p - cp||^2
+__device__ __forceinline__ void shifted_moment_point(int i, const int *__restrict__ idx,
+                                                     const double4 *__restrict__ m4, const double *__restrict__ px,
+                                                     const double *__restrict__ py, const double *__restrict__ pz,
+                                                     double *__restrict__ yx, double *__restrict__ yy,
+                                                     double *__restrict__ yz, double cp0, double cp1, double cp2,
+                                                     double cy0, double cy1, double cy2, double (&a)[17])
+{
+    const double4 m = m4[idx[i]];
+    yx[i] = m.x;
+    yy[i] = m.y;
+    yz[i] = m.z;
+    const double p0 = px[i] - cp0, p1 = py[i] - cp1, p2 = pz[i] - cp2;
+    const double y0 = m.x - cy0, y1 = m.y - cy1, y2 = m.z - cy2;
+    a[0] += p0;
+    a[1] += p1;
+    a[2] += p2;
+    a[3] += y0;
+    a[4] += y1;
+    a[5] += y2;
+    a[6] += p0 * y0;
+    a[7] += p0 * y1;
+    a[8] += p0 * y2;
+    a[9] += p1 * y0;
+    a[10] += p1 * y1;
+    a[11] += p1 * y2;
+    a[12] += p2 * y0;
+    a[13] += p2 * y1;
+    a[14] += p2 * y2;
+    a[15] += (y0 * y0 + y1 * y1) + y2 * y2;
+    a[16] += (p0 * p0 + p1 * p1) + p2 * p2;
+}
+
+// sR p + t in Eigen's column-sweep order (compute.cu:330-339, cpu.cc:33)
+__device__ __forceinline__ void transform_point(const Xform &xf, double p0, double p1, double p2, double &q0,
+                                                double &q1, double &q2)
+{
+    q0 = ((xf.sR[0] * p0 + xf.sR[1] * p1) + xf.sR[2] * p2) + xf.t[0];
+    q1 = ((xf.sR[3] * p0 + xf.sR[4] * p1) + xf.sR[5] * p2) + xf.t[1];
+    q2 = ((xf.sR[6] * p0 + xf.sR[7] * p1) + xf.sR[8] * p2) + xf.t[2];
+}
+
+// ||y - q||^2 (compute.cu:344-345)
+__device__ __forceinline__ double residual2(double y0, double y1, double y2, double q0, double q1, double q2)
+{
+    const double e0 = y0 - q0, e1 = y1 - q1, e2 = y2 - q2;
+    return (e0 * e0 + e1 * e1) + e2 * e2;
+}
+
+} // namespace icp

@@ -84,7 +84,10 @@ struct icp_ctx {
     size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
-    IterState *h_iter = nullptr;     // pinned copy
+    IterState *h_iter = nullptr;     // mapped host mirror of the last recorded iteration's state
+    IterState *d_iter_mirror = nullptr; // its device address
+    double *h_trace = nullptr, *d_trace = nullptr; // mapped host error trace
+    size_t trace_cap = 0;
     double *h_few = nullptr;         // mapped host staging of the few-query path: q (3 x kFewQueries),
     double *d_few = nullptr;         //   y (3 x kFewQueries), idx (kFewQueries ints); device address
     int *h_flags = nullptr;          // mapped host (done, iter, ticket, -) per in-flight iteration
@@ -97,6 +100,7 @@ struct icp_ctx {
     size_t m4_cap = 0;
     unsigned *seed16 = nullptr; // seeded f16 filter: per-query shift (icp_run iterations >= 2)
     size_t seed16_cap = 0;
+    bool last_search_timed = false; // the per-operation search recorded its events
     bool seeds_valid = false;   // idx holds the previous search over the resident scene
     int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
     int *fb_list = nullptr;                           // queries the grid hands back
@@ -321,6 +325,8 @@ GridView grid_view(const icp_ctx *ctx)
     return gv;
 }
 
+constexpr size_t kInlineFallbackModel = 65536;
+
 // Launches the complete NN search of the n queries in q against the resident model ->
 // ctx->idx, with no host synchronisation: every level is sized on the device.  Queue sizes:
 // amb_count [0] queue of the VALU certificate, [1] grid -> fp64 brute-force fallback,
@@ -328,10 +334,13 @@ GridView grid_view(const icp_ctx *ctx)
 // O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
 // zero_counts = false: amb_count is already zero (icp_run: horn_step clears it)
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
-                    bool zero_counts = true, bool seeds_ready = false)
+                    bool zero_counts = true, bool seeds_ready = false, const int *stop = nullptr)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     if (!n) return ICP_OK;
+    // small models: the grid resolver scans its rare leftovers exactly in place (no fp64
+    // brute-force launch, which would almost always find an empty queue)
+    const int inline_nm = ctx->nm <= (size_t)kInlineFallbackModel ? (int)ctx->nm : 0;
     TRY(ensure_queue(ctx, n));
     if (zero_counts) HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
     if (ctx->nn_mode == ICP_NN_FP64) {
@@ -379,14 +388,14 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         if (l1 == 2)
             launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, seeds, ctx->mimg16, (int)ctx->nm_pad,
-                             pl, pb, ps, pi, ctx->st);
+                             pl, pb, ps, pi, ctx->st, stop);
         else
             launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
-                                      ctx->amb1_hint, ctx->st);
+                                      ctx->amb1_hint, ctx->st, stop);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
@@ -394,9 +403,11 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // what it cannot take (none at C4): fp64 over every model point, one workgroup each
         launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                                grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
-                               ctx->fb_T, ctx->st);
-        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
+                               ctx->fb_T, ctx->st, stop, inline_nm);
+        if (!inline_nm)
+            launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st,
+                              stop);
         LAUNCHCHK("nn_mfma");
     } else {
         const NNPlan pl = plan_nn32(n, ctx->nm_pad);
@@ -409,18 +420,20 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
-        launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
+        launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st, stop);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         CertParams cp{ctx->rm};
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, (int)n, cp, ctx->idx, ctx->amb_count, ctx->amb_list,
-                           ctx->amb_T, ctx->amb_hint, ctx->st);
+                           ctx->amb_T, ctx->amb_hint, ctx->st, stop);
         // near ties: exact through the model grid; what it cannot take, fp64 brute force
         // (sized on the device: no host round trip on this path)
         launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z, ctx->m4,
                                grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list,
-                               ctx->amb_T, ctx->fb_T, ctx->st);
-        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
+                               ctx->amb_T, ctx->fb_T, ctx->st, stop, inline_nm);
+        if (!inline_nm)
+            launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
+                              ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st,
+                              stop);
         LAUNCHCHK("nn_certified");
     }
     return ICP_OK;
@@ -435,9 +448,14 @@ int nn_counts_to_host(icp_ctx *ctx)
 
 // NN search for the per-operation surface: queues the counts to h_amb; the caller
 // synchronises, then calls account_nn.
+// searches below this many pairs are not timed: two event markers cost the stream ~9 us
+constexpr double kTimedPairs = 4294967296.0;
+
 int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
 {
-    TRY(nn_search_begin(ctx, q, n, false, ctx->ev[0], ctx->ev[1]));
+    ctx->last_search_timed = n && (double)n * (double)ctx->nm >= kTimedPairs;
+    TRY(nn_search_begin(ctx, q, n, false, ctx->last_search_timed ? ctx->ev[0] : nullptr,
+                        ctx->last_search_timed ? ctx->ev[1] : nullptr));
     return n ? nn_counts_to_host(ctx) : ICP_OK;
 }
 
@@ -446,9 +464,14 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
 void account_nn(icp_ctx *ctx, size_t n)
 {
     float ms = 0.f;
-    if (n && hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) ctx->stats.nn_ms += ms;
-    (void)hipGetLastError(); // (n == 0 records no events)
-    ctx->stats.nn_launches += 1;
+    if (ctx->last_search_timed) {
+        if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) {
+            ctx->stats.nn_ms += ms;
+            ctx->stats.nn_launches += 1;
+        } else {
+            (void)hipGetLastError(); // a failed query must not surface at the next launch check
+        }
+    }
     ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
     if (ctx->nn_mode == ICP_NN_CERTIFIED && n) {
         ctx->stats.ambiguous += ctx->h_amb[0];
@@ -618,6 +641,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->h_iter) (void)hipHostFree(ctx->h_iter);
     if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
     if (ctx->h_few) (void)hipHostFree(ctx->h_few);
+    if (ctx->h_trace) (void)hipHostFree(ctx->h_trace);
     if (ctx->h_io) (void)hipHostFree(ctx->h_io);
     for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
     for (auto &e : ctx->ev)
@@ -809,7 +833,18 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     DevCloud &P = ctx->scene, &Y = ctx->Y;
     constexpr int kAhead = 1, kRing = 4; // iterations in flight beyond the one waited on
     TRY(grow(ctx, &ctx->iter_state, &ctx->iter_state_cap, 1));
-    if (!ctx->h_iter) HIPCHK(hipHostMalloc((void **)&ctx->h_iter, sizeof(IterState), hipHostMallocDefault));
+    if (!ctx->h_iter) {
+        HIPCHK(hipHostMalloc((void **)&ctx->h_iter, sizeof(IterState), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_iter_mirror, ctx->h_iter, 0));
+    }
+    if (ctx->trace_cap < (size_t)std::max(max_iter, 1)) { // (the previous run ended with a sync)
+        if (ctx->h_trace) HIPCHK(hipHostFree(ctx->h_trace));
+        ctx->trace_cap = (size_t)std::max(max_iter, 64);
+        HIPCHK(hipHostMalloc((void **)&ctx->h_trace, sizeof(double) * ctx->trace_cap,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_trace, ctx->h_trace, 0));
+    }
+    std::memset(ctx->h_iter, 0, sizeof(IterState));
     if (!ctx->h_flags) {
         HIPCHK(hipHostMalloc((void **)&ctx->h_flags, sizeof(int) * 4 * kRing,
                              hipHostMallocMapped | hipHostMallocCoherent));
@@ -832,7 +867,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         ctx->iter_ev.push_back(e);
     }
-    HIPCHK(hipMemsetAsync(ctx->iter_state, 0, sizeof(IterState), ctx->st));
+    launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     IterState *sd = ctx->iter_state;
     int enqueued = 0, waited = 0, recorded = 0;
     bool stop = false;
@@ -841,17 +876,21 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     // one iteration late (before this iteration's Horn solve, so a converged state is still
     // frozen at the same point).  Without one, err_step follows its own transform.
     const bool lag = ctx->comm != nullptr || ctx->world > 1;
-    // the O(N*M) kernel is timed (two events) every timing_stride-th iteration
-    static const int timing_stride = [] {
+    // The O(N*M) kernel is timed (two events) every timing_stride-th iteration: every one for
+    // large searches; every 8th for small ones, where each event marker's ~4.5 us stream gap
+    // is a sizeable share of a ~70 us iteration (stats.nn_ms / nn_launches stays the mean of
+    // the timed launches).  ICP_NN_TIMING_STRIDE overrides.
+    static const int forced_stride = [] {
         const char *e = getenv("ICP_NN_TIMING_STRIDE");
-        return e ? std::max(1, atoi(e)) : 1;
+        return e ? std::max(1, atoi(e)) : 0;
     }();
+    const int timing_stride = forced_stride ? forced_stride : ((double)n * (double)ctx->nm >= kTimedPairs ? 1 : 8);
     auto enqueue_err_step = [&](int it) -> int {
         const int sl = it % kRing;
         // (done, iter) straight into mapped host memory, then the slot's ticket
         slot_ticket[sl] = ++ctx->flag_ticket;
         launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->d_flags + 4 * sl,
-                        slot_ticket[sl], ctx->st);
+                        slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace, ctx->st);
         LAUNCHCHK("err_step");
         return ICP_OK;
     };
@@ -860,10 +899,24 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == 0;
+            // (the search of an iteration queued behind the converged one returns at once)
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[3 * slot] : nullptr,
-                                timed ? ctx->iter_ev[3 * slot + 1] : nullptr, enqueued == 0,
-                                fuse_seeds && enqueued > 0));
+                                timed ? ctx->iter_ev[3 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
+                                &sd->done)); // (run_init zeroed the counters)
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
+            if (!lag && enqueued > 0 && n > 0 && n <= (size_t)kRedSingle) {
+                // small cloud, one rank: steps 2-6 in one workgroup, the same arithmetic in the
+                // same order as the separate launches below (launch latency dominates there)
+                const int sl = enqueued % kRing;
+                slot_ticket[sl] = ++ctx->flag_ticket;
+                launch_iteration_tail_small(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, P.f, ctx->sums,
+                                            N, ctx->c, ctx->amb_count, sd, threshold, max_iter, ctx->err_trace_dev,
+                                            ctx->d_flags + 4 * sl, slot_ticket[sl], ctx->d_iter_mirror,
+                                            ctx->d_trace, ctx->st);
+                LAUNCHCHK("iteration_tail_small");
+                ++enqueued;
+                continue;
+            }
             // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142): the first
             // iteration two-pass (the reference's order); later ones in one pass around the shifts
             // the previous Horn step left (its transformed centroid, its correspondence centroid)
@@ -914,18 +967,16 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         }
         stop = done != 0;
     }
-    HIPCHK(hipMemcpyAsync(ctx->h_iter, sd, sizeof(IterState), hipMemcpyDeviceToHost, ctx->st));
-    HIPCHK(hipStreamSynchronize(ctx->st));
-    const IterState &hs = *ctx->h_iter;
+    HIPCHK(hipStreamSynchronize(ctx->st)); // (the iterations queued behind the last one drain)
+    const IterState &hs = *ctx->h_iter;    // mirrored by the last recorded err_step
     icp_result r{};
     r.iterations = hs.iter;
     r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55) when no iteration ran
     r.R[0] = r.R[4] = r.R[8] = 1.0;
     if (hs.iter > 0) {
-        std::vector<double> tr((size_t)hs.iter);
-        HIPCHK(hipMemcpy(tr.data(), ctx->err_trace_dev, sizeof(double) * tr.size(), hipMemcpyDeviceToHost));
-        if (err_trace) std::memcpy(err_trace, tr.data(), sizeof(double) * tr.size());
-        r.err = tr.back();
+        const double *tr = ctx->h_trace;
+        if (err_trace) std::memcpy(err_trace, tr, sizeof(double) * (size_t)hs.iter);
+        r.err = tr[hs.iter - 1];
         r.converged = r.err < threshold ? 1 : 0;
         r.s = hs.srt[0];
         for (int k = 0; k < 9; ++k) r.R[k] = hs.srt[1 + k];

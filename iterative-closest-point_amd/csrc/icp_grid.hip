@@ -185,8 +185,10 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count,
-    int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out)
+    int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out, const int *__restrict__ stop,
+    int inline_nm)
 {
+    if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int count = *count_ptr;
     const int sub = threadIdx.x & (G - 1);
     const int groups = gridDim.x * (kBlock / G);
@@ -207,10 +209,20 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
             scan_box<G>(q, c0, c1, gv, sub, best, bi);
             group_lex_min<G>(best, bi);
             if (sub == 0) idx[j] = bi;
+        } else if (inline_nm > 0) { // small model: the exact fp64 scan of every point, right here
+            best = INFINITY;
+            bi = -1;
+            for (int k = sub; k < inline_nm; k += G) {
+                const double4 m = m4[k];
+                lex_min(best, bi, d64g(q[0], q[1], q[2], m.x, m.y, m.z), k);
+            }
+            group_lex_min<G>(best, bi);
+            if (sub == 0) idx[j] = bi;
         }
+        // queue for nn_resolve -- or, scanned inline, only counted (the fallback statistic)
         const bool fb = !ok && sub == 0;
         const int slot = wave_append(fb_count, fb);
-        if (fb) {
+        if (fb && inline_nm == 0) {
             fb_list[slot] = j;
             T_out[slot] = T_in ? T_in[t] : INFINITY; // +inf: every model point
         }
@@ -368,7 +380,7 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
-                            const double *T_in, double *T_out, hipStream_t st)
+                            const double *T_in, double *T_out, hipStream_t st, const int *stop, int inline_nm)
 {
     // 16 lanes per queued query (measured against 4 at C4 and at its 8-way shard: 16 is
     // faster at both; the queue holds the hard near ties).  ICP_GRID_RGROUP overrides (4 | 16).
@@ -381,10 +393,10 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
     const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, 4096));
     if (g == 4)
         nn_grid_resolve_kernel<4><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
-                                                            fb_count, fb_list, T_in, T_out);
+                                                            fb_count, fb_list, T_in, T_out, stop, inline_nm);
     else
         nn_grid_resolve_kernel<16><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget,
-                                                             idx, fb_count, fb_list, T_in, T_out);
+                                                             idx, fb_count, fb_list, T_in, T_out, stop, inline_nm);
 }
 
 } // namespace icp

@@ -81,12 +81,12 @@ NNPlan plan_nn64(size_t np, size_t nm_pad);
 
 // fp32 direct-form filter: partial (best, second, argbest) per (split, query)
 void launch_nn_filter(const float4 *p32, int nslots, const float4 *m32, int nm_pad, const NNPlan &plan,
-                      float *part_best, float *part_second, int *part_idx, hipStream_t st);
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st, const int *stop = nullptr);
 // merge splits, certify, write idx for certified queries, queue the rest (window T, and the
 // fp32 winner in amb_hint: the grid resolver's candidate).
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
                         int splits, const float4 *p32, int nslots, CertParams cp, int *idx, int *amb_count,
-                        int *amb_list, double *amb_T, int *amb_hint, hipStream_t st);
+                        int *amb_list, double *amb_T, int *amb_hint, hipStream_t st, const int *stop = nullptr);
 // MFMA expanded-form filter (G = |m|^2 - 2 p.m) and its certificate; uncertified queries
 // are appended to amb_list (no window: they go through the direct-form filter next).
 constexpr int kMfmaQG = 4; // 16-query groups per wave
@@ -107,17 +107,17 @@ void launch_build_mimage16(const double *mx, const double *my, const double *mz,
 // seed16 == nullptr: unseeded filter
 void launch_nn_mfma16(const double *px, const double *py, const double *pz, int np, const double c[3],
                       double scale, const unsigned *seed16, const void *img, int nm_pad, const NNPlan &plan,
-                      float *part_best, float *part_second, int *part_idx, hipStream_t st);
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st, const int *stop = nullptr);
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
-                               hipStream_t st);
+                               hipStream_t st, const int *stop = nullptr);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
                        const float4 *m32, const double *mx, const double *my, const double *mz,
-                       int nm, int max_items, int *idx, hipStream_t st);
+                       int nm, int max_items, int *idx, hipStream_t st, const int *stop = nullptr);
 // fp64 brute force: partial (best d64, argbest) per (split, query), then merge.
 void launch_nn_fp64(const double *px, const double *py, const double *pz, int np,
                     const double *mx, const double *my, const double *mz, int nm,
@@ -151,10 +151,13 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 // over the grid box that must contain every point at least as close as the candidate ->
 // idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its window T_in[t]
 // (T = +inf without T_in: every model point) for nn_resolve.
+// inline_nm > 0 (a model of that many points): queries the grid cannot take are scanned
+// exactly in place (no fallback queue, no nn_resolve launch)
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
-                            const double *T_in, double *T_out, hipStream_t st);
+                            const double *T_in, double *T_out, hipStream_t st, const int *stop = nullptr,
+                            int inline_nm = 0);
 
 // Exact grid NN of all np queries (ICP_NN_VARIANT_GRID): idx, or fb_list (+ fb_T = +inf)
 // for the queries whose ring or box would exceed `budget` cells.
@@ -212,6 +215,8 @@ void launch_transform_err_dev(double *px, double *py, double *pz, const double *
                               double *partials, const SeedArgs &sa, hipStream_t st);
 
 // ---- device-resident ICP iteration (icp_iter.hip) -----------------------------------
+// `stop` (NN launchers): when non-null and *stop != 0 the kernels return at once -- the
+// search of an ICP iteration queued behind the one that converged.
 // Per-run device state: done flag, iterations recorded, error trace, last (s, R, t),
 // the transform for launch_transform_err_dev, NN queue-size totals.
 struct IterState {
@@ -236,10 +241,20 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
 void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,
                       IterState *st_dev, hipStream_t st);
 // (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold
-// or iter == max_iter; finally hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope,
-// mapped host memory)
+// or iter == max_iter; a recorded iteration is mirrored to mapped host memory (h_state, h_trace[iter]);
+// finally hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope, mapped host memory)
 void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
-                     IterState *st_dev, int *hflag_dev, int ticket, hipStream_t st);
+                     IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
+                     hipStream_t st);
+// iterations >= 2 of a <= kRedSingle-point single-rank run, after the NN search: moments,
+// Horn step, transform + residual and error step in one workgroup (same arithmetic)
+void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, double *py, double *pz, int n,
+                                 double *yx, double *yy, double *yz, float4 *p32, double *sums, double n_total,
+                                 const double c[3], int *amb_count, IterState *st_dev, double threshold,
+                                 int max_iter, double *err_trace, int *hflag_dev, int ticket,
+                                 IterState *h_state_dev, double *h_trace_dev, hipStream_t st);
+// zero a run's IterState and the NN queue counters (amb_count[0..3])
+void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st);
 
 // exact NN of nq (few) queries, one workgroup each: q_aos (3 x nq) in, idx and y = m[idx]
 // (3 x nq) out -- all three may be mapped host memory

@@ -27,6 +27,7 @@
 // Result: bit-identical indices to the fp64 brute force, at fp32 VALU cost.
 // ---------------------------------------------------------------------------------
 #include "icp_kernels.h"
+#include "icp_device.h"
 
 #include <cmath>
 #include <cstdio>
@@ -89,27 +90,6 @@ template <class V> __device__ __forceinline__ float min16_nocanon(const V &d)
     return fminf(fminf(fminf(a, b), c), fminf(fminf(e, f), d[15]));
 }
 
-// Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
-// out[k].  Fixed shuffle tree + fixed LDS order: deterministic.
-template <int K>
-__device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
-{
-    __shared__ double sh[kBlock / 64][K];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-        for (int k = 0; k < K; ++k) a[k] += __shfl_down(a[k], off, 64);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
-    __syncthreads();
-    if (threadIdx.x < K) {
-        const int k = threadIdx.x;
-        out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
-    }
-}
-
 // ---- layout ------------------------------------------------------------------------
 
 __global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const double *__restrict__ aos,
@@ -159,9 +139,11 @@ __global__ __launch_bounds__(kBlock) void make_f32_kernel(const double *__restri
 template <int Q, int TILE>
 __global__ __launch_bounds__(kBlock) void nn_filter_kernel(
     const float4 *__restrict__ p32, int nslots, const float4 *__restrict__ m32, int nm_pad, int chunk,
-    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx)
+    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx,
+    const int *__restrict__ stop)
 {
     __shared__ float4 tile[TILE];
+    if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int tid = threadIdx.x;
     const int split = blockIdx.y;
     const int m0 = split * chunk;
@@ -261,22 +243,65 @@ __device__ __forceinline__ void merge_splits(const float *__restrict__ part_best
     }
 }
 
+// (best, second, index) of two partial results, lexicographic on (value, index): the split
+// order of merge_splits (splits are increasing index ranges, so "earlier split keeps ties"
+// is "smaller index wins"), but associative and commutative -- any fold order is the same
+__device__ __forceinline__ void combine_partial(float &b, float &s2, int &id, float ob, float os, int oi)
+{
+    if (ob < b || (ob == b && (unsigned)oi < (unsigned)id)) {
+        s2 = fminf(b, os);
+        b = ob;
+        id = oi;
+    } else {
+        s2 = fminf(s2, ob);
+    }
+}
+
+// merge_splits with G lanes per query (lane `sub` folds splits sub, sub + G, ...; then an
+// xor-shuffle fold): G independent load chains instead of one, for searches cut in many splits
+template <int G>
+__device__ __forceinline__ void merge_splits_group(const float *__restrict__ part_best,
+                                                   const float *__restrict__ part_second,
+                                                   const int *__restrict__ part_idx, int splits, int nslots, int s,
+                                                   int sub, float &b, float &s2, int &id)
+{
+    if (G == 1) {
+        merge_splits(part_best, part_second, part_idx, splits, nslots, s, b, s2, id);
+        return;
+    }
+    b = INFINITY;
+    s2 = INFINITY;
+    id = -1;
+    for (int sp = sub; sp < splits; sp += G) {
+        const size_t o = (size_t)sp * nslots + s;
+        combine_partial(b, s2, id, part_best[o], part_second[o], part_idx[o]);
+    }
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) {
+        const float ob = __shfl_xor(b, off, G), os = __shfl_xor(s2, off, G);
+        const int oi = __shfl_xor(id, off, G);
+        combine_partial(b, s2, id, ob, os, oi);
+    }
+}
+
+template <int G>
 __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int nslots, double rm,
-    int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint)
+    int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint, const int *__restrict__ stop)
 {
-    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (stop && *stop) return; // a frozen (converged) ICP iteration
+    const int j = blockIdx.x * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
     const bool valid = j < nslots; // no early exit: block_append is workgroup-wide
     bool ok = true;
     double T = 0.0;
     int id = -1;
     if (valid) {
         float b, s2;
-        merge_splits(part_best, part_second, part_idx, splits, nslots, j, b, s2, id);
+        merge_splits_group<G>(part_best, part_second, part_idx, splits, nslots, j, sub, b, s2, id);
         T = cert_window(b, p32[j], rm);
-        ok = (double)s2 > T;
-        if (ok) idx[j] = id; // unique candidate => exact fp64 first-min
+        ok = (double)s2 > T || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
+        if (ok && sub == 0) idx[j] = id; // unique candidate => exact fp64 first-min
     }
     const int slot = block_append(amb_count, !ok);
     if (!ok) {
@@ -479,8 +504,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
-    float *__restrict__ part_second, int *__restrict__ part_idx)
+    float *__restrict__ part_second, int *__restrict__ part_idx, const int *__restrict__ stop)
 {
+    if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     // two 512-point tiles (16 KiB each): the next tile streams in by LDS-DMA
     // (global_load_lds_dwordx4, one 1-KiB block per wave-instruction) while this one is used
     __shared__ half8_t tiles[2][kTile16 * 2];
@@ -648,8 +674,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
-    float *__restrict__ part_second, int *__restrict__ part_idx)
+    float *__restrict__ part_second, int *__restrict__ part_idx, const int *__restrict__ stop)
 {
+    if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     constexpr int QG = 4;
     __shared__ half8_t tiles[2][kTile16 * 2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -848,8 +875,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
-    float *__restrict__ part_second, int *__restrict__ part_idx)
+    float *__restrict__ part_second, int *__restrict__ part_idx, const int *__restrict__ stop)
 {
+    if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     constexpr int QG = 4;
     __shared__ half8_t tiles[2][kTile16 * 2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1029,8 +1057,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     int np, double cx, double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const half8_t *__restrict__ mimg, int nm_pad, int chunk, float *__restrict__ part_best,
-    float *__restrict__ part_second, int *__restrict__ part_idx)
+    float *__restrict__ part_second, int *__restrict__ part_idx, const int *__restrict__ stop)
 {
+    if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     static_assert(QG >= 4, "the pipeline issues two MFMAs ahead");
     __shared__ half8_t tiles[2][kTile16 * 2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1262,20 +1291,22 @@ __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
 // products (the shift) enter the accumulation: (16 + 3 + 4) u sum|p| with sum|p| including
 // |s0'|, so delta_s(R) = 28u R^2 + 64u A R + 24u |s0'| + 4u (A + R) + 1e-3.  Any s0' keeps
 // the test sound; a poor one only queues the query.
-template <bool SEEDED>
+template <bool SEEDED, int G>
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int np, int nm, double cx,
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
-    const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
+    const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint,
+    const int *__restrict__ stop)
 {
-    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
+    const int j = blockIdx.x * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
     const bool valid = j < np; // no early exit: block_append is workgroup-wide
     const int jj = valid ? j : 0;
     float b = 0.0f, s2 = 0.0f;
     int id = -1;
-    if (valid) merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    if (valid) merge_splits_group<G>(part_best, part_second, part_idx, splits, np, j, sub, b, s2, id);
     if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
     const double ax = (px[jj] - cx) * scale, ay = (py[jj] - cy) * scale, az = (pz[jj] - cz) * scale;
     bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
@@ -1298,8 +1329,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
         ok = sg > T;
     }
-    ok = ok || !valid;
-    if (ok && valid) idx[j] = id;
+    ok = ok || !valid || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
+    if (ok && valid && sub == 0) idx[j] = id;
     // queue + the statistic of queries without a level-1 candidate, one atomic each per workgroup
     const int slot = block_append(amb_count, !ok, amb_count + 1, !ok && id < 0);
     if (!ok) {
@@ -1390,9 +1421,11 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
     const double *__restrict__ amb_T, const float4 *__restrict__ p32,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const float4 *__restrict__ m32, const double *__restrict__ mx, const double *__restrict__ my,
-    const double *__restrict__ mz, int nm, int *__restrict__ idx)
+    const double *__restrict__ mz, int nm, int *__restrict__ idx, const int *__restrict__ stop)
 {
     __shared__ double shd[kBlock];
+    if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
+
     __shared__ int shi[kBlock];
     const int count = *amb_count;
     for (int item = blockIdx.x; item < count; item += gridDim.x) {
@@ -1613,36 +1646,14 @@ __global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
     double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st,
     double *__restrict__ partials)
 {
+    if (st->done) return; // a frozen (converged) ICP iteration: its sums are never used
     const double cp0 = st->shift_p[0], cp1 = st->shift_p[1], cp2 = st->shift_p[2];
     const double cy0 = st->shift_y[0], cy1 = st->shift_y[1], cy2 = st->shift_y[2];
     double a[17];
 #pragma unroll
     for (int k = 0; k < 17; ++k) a[k] = 0.0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const double4 m = m4[idx[i]];
-        yx[i] = m.x;
-        yy[i] = m.y;
-        yz[i] = m.z;
-        const double p0 = px[i] - cp0, p1 = py[i] - cp1, p2 = pz[i] - cp2;
-        const double y0 = m.x - cy0, y1 = m.y - cy1, y2 = m.z - cy2;
-        a[0] += p0;
-        a[1] += p1;
-        a[2] += p2;
-        a[3] += y0;
-        a[4] += y1;
-        a[5] += y2;
-        a[6] += p0 * y0;
-        a[7] += p0 * y1;
-        a[8] += p0 * y2;
-        a[9] += p1 * y0;
-        a[10] += p1 * y1;
-        a[11] += p1 * y2;
-        a[12] += p2 * y0;
-        a[13] += p2 * y1;
-        a[14] += p2 * y2;
-        a[15] += (y0 * y0 + y1 * y1) + y2 * y2;
-        a[16] += (p0 * p0 + p1 * p1) + p2 * p2;
-    }
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+        shifted_moment_point(i, idx, m4, px, py, pz, yx, yy, yz, cp0, cp1, cp2, cy0, cy1, cy2, a);
     block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
 }
 
@@ -1748,13 +1759,9 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     const Xform xf = sxf;
     double a[1] = {0.0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const double p0 = px[i], p1 = py[i], p2 = pz[i];
-        // sr * p + t in Eigen's column-sweep order (compute.cu:330-339, cpu.cc:33)
-        const double q0 = ((xf.sR[0] * p0 + xf.sR[1] * p1) + xf.sR[2] * p2) + xf.t[0];
-        const double q1 = ((xf.sR[3] * p0 + xf.sR[4] * p1) + xf.sR[5] * p2) + xf.t[1];
-        const double q2 = ((xf.sR[6] * p0 + xf.sR[7] * p1) + xf.sR[8] * p2) + xf.t[2];
-        const double e0 = yx[i] - q0, e1 = yy[i] - q1, e2 = yz[i] - q2;
-        a[0] += (e0 * e0 + e1 * e1) + e2 * e2; // compute.cu:344-345
+        double q0, q1, q2;
+        transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
+        a[0] += residual2(yx[i], yy[i], yz[i], q0, q1, q2);
         if (write_p) {
             px[i] = q0;
             py[i] = q1;
@@ -1932,27 +1939,34 @@ NNPlan plan_nn64(size_t np, size_t nm)
 }
 
 void launch_nn_filter(const float4 *p32, int nslots, const float4 *m32, int nm_pad, const NNPlan &pl,
-                      float *part_best, float *part_second, int *part_idx, hipStream_t st)
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st, const int *stop)
 {
     dim3 grid(pl.qblocks, pl.splits);
     if (pl.q_per_lane == 4)
         nn_filter_kernel<4, kTile32><<<grid, kBlock, 0, st>>>(p32, nslots, m32, nm_pad, pl.chunk, part_best,
-                                                               part_second, part_idx);
+                                                               part_second, part_idx, stop);
     else if (pl.tile == kTileSmall)
         nn_filter_kernel<1, kTileSmall><<<grid, kBlock, 0, st>>>(p32, nslots, m32, nm_pad, pl.chunk, part_best,
-                                                                  part_second, part_idx);
+                                                                  part_second, part_idx, stop);
     else
         nn_filter_kernel<1, kTile32><<<grid, kBlock, 0, st>>>(p32, nslots, m32, nm_pad, pl.chunk, part_best,
-                                                               part_second, part_idx);
+                                                               part_second, part_idx, stop);
 }
+
+// lanes per query of the finalize kernels: the split merge is a latency chain of `splits` loads
+static int finalize_lanes(int splits) { return splits >= 12 ? 8 : (splits >= 4 ? 4 : 1); }
 
 void launch_nn_finalize(const float *part_best, const float *part_second, const int *part_idx,
                         int splits, const float4 *p32, int nslots, CertParams cp, int *idx, int *amb_count,
-                        int *amb_list, double *amb_T, int *amb_hint, hipStream_t st)
+                        int *amb_list, double *amb_T, int *amb_hint, hipStream_t st, const int *stop)
 {
-    const int grid = (nslots + kBlock - 1) / kBlock;
-    nn_finalize_kernel<<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32, nslots, cp.rm, idx,
-                                                amb_count, amb_list, amb_T, amb_hint);
+    const int g = finalize_lanes(splits), per_block = kBlock / g;
+    const int grid = (nslots + per_block - 1) / per_block;
+#define FIN(G)                                                                                                    \
+    nn_finalize_kernel<G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32, nslots, cp.rm, \
+                                                   idx, amb_count, amb_list, amb_T, amb_hint, stop)
+    if (g == 8) FIN(8); else if (g == 4) FIN(4); else FIN(1);
+#undef FIN
 }
 
 NNPlan plan_nn_mfma(size_t np, size_t nm_pad)
@@ -2039,13 +2053,13 @@ void launch_build_mimage16(const double *mx, const double *my, const double *mz,
 
 void launch_nn_mfma16(const double *px, const double *py, const double *pz, int np, const double c[3],
                       double scale, const unsigned *seed16, const void *img, int nm_pad, const NNPlan &pl,
-                      float *part_best, float *part_second, int *part_idx, hipStream_t st)
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st, const int *stop)
 {
     dim3 grid(pl.qblocks, pl.splits);
     const half8_t *im = (const half8_t *)img;
 #define LAUNCH16(K)                                                                               \
     K<<<grid, kBlock, 0, st>>>(px, py, pz, np, c[0], c[1], c[2], scale, seed16, im, nm_pad, pl.chunk, \
-                               part_best, part_second, part_idx)
+                               part_best, part_second, part_idx, stop)
     const bool sd = seed16 != nullptr;
     switch (mfma16_kernel_choice(sd)) {
     case kK16R8: LAUNCH16(nn_mfma16r_kernel<8>); break;
@@ -2070,17 +2084,26 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
-                               hipStream_t st)
+                               hipStream_t st, const int *stop)
 {
-    const int grid = (np + kBlock - 1) / kBlock;
-    if (seed16)
-        nn_finalize_mfma16_kernel<true><<<grid, kBlock, 0, st>>>(
-            part_best, part_second, part_idx, splits, px, py, pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,
-            idx, amb_count, amb_list, amb_hint);
-    else
-        nn_finalize_mfma16_kernel<false><<<grid, kBlock, 0, st>>>(
-            part_best, part_second, part_idx, splits, px, py, pz, np, nm, c[0], c[1], c[2], scale, nullptr, mms,
-            idx, amb_count, amb_list, amb_hint);
+    // (its fp64 certificate is heavy and every lane of a group repeats it: lanes only pay off
+    // for very many splits; ICP_FIN16_LANES = 1 | 4 | 8 overrides, for experiments)
+    static const int forced = [] {
+        const char *e = getenv("ICP_FIN16_LANES");
+        return e ? atoi(e) : 0;
+    }();
+    const int g = forced == 1 || forced == 4 || forced == 8 ? forced : 1, per_block = kBlock / g;
+    const int grid = (np + per_block - 1) / per_block;
+#define FIN16(SD, G)                                                                                         \
+    nn_finalize_mfma16_kernel<SD, G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
+                                                              pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
+                                                              idx, amb_count, amb_list, amb_hint, stop)
+    if (seed16) {
+        if (g == 8) FIN16(true, 8); else if (g == 4) FIN16(true, 4); else FIN16(true, 1);
+    } else {
+        if (g == 8) FIN16(false, 8); else if (g == 4) FIN16(false, 4); else FIN16(false, 1);
+    }
+#undef FIN16
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
@@ -2094,12 +2117,12 @@ void launch_nn_finalize_mfma(const float *part_best, const float *part_second, c
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
                        const float4 *m32, const double *mx, const double *my, const double *mz,
-                       int nm, int max_items, int *idx, hipStream_t st)
+                       int nm, int max_items, int *idx, hipStream_t st, const int *stop)
 {
     int grid = max_items < 2048 ? max_items : 2048;
     if (grid < 1) grid = 1;
     nn_resolve_kernel<<<grid, kBlock, 0, st>>>(amb_count, amb_list, amb_T, p32, px, py, pz, m32, mx,
-                                                my, mz, nm, idx);
+                                                my, mz, nm, idx, stop);
 }
 
 void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm, int *idx_out, double *y_aos,

@@ -62,6 +62,10 @@ for s in $STEPS; do
            set -- $COW
            run rocprof_cow 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_cow" -o cow -- \
                ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.3 --only opti_gpu_loop ;;
+    profcowapi) COW=$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_ref"), datasets.path("cow_tr1"))')
+           set -- $COW
+           run rocprof_cowapi 300 rocprofv3 --kernel-trace --hip-trace --output-format csv -d "$OUT/prof_cowapi" -o cow -- \
+               ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.1 --only opti_gpu_loop ;;
     sqseed) run sqs1 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE \
                 --output-format csv -d "$OUT/sqs1" -o sq -- python3 tools/nn_probe.py --variant mfma16 --icp 4 &&
             run sqs2 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE \
@@ -83,6 +87,7 @@ for s in $STEPS; do
     cases) COW=$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_ref"), datasets.path("cow_tr1"))')
            set -- $COW
            run cases 300 ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.3 ;;
+    fin16) for g in 1 4 8 1 4 8; do ICP_FIN16_LANES=$g run fin16_$g 300 python tools/shard_probe.py --worlds 8 1 --steps 20 || exit 1; cat $OUT/fin16_$g.log >> $OUT/fin16_all_$g.log; done ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
