@@ -125,6 +125,105 @@ ICP_HD inline void largest_eigvec_sym4(const double Nin[16], double q[4], double
     for (int r = 0; r < 4; ++r) q[r] = col[r] / nrm;
 }
 
+// Adjugate of a 4x4 (b = det(a) a^-1), from the 2x2 minors of rows (0,1) and (2,3).
+ICP_HD inline void adj4(const double (&a)[4][4], double (&b)[4][4])
+{
+    const double s0 = a[0][0] * a[1][1] - a[1][0] * a[0][1], s1 = a[0][0] * a[1][2] - a[1][0] * a[0][2];
+    const double s2 = a[0][0] * a[1][3] - a[1][0] * a[0][3], s3 = a[0][1] * a[1][2] - a[1][1] * a[0][2];
+    const double s4 = a[0][1] * a[1][3] - a[1][1] * a[0][3], s5 = a[0][2] * a[1][3] - a[1][2] * a[0][3];
+    const double c5 = a[2][2] * a[3][3] - a[3][2] * a[2][3], c4 = a[2][1] * a[3][3] - a[3][1] * a[2][3];
+    const double c3 = a[2][1] * a[3][2] - a[3][1] * a[2][2], c2 = a[2][0] * a[3][3] - a[3][0] * a[2][3];
+    const double c1 = a[2][0] * a[3][2] - a[3][0] * a[2][2], c0 = a[2][0] * a[3][1] - a[3][0] * a[2][1];
+    b[0][0] = (a[1][1] * c5 - a[1][2] * c4) + a[1][3] * c3;
+    b[0][1] = (-a[0][1] * c5 + a[0][2] * c4) - a[0][3] * c3;
+    b[0][2] = (a[3][1] * s5 - a[3][2] * s4) + a[3][3] * s3;
+    b[0][3] = (-a[2][1] * s5 + a[2][2] * s4) - a[2][3] * s3;
+    b[1][0] = (-a[1][0] * c5 + a[1][2] * c2) - a[1][3] * c1;
+    b[1][1] = (a[0][0] * c5 - a[0][2] * c2) + a[0][3] * c1;
+    b[1][2] = (-a[3][0] * s5 + a[3][2] * s2) - a[3][3] * s1;
+    b[1][3] = (a[2][0] * s5 - a[2][2] * s2) + a[2][3] * s1;
+    b[2][0] = (a[1][0] * c4 - a[1][1] * c2) + a[1][3] * c0;
+    b[2][1] = (-a[0][0] * c4 + a[0][1] * c2) - a[0][3] * c0;
+    b[2][2] = (a[3][0] * s4 - a[3][1] * s2) + a[3][3] * s0;
+    b[2][3] = (-a[2][0] * s4 + a[2][1] * s2) - a[2][3] * s0;
+    b[3][0] = (-a[1][0] * c3 + a[1][1] * c1) - a[1][2] * c0;
+    b[3][1] = (a[0][0] * c3 - a[0][1] * c1) + a[0][2] * c0;
+    b[3][2] = (-a[3][0] * s3 + a[3][1] * s1) - a[3][2] * s0;
+    b[3][3] = (a[2][0] * s3 - a[2][1] * s1) + a[2][2] * s0;
+}
+
+// Eigenvector of the largest eigenvalue of a symmetric 4x4 through its characteristic
+// polynomial (as in Theobald's QCP): Newton on P(l) = det(l I - A) from an upper bound of the
+// largest root -- all roots are real, so the iterates fall monotonically onto it -- then q is
+// the column of adj(A - l I) = prod_j (l_j - l) v v^T with the largest diagonal entry.
+// About a tenth of the dependent fp64 chain of the Jacobi sweeps.  Accuracy: P'(l) is the
+// product of the gaps to the other eigenvalues; when it falls below 1e-3 |A|^3 (a near-multiple
+// largest eigenvalue, where the cofactors cancel) this returns false and the caller runs
+// Jacobi.  `bound`: a known upper bound of the largest eigenvalue (or +inf).
+ICP_HD inline bool largest_eigvec_sym4_poly(const double Nin[16], double bound, double q[4])
+{
+    double a[4][4];
+    double nrm = 0.0, gersh = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double row = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a[r][c] = 0.5 * (Nin[4 * r + c] + Nin[4 * c + r]);
+            row += fabs(a[r][c]);
+        }
+        nrm = fmax(nrm, row);
+        gersh = fmax(gersh, a[r][r] + (row - fabs(a[r][r])));
+    }
+    if (!(nrm > 0.0) || !(nrm < INFINITY)) return false;
+    double b[4][4];
+    adj4(a, b);
+    const double c3 = -(((a[0][0] + a[1][1]) + a[2][2]) + a[3][3]);
+    double c2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i + 1; j < 4; ++j) c2 += a[i][i] * a[j][j] - a[i][j] * a[i][j];
+    const double c1 = -(((b[0][0] + b[1][1]) + b[2][2]) + b[3][3]);
+    const double c0 = ((a[0][0] * b[0][0] + a[0][1] * b[1][0]) + a[0][2] * b[2][0]) + a[0][3] * b[3][0];
+    // start just above the tighter bound (the bounds are exact; the inflation covers rounding)
+    double lam = fmin(gersh, bound);
+    lam += fabs(lam) * 1e-12 + nrm * 1e-15;
+    double dp = 0.0;
+    for (int it = 0; it < 64; ++it) {
+        const double p = (((lam + c3) * lam + c2) * lam + c1) * lam + c0;
+        dp = ((4.0 * lam + 3.0 * c3) * lam + 2.0 * c2) * lam + c1;
+        if (!(p > 0.0) || !(dp > 0.0)) break; // at the root to rounding
+        const double step = p / dp;
+        lam -= step;
+        if (!(step > fabs(lam) * 0x1.0p-52)) break;
+    }
+    dp = ((4.0 * lam + 3.0 * c3) * lam + 2.0 * c2) * lam + c1;
+    if (!(dp > 1e-3 * nrm * nrm * nrm)) return false; // near-multiple largest eigenvalue
+    double m[4][4], adj[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) m[r][c] = r == c ? a[r][c] - lam : a[r][c];
+    adj4(m, adj);
+    // the column with the largest diagonal entry (selects only: no dynamic index)
+    double best = fabs(adj[0][0]);
+    double v[4] = {adj[0][0], adj[1][0], adj[2][0], adj[3][0]};
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const bool take = fabs(adj[k][k]) > best;
+        best = take ? fabs(adj[k][k]) : best;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = take ? adj[r][k] : v[r];
+    }
+    const double n2 = ((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]) + v[3] * v[3];
+    if (!(n2 > 0.0) || !(n2 < INFINITY)) return false;
+    const double inv = 1.0 / sqrt(n2);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[r] = v[r] * inv;
+    return true;
+}
+
 // 3x3 row-major matrix times vector in the reference's accumulation order
 // ((a0 x0 + a1 x1) + a2 x2) — this file is compiled with -ffp-contract=off.
 ICP_HD inline void matvec3(const double A[9], const double x[3], double out[3])
@@ -146,7 +245,9 @@ ICP_HD inline void horn_solve(const double S[9], const double mu_p[3], const dou
         s(2, 0) - s(0, 2), s(1, 0) + s(0, 1), s(1, 1) - s(2, 2) - s(0, 0), s(1, 2) + s(2, 1),
         -1 * s(1, 0) + s(0, 1), s(2, 0) + s(0, 2), s(2, 1) + s(1, 2), s(2, 2) - s(1, 1) - s(0, 0)};
     double q[4], ev[4];
-    largest_eigvec_sym4(N, q, ev);
+    // polynomial path (bound: max_q q^T N q = max_R sum y'.R p' <= (d_caps + sp) / 2), Jacobi
+    // when the largest eigenvalue is near-multiple
+    if (!largest_eigvec_sym4_poly(N, 0.5 * (d_caps + sp), q)) largest_eigvec_sym4(N, q, ev);
     // R = (Qbar^T Q)[1:4, 1:4]  (gpu.cc:119-133)
     const double qb[16] = {q[0], -q[1], -q[2], -q[3], q[1], q[0], q[3], -q[2],
                            q[2], -q[3], q[0], q[1], q[3], q[2], -q[1], q[0]};

@@ -12,7 +12,7 @@
 namespace icp {
 namespace {
 
-__device__ void horn_step_body(const double *__restrict__ sums, double N, double c0, double c1, double c2,
+__device__ __forceinline__ void horn_step_body(const double *__restrict__ sums, double N, double c0, double c1, double c2,
                                int shifted, int *__restrict__ cnt, IterState *__restrict__ s)
 {
     // the search's queue sizes: into the statistics, then zeroed for the next search (always:
@@ -67,7 +67,7 @@ __device__ void horn_step_body(const double *__restrict__ sums, double N, double
     }
 }
 
-__device__ void err_step_body(const double *__restrict__ sums, double N, double threshold, int max_iter,
+__device__ __forceinline__ void err_step_body(const double *__restrict__ sums, double N, double threshold, int max_iter,
                               double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag, int ticket,
                               IterState *h_state, double *h_trace)
 {
@@ -88,13 +88,13 @@ __device__ void err_step_body(const double *__restrict__ sums, double N, double 
     __hip_atomic_store(hflag + 2, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void horn_step_kernel(const double *__restrict__ sums, double N, double c0, double c1, double c2,
+__global__ __launch_bounds__(64) void horn_step_kernel(const double *__restrict__ sums, double N, double c0, double c1, double c2,
                                  int shifted, int *__restrict__ cnt, IterState *__restrict__ s)
 {
     horn_step_body(sums, N, c0, c1, c2, shifted, cnt, s);
 }
 
-__global__ void err_step_kernel(const double *__restrict__ sums, double N, double threshold, int max_iter,
+__global__ __launch_bounds__(64) void err_step_kernel(const double *__restrict__ sums, double N, double threshold, int max_iter,
                                 double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag, int ticket,
                                 IterState *h_state, double *h_trace)
 {

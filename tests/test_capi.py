@@ -178,3 +178,53 @@ def test_write_matrix_byte_identical(icp_lib, oracle, tmp_path):
     oracle.lib().oracle_write_matrix(str(b).encode(), oracle._dp(np.ascontiguousarray(x)), x.shape[0])
     assert a.read_bytes() == b.read_bytes()
     assert a.read_text().splitlines()[0] == "Points_0,Points_1,Points_2"
+
+
+def _rot(ax, ang):
+    ax = np.asarray(ax, float) / np.linalg.norm(ax)
+    K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+@pytest.mark.parametrize("case", ["scaled_small", "scaled_large", "half_turn", "identity", "planar",
+                                  "cube_corners", "line", "two_points_dup", "noise_only"])
+def test_horn_solve_edge_cases(icp_lib, oracle, case):
+    """The Horn step's eigen-solver (characteristic-polynomial path, Jacobi fallback for a
+    near-multiple largest eigenvalue) against the oracle's Jacobi: the same rotation where it
+    is unique, and the same residual where it is not (a line's spin is undetermined)."""
+    rng = np.random.default_rng(hash(case) % 2**32)
+    n = 40
+    p = rng.normal(size=(n, 3))
+    R0 = _rot(rng.normal(size=3), 0.7)
+    if case == "scaled_small":
+        p *= 1e-5
+    elif case == "scaled_large":
+        p = p * 1e5 + 3e6
+    elif case == "half_turn":
+        R0 = _rot([0.3, -0.5, 0.8], np.pi)
+    elif case == "identity":
+        R0 = np.eye(3)
+    elif case == "planar":
+        p[:, 2] = 0.0
+        R0 = _rot([0, 0, 1], 0.4)
+    elif case == "cube_corners":
+        p = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)], float)
+    elif case == "line":
+        p = np.outer(np.linspace(-1, 1, n), [1.0, 2.0, -0.5])
+    elif case == "two_points_dup":
+        p = np.array([[1.0, 0, 0], [1.0, 0, 0], [-1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0]])
+    y = p @ R0.T + np.array([0.1, -0.2, 0.3])
+    if case == "noise_only":
+        y = rng.normal(size=(n, 3))
+    al = oracle.find_alignment(p, y)
+    s, Rh, t = icp_lib.horn_solve(al.S, al.mu_p, al.mu_y, al.d_caps, al.sp)
+    Rh = np.asarray(Rh).reshape(3, 3)
+    np.testing.assert_allclose(Rh @ Rh.T, np.eye(3), atol=1e-12)
+    assert abs(np.linalg.det(Rh) - 1.0) < 1e-12
+    def resid(R_, s_, t_):
+        return float(((y - (s_ * p @ np.asarray(R_).reshape(3, 3).T + np.asarray(t_))) ** 2).sum())
+    r_ours, r_ref = resid(Rh, s, t), resid(al.R, al.s, al.t)
+    scale = float((y ** 2).sum()) + 1.0
+    assert abs(r_ours - r_ref) <= 1e-9 * scale, (r_ours, r_ref)
+    if case not in ("line", "two_points_dup", "noise_only"):
+        np.testing.assert_allclose(Rh, np.array(al.R).reshape(3, 3), atol=1e-9)
