@@ -193,6 +193,36 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
             "final_err": float(errs[-1]), "kernel": "nn_grid_search_kernel"}
 
 
+def baseline_configs(device, reps=3):
+    """BASELINE.json configs C2 (bun000 vs bun045, allow_unequal) and C3 (horse_ref vs horse_tr1):
+    complete 50-iteration registrations (reference semantics, threshold 1e-5; neither converges
+    within 50) on this GPU with the default NN path."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import datasets
+    out = {}
+    for name, (ref, scene, unequal) in {"C2_bun000_bun045": ("bun000", "bun045", True),
+                                        "C3_horse_ref_tr1": ("horse_ref", "horse_tr1", False)}.items():
+        m = icp_amd.load_matrix(datasets.path(ref))
+        p = icp_amd.load_matrix(datasets.path(scene))
+        with icp_amd.Context(device) as ctx:
+            ctx.set_allow_unequal(unequal)
+            ctx.set_model(m)
+            ctx.set_scene(p)
+            ctx.run(50)  # warm
+            ctx.reset_stats()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.set_scene(p)
+                res, errs = ctx.run(50)
+            dt = (time.perf_counter() - t0) / reps
+            st = ctx.stats()
+        out[name] = {"n_model": int(m.shape[0]), "n_scene": int(p.shape[0]), "iterations": res.iterations,
+                     "ms_per_registration": dt * 1e3, "iterations_per_s": res.iterations / dt,
+                     "nn_filter_ms": st["nn_ms"] / max(st["nn_launches"], 1),
+                     "final_err": float(errs[res.iterations - 1])}
+    return out
+
+
 def csv_io(m):
     """load.cc:3-97 at C4 size: write the model (ostream %g rows) and load it back
     (sscanf %lf rows) with the product's parallel exact parser / formatter."""
@@ -286,7 +316,7 @@ def main():
     ctx.set_nn_variant(variant)
     m, p = icp_amd.synthetic_pair(args.n, seed=42)
     b, c = icp_amd.shard_range(args.n, rank, world)
-    big = c >= 65536 and args.n >= 65536
+    big = c >= 8192 and args.n >= 8192  # level1_kind's f16 MFMA threshold
     level1 = None if args.nn != "certified" else (
         "mfma16" if args.variant == "mfma16" or (args.variant == "auto" and big) else
         ("mfma" if args.variant == "mfma" else None))
@@ -382,6 +412,7 @@ def main():
             out["cow_frame_rate"] = cow_frame_rate(local)
         if world == 1 and not args.no_cases:
             out["reference_cases"] = reference_cases_gpu()
+            out["baseline_configs"] = baseline_configs(local)
             out["csv_io"] = csv_io(m)
             if args.variant != "grid" and args.nn == "certified":
                 out["grid_nn"] = grid_nn_rate(local, m, p, args.steps)

@@ -301,15 +301,16 @@ int ensure_queue(icp_ctx *ctx, size_t n)
     return ICP_OK;
 }
 
-// The MFMA filter pays off once both clouds are large (its uncertified queries cost a
-// host round trip to size the second-level launch).
 // level-1 filter of a certified search: 0 = none (VALU filter only), 1 = f32 MFMA, 2 = f16 MFMA
 int level1_kind(const icp_ctx *ctx, size_t n)
 {
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return 1;
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA16) return 2;
     if (ctx->nn_variant == ICP_NN_VARIANT_VALU || ctx->nn_variant == ICP_NN_VARIANT_GRID) return 0;
-    return (n >= 65536 && ctx->nm >= 65536) ? 2 : 0;
+    // measured crossover (tools/configs_probe.py, 50-iteration registrations of synthetic n x n
+    // pairs): VALU wins at 4,096 (2.4 vs 8.9 ms), the f16 MFMA filter from 8,192 (3.3 vs 3.7
+    // ms) and by 2.2-2.6x at bunny / horse size, 8x at 65,536
+    return (n >= 8192 && ctx->nm >= 8192) ? 2 : 0;
 }
 
 GridView grid_view(const icp_ctx *ctx)

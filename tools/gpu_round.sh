@@ -88,6 +88,7 @@ for s in $STEPS; do
            set -- $COW
            run cases 300 ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.3 ;;
     fin16) for g in 1 4 8 1 4 8; do ICP_FIN16_LANES=$g run fin16_$g 300 python tools/shard_probe.py --worlds 8 1 --steps 20 || exit 1; cat $OUT/fin16_$g.log >> $OUT/fin16_all_$g.log; done ;;
+    configs) run configs 300 python tools/configs_probe.py ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
