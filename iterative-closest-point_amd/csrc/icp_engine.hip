@@ -326,7 +326,7 @@ GridView grid_view(const icp_ctx *ctx)
     return gv;
 }
 
-constexpr size_t kInlineFallbackModel = 65536;
+constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger model: nn_resolve, 256 per query)
 
 // Launches the complete NN search of the n queries in q against the resident model ->
 // ctx->idx, with no host synchronisation: every level is sized on the device.  Queue sizes:

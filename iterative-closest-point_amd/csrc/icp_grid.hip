@@ -382,18 +382,23 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st, const int *stop, int inline_nm)
 {
-    // 16 lanes per queued query (measured against 4 at C4 and at its 8-way shard: 16 is
-    // faster at both; the queue holds the hard near ties).  ICP_GRID_RGROUP overrides (4 | 16).
+    // lanes per queued query, measured: a whole wave for searches of 8,192 to 2^18 queries (horse /
+    // bunny surfaces: big boxes of dense surface cells; 64 lanes 4,289 vs 16 lanes 3,231 it/s
+    // on horse; equal at C4's 8-way shard), 16 lanes at C4 (0.18 vs 0.25 ms per iteration;
+    // 4 lanes slower everywhere).  ICP_GRID_RGROUP overrides (4 | 16 | 64).
     static const int forced = [] {
         const char *e = getenv("ICP_GRID_RGROUP");
         return e ? atoi(e) : 0;
     }();
-    const int g = forced == 4 ? 4 : 16;
+    const int g = forced == 4 || forced == 16 || forced == 64 ? forced : (max_items >= 8192 && max_items < (1 << 18) ? 64 : 16);
     const int per_block = kBlock / g;
     const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, 4096));
     if (g == 4)
         nn_grid_resolve_kernel<4><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
                                                             fb_count, fb_list, T_in, T_out, stop, inline_nm);
+    else if (g == 64)
+        nn_grid_resolve_kernel<64><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget,
+                                                             idx, fb_count, fb_list, T_in, T_out, stop, inline_nm);
     else
         nn_grid_resolve_kernel<16><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget,
                                                              idx, fb_count, fb_list, T_in, T_out, stop, inline_nm);

@@ -57,6 +57,8 @@ def main():
                               "iterations": res.iterations, "ms_per_registration": dt * 1e3,
                               "iterations_per_s": res.iterations / dt,
                               "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1),
+                              "queued_per_iter": st["level1_queued"] / max(st["iterations"], 1),
+                              "fallback_per_iter": st["grid_fallback"] / max(st["iterations"], 1),
                               "final_err": float(errs[res.iterations - 1])}), flush=True)
 
 

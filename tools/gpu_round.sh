@@ -88,6 +88,10 @@ for s in $STEPS; do
            set -- $COW
            run cases 300 ./iterative-closest-point_amd/build/icp-bench --ref "$1" --scene "$2" --min-time 0.3 ;;
     fin16) for g in 1 4 8 1 4 8; do ICP_FIN16_LANES=$g run fin16_$g 300 python tools/shard_probe.py --worlds 8 1 --steps 20 || exit 1; cat $OUT/fin16_$g.log >> $OUT/fin16_all_$g.log; done ;;
+    profhorse) run rocprof_horse 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_horse" -o horse -- \
+               python3 tools/configs_probe.py --configs C3_horse --variants auto --reps 3 ;;
+    gridrh) for g in 16 64 4 16 64; do ICP_GRID_RGROUP=$g run gridrh_$g 300 python tools/configs_probe.py --configs C3_horse C2_bunny --variants auto || exit 1; cat $OUT/gridrh_$g.log >> $OUT/gridrh_all_$g.log; done ;;
+    gridr64) for g in 16 64 16 64; do ICP_GRID_RGROUP=$g run gridr64_$g 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1; cat $OUT/gridr64_$g.log >> $OUT/gridr64_all_$g.log; done ;;
     configs) run configs 300 python tools/configs_probe.py ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
