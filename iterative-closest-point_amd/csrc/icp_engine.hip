@@ -398,7 +398,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
                                       ctx->amb1_hint, ctx->st, stop);
         else
-            launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, ctx->idx, ctx->amb_count + 2,
+            launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
         // exact resolution of the near ties through the model grid, around each candidate;
         // what it cannot take (none at C4): fp64 over every model point, one workgroup each
@@ -423,7 +423,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_filter(q.f, (int)n, ctx->m32, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st, stop);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
-        CertParams cp{ctx->rm};
+        CertParams cp{ctx->rm, (int)ctx->nm};
         launch_nn_finalize(pb, ps, pi, pl.splits, q.f, (int)n, cp, ctx->idx, ctx->amb_count, ctx->amb_list,
                            ctx->amb_T, ctx->amb_hint, ctx->st, stop);
         // near ties: exact through the model grid; what it cannot take, fp64 brute force

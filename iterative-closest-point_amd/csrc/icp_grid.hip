@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
                 lex_min(best, bi, d64g(q[0], q[1], q[2], m.x, m.y, m.z), k);
             }
             group_lex_min<G>(best, bi);
-            if (sub == 0) idx[j] = bi;
+            if (sub == 0) idx[j] = bi < 0 ? 0 : bi; // (no comparison held: a NaN query -> index 0)
         }
         // queue for nn_resolve -- or, scanned inline, only counted (the fallback statistic)
         const bool fb = !ok && sub == 0;

@@ -56,6 +56,7 @@ __device__ __forceinline__ int block_append(int *counter, bool pred, int *counte
 // Parameters of the fp32 certificate (see icp_kernels.hip, "certified NN").
 struct CertParams {
     double rm; // max |coordinate| of the centred fp32 model (real points only)
+    int nm;    // real model points (indices >= nm are padding: never a candidate)
 };
 
 // ---- layout conversion -------------------------------------------------------
@@ -94,7 +95,7 @@ NNPlan plan_nn_mfma(size_t np, size_t nm_pad);
 void launch_nn_mfma(const float4 *p32, int np, const float4 *mperm, int nm_pad, const NNPlan &plan,
                     float *part_best, float *part_second, int *part_idx, hipStream_t st);
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
-                             int splits, const float4 *p32, int np, const float *mm, int *idx,
+                             int splits, const float4 *p32, int np, const float *mm, int nm, int *idx,
                              int *amb_count, int *amb_list, int *amb_hint, hipStream_t st);
 // f16 split-precision MFMA filter (v_mfma_f32_32x32x16_f16): model image (1 KiB per 32
 // points) built once per model; uncertified queries appended to amb_list.

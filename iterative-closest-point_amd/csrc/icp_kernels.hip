@@ -287,7 +287,7 @@ __device__ __forceinline__ void merge_splits_group(const float *__restrict__ par
 template <int G>
 __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
-    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int nslots, double rm,
+    const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int nslots, double rm, int nm,
     int *__restrict__ idx, int *amb_count, int *amb_list, double *amb_T, int *amb_hint, const int *__restrict__ stop)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
@@ -299,8 +299,9 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_kernel(
     if (valid) {
         float b, s2;
         merge_splits_group<G>(part_best, part_second, part_idx, splits, nslots, j, sub, b, s2, id);
+        if (id >= nm) id = -1; // a padding point (a query beyond ~1e18): no candidate
         T = cert_window(b, p32[j], rm);
-        ok = (double)s2 > T || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
+        ok = ((double)s2 > T && id >= 0) || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
         if (ok && sub == 0) idx[j] = id; // unique candidate => exact fp64 first-min
     }
     const int slot = block_append(amb_count, !ok);
@@ -1383,13 +1384,14 @@ __global__ __launch_bounds__(kBlock) void build_mimage16_kernel(
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const float4 *__restrict__ p32, int np,
-    const float *__restrict__ mm, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
+    const float *__restrict__ mm, int nm, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint)
 {
     const int j = blockIdx.x * kBlock + threadIdx.x;
     const bool valid = j < np; // no early exit: block_append is workgroup-wide
     float b = 0.0f, s2 = 0.0f;
     int id = -1;
     if (valid) merge_splits(part_best, part_second, part_idx, splits, np, j, b, s2, id);
+    if (id >= nm) id = -1; // a padding point: no candidate
     bool ok = id >= 0;
     if (ok) {
         const double u = 0x1.0p-24;
@@ -1459,7 +1461,8 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) idx[j] = shi[0];
+        // (no comparison held -- a NaN query: index 0, the reference GPU scan's answer)
+        if (threadIdx.x == 0) idx[j] = shi[0] == 0x7fffffff ? 0 : shi[0];
         __syncthreads();
     }
 }
@@ -1508,6 +1511,7 @@ __global__ __launch_bounds__(kBlock) void nn_exact_few_kernel(const double *__re
                 bd = shd[w];
                 bi = shi[w];
             }
+        if (bi == 0x7fffffff) bi = 0; // no comparison held (a NaN query): index 0, as the reference's scan
         idx_out[j] = bi;
         const double4 m = m4[bi];
         y_aos[3 * j] = m.x;
@@ -1964,7 +1968,7 @@ void launch_nn_finalize(const float *part_best, const float *part_second, const 
     const int grid = (nslots + per_block - 1) / per_block;
 #define FIN(G)                                                                                                    \
     nn_finalize_kernel<G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, p32, nslots, cp.rm, \
-                                                   idx, amb_count, amb_list, amb_T, amb_hint, stop)
+                                                   cp.nm, idx, amb_count, amb_list, amb_T, amb_hint, stop)
     if (g == 8) FIN(8); else if (g == 4) FIN(4); else FIN(1);
 #undef FIN
 }
@@ -2107,11 +2111,11 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
-                             int splits, const float4 *p32, int np, const float *mm, int *idx,
+                             int splits, const float4 *p32, int np, const float *mm, int nm, int *idx,
                              int *amb_count, int *amb_list, int *amb_hint, hipStream_t st)
 {
     nn_finalize_mfma_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(
-        part_best, part_second, part_idx, splits, p32, np, mm, idx, amb_count, amb_list, amb_hint);
+        part_best, part_second, part_idx, splits, p32, np, mm, nm, idx, amb_count, amb_list, amb_hint);
 }
 
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,

@@ -295,3 +295,41 @@ def test_nn_few_queries_exact(amd, oracle, nq):
     _, ref = oracle.closest(p, m)
     np.testing.assert_array_equal(idx, ref)
     np.testing.assert_array_equal(y, m[ref])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_nn_non_finite_and_far_queries(amd, ctxs, oracle, mode):
+    """NaN, +-inf and astronomically far queries must neither fault nor return an index outside
+    the model (a NaN query gets index 0, what the reference's GPU scan returns when no
+    comparison holds); the finite queries beside them keep their exact answers."""
+    m = RNG.normal(size=(3000, 3))
+    good = RNG.normal(size=(200, 3))
+    bad = np.array([[np.nan, 0, 0], [np.inf, 0, 0], [-np.inf, 1, 1], [1e30, 0, 0], [-1e20, 5, 5],
+                    [np.nan, np.nan, np.nan], [0, 0, np.inf], [3e18, -3e18, 1e18]])
+    p = np.concatenate([good, bad, good[:50]])
+    ctxs[mode].set_model(m)
+    _, idx = ctxs[mode].closest_matrix(p)
+    assert idx.min() >= 0 and idx.max() < m.shape[0]
+    _, ref = oracle.closest(good, m)
+    np.testing.assert_array_equal(idx[:200], ref)
+    np.testing.assert_array_equal(idx[208:], ref[:50])
+    # few-query path (automatic variant, <= 32 queries)
+    with amd.Context(0, amd.NN_CERTIFIED) as ctx:
+        ctx.set_model(m)
+        _, idx_few = ctx.closest_matrix(bad)
+    assert idx_few.min() >= 0 and idx_few.max() < m.shape[0]
+
+
+def test_icp_degenerate_scene_does_not_fault(amd):
+    """All scene points identical: sum ||p'||^2 = 0, so Horn's scale is infinite and the next
+    iterations search with non-finite queries (the reference computes the same inf/NaN).  The
+    run must complete and report, not fault."""
+    m = RNG.normal(size=(5000, 3))
+    p = np.tile([[0.3, -0.2, 0.1]], (5000, 1))
+    with amd.Context(0, amd.NN_CERTIFIED) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        res, errs = ctx.run(5)
+        out = ctx.get_scene()
+    assert res.iterations == 5
+    assert out.shape == p.shape
