@@ -368,8 +368,20 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
         LAUNCHCHK("nn_grid_search");
     } else if (const int l1 = level1_kind(ctx, n)) {
-        // level 1: MFMA expanded-form filter over every query
-        const bool sd = seeded && l1 == 2;
+        // level 1: MFMA expanded-form filter over every query.  An unseeded f16 search is
+        // seeded from the model grid first (a near point per query; ICP_GRID_SEED=0 disables):
+        // the full N x M pass then runs the seeded kernel, 35.9 -> ~28 ms at C4
+        static const bool grid_seed = [] {
+            const char *e = getenv("ICP_GRID_SEED");
+            return !(e && atoi(e) == 0);
+        }();
+        const bool gseed = l1 == 2 && !seeded && grid_seed && ctx->g_pts;
+        if (gseed) {
+            launch_nn_grid_seed((int)n, q.x, q.y, q.z, grid_view(ctx), (int)ctx->nm, ctx->idx, ctx->st);
+            LAUNCHCHK("nn_grid_seed");
+            seeds_ready = false; // the seeds come from these candidates, below
+        }
+        const bool sd = (seeded || gseed) && l1 == 2;
         const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd) : plan_nn_mfma(n, ctx->nm_pad);
         if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));

@@ -290,6 +290,39 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
     }
 }
 
+// Seeds for an unseeded f16 brute-force search: a near model point per query from the rings
+// of cells around its own cell (at most max_ring rings; else an arbitrary valid index).  Any
+// model point gives a valid upper bound: the seed only decides which blocks of the full
+// N x M pass take the update path, never the answer (which the certificate proves).
+template <int G>
+__global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const double *__restrict__ px,
+                                                             const double *__restrict__ py,
+                                                             const double *__restrict__ pz, GridView gv,
+                                                             int max_ring, int nm, int *__restrict__ idx)
+{
+    const int sub = threadIdx.x & (G - 1);
+    const int groups = gridDim.x * (kBlock / G);
+    for (int j = (blockIdx.x * kBlock + threadIdx.x) / G; j < np; j += groups) {
+        const double q[3] = {px[j], py[j], pz[j]};
+        int c[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) c[a] = cell1(q[a], gv.lo[a], gv.inv_h, gv.g[a]);
+        double best = INFINITY;
+        int bi = -1;
+        for (int r = 0; r <= max_ring && bi < 0; ++r) {
+            int c0[3], c1[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                c0[a] = max(c[a] - r, 0);
+                c1[a] = min(c[a] + r, gv.g[a] - 1);
+            }
+            scan_box<G>(q, c0, c1, gv, sub, best, bi);
+            group_lex_min<G>(best, bi);
+        }
+        if (sub == 0) idx[j] = bi >= 0 ? bi : j % nm;
+    }
+}
+
 } // namespace
 
 GridParams grid_params(const double *m_xyz, size_t nm)
@@ -375,6 +408,15 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
         nn_grid_search_kernel<4><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
     else
         nn_grid_search_kernel<16><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
+}
+
+void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,
+                         int nm, int *idx, hipStream_t st)
+{
+    constexpr int kG = 4, kMaxRing = 2;
+    const int per_block = kBlock / kG;
+    const int blocks = std::max(1, std::min((np + per_block - 1) / per_block, 16384));
+    nn_grid_seed_kernel<kG><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, kMaxRing, nm, idx);
 }
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,

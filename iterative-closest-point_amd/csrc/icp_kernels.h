@@ -152,6 +152,10 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 // over the grid box that must contain every point at least as close as the candidate ->
 // idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its window T_in[t]
 // (T = +inf without T_in: every model point) for nn_resolve.
+// idx[j] = a near model point of query j (the rings of grid cells around it; else any valid
+// index): seeds for an unseeded f16 brute-force search
+void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,
+                         int nm, int *idx, hipStream_t st);
 // inline_nm > 0 (a model of that many points): queries the grid cannot take are scanned
 // exactly in place (no fallback queue, no nn_resolve launch)
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,

@@ -92,6 +92,7 @@ for s in $STEPS; do
                python3 tools/configs_probe.py --configs C3_horse --variants auto --reps 3 ;;
     gridrh) for g in 16 64 4 16 64; do ICP_GRID_RGROUP=$g run gridrh_$g 300 python tools/configs_probe.py --configs C3_horse C2_bunny --variants auto || exit 1; cat $OUT/gridrh_$g.log >> $OUT/gridrh_all_$g.log; done ;;
     gridr64) for g in 16 64 16 64; do ICP_GRID_RGROUP=$g run gridr64_$g 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1; cat $OUT/gridr64_$g.log >> $OUT/gridr64_all_$g.log; done ;;
+    gseed) for v in 0 1 0 1; do ICP_GRID_SEED=$v run gseed_$v 300 python3 tools/nn_probe.py --variant mfma16 --reps 3 || exit 1; cat $OUT/gseed_$v.log >> $OUT/gseed_all_$v.log; done ;;
     configs) run configs 300 python tools/configs_probe.py ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
