@@ -122,6 +122,8 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_small_kernel(
         double a[17];
 #pragma unroll
         for (int k = 0; k < 17; ++k) a[k] = 0.0;
+        // (unrolled: the gathers of several points in flight; per-thread order unchanged)
+#pragma unroll 4
         for (int i = threadIdx.x; i < n; i += kBlock)
             shifted_moment_point(i, idx, m4, px, py, pz, yx, yy, yz, cp0, cp1, cp2, cy0, cy1, cy2, a);
         block_sum_store<17>(a, sums);
@@ -132,6 +134,7 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_small_kernel(
     if (!s_done && !s->done) {
         const Xform xf = s->xf;
         double e[1] = {0.0};
+#pragma unroll 4
         for (int i = threadIdx.x; i < n; i += kBlock) {
             double q0, q1, q2;
             transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
