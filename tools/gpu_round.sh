@@ -36,14 +36,14 @@ for s in $STEPS; do
     bench_valu) run bench_valu 300 python bench.py --variant valu --no-cpu-baseline --no-cow ;;
     bench_fp64) run bench_fp64 300 python bench.py --nn fp64 --steps 5 --warmup 1 --no-cpu-baseline --no-cow ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cow ;;
+               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cow --no-cases ;;
     profv) for v in ${PROFV:-mfma16 valu}; do
                run rocprof_$v 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$v" -o bench -- \
                    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cow --variant $v; done ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc1" -o fetch -- \
-               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow &&
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc2" -o write -- \
-               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow ;;
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases ;;
     sq)    for v in ${SQV:-mfma valu}; do
                run sq1_$v 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE \
                    --output-format csv -d "$OUT/sq1_$v" -o sq -- python3 tools/nn_probe.py --variant $v --reps 1
