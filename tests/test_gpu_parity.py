@@ -333,3 +333,38 @@ def test_icp_degenerate_scene_does_not_fault(amd):
         out = ctx.get_scene()
     assert res.iterations == 5
     assert out.shape == p.shape
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_paths_bitwise_consistent_random(amd, seed):
+    """Random scenes whose sizes straddle the engine's path thresholds (fused small tail at
+    n <= 4096, f16 MFMA filter at 8192, model larger/smaller than the scene): every certified
+    filter variant must follow the fp64 brute-force trajectory bit for bit (errs and final
+    scene), since each certifies the reference's exact first minimum."""
+    rng = np.random.default_rng(1000 + seed)
+    n = [7, 300, 4096, 4097, 8191, 8192, 12000, 20000][seed]
+    nm = int(rng.choice([n, max(4, n // 2), n + 1000]))
+    m = rng.normal(size=(nm, 3)) if seed % 3 == 0 else rng.uniform(-1, 1, size=(nm, 3))
+    if seed % 3 == 2:
+        m[:, 2] *= 1e-3  # nearly planar model: many near ties
+    a = rng.uniform(0.02, 0.3)
+    axis = rng.normal(size=3); axis /= np.linalg.norm(axis)
+    k = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    rot = np.eye(3) + np.sin(a) * k + (1 - np.cos(a)) * k @ k
+    p = m[rng.integers(0, nm, n)] @ rot.T + rng.normal(scale=0.05, size=3) \
+        + rng.normal(scale=0.01, size=(n, 3))
+    runs = {}
+    for name, (mode, variant) in list(_MODE_ARGS.items()) + [("auto", (0, 0))]:
+        with amd.Context(0, mode) as ctx:
+            ctx.set_nn_variant(variant)
+            ctx.set_allow_unequal(n != nm)
+            ctx.set_model(m)
+            ctx.set_scene(p)
+            res, errs = ctx.run(8, -1.0)
+            runs[name] = (res.iterations, errs, ctx.get_scene())
+    ref_it, ref_errs, ref_scene = runs["fp64"]
+    assert ref_it == 8
+    for name, (it, errs, scene) in runs.items():
+        assert it == ref_it, name
+        np.testing.assert_array_equal(errs, ref_errs, err_msg=name)
+        np.testing.assert_array_equal(scene, ref_scene, err_msg=name)
