@@ -21,6 +21,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <string>
 
 #include "icp_kernels.h"
 
@@ -152,6 +154,68 @@ __device__ __forceinline__ void scan_box(const double q[3], const int c0[3], con
     }
 }
 
+// Flattened scan of the same box: its points are numbered 0, 1, ... row after row and lane `sub`
+// takes numbers sub, sub + G, ...  A long x-run (a dense surface cell: tens of points) spreads
+// over the whole group instead of one lane walking it point by point, and a lane's loads do
+// not depend on each other, so kU of them are in flight at once.  Rows are taken G at a time:
+// lane s reads row s's run [k0, k0 + len), an inclusive scan of len numbers the points, and
+// point f's row is found by a binary search of the scan over the group's lanes (shuffles).
+template <int G>
+__device__ __forceinline__ void scan_box_flat(const double q[3], const int c0[3], const int c1[3],
+                                              const GridView &gv, int sub, double &best, int &bi)
+{
+    constexpr int kU = 4;
+    const int ny = c1[1] - c0[1] + 1;
+    const int nrows = ny * (c1[2] - c0[2] + 1);
+    for (int r0 = 0; r0 < nrows; r0 += G) {
+        int k0 = 0, len = 0;
+        const int r = r0 + sub;
+        if (r < nrows) {
+            const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+            const int row = (cz * gv.g[1] + cy) * gv.g[0];
+            k0 = gv.start[row + c0[0]];
+            len = gv.start[row + c1[0] + 1] - k0;
+        }
+        int incl = len;
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+            const int v = __shfl_up(incl, o, G);
+            if (sub >= o) incl += v;
+        }
+        const int total = __shfl(incl, G - 1, G);
+        const int base = k0 - (incl - len); // point number f of this lane's row sits at base + f
+        for (int b = 0; b < total; b += kU * G) { // uniform over the group: the shuffles see every lane
+            int k[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int f = b + u * G + sub;
+                int pos = 0; // number of rows whose points all precede f (incl is non-decreasing)
+#pragma unroll
+                for (int step = G / 2; step >= 1; step >>= 1)
+                    if (__shfl(incl, pos + step - 1, G) <= f) pos += step;
+                const int kb = __shfl(base, pos, G);
+                k[u] = f < total ? kb + f : -1;
+            }
+            double4 m[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (k[u] >= 0) m[u] = gv.pts[k[u]];
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (k[u] >= 0) lex_min(best, bi, d64g(q[0], q[1], q[2], m[u].x, m[u].y, m[u].z), (int)m[u].w);
+        }
+    }
+}
+
+// resolver box scan: flattened (default) or one x-run per lane (ICP_GRID_SCAN=rows, for A/B)
+template <int G, bool FLAT>
+__device__ __forceinline__ void scan_box_sel(const double q[3], const int c0[3], const int c1[3],
+                                             const GridView &gv, int sub, double &best, int &bi)
+{
+    if constexpr (FLAT) scan_box_flat<G>(q, c0, c1, gv, sub, best, bi);
+    else scan_box<G>(q, c0, c1, gv, sub, best, bi);
+}
+
 template <int G = kGroup> __device__ __forceinline__ void group_lex_min(double &best, int &bi)
 {
 #pragma unroll
@@ -180,7 +244,7 @@ __device__ __forceinline__ bool complete_box(const double q[3], double r2, const
 
 // One G-lane group per queued query (grid-stride over *count; the trip count is uniform
 // within a group, so a group is always entirely active).
-template <int G>
+template <int G, bool FLAT>
 __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int *__restrict__ count_ptr, const int *__restrict__ list, const int *__restrict__ hint,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
@@ -206,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
             ok = complete_box(q, best, gv, budget, c0, c1);
         }
         if (ok) {
-            scan_box<G>(q, c0, c1, gv, sub, best, bi);
+            scan_box_sel<G, FLAT>(q, c0, c1, gv, sub, best, bi);
             group_lex_min<G>(best, bi);
             if (sub == 0) idx[j] = bi;
         } else if (inline_nm > 0) { // small model: the exact fp64 scan of every point, right here
@@ -234,7 +298,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
 // (clamped) cell that holds a point; then the complete box around that candidate, exactly
 // as in nn_grid_resolve_kernel.  Either step over `budget` cells -> the query goes to the
 // fp64 brute force (window T = +inf).
-template <int G>
+template <int G, bool FLAT>
 __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
     int np, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     GridView gv, int budget, int *__restrict__ idx, int *fb_count, int *__restrict__ fb_list,
@@ -264,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
                 ok = false;
                 break;
             }
-            scan_box<G>(q, c0, c1, gv, sub, best, bi);
+            scan_box_sel<G, FLAT>(q, c0, c1, gv, sub, best, bi);
             group_lex_min<G>(best, bi);
             if (c0[0] == 0 && c0[1] == 0 && c0[2] == 0 && c1[0] == gv.g[0] - 1 && c1[1] == gv.g[1] - 1 &&
                 c1[2] == gv.g[2] - 1)
@@ -275,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
             int c0[3], c1[3];
             ok = complete_box(q, best, gv, budget, c0, c1);
             if (ok) {
-                scan_box<G>(q, c0, c1, gv, sub, best, bi);
+                scan_box_sel<G, FLAT>(q, c0, c1, gv, sub, best, bi);
                 group_lex_min<G>(best, bi);
             }
         }
@@ -294,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_search_kernel(
 // of cells around its own cell (at most max_ring rings; else an arbitrary valid index).  Any
 // model point gives a valid upper bound: the seed only decides which blocks of the full
 // N x M pass take the update path, never the answer (which the certificate proves).
-template <int G>
+template <int G, bool FLAT>
 __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const double *__restrict__ px,
                                                              const double *__restrict__ py,
                                                              const double *__restrict__ pz, GridView gv,
@@ -316,7 +380,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const doub
                 c0[a] = max(c[a] - r, 0);
                 c1[a] = min(c[a] + r, gv.g[a] - 1);
             }
-            scan_box<G>(q, c0, c1, gv, sub, best, bi);
+            scan_box_sel<G, FLAT>(q, c0, c1, gv, sub, best, bi);
             group_lex_min<G>(best, bi);
         }
         if (sub == 0) idx[j] = bi >= 0 ? bi : j % nm;
@@ -362,6 +426,16 @@ GridParams grid_params(const double *m_xyz, size_t nm)
     return p;
 }
 
+// box scans flattened over the group's lanes (default) or one x-run per lane (ICP_GRID_SCAN=rows)
+static bool grid_flat_scan()
+{
+    static const bool flat = [] {
+        const char *e = getenv("ICP_GRID_SCAN");
+        return !(e && std::string(e) == "rows");
+    }();
+    return flat;
+}
+
 long long grid_cells(const GridParams &p) { return (long long)p.g[0] * p.g[1] * p.g[2]; }
 
 size_t grid_scan_blocks(long long n) { return (size_t)((n + kScanChunk - 1) / kScanChunk); }
@@ -402,12 +476,17 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
     const int g = forced == 1 || forced == 4 || forced == 16 ? forced : (np >= (1 << 16) ? 4 : 16);
     const int per_block = kBlock / g;
     const int blocks = std::max(1, std::min((np + per_block - 1) / per_block, 16384));
-    if (g == 1)
-        nn_grid_search_kernel<1><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
-    else if (g == 4)
-        nn_grid_search_kernel<4><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
-    else
-        nn_grid_search_kernel<16><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T);
+#define SEARCH(GG, F) nn_grid_search_kernel<GG, F><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T)
+    if (grid_flat_scan()) {
+        if (g == 1) SEARCH(1, true);
+        else if (g == 4) SEARCH(4, true);
+        else SEARCH(16, true);
+    } else {
+        if (g == 1) SEARCH(1, false);
+        else if (g == 4) SEARCH(4, false);
+        else SEARCH(16, false);
+    }
+#undef SEARCH
 }
 
 void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,
@@ -416,7 +495,8 @@ void launch_nn_grid_seed(int np, const double *px, const double *py, const doubl
     constexpr int kG = 4, kMaxRing = 2;
     const int per_block = kBlock / kG;
     const int blocks = std::max(1, std::min((np + per_block - 1) / per_block, 16384));
-    nn_grid_seed_kernel<kG><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, kMaxRing, nm, idx);
+    if (grid_flat_scan()) nn_grid_seed_kernel<kG, true><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, kMaxRing, nm, idx);
+    else nn_grid_seed_kernel<kG, false><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, kMaxRing, nm, idx);
 }
 
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
@@ -435,15 +515,19 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
     const int g = forced == 4 || forced == 16 || forced == 64 ? forced : (max_items >= 8192 && max_items < (1 << 18) ? 64 : 16);
     const int per_block = kBlock / g;
     const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, 4096));
-    if (g == 4)
-        nn_grid_resolve_kernel<4><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx,
-                                                            fb_count, fb_list, T_in, T_out, stop, inline_nm);
-    else if (g == 64)
-        nn_grid_resolve_kernel<64><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget,
-                                                             idx, fb_count, fb_list, T_in, T_out, stop, inline_nm);
-    else
-        nn_grid_resolve_kernel<16><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget,
-                                                             idx, fb_count, fb_list, T_in, T_out, stop, inline_nm);
+#define RESOLVE(GG, F)                                                                                  \
+    nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx, \
+                                                             fb_count, fb_list, T_in, T_out, stop, inline_nm)
+    if (grid_flat_scan()) {
+        if (g == 4) RESOLVE(4, true);
+        else if (g == 64) RESOLVE(64, true);
+        else RESOLVE(16, true);
+    } else {
+        if (g == 4) RESOLVE(4, false);
+        else if (g == 64) RESOLVE(64, false);
+        else RESOLVE(16, false);
+    }
+#undef RESOLVE
 }
 
 } // namespace icp
