@@ -76,6 +76,7 @@ struct NNPlan {
     int splits;     // workgroups along the model axis
     int chunk;      // model points per split (multiple of the tile)
     int tile = 0;   // LDS tile of the VALU filter when not the default (kTileSmall)
+    int kernel = -1; // f16 filter kernel picked for this size (plan_nn_mfma16)
 };
 NNPlan plan_nn32(size_t np, size_t nm_pad);
 NNPlan plan_nn64(size_t np, size_t nm_pad);

@@ -1870,6 +1870,8 @@ static int resident_wgs(const void *kernel)
 // Split the model axis so the grid fills whole rounds of resident workgroups: a grid of
 // 1.35 rounds runs its second round at a third of the chip.  Smallest split count with
 // >= 90% round efficiency and at least one full round, else the most efficient one.
+static bool min_rounds_forced() { return getenv("ICP_NN_MIN_ROUNDS") != nullptr; }
+
 static int min_rounds()
 {
     // experiment knob: ICP_NN_MIN_ROUNDS = k asks for >= k rounds of resident workgroups (a
@@ -1881,9 +1883,9 @@ static int min_rounds()
     return r;
 }
 
-static void choose_splits(NNPlan &pl, int tiles, int tile, int cap)
+static void choose_splits(NNPlan &pl, int tiles, int tile, int cap, int rounds)
 {
-    cap *= min_rounds();
+    cap *= rounds;
     int best_tps = tiles, best_s = 1;
     double best_eff = -1.0;
     for (int s = 1; s <= tiles; ++s) {
@@ -1908,7 +1910,8 @@ static void choose_splits(NNPlan &pl, int tiles, int tile, int cap)
     pl.splits = best_s;
 }
 
-static NNPlan make_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel)
+static NNPlan make_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel,
+                        int rounds = 0)
 {
     NNPlan pl;
     pl.q_per_lane = q;
@@ -1917,7 +1920,7 @@ static NNPlan make_plan(size_t np, size_t nm, int tile, int q, int queries_per_l
     if (pl.qblocks < 1) pl.qblocks = 1;
     const int tiles = (int)((nm + tile - 1) / tile);
     const int cap = resident_wgs(kernel);
-    choose_splits(pl, tiles, tile, cap);
+    choose_splits(pl, tiles, tile, cap, rounds > 0 && !min_rounds_forced() ? rounds : min_rounds());
     if (getenv("ICP_DEBUG_PLAN"))
         fprintf(stderr, "[plan] np=%zu nm=%zu q=%d qblocks=%d splits=%d chunk=%d resident=%d wgs=%ld\n", np, nm,
                 pl.q_per_lane, pl.qblocks, pl.splits, pl.chunk, cap, (long)pl.qblocks * pl.splits);
@@ -2002,7 +2005,7 @@ static int mfma16_qg()
 // Knob for experiments: ICP_MFMA16_KERNEL = plain | pipe | unroll | r4 | r8 (the r kernels
 // are seeded-only; unseeded searches then use plain), ICP_MFMA16_QG = 2 (plain).
 enum { kK16Plain = 0, kK16Pipe, kK16Unroll, kK16R4, kK16R8 };
-static int mfma16_kernel_choice(bool seeded)
+static int mfma16_forced()
 {
     static int forced = [] {
         const char *e = getenv("ICP_MFMA16_KERNEL");
@@ -2014,6 +2017,12 @@ static int mfma16_kernel_choice(bool seeded)
         if (v == "r8") return (int)kK16R8;
         return -1;
     }();
+    return forced;
+}
+
+static int mfma16_kernel_choice(bool seeded)
+{
+    const int forced = mfma16_forced();
     if (mfma16_qg() != 4) return kK16Plain;
     if (forced >= 0) return (!seeded && forced >= kK16R4) ? (int)kK16Plain : forced;
     return seeded ? (int)kK16R8 : (int)kK16Plain;
@@ -2021,9 +2030,9 @@ static int mfma16_kernel_choice(bool seeded)
 
 static int mfma16_groups(int kc) { return kc == kK16R8 ? 8 : (kc == kK16Plain ? mfma16_qg() : 4); }
 
-static const void *mfma16_kernel_ptr(bool seeded)
+static const void *mfma16_kernel_ptr(int kc, bool seeded)
 {
-    switch (mfma16_kernel_choice(seeded)) {
+    switch (kc) {
     case kK16R8: return (const void *)nn_mfma16r_kernel<8>;
     case kK16R4: return (const void *)nn_mfma16r_kernel<4>;
     case kK16Unroll: return seeded ? (const void *)nn_mfma16x_kernel<true> : (const void *)nn_mfma16x_kernel<false>;
@@ -2035,10 +2044,26 @@ static const void *mfma16_kernel_ptr(bool seeded)
     return seeded ? (const void *)nn_mfma16_kernel<4, true> : (const void *)nn_mfma16_kernel<4, false>;
 }
 
+// Mid-size searches (bunny / horse, ~40-50k points): the 256 queries per wave of the r8 kernel
+// leave so few query blocks that the splits needed to fill the chip cut the model into a single
+// tile per workgroup, and per-workgroup setup, epilogue and the split merge dominate.  Below
+// kMinTilesR8 tiles per split the r4 kernel (128 queries per wave) runs instead: twice the query
+// blocks, half the splits, and two rounds of resident workgroups instead of four (measured,
+// it/s: C2 bunny 6,543 -> 7,574, C3 horse 4,810 -> 5,543, 2 x 16,384 points 13,481 -> 16,978,
+// 2 x 65,536 points 4,368 -> 5,123; profiles/r01dc).
+constexpr int kMinTilesR8 = 4, kRoundsR4 = 2;
+
 NNPlan plan_nn_mfma16(size_t np, size_t nm_pad, bool seeded)
 {
-    const int g = mfma16_groups(mfma16_kernel_choice(seeded));
-    return make_plan(np, nm_pad, kTile32, g, 4 * g * 32, mfma16_kernel_ptr(seeded));
+    int kc = mfma16_kernel_choice(seeded);
+    NNPlan pl = make_plan(np, nm_pad, kTile32, mfma16_groups(kc), 4 * mfma16_groups(kc) * 32,
+                          mfma16_kernel_ptr(kc, seeded));
+    if (kc == kK16R8 && mfma16_forced() < 0 && pl.chunk / kTile32 < kMinTilesR8) {
+        kc = kK16R4;
+        pl = make_plan(np, nm_pad, kTile32, 4, 4 * 4 * 32, mfma16_kernel_ptr(kc, seeded), kRoundsR4);
+    }
+    pl.kernel = kc;
+    return pl;
 }
 
 void launch_mfma16_seed(const double *px, const double *py, const double *pz, int np, const int *prev,
@@ -2065,7 +2090,7 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
     K<<<grid, kBlock, 0, st>>>(px, py, pz, np, c[0], c[1], c[2], scale, seed16, im, nm_pad, pl.chunk, \
                                part_best, part_second, part_idx, stop)
     const bool sd = seed16 != nullptr;
-    switch (mfma16_kernel_choice(sd)) {
+    switch (pl.kernel >= 0 ? pl.kernel : mfma16_kernel_choice(sd)) {
     case kK16R8: LAUNCH16(nn_mfma16r_kernel<8>); break;
     case kK16R4: LAUNCH16(nn_mfma16r_kernel<4>); break;
     case kK16Unroll:
