@@ -99,7 +99,7 @@ def test_uneven_shards_including_empty(icp_lib):
 
 
 @pytest.mark.parametrize("name,n,iters", [("cow", 0, 20), ("cow", 0, 1), ("cow", 0, 2), ("cow", 0, 12),
-                                          ("synthetic", 1 << 17, 4)])
+                                          ("synthetic", 1 << 17, 4), ("horse", 0, 50)])
 def test_rccl_single_rank_communicator(icp_lib, name, n, iters):
     """The RCCL data path itself on one GPU: icp_ctx_create_dist(world_size=1, id) builds a
     1-rank communicator and every per-iteration sum goes through ncclAllReduce on the
@@ -107,12 +107,16 @@ def test_rccl_single_rank_communicator(icp_lib, name, n, iters):
     bit for bit (same kernels, same reduction order), although with a communicator each
     iteration's residual rides on the next iteration's all-reduce and its convergence test
     runs one iteration late: iters = 1, 2 and 12 (cow_tr2 converges at exactly 12) pin the
-    loop's edges."""
+    loop's edges.  The plain context folds each pass of a > 4096-point cloud in its last
+    workgroup (launch_moments_horn / launch_transform_err_step); horse (48,485 points, converges
+    before 50) and the synthetic case pin those fused passes to the separate launches."""
     amd = icp_lib
-    if name == "cow":
-        m = amd.load_matrix(datasets.path("cow_ref"))
-        p = amd.load_matrix(datasets.path("cow_tr2"))
+    if name in ("cow", "horse"):
+        m = amd.load_matrix(datasets.path(f"{name}_ref"))
+        p = amd.load_matrix(datasets.path("cow_tr2" if name == "cow" else "horse_tr1"))
         thr = 1e-5
+        if name == "horse":  # (1e-5 is never reached in 50) stop at about iteration 31 instead
+            thr = float(run_single(amd, m, p, iters, -1.0)[1][30]) * (1 + 1e-9)
     else:
         m, p = amd.synthetic_pair(n, seed=42)
         thr = -1.0
@@ -122,7 +126,11 @@ def test_rccl_single_rank_communicator(icp_lib, name, n, iters):
         ctx.set_scene(p)
         res, errs = ctx.run(iters, thr)
         out = ctx.get_scene()
-    assert res.iterations == ref[0].iterations == min(iters, 12 if name == "cow" else iters)
+    assert res.iterations == ref[0].iterations
+    if name != "horse":
+        assert res.iterations == min(iters, 12 if name == "cow" else iters)
+    else:
+        assert res.iterations <= 31
     np.testing.assert_array_equal(errs, ref[1])
     np.testing.assert_array_equal(np.array(res.R), np.array(ref[0].R))
     np.testing.assert_array_equal(out, ref[2])
