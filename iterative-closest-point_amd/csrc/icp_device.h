@@ -12,20 +12,7 @@ namespace icp {
 
 // Wave-then-workgroup sum of K doubles per thread; thread k < K of the workgroup writes
 // out[k].  Fixed shuffle tree + fixed LDS order: deterministic.
-// SC1: the sums are stored write-through (agent-scope relaxed atomic stores), for a last-arriver
-// fold in the same launch that reads them with agent-scope loads (no release / acquire fence).
-__device__ __forceinline__ void store_sc1(double *p, double v)
-{
-    __hip_atomic_store((unsigned long long *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_sc1(const double *p)
-{
-    return __builtin_bit_cast(double, __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT));
-}
-
-template <int K, bool SC1 = false>
+template <int K>
 __device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
 {
     __shared__ double sh[kBlock / 64][K];
@@ -40,43 +27,7 @@ __device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
     __syncthreads();
     if (threadIdx.x < K) {
         const int k = threadIdx.x;
-        const double v = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
-        if constexpr (SC1) store_sc1(out + k, v);
-        else out[k] = v;
-    }
-}
-
-// out[k] = sum_b partials[b*K + k], one workgroup, fixed order (deterministic): thread t
-// accumulates the rows b = t, t + kBlock, ... (contiguous K-double rows: coalesced), then each
-// column is folded by a fixed xor-shuffle tree per wave and the 4 wave sums in wave order.
-// (reduce_kernel, and the last workgroup of the fused passes in icp_iter.hip.)
-template <int K, bool SC1 = false>
-__device__ __forceinline__ void fold_rows(const double *__restrict__ partials, int nblocks, double *__restrict__ out)
-{
-    __shared__ double sh[kBlock / 64][K];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    double a[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) a[k] = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) a[k] += SC1 ? load_sc1(partials + (size_t)b * K + k) : partials[(size_t)b * K + k];
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
-    }
-    __syncthreads();
-    if (threadIdx.x < K) {
-        double r = sh[0][threadIdx.x];
-#pragma unroll
-        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
-        out[threadIdx.x] = r;
+        out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
     }
 }
 
@@ -128,57 +79,6 @@ __device__ __forceinline__ double residual2(double y0, double y1, double y2, dou
 {
     const double e0 = y0 - q0, e1 = y1 - q1, e2 = y2 - q2;
     return (e0 * e0 + e1 * e1) + e2 * e2;
-}
-
-constexpr double kF16QueryClamp = 32000.0; // |scaled query coordinate| bound of the f16 filter
-
-// Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
-// s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see
-// nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
-// seed of query p (unscaled fp64) from a model point m: packed f16 (hi | lo << 16) of -s0 / 2^14
-__device__ __forceinline__ unsigned mfma16_seed_value(double p0, double p1, double p2, double m0, double m1,
-                                                      double m2, double cx, double cy, double cz, double scale)
-{
-    const double a0 = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double a1 = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double a2 = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double b0 = (m0 - cx) * scale, b1 = (m1 - cy) * scale, b2 = (m2 - cz) * scale;
-    const double bb = b0 * b0 + b1 * b1 + b2 * b2;
-    const double G = bb - 2.0 * (a0 * b0 + a1 * b1 + a2 * b2);
-    const double u = 0x1.0p-24;
-    const double A = sqrt(a0 * a0 + a1 * a1 + a2 * a2), R = sqrt(bb);
-    const double span = R * R + 2.0 * A * R;
-    const double ds = 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * (fabs(G) + 1e-3 * span) +
-                      4.0 * u * (A + R) + 1e-3;
-    double s0 = G + 4.0 * ds + 1.0;
-    s0 += fabs(s0) * 0x1.0p-20;
-    const double x = fmin(fmax(-s0 / 16384.0, -65000.0), 65000.0);
-    const _Float16 hi = (_Float16)x;
-    const _Float16 lo = (_Float16)(x - (double)hi);
-    return (unsigned)__builtin_bit_cast(unsigned short, hi) | ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
-}
-
-// Point i of the transform pass: new_p_i <- sR p_i + t (and its centred fp32 copy, and the next
-// seeded search's seed against this iteration's correspondence y_i = m[idx_i]); returns
-// ||y_i - new_p_i||^2.  (transform_err_kernel, and the fused pass of icp_iter.hip.)
-__device__ __forceinline__ double transform_residual_point(int i, const Xform &xf, double *__restrict__ px,
-                                                           double *__restrict__ py, double *__restrict__ pz,
-                                                           const double *__restrict__ yx, const double *__restrict__ yy,
-                                                           const double *__restrict__ yz, int write_p,
-                                                           float4 *__restrict__ p32, const SeedArgs &sa)
-{
-    double q0, q1, q2;
-    transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
-    const double e = residual2(yx[i], yy[i], yz[i], q0, q1, q2);
-    if (write_p) {
-        px[i] = q0;
-        py[i] = q1;
-        pz[i] = q2;
-        if (p32) p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
-        if (sa.seed16)
-            sa.seed16[i] = mfma16_seed_value(q0, q1, q2, yx[i], yy[i], yz[i], sa.c[0], sa.c[1], sa.c[2], sa.scale);
-    }
-    return e;
 }
 
 } // namespace icp

@@ -272,9 +272,8 @@ int ensure_reduction_space(icp_ctx *ctx)
     HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));
     // NN queue counters: present even for an empty shard (horn_step folds and resets them
     // every iteration, whether or not this rank searched anything)
-    // (+ [4..5]: the tickets of the fused single-rank passes, launch_moments_horn / _transform_err_step)
-    HIPCHK(hipMalloc((void **)&ctx->amb_count, sizeof(int) * 8));
-    HIPCHK(hipMemset(ctx->amb_count, 0, sizeof(int) * 8));
+    HIPCHK(hipMalloc((void **)&ctx->amb_count, sizeof(int) * 4));
+    HIPCHK(hipMemset(ctx->amb_count, 0, sizeof(int) * 4));
     return ICP_OK;
 }
 
@@ -833,18 +832,6 @@ static int wait_flag(icp_ctx *ctx, const int *flag, int ticket)
 // After the iteration whose err < threshold the device flag freezes the state (the one
 // iteration already enqueued behind it changes nothing), which is exactly where the
 // reference's loop breaks (gpu.cc:79-80).
-// single-rank runs over more than kRedSingle points fold each streaming pass in its last
-// workgroup (launch_moments_horn / launch_transform_err_step); ICP_FUSED_PASSES=0 restores the
-// separate reduce / Horn / error launches, for A/B runs
-static bool fused_passes()
-{
-    static const bool on = [] {
-        const char *e = getenv("ICP_FUSED_PASSES");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res)
 {
     TRY(check_ready(ctx, true));
@@ -946,14 +933,8 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142): the first
             // iteration two-pass (the reference's order); later ones in one pass around the shifts
             // the previous Horn step left (its transformed centroid, its correspondence centroid)
-            unsigned *tickets = (unsigned *)(ctx->amb_count + 4);
-            const bool fused = !lag && fused_passes() && red_blocks(n) > 1;
             if (enqueued == 0) {
                 TRY(moments_phase(ctx, n));
-            } else if (fused) { // + the fold and the Horn step, in the pass's last workgroup
-                launch_moments_horn(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, ctx->partials, tickets,
-                                    ctx->sums, N, ctx->c, ctx->amb_count, sd, ctx->st);
-                LAUNCHCHK("moments_horn");
             } else {
                 launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
                                        red_target(ctx, n, ctx->sums), ctx->st);
@@ -965,24 +946,14 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
                 }
             }
             // 4. Horn solve (gpu.cc:106-146) on the device
-            if (!(fused && enqueued > 0)) launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
+            launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
+            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f,
+                                     red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
+            red_finish(ctx, n, 1, ctx->sums + kSumErr);
+            LAUNCHCHK("transform_err");
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
-            if (fused) { // 5 + 6 in one launch
-                const int sl = enqueued % kRing;
-                slot_ticket[sl] = ++ctx->flag_ticket;
-                launch_transform_err_step(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, P.f, sa, ctx->partials, tickets + 1,
-                                          ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd,
-                                          ctx->d_flags + 4 * sl, slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace,
-                                          ctx->st);
-                LAUNCHCHK("transform_err_step");
-            } else {
-                launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f,
-                                         red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
-                red_finish(ctx, n, 1, ctx->sums + kSumErr);
-                LAUNCHCHK("transform_err");
-                if (!lag) TRY(enqueue_err_step(enqueued));
-            }
+            if (!lag) TRY(enqueue_err_step(enqueued));
             ++enqueued;
             if (lag && enqueued == max_iter) { // the last residual has no next iteration to ride on
                 TRY(allreduce(ctx, ctx->sums + kSumErr, 1));

@@ -150,112 +150,7 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_small_kernel(
     if (threadIdx.x == 0) err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
 }
 
-// Last-arriver hand-off of a streaming pass's per-workgroup partial rows, in-launch (the split-K
-// seam of cdna_hip_programming.md, write-through form: per-XCD L2s are not coherent, so the rows
-// are stored sc1 (block_sum_store<K, true>) and read back with sc1 loads (fold_rows<K, true>),
-// which needs no release / acquire fence): every wave drains its stores, the workgroup's barrier,
-// lane 0 takes a ticket; the workgroup drawing the last ticket re-arms it for the next launch
-// and folds every row.  Returns true in that workgroup.
-__device__ __forceinline__ bool last_arriver(unsigned *ticket, int *s_last)
-{
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // every wave's write-through partial stores
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = t == gridDim.x - 1;
-        if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = last;
-    }
-    __syncthreads();
-    return *s_last != 0;
-}
-
-// Iterations >= 2 of a single-rank run over more than kRedSingle points: the one-pass moments
-// (shifted_moments_kernel), the fold of their partials (reduce_kernel<17>) and the Horn step
-// (horn_step_kernel) in one launch -- the last workgroup to finish folds and solves.  The same
-// arithmetic in the same order as the three launches it replaces.
-__global__ __launch_bounds__(kBlock) void moments_horn_kernel(
-    const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
-    const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
-    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials, unsigned *ticket,
-    double *__restrict__ sums, double N, double c0, double c1, double c2, int *__restrict__ cnt,
-    IterState *__restrict__ s)
-{
-    __shared__ int s_done, s_last;
-    if (threadIdx.x == 0) s_done = s->done;
-    __syncthreads();
-    const int done = s_done; // (a frozen iteration: no sums, the Horn step only folds counters)
-    if (!done) {
-        const double cp0 = s->shift_p[0], cp1 = s->shift_p[1], cp2 = s->shift_p[2];
-        const double cy0 = s->shift_y[0], cy1 = s->shift_y[1], cy2 = s->shift_y[2];
-        double a[17];
-#pragma unroll
-        for (int k = 0; k < 17; ++k) a[k] = 0.0;
-        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-            shifted_moment_point(i, idx, m4, px, py, pz, yx, yy, yz, cp0, cp1, cp2, cy0, cy1, cy2, a);
-        block_sum_store<17, true>(a, partials + (size_t)blockIdx.x * 17);
-    }
-    if (!last_arriver(ticket, &s_last)) return;
-    if (!done) {
-        fold_rows<17, true>(partials, gridDim.x, sums);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) horn_step_body(sums, N, c0, c1, c2, 1, cnt, s);
-}
-
-// The transform pass (transform_err_kernel, device transform), the fold of its residual
-// partials (reduce_kernel<1>) and the error step (err_step_kernel) in one launch: the last
-// workgroup to finish folds, tests convergence and signals the host.
-__global__ __launch_bounds__(kBlock) void transform_err_step_kernel(
-    double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, const double *__restrict__ yx,
-    const double *__restrict__ yy, const double *__restrict__ yz, int n, float4 *__restrict__ p32,
-    SeedArgs sa, double *__restrict__ partials, unsigned *ticket, double *__restrict__ sums, double N,
-    double threshold, int max_iter, double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag,
-    int hticket, IterState *h_state, double *h_trace)
-{
-    __shared__ Xform sxf;
-    __shared__ int s_done, s_last;
-    if (threadIdx.x == 0) {
-        s_done = s->done;
-        sxf = s->xf;
-    }
-    __syncthreads();
-    const int done = s_done;
-    if (!done) {
-        const Xform xf = sxf;
-        double a[1] = {0.0};
-        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-            a[0] += transform_residual_point(i, xf, px, py, pz, yx, yy, yz, 1, p32, sa);
-        block_sum_store<1, true>(a, partials + blockIdx.x);
-    }
-    if (!last_arriver(ticket, &s_last)) return;
-    if (!done) {
-        fold_rows<1, true>(partials, gridDim.x, sums + kSumErr);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, hticket, h_state, h_trace);
-}
-
 } // namespace
-
-void launch_moments_horn(const int *idx, const double4 *m4, const double *px, const double *py, const double *pz,
-                         int n, double *yx, double *yy, double *yz, double *partials, unsigned *ticket, double *sums,
-                         double n_total, const double c[3], int *amb_count, IterState *st_dev, hipStream_t st)
-{
-    moments_horn_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials, ticket, sums,
-                                                          n_total, c[0], c[1], c[2], amb_count, st_dev);
-}
-
-void launch_transform_err_step(double *px, double *py, double *pz, const double *yx, const double *yy,
-                               const double *yz, int n, float4 *p32, const SeedArgs &sa, double *partials,
-                               unsigned *ticket, double *sums, double n_total, double threshold, int max_iter,
-                               double *err_trace, IterState *st_dev, int *hflag_dev, int hticket,
-                               IterState *h_state_dev, double *h_trace_dev, hipStream_t st)
-{
-    transform_err_step_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, p32, sa, partials, ticket,
-                                                                sums, n_total, threshold, max_iter, err_trace, st_dev,
-                                                                hflag_dev, hticket, h_state_dev, h_trace_dev);
-}
 
 void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,
                       IterState *st_dev, hipStream_t st)
@@ -287,7 +182,7 @@ __global__ void run_init_kernel(IterState *__restrict__ s, int *__restrict__ cnt
 {
     constexpr int kWords = (int)(sizeof(IterState) / sizeof(int));
     for (int k = threadIdx.x; k < kWords; k += blockDim.x) ((int *)s)[k] = 0;
-    if (threadIdx.x < 8) cnt[threadIdx.x] = 0; // queue counters [0..3], fused-pass tickets [4..5]
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
 }
 
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st)

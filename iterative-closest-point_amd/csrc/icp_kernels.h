@@ -259,19 +259,7 @@ void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, 
                                  const double c[3], int *amb_count, IterState *st_dev, double threshold,
                                  int max_iter, double *err_trace, int *hflag_dev, int ticket,
                                  IterState *h_state_dev, double *h_trace_dev, hipStream_t st);
-// larger single-rank runs: the one-pass moments + their fold + the Horn step in one launch
-// (iterations >= 2), and the transform pass + its fold + the error step in one launch; the last
-// workgroup to finish a pass folds its partials (ticket: a zeroed word, re-armed in-kernel)
-void launch_moments_horn(const int *idx, const double4 *m4, const double *px, const double *py, const double *pz,
-                         int n, double *yx, double *yy, double *yz, double *partials, unsigned *ticket, double *sums,
-                         double n_total, const double c[3], int *amb_count, IterState *st_dev, hipStream_t st);
-void launch_transform_err_step(double *px, double *py, double *pz, const double *yx, const double *yy,
-                               const double *yz, int n, float4 *p32, const SeedArgs &sa, double *partials,
-                               unsigned *ticket, double *sums, double n_total, double threshold, int max_iter,
-                               double *err_trace, IterState *st_dev, int *hflag_dev, int hticket,
-                               IterState *h_state_dev, double *h_trace_dev, hipStream_t st);
-// zero a run's IterState, the NN queue counters (amb_count[0..3]) and the fused-pass tickets
-// (amb_count[4..5])
+// zero a run's IterState and the NN queue counters (amb_count[0..3])
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st);
 
 // exact NN of nq (few) queries, one workgroup each: q_aos (3 x nq) in, idx and y = m[idx]

@@ -473,6 +473,7 @@ __device__ __forceinline__ double seed_shift(unsigned seed)
     return -(hi + lo) * 16384.0;
 }
 
+constexpr double kF16QueryClamp = 32000.0;
 constexpr int kTile16 = 512; // model points per LDS tile of the f16 filter (16 KiB), x2 buffers
 // s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8])
 constexpr int kVmcnt0 = 0x0F70;                   // vmcnt(0)
@@ -1234,7 +1235,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     }
 }
 
-// (seed values: mfma16_seed_value, icp_device.h)
+// Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
+// s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see
+// nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
+// seed of query p (unscaled fp64) from a model point m: packed f16 (hi | lo << 16) of -s0 / 2^14
+__device__ __forceinline__ unsigned mfma16_seed_value(double p0, double p1, double p2, double m0, double m1,
+                                                      double m2, double cx, double cy, double cz, double scale)
+{
+    const double a0 = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double a1 = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double a2 = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double b0 = (m0 - cx) * scale, b1 = (m1 - cy) * scale, b2 = (m2 - cz) * scale;
+    const double bb = b0 * b0 + b1 * b1 + b2 * b2;
+    const double G = bb - 2.0 * (a0 * b0 + a1 * b1 + a2 * b2);
+    const double u = 0x1.0p-24;
+    const double A = sqrt(a0 * a0 + a1 * a1 + a2 * a2), R = sqrt(bb);
+    const double span = R * R + 2.0 * A * R;
+    const double ds = 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * (fabs(G) + 1e-3 * span) +
+                      4.0 * u * (A + R) + 1e-3;
+    double s0 = G + 4.0 * ds + 1.0;
+    s0 += fabs(s0) * 0x1.0p-20;
+    const double x = fmin(fmax(-s0 / 16384.0, -65000.0), 65000.0);
+    const _Float16 hi = (_Float16)x;
+    const _Float16 lo = (_Float16)(x - (double)hi);
+    return (unsigned)__builtin_bit_cast(unsigned short, hi) | ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
+}
+
 __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     int np, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx, double cy,
@@ -1736,17 +1762,59 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     if (sdone) return;
     const Xform xf = sxf;
     double a[1] = {0.0};
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-        a[0] += transform_residual_point(i, xf, px, py, pz, yx, yy, yz, write_p, p32, sa);
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        double q0, q1, q2;
+        transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
+        a[0] += residual2(yx[i], yy[i], yz[i], q0, q1, q2);
+        if (write_p) {
+            px[i] = q0;
+            py[i] = q1;
+            pz[i] = q2;
+            if (p32)
+                p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]),
+                                     (float)(q2 - xf.c[2]), 0.0f);
+            // the next seeded f16 search's seed: the new position against this iteration's
+            // correspondence (y = m[idx], exactly what mfma16_seed_kernel would gather)
+            if (sa.seed16)
+                sa.seed16[i] = mfma16_seed_value(q0, q1, q2, yx[i], yy[i], yz[i], sa.c[0], sa.c[1], sa.c[2],
+                                                 sa.scale);
+        }
+    }
     block_sum_store<1>(a, partials + blockIdx.x);
 }
 
-// out[k] = sum_b partials[b*K + k] in a fixed order (fold_rows, icp_device.h)
+// out[k] = sum_b partials[b*K + k], one workgroup, fixed order (deterministic): thread t
+// accumulates the rows b = t, t + kBlock, ... (contiguous K-double rows: coalesced), then each
+// column is folded by a fixed xor-shuffle tree per wave and the 4 wave sums in wave order.
 template <int K>
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict__ partials, int nblocks,
                                                        double *__restrict__ out)
 {
-    fold_rows<K>(partials, nblocks, out);
+    __shared__ double sh[kBlock / 64][K];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += partials[(size_t)b * K + k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        double r = sh[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
+        out[threadIdx.x] = r;
+    }
 }
 
 inline int grid_for(size_t n, int cap = 2048)

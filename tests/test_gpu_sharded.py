@@ -107,9 +107,8 @@ def test_rccl_single_rank_communicator(icp_lib, name, n, iters):
     bit for bit (same kernels, same reduction order), although with a communicator each
     iteration's residual rides on the next iteration's all-reduce and its convergence test
     runs one iteration late: iters = 1, 2 and 12 (cow_tr2 converges at exactly 12) pin the
-    loop's edges.  The plain context folds each pass of a > 4096-point cloud in its last
-    workgroup (launch_moments_horn / launch_transform_err_step); horse (48,485 points, converges
-    before 50) and the synthetic case pin those fused passes to the separate launches."""
+    loop's edges; horse (48,485 points, stopped by its threshold before 50) pins a mid-size
+    run that converges."""
     amd = icp_lib
     if name in ("cow", "horse"):
         m = amd.load_matrix(datasets.path(f"{name}_ref"))
