@@ -4,7 +4,9 @@ The multi-GPU engine shards the scene contiguously (icp_shard_range), computes p
 sums, all-reduces {sum p, sum y} then {S, d_caps, sp} then {e}, and every rank runs the
 same host Horn solve (icp_horn_solve).  Here each gloo rank does exactly that with the
 oracle's NN standing in for the device kernel, and must reproduce the unsharded oracle
-trajectory.  (The device side of the same path is tests/test_gpu_sharded.py.)"""
+trajectory.  A second test runs the engine's actual multi-rank protocol: one 18-double
+all-reduce per iteration (one-pass shifted moments + the previous residual, error test one
+iteration late).  (The device side of the same path is tests/test_gpu_sharded.py.)"""
 import os
 import socket
 import sys
@@ -82,5 +84,81 @@ def test_two_rank_gloo_matches_unsharded(oracle):
         pr.join(timeout=60)
         assert pr.exitcode == 0
     assert len(errs) == ref["iterations"] == 12
+    np.testing.assert_allclose(errs, ref["err"], rtol=1e-9)
+    np.testing.assert_allclose(new_p, ref["new_p"], atol=1e-9)
+
+
+def _rank_main_one_allreduce(rank, world, port, q, max_iter):
+    """The engine's own multi-rank protocol (icp_engine.hip icp_run, lag mode): the first
+    iteration's two-pass sums (6 + 11 doubles); every later iteration ONE all-reduce of 18
+    doubles -- the 17 one-pass moments around the shifts the previous Horn step left
+    (cp = sR mu_p + t, cy = mu_y) plus the previous iteration's local residual, whose error
+    test therefore runs one iteration late and freezes the state before this iteration's
+    Horn step is applied."""
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "oracle"),
+                    os.path.join(os.path.dirname(HERE), "iterative-closest-point_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datasets
+    import icp_amd
+    import oracle_py as O
+    m = O.load_matrix(datasets.path("cow_ref"))
+    p = O.load_matrix(datasets.path("cow_tr2"))
+    N = p.shape[0]
+    b, c = icp_amd.shard_range(N, rank, world)
+    new_p = p[b:b + c].copy()
+    errs, e_prev, cp, cy = [], None, None, None
+    for it in range(max_iter):
+        y, _ = O.closest(new_p, m)
+        if it == 0:
+            s1 = _allreduce(np.concatenate([new_p.sum(0), y.sum(0)]))
+            mu_p, mu_y = s1[:3] / N, s1[3:] / N
+            pp, yp = new_p - mu_p, y - mu_y
+            s2 = _allreduce(np.concatenate([(pp.T @ yp).reshape(9), [(yp * yp).sum(), (pp * pp).sum()]]))
+            S, d_caps, sp = s2[:9], s2[9], s2[10]
+        else:
+            pp, yp = new_p - cp, y - cy
+            loc = np.concatenate([pp.sum(0), yp.sum(0), (pp.T @ yp).reshape(9),
+                                  [(yp * yp).sum(), (pp * pp).sum(), e_prev]])
+            g = _allreduce(loc)
+            err = (g[17] + g[17]) / N  # iteration it-1's error test, one all-reduce late
+            errs.append(err)
+            if err < 1e-5:
+                break  # frozen: this iteration's Horn step is never applied
+            dp, dy = g[0:3] / N, g[3:6] / N
+            mu_p, mu_y = cp + dp, cy + dy
+            S = g[6:15] - np.outer(g[0:3], dy).reshape(9)
+            d_caps = g[15] - g[3:6] @ dy
+            sp = g[16] - g[0:3] @ dp
+        s, R, t = icp_amd.horn_solve(S, mu_p, mu_y, d_caps, sp)
+        cp, cy = s * (np.asarray(R).reshape(3, 3) @ mu_p) + np.asarray(t), mu_y
+        e_prev, new_p = O.err_compute(new_p, y, s, R, t)
+    else:  # max_iter reached: the last residual rides on one more all-reduce
+        e = _allreduce([e_prev])[0]
+        errs.append((e + e) / N)
+    full = [None] * world
+    dist.all_gather_object(full, new_p)
+    if rank == 0:
+        q.put((errs, np.concatenate(full)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,max_iter", [(2, 20), (3, 20), (2, 5)])
+def test_gloo_one_allreduce_protocol_matches_unsharded(oracle, world, max_iter):
+    import datasets
+    m = oracle.load_matrix(datasets.path("cow_ref"))
+    p = oracle.load_matrix(datasets.path("cow_tr2"))
+    ref = oracle.icp(m, p, max_iter)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main_one_allreduce, args=(r, world, port, q, max_iter)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    errs, new_p = q.get(timeout=300)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert len(errs) == ref["iterations"] == min(max_iter, 12)
     np.testing.assert_allclose(errs, ref["err"], rtol=1e-9)
     np.testing.assert_allclose(new_p, ref["new_p"], atol=1e-9)
