@@ -326,6 +326,20 @@ GridView grid_view(const icp_ctx *ctx)
     return gv;
 }
 
+// Cells a query box may span before the query goes to the brute-force levels.  A box costs
+// about 2 point evaluations per cell (the grid holds ~2 model points per cell of the bounding
+// box; fewer on surface clouds, whose cells are mostly empty), a brute-force fallback nm: up to
+// nm / 8 cells the box is still the cheaper one.  ICP_GRID_BUDGET overrides.
+static int grid_budget(const icp_ctx *ctx)
+{
+    static const int forced = [] {
+        const char *e = getenv("ICP_GRID_BUDGET");
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
+    if (forced) return forced;
+    return (int)std::min<size_t>(std::max<size_t>(kGridBudget, ctx->nm / 8), (size_t)1 << 16);
+}
+
 constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger model: nn_resolve, 256 per query)
 
 // Launches the complete NN search of the n queries in q against the resident model ->
@@ -361,7 +375,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
-        launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1,
+        launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1,
                               ctx->fb_list, ctx->fb_T, ctx->st);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
@@ -415,7 +429,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // exact resolution of the near ties through the model grid, around each candidate;
         // what it cannot take (none at C4): fp64 over every model point, one workgroup each
         launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
-                               grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
+                               grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
                                ctx->fb_T, ctx->st, stop, inline_nm);
         if (!inline_nm)
             launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
@@ -441,7 +455,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // near ties: exact through the model grid; what it cannot take, fp64 brute force
         // (sized on the device: no host round trip on this path)
         launch_nn_grid_resolve(ctx->amb_count, (int)n, ctx->amb_list, ctx->amb_hint, q.x, q.y, q.z, ctx->m4,
-                               grid_view(ctx), kGridBudget, ctx->idx, ctx->amb_count + 1, ctx->fb_list,
+                               grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list,
                                ctx->amb_T, ctx->fb_T, ctx->st, stop, inline_nm);
         if (!inline_nm)
             launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,

@@ -129,7 +129,7 @@ void launch_nn_finalize64(const double *part_best, const int *part_idx, int spli
 
 // ---- uniform grid over the model: exact resolver of queued queries (icp_grid.hip) ---
 constexpr long long kGridMaxCells = 1LL << 24;
-constexpr int kGridBudget = 1024; // cells per query box; larger boxes go back to brute force
+constexpr int kGridBudget = 1024; // min cells per query box (grid_budget); larger boxes go back to brute force
 struct GridParams {
     int g[3];
     double lo[3];
