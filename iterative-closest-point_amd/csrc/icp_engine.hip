@@ -327,9 +327,11 @@ GridView grid_view(const icp_ctx *ctx)
 }
 
 // Cells a query box may span before the query goes to the brute-force levels.  A box costs
-// about 2 point evaluations per cell (the grid holds ~2 model points per cell of the bounding
-// box; fewer on surface clouds, whose cells are mostly empty), a brute-force fallback nm: up to
-// nm / 8 cells the box is still the cheaper one.  ICP_GRID_BUDGET overrides.
+// at most about 2 point evaluations per cell (the grid holds ~2 model points per cell of the
+// bounding box; far fewer on surface clouds, whose cells are mostly empty), a brute-force
+// fallback nm.  Measured (profiles/r01dr/, cells): horse (48,485 points, 25,840 cells) 1,024 ->
+// 6,060 -> 12,000 took the grid variant 3,700 -> 4,277 -> 5,003 it/s and the default 5,560 ->
+// 5,977 -> 6,012, with no gain beyond; bunny likewise.  ICP_GRID_BUDGET overrides.
 static int grid_budget(const icp_ctx *ctx)
 {
     static const int forced = [] {
@@ -337,7 +339,7 @@ static int grid_budget(const icp_ctx *ctx)
         return e ? std::max(1, atoi(e)) : 0;
     }();
     if (forced) return forced;
-    return (int)std::min<size_t>(std::max<size_t>(kGridBudget, ctx->nm / 8), (size_t)1 << 16);
+    return (int)std::min<size_t>(std::max<size_t>(kGridBudget, ctx->nm / 4), (size_t)1 << 16);
 }
 
 constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger model: nn_resolve, 256 per query)
