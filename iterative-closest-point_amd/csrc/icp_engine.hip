@@ -377,8 +377,12 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
-        launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1,
-                              ctx->fb_list, ctx->fb_T, ctx->st);
+        if (seeded) // (icp_run: the previous correspondence is each query's candidate; no ring search)
+            launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), grid_budget(ctx), ctx->idx,
+                                       ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop);
+        else
+            launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx,
+                                  ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);

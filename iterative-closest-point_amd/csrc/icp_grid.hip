@@ -250,15 +250,17 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count,
     int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out, const int *__restrict__ stop,
-    int inline_nm)
+    int inline_nm, int n_all)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
-    const int count = *count_ptr;
+    // list == nullptr: every query t = 0 .. n_all-1, its candidate the previous correspondence
+    // already in idx[t] (the seeded grid variant)
+    const int count = list ? *count_ptr : n_all;
     const int sub = threadIdx.x & (G - 1);
     const int groups = gridDim.x * (kBlock / G);
     for (int t = (blockIdx.x * kBlock + threadIdx.x) / G; t < count; t += groups) {
-        const int j = list[t];
-        const int h = hint[t];
+        const int j = list ? list[t] : t;
+        const int h = list ? hint[t] : idx[t];
         bool ok = h >= 0;
         int c0[3], c1[3];
         const double q[3] = {px[j], py[j], pz[j]};
@@ -522,7 +524,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
     const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, 4096));
 #define RESOLVE(GG, F)                                                                                  \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx, \
-                                                             fb_count, fb_list, T_in, T_out, stop, inline_nm)
+                                                             fb_count, fb_list, T_in, T_out, stop, inline_nm, 0)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE(4, true);
         else if (g == 64) RESOLVE(64, true);
@@ -533,6 +535,28 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
         else RESOLVE(16, false);
     }
 #undef RESOLVE
+}
+
+void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const double *pz, const double4 *m4,
+                                const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list, double *fb_T,
+                                hipStream_t st, const int *stop, int inline_nm)
+{
+    // lanes per query as the unseeded search (launch_nn_grid_search): many queries a few lanes
+    // each, few queries 16 lanes each
+    const int g = n >= (1 << 16) ? 4 : 16;
+    const int per_block = kBlock / g;
+    const int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
+#define RESOLVE_ALL(GG, F)                                                                                       \
+    nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(nullptr, nullptr, nullptr, px, py, pz, m4, gv, budget, \
+                                                             idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n)
+    if (grid_flat_scan(g)) {
+        if (g == 4) RESOLVE_ALL(4, true);
+        else RESOLVE_ALL(16, true);
+    } else {
+        if (g == 4) RESOLVE_ALL(4, false);
+        else RESOLVE_ALL(16, false);
+    }
+#undef RESOLVE_ALL
 }
 
 } // namespace icp

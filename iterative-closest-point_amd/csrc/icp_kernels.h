@@ -159,6 +159,11 @@ void launch_nn_grid_seed(int np, const double *px, const double *py, const doubl
                          int nm, int *idx, hipStream_t st);
 // inline_nm > 0 (a model of that many points): queries the grid cannot take are scanned
 // exactly in place (no fallback queue, no nn_resolve launch)
+// seeded grid variant: every query's previous correspondence (idx[t]) as the candidate, its
+// complete box scanned (no ring search); idx is overwritten with the exact answer
+void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const double *pz, const double4 *m4,
+                                const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list, double *fb_T,
+                                hipStream_t st, const int *stop = nullptr, int inline_nm = 0);
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
