@@ -542,18 +542,24 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
                                 hipStream_t st, const int *stop, int inline_nm)
 {
     // lanes per query as the unseeded search (launch_nn_grid_search): many queries a few lanes
-    // each, few queries 16 lanes each
-    const int g = n >= (1 << 16) ? 4 : 16;
+    // each, few queries 16 lanes each; ICP_GRID_GROUP overrides (1 | 4 | 16)
+    static const int forced = [] {
+        const char *e = getenv("ICP_GRID_GROUP");
+        return e ? atoi(e) : 0;
+    }();
+    const int g = forced == 1 || forced == 4 || forced == 16 ? forced : (n >= (1 << 16) ? 4 : 16);
     const int per_block = kBlock / g;
     const int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
 #define RESOLVE_ALL(GG, F)                                                                                       \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(nullptr, nullptr, nullptr, px, py, pz, m4, gv, budget, \
                                                              idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n)
     if (grid_flat_scan(g)) {
-        if (g == 4) RESOLVE_ALL(4, true);
+        if (g == 1) RESOLVE_ALL(1, true);
+        else if (g == 4) RESOLVE_ALL(4, true);
         else RESOLVE_ALL(16, true);
     } else {
-        if (g == 4) RESOLVE_ALL(4, false);
+        if (g == 1) RESOLVE_ALL(1, false);
+        else if (g == 4) RESOLVE_ALL(4, false);
         else RESOLVE_ALL(16, false);
     }
 #undef RESOLVE_ALL
