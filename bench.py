@@ -196,15 +196,14 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
 def baseline_configs(device, reps=3):
     """BASELINE.json configs C2 (bun000 vs bun045, allow_unequal) and C3 (horse_ref vs horse_tr1):
     complete 50-iteration registrations (reference semantics, threshold 1e-5; neither converges
-    within 50) on this GPU with the default NN path."""
+    within 50) on this GPU with the default NN path, and with the exact grid variant beside it
+    (the same trajectory bit for bit)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import datasets
-    out = {}
-    for name, (ref, scene, unequal) in {"C2_bun000_bun045": ("bun000", "bun045", True),
-                                        "C3_horse_ref_tr1": ("horse_ref", "horse_tr1", False)}.items():
-        m = icp_amd.load_matrix(datasets.path(ref))
-        p = icp_amd.load_matrix(datasets.path(scene))
+
+    def registration(m, p, unequal, variant):
         with icp_amd.Context(device) as ctx:
+            ctx.set_nn_variant(variant)
             ctx.set_allow_unequal(unequal)
             ctx.set_model(m)
             ctx.set_scene(p)
@@ -214,12 +213,21 @@ def baseline_configs(device, reps=3):
             for _ in range(reps):
                 ctx.set_scene(p)
                 res, errs = ctx.run(50)
-            dt = (time.perf_counter() - t0) / reps
-            st = ctx.stats()
+            return res, errs, (time.perf_counter() - t0) / reps, ctx.stats()
+
+    out = {}
+    for name, (ref, scene, unequal) in {"C2_bun000_bun045": ("bun000", "bun045", True),
+                                        "C3_horse_ref_tr1": ("horse_ref", "horse_tr1", False)}.items():
+        m = icp_amd.load_matrix(datasets.path(ref))
+        p = icp_amd.load_matrix(datasets.path(scene))
+        res, errs, dt, st = registration(m, p, unequal, icp_amd.VARIANT_AUTO)
+        gres, gerrs, gdt, _ = registration(m, p, unequal, icp_amd.VARIANT_GRID)
         out[name] = {"n_model": int(m.shape[0]), "n_scene": int(p.shape[0]), "iterations": res.iterations,
                      "ms_per_registration": dt * 1e3, "iterations_per_s": res.iterations / dt,
                      "nn_filter_ms": st["nn_ms"] / max(st["nn_launches"], 1),
-                     "final_err": float(errs[res.iterations - 1])}
+                     "final_err": float(errs[res.iterations - 1]),
+                     "grid_variant": {"iterations_per_s": gres.iterations / gdt, "ms_per_registration": gdt * 1e3,
+                                      "same_trajectory": bool(np.array_equal(gerrs, errs))}}
     return out
 
 
