@@ -14,11 +14,18 @@ sums are all-reduced with RCCL inside libicp_hip.so; total work is fixed => "str
 Timed region: K iterations of icp_run on clouds already resident in HBM, bracketed by a
 barrier + device synchronisation on both sides; ms_per_step = max over ranks.
 roofline: the level-1 O(N*M) NN filter kernel, timed with HIP events on the engine's stream.
-For the f16 MFMA filter (default at C4): executed MFMA flop (32 per pair) against the 2.5 PF
-dense f16 peak; for the fp32 filters: 8 flop/pair against 157.3 TF.  traffic: HBM bytes per
-launch from the committed rocprofv3 PMC summary (profiles/*_pmc_traffic.json).
+achieved = ALGORITHMIC flop (8 per (query, model) pair, this rank's shard x the
+whole model) / average launch time, against the peak of the unit the kernel runs on: the 2.5 PF
+dense f16 MFMA peak for the default f16 filter, 157.3 TF for the fp32 filters.  The executed MFMA
+rate (32 flop per pair, K = 16) is reported beside it as the matrix-pipe utilisation.  traffic:
+HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/*_pmc_traffic.json) when
+the run matches its workload; nn_hbm: the metric's "NN achieved HBM GB/s" (PMC bytes and the
+compulsory bytes of §8d over the live launch time).  streaming: the bandwidth-bound kernels of
+the iteration from the committed profiles (tools/roofline.py recomputes every figure).
 cpu_baseline: the oracle (C restatement of src/cpu.cc, 1 core) on rank 0: NN on a
 4096-query sample against the full model, scaled by N/4096, + the O(N) steps in full.
+N > 1: rank 0 also reports every rank's filter time and its measured per-iteration all-reduce
+latency (HIP events around the collective on the engine stream).
 """
 from __future__ import annotations
 
@@ -56,7 +63,10 @@ def pmc_traffic(kernel):
     (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
     WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950 correction)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from roofline import _tag_key
+    paths = glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))
+    for path in sorted(paths, key=lambda f: _tag_key(os.path.basename(f).split("_")[0]), reverse=True):
         try:
             k = json.load(open(path))["kernels"].get(kernel)
         except (OSError, ValueError, KeyError):
@@ -190,7 +200,7 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
         st = ctx.stats()
     return {"iterations_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps,
             "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1), "brute_force_fallbacks": st["grid_fallback"],
-            "final_err": float(errs[-1]), "kernel": "nn_grid_search_kernel"}
+            "final_err": float(errs[-1]), "kernel": "nn_grid_resolve_kernel (seeded, every query)"}
 
 
 def baseline_configs(device, reps=3):
@@ -346,13 +356,16 @@ def main():
         dt = float(t.item())
 
     nn_avg_ms = st["nn_ms"] / max(st["nn_launches"], 1)
+    ar_ms = st["allreduce_ms"] / st["allreduce_calls"] if st["allreduce_calls"] else None
+    per_rank = [(rank, nn_avg_ms, ar_ms, c)]
+    if dist is not None:
+        got = [None] * world
+        dist.all_gather_object(got, per_rank[0])
+        per_rank = got
     pairs = c * args.n
-    algo_tflops = FLOP_PER_PAIR * pairs / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
-    if level1 == "mfma16":
-        # the kernel runs on the f16 matrix cores: executed MFMA flop vs the dense f16 peak
-        flops, peak, achieved = MFMA16_FLOP_PER_PAIR * pairs, PEAK_F16_MFMA_TFLOPS, None
-    else:
-        flops, peak, achieved = FLOP_PER_PAIR * pairs, PEAK_FP32_TFLOPS, None
+    # algorithmic flop against the peak of the unit the kernel runs on
+    flops = FLOP_PER_PAIR * pairs
+    peak = PEAK_F16_MFMA_TFLOPS if level1 == "mfma16" else PEAK_FP32_TFLOPS
     achieved = flops / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
     # timed iterations are seeded (the first icp_run iteration after set_scene is warm-up)
     k16 = {"plain": "nn_mfma16_kernel<seeded>", "pipe": "nn_mfma16p_kernel<seeded>",
@@ -361,8 +374,19 @@ def main():
     kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel"}.get(
         level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
     if args.variant == "grid":
-        kernel = "nn_grid_search_kernel"
+        # timed iterations are seeded (warm-up leaves every query a correspondence): the seeded
+        # resolve (launch_nn_grid_resolve_all) scans each query's complete candidate box
+        kernel = "nn_grid_resolve_kernel"
     traffic, traffic_src = pmc_traffic(kernel) if world == 1 and args.n == 1 << 20 else (None, None)
+    nn_s = nn_avg_ms * 1e-3
+    compulsory = 16.0 * c + 12.0 * args.n  # §8d: fp32 xyz in (scene shard + model), int32 index out
+    nn_hbm = {"compulsory_bytes": compulsory,
+              "compulsory_gbps": compulsory / nn_s / 1e9 if nn_s > 0 else None,
+              "pmc_bytes": traffic,
+              "pmc_gbps": traffic / nn_s / 1e9 if traffic and nn_s > 0 else None,
+              "peak_gbps": 8000.0,
+              "pmc_hbm_frac": traffic / nn_s / 1e9 / 8000.0 if traffic and nn_s > 0 else None,
+              "note": "the O(N*M) filter is compute-bound: its HBM fraction is small by construction (§8d)"}
     dtype = {"mfma16": "f16 hi/lo-split MFMA filter (fp32 accumulate); fp64 certificate, resolve and reductions",
              "mfma": "f32 MFMA filter; fp64 certificate, resolve and reductions"}.get(
         level1, "f64" if args.nn == "fp64" else "f32 VALU filter; fp64 certificate, resolve and reductions")
@@ -387,7 +411,7 @@ def main():
                                       + ("gloo host all-reduce (rehearsal)" if os.environ.get("ICP_BENCH_HOST_REDUCE") == "1" and world > 1
                                          else "RCCL all-reduce" if world > 1 or args.rccl else "no all-reduce (1 rank)")
                                       + " of 18 fp64 sums/iter"},
-            "roofline": {"bound": "mfma",
+            "roofline": {"bound": "mfma" if level1 in ("mfma16", "mfma") else "valu",
                          "compute_unit": {"mfma16": "v_mfma_f32_32x32x16_f16 (hi/lo split, 14 products/pair) + joint v_min3 skip test (1 VALU per 2 pair values)",
                                           "mfma": "v_mfma_f32_16x16x4_f32 (G = |m|^2 - 2p.m, 4 fma/pair)"}.get(
                              level1, "VALU fp64" if args.nn == "fp64" else "VALU fp32 direct form (peak = f32 MFMA peak)"),
@@ -397,18 +421,39 @@ def main():
                          "frac": achieved / peak, "traffic": traffic,
                          "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
                          "avg_launch_ms": nn_avg_ms, "flop_per_launch": flops,
-                         "flop_definition": ("executed f16 MFMA flop: 32 per (query, model) pair (K = 16 slots, 14 used)"
-                                             if level1 == "mfma16" else "8 flop per (query, model) pair"),
-                         "algorithmic_tflops_8flop_per_pair": algo_tflops,
-                         "pairs_per_s": pairs / (nn_avg_ms * 1e-3) if nn_avg_ms > 0 else 0.0},
+                         "flop_definition": "algorithmic: 8 flop per (query, model) pair (SURVEY.md §8d); "
+                                            f"pairs = {c} local queries x {args.n} model points",
+                         "pairs_per_s": pairs / nn_s if nn_s > 0 else 0.0,
+                         "nn_hbm": nn_hbm},
+            "per_rank": [{"rank": r, "filter_ms": f, "allreduce_ms_per_iter": a, "n_scene_local": cc}
+                         for r, f, a, cc in per_rank],
             "mfma_uncertified_per_iter": st["level1_queued"] / max(st["iterations"], 1),
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
         }
+        if level1 == "mfma16" and nn_s > 0:
+            ex = MFMA16_FLOP_PER_PAIR * pairs / nn_s / 1e12
+            out["roofline"]["mfma_pipe"] = {
+                "executed_tflops": ex, "util": ex / PEAK_F16_MFMA_TFLOPS,
+                "note": "v_mfma_f32_32x32x16_f16 executes 32 flop per pair (K = 16, 14 slots used): "
+                        "matrix-pipe utilisation, not the roofline fraction"}
+        if args.nn == "certified" and args.variant == "auto" and world == 1 and args.n == 1 << 20:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            try:
+                import roofline as RF
+                rf = RF.roofline(None, args.n, world)
+            except Exception as e:  # a missing / malformed profile must not break the bench line
+                rf = {"error": str(e)}
+            if rf and "kernels" in rf:
+                keep = ("shifted_moments_kernel", "gather_moments_kernel", "centred_moments_kernel",
+                        "transform_err_kernel")
+                out["streaming"] = {"source": f"profiles/{rf['tag']}_bench_kernel_stats.csv + "
+                                              f"profiles/{rf['tag']}_pmc_traffic.json (tools/roofline.py)",
+                                    "kernels": {k: v for k, v in rf["kernels"].items() if k in keep}}
         if args.variant == "grid":
-            # no brute-force filter: the grid search streams queries and the model points
-            # near each one; algorithmic bytes = 24 (query) + 4 (index) per query + the
-            # model's 32-byte grid records once
+            # no brute-force filter: the seeded resolve reads each query (24 B) and its previous
+            # correspondence (4 B, rewritten in place) and scans the model's 32-byte grid records
+            # in the query's candidate box; algorithmic bytes = 28 per query + the records once
             gbytes = 28.0 * c + 32.0 * args.n
             ach = gbytes / (nn_avg_ms * 1e-3) / 1e9 if nn_avg_ms > 0 else 0.0
             out["roofline"] = {"bound": "hbm", "kernel": kernel, "achieved": ach, "peak": 8000.0,
@@ -424,7 +469,7 @@ def main():
             out["csv_io"] = csv_io(m)
             if args.variant != "grid" and args.nn == "certified":
                 out["grid_nn"] = grid_nn_rate(local, m, p, args.steps)
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:  # rank 0 at every N: the same host-side baseline
             out["cpu_baseline"] = cpu_baseline(m, p)
             if not args.no_cases:
                 out["cpu_baseline"]["reference_cases_cpu"] = reference_cases_cpu()

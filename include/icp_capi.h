@@ -82,6 +82,17 @@ typedef struct icp_stats {
     double iter_ms;        /* host wall time inside icp_run                             */
     long long iterations;  /* iterations executed by icp_run                            */
     long long grid_fallback; /* near ties the grid resolver handed back to brute force     */
+    double allreduce_ms;   /* summed device time of icp_run's per-iteration all-reduce
+                              (HIP events around the collective on the engine stream; timed
+                              iterations only, like nn_ms)                                   */
+    long long allreduce_calls; /* number of all-reduces timed                              */
+    /* f16 certificate audit (icp_set_cert_audit; -1 / 0 when off), over every query the f16
+     * filter certified since the last reset: the largest |filter value - fp64 value| of the
+     * winner over its error bound delta_b (< 1 means the bound held with room), the smallest
+     * (second - T) / (T - best) margin, and the number of certified queries audited.          */
+    double cert_max_err_ratio;
+    double cert_min_margin;
+    long long cert_audited;
 } icp_stats;
 
 /* ---- context ------------------------------------------------------------ */
@@ -119,6 +130,11 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm);
 int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total);
 /* Copy this rank's current new_p (gpu.hh:88) back to the host. */
 int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
+/* icp_set_model, unless the resident model already holds exactly these nm points (memcmp
+ * against the engine's host copy of the last model uploaded): the safe form of "upload the
+ * model once" for wrappers that receive the model on every call (compute_Y_w_opti,
+ * compute.cu:154-160, re-uploads per call).  *uploaded (nullable) = 1 if it uploaded. */
+int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded);
 /* Reference behaviour is to refuse np != nm (gpu.cc:54-57); 1 lifts that check. */
 int icp_set_allow_unequal(icp_ctx *ctx, int allow);
 /* ICP_NN_VARIANT_* (default AUTO). */
@@ -140,6 +156,9 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
  * mu = mean of the n points; centred_out (nullable) = points - mu. */
 int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3],
                          double *centred_out);
+/* substract_col_w (compute.cu:381-416): out[:, j] = xyz[:, j] - m for ANY 3-vector m
+ * (gpu.cc:101-102 passes the host means rowwise().mean()).  out may alias xyz. */
+int icp_subtract_col(icp_ctx *ctx, const double *xyz, size_t n, const double m[3], double *out);
 /* y_p_norm_w (compute.cu:418-469): d_caps = sum ||y_j||^2, sp = sum ||p_j||^2 */
 int icp_y_p_norm(icp_ctx *ctx, const double *y_xyz, const double *p_xyz, size_t n,
                  double *d_caps, double *sp);
@@ -175,6 +194,20 @@ int icp_write_matrix(const char *path, const double *xyz, size_t n);
 void icp_free(void *p);
 
 /* ---- instrumentation ----------------------------------------------------- */
+/* Correspondences of the last NN search over the resident scene (the last icp_run
+ * iteration's compute_Y_w_opti, gpu.cc:69): idx_out[j] = model index of this rank's scene
+ * point j (np_local entries).  ICP_E_NO_MODEL if no search has run since icp_set_scene. */
+int icp_get_indices(icp_ctx *ctx, int32_t *idx_out);
+/* Test instrumentation: with cap > 0, every icp_run iteration k < cap records a digest of its
+ * correspondence indices (this rank's shard, local j): (sum idx[j], sum (j+1) idx[j],
+ * #{idx[j] == j}), all mod 2^64, order-independent.  Each icp_run restarts at k = 0.
+ * cap = 0 disables (the default: no extra launch). */
+int icp_set_index_digest(icp_ctx *ctx, size_t cap);
+/* Test instrumentation: 1 = audit every f16-certified query (extra fp64 work per query and
+ * three atomics; results in icp_stats.cert_*), 0 = off (the default). */
+int icp_set_cert_audit(icp_ctx *ctx, int enable);
+int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap);
+
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out);
 int icp_reset_stats(icp_ctx *ctx);
 

@@ -56,6 +56,7 @@ struct icp_ctx {
     size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0, mimg16_cap = 0, mms16_cap = 0;
     int nn_variant = ICP_NN_VARIANT_AUTO;
     double c[3] = {0, 0, 0}; // centring point = model centroid
+    std::vector<double> model_host; // the last model uploaded (icp_ensure_model compares against it)
     double rm = 0.0;         // max |centred fp32 model coordinate|
     bool has_model = false;
 
@@ -95,7 +96,10 @@ struct icp_ctx {
     int flag_ticket = 0;             // last ticket handed to an iteration
     double *err_trace_dev = nullptr;
     size_t err_trace_cap = 0;
-    std::vector<hipEvent_t> iter_ev; // per-iteration (begin, end) of the O(N*M) kernel
+    std::vector<hipEvent_t> iter_ev; // per ring slot: (nn begin, nn end, -, all-reduce begin, all-reduce end)
+    unsigned long long *digest = nullptr; // icp_set_index_digest: 3 x digest_cap per-iteration digests
+    unsigned *cert_audit = nullptr;       // icp_set_cert_audit: (max err ratio, min margin) float bits, count
+    size_t digest_cap = 0;
     double4 *m4 = nullptr;      // model as (x, y, z, 0) doubles: one read per random gather
     size_t m4_cap = 0;
     unsigned *seed16 = nullptr; // seeded f16 filter: per-query shift (icp_run iterations >= 2)
@@ -385,7 +389,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                                   ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
-                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st);
+                          ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st,
+                          stop);
         LAUNCHCHK("nn_grid_search");
     } else if (const int l1 = level1_kind(ctx, n)) {
         // level 1: MFMA expanded-form filter over every query.  An unseeded f16 search is
@@ -428,7 +433,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (l1 == 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
-                                      ctx->amb1_hint, ctx->st, stop);
+                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
@@ -667,7 +672,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
-                    (void *)ctx->iter_state, (void *)ctx->err_trace_dev})
+                    (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
+                    (void *)ctx->cert_audit})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -773,6 +779,7 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
                       ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->st);
     LAUNCHCHK("grid_build");
     HIPCHK(hipStreamSynchronize(ctx->st));
+    ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
     ctx->nm = nm;
     ctx->nm_pad = nm_pad;
     ctx->has_model = true;
@@ -784,6 +791,18 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         LAUNCHCHK("make_f32");
         HIPCHK(hipStreamSynchronize(ctx->st));
     }
+    return ICP_OK;
+}
+
+int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded)
+{
+    if (!ctx || !m_xyz || nm == 0) return ICP_E_ARG;
+    if (uploaded) *uploaded = 0;
+    if (ctx->has_model && ctx->nm == nm && ctx->model_host.size() == 3 * nm &&
+        std::memcmp(ctx->model_host.data(), m_xyz, sizeof(double) * 3 * nm) == 0)
+        return ICP_OK;
+    TRY(icp_set_model(ctx, m_xyz, nm));
+    if (uploaded) *uploaded = 1;
     return ICP_OK;
 }
 
@@ -895,12 +914,14 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     }
     int slot_ticket[kRing] = {};
     TRY(grow(ctx, &ctx->err_trace_dev, &ctx->err_trace_cap, (size_t)(max_iter > 0 ? max_iter : 1)));
-    while (ctx->iter_ev.size() < 3 * (size_t)kRing) { // (nn begin, nn end, iteration done) per slot
+    while (ctx->iter_ev.size() < 5 * (size_t)kRing) { // (nn begin, nn end, -, all-reduce begin, end) per slot
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         ctx->iter_ev.push_back(e);
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
+    if (ctx->digest_cap) HIPCHK(hipMemsetAsync(ctx->digest, 0, sizeof(unsigned long long) * 3 * ctx->digest_cap, ctx->st));
+    bool ar_timed[kRing] = {};
     IterState *sd = ctx->iter_state;
     int enqueued = 0, waited = 0, recorded = 0;
     bool stop = false;
@@ -933,10 +954,15 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == 0;
             // (the search of an iteration queued behind the converged one returns at once)
-            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[3 * slot] : nullptr,
-                                timed ? ctx->iter_ev[3 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
+            TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
+                                timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
                                 &sd->done)); // (run_init zeroed the counters)
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
+            ar_timed[slot] = false;
+            if ((size_t)enqueued < ctx->digest_cap) {
+                launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st);
+                LAUNCHCHK("idx_digest");
+            }
             if (!lag && enqueued > 0 && n > 0 && n <= (size_t)kRedSingle) {
                 // small cloud, one rank: steps 2-6 in one workgroup, the same arithmetic in the
                 // same order as the separate launches below (launch latency dominates there)
@@ -961,7 +987,10 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
                 red_finish(ctx, n, 17, ctx->sums);
                 LAUNCHCHK("shifted_moments");
                 if (lag) { // + the previous iteration's residual (sums[kSumErr], local until now)
+                    if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 3], ctx->st));
                     TRY(allreduce(ctx, ctx->sums, kNumSums));
+                    if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 4], ctx->st));
+                    ar_timed[slot] = timed;
                     TRY(enqueue_err_step(enqueued - 1));
                 }
             }
@@ -988,11 +1017,19 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;
             if (n && (waited - 1) % timing_stride == 0) { // (an empty shard records no events)
-                if (hipEventElapsedTime(&ms, ctx->iter_ev[3 * slot], ctx->iter_ev[3 * slot + 1]) == hipSuccess) {
+                if (hipEventElapsedTime(&ms, ctx->iter_ev[5 * slot], ctx->iter_ev[5 * slot + 1]) == hipSuccess) {
                     ctx->stats.nn_ms += ms;
                     ctx->stats.nn_launches += 1;
                 } else {
                     (void)hipGetLastError(); // a failed query must not surface at the next launch check
+                }
+            }
+            if (ar_timed[slot]) { // the all-reduce rode on this slot's iteration
+                if (hipEventElapsedTime(&ms, ctx->iter_ev[5 * slot + 3], ctx->iter_ev[5 * slot + 4]) == hipSuccess) {
+                    ctx->stats.allreduce_ms += ms;
+                    ctx->stats.allreduce_calls += 1;
+                } else {
+                    (void)hipGetLastError();
                 }
             }
             ctx->stats.nn_pairs += (long long)n * (long long)ctx->nm;
@@ -1118,6 +1155,29 @@ int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3]
     return ICP_OK;
 }
 
+int icp_subtract_col(icp_ctx *ctx, const double *xyz, size_t n, const double m[3], double *out)
+{
+    if (!ctx || !m || ((!xyz || !out) && n)) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    if (!n) return ICP_OK;
+    if (3 * n <= kMappedIo) { // small: straight from / into mapped host memory
+        double *hin, *din;
+        TRY(io_take(ctx, 6 * n, &hin, &din));
+        std::memcpy(hin, xyz, sizeof(double) * 3 * n);
+        launch_subtract_aos(din, (int)n, m, din + 3 * n, ctx->st);
+        LAUNCHCHK("subtract_col");
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        std::memcpy(out, hin + 3 * n, sizeof(double) * 3 * n);
+        return ICP_OK;
+    }
+    TRY(upload_cloud(ctx, ctx->qa, xyz, n, false));
+    launch_subtract(ctx->qa.x, ctx->qa.y, ctx->qa.z, (int)n, m[0], m[1], m[2], ctx->st);
+    LAUNCHCHK("subtract_col");
+    return download_cloud(ctx, ctx->qa, n, out);
+}
+
 int icp_y_p_norm(icp_ctx *ctx, const double *y_xyz, const double *p_xyz, size_t n, double *d_caps,
                  double *sp)
 {
@@ -1200,16 +1260,92 @@ int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, s
     return ICP_OK;
 }
 
+int icp_get_indices(icp_ctx *ctx, int32_t *idx_out)
+{
+    if (!ctx || (!idx_out && ctx->scene.n)) return ICP_E_ARG;
+    if (!ctx->has_scene || !ctx->seeds_valid)
+        return fail(ctx, ICP_E_NO_MODEL, "no NN search over the resident scene since icp_set_scene");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->scene.n)
+        HIPCHK(hipMemcpyAsync(idx_out, ctx->idx, sizeof(int32_t) * ctx->scene.n, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    return ICP_OK;
+}
+
+int icp_set_index_digest(icp_ctx *ctx, size_t cap)
+{
+    if (!ctx) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (cap) {
+        size_t have = ctx->digest ? ctx->digest_cap : 0;
+        if (have < cap) {
+            if (ctx->digest) HIPCHK(hipFree(ctx->digest));
+            ctx->digest = nullptr;
+            HIPCHK(hipMalloc((void **)&ctx->digest, sizeof(unsigned long long) * 3 * cap));
+        }
+        HIPCHK(hipMemset(ctx->digest, 0, sizeof(unsigned long long) * 3 * cap));
+    }
+    ctx->digest_cap = cap;
+    return ICP_OK;
+}
+
+int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap)
+{
+    if (!ctx || !out || cap > ctx->digest_cap) return ICP_E_ARG;
+    if (!cap) return ICP_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(out, ctx->digest, sizeof(uint64_t) * 3 * cap, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    return ICP_OK;
+}
+
+static int cert_audit_reset(icp_ctx *ctx)
+{
+    const unsigned init[3] = {0u, 0x7f800000u, 0u}; // max ratio 0, min margin +inf, count 0
+    HIPCHK(hipMemcpy(ctx->cert_audit, init, sizeof(init), hipMemcpyHostToDevice));
+    return ICP_OK;
+}
+
+int icp_set_cert_audit(icp_ctx *ctx, int enable)
+{
+    if (!ctx) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (!enable) {
+        if (ctx->cert_audit) HIPCHK(hipFree(ctx->cert_audit));
+        ctx->cert_audit = nullptr;
+        return ICP_OK;
+    }
+    if (!ctx->cert_audit) HIPCHK(hipMalloc((void **)&ctx->cert_audit, 4 * sizeof(unsigned)));
+    return cert_audit_reset(ctx);
+}
+
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out)
 {
     if (!ctx || !out) return ICP_E_ARG;
     *out = ctx->stats;
+    out->cert_max_err_ratio = -1.0;
+    out->cert_min_margin = -1.0;
+    out->cert_audited = 0;
+    if (ctx->cert_audit) {
+        unsigned a[3] = {0, 0, 0};
+        if (hipStreamSynchronize(ctx->st) != hipSuccess ||
+            hipMemcpy(a, ctx->cert_audit, sizeof(a), hipMemcpyDeviceToHost) != hipSuccess)
+            return ICP_E_HIP;
+        float r, mg;
+        std::memcpy(&r, &a[0], 4);
+        std::memcpy(&mg, &a[1], 4);
+        out->cert_max_err_ratio = r;
+        out->cert_min_margin = mg;
+        out->cert_audited = a[2];
+    }
     return ICP_OK;
 }
 
 int icp_reset_stats(icp_ctx *ctx)
 {
     if (!ctx) return ICP_E_ARG;
+    if (ctx->cert_audit) TRY(cert_audit_reset(ctx));
     ctx->stats = icp_stats{};
     return ICP_OK;
 }

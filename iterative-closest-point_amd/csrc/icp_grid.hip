@@ -269,7 +269,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
         if (ok) {
             const double4 mh = m4[h];
             best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
-            ok = complete_box(q, best, gv, budget, c0, c1);
+            // a non-finite seed distance (a NaN / inf query) bounds no box: such a query goes
+            // to the brute-force levels and their first-minimum rule (index 0 for NaN)
+            ok = best == best && best < INFINITY && complete_box(q, best, gv, budget, c0, c1);
         }
         if (ok) {
             scan_box_sel<G, FLAT>(q, c0, c1, gv, sub, best, bi);
@@ -475,22 +477,20 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 {
     // lanes per query: many queries fill the chip one per lane; few (a shard, small clouds)
     // share lanes to shorten each query's serial chain (measured at 2^20 and 2^17 queries: 4 lanes
-    // 0.35 / 0.066 ms, 1 lane 0.40 / 0.155, 16 lanes 0.445 / 0.068).  ICP_GRID_GROUP overrides (1|4|16).
+    // 0.35 / 0.066 ms, 1 lane 0.40 / 0.155, 16 lanes 0.445 / 0.068).  ICP_GRID_GROUP overrides (4|16).
     static const int forced = [] {
         const char *e = getenv("ICP_GRID_GROUP");
         return e ? atoi(e) : 0;
     }();
-    const int g = forced == 1 || forced == 4 || forced == 16 ? forced : (np >= (1 << 16) ? 4 : 16);
+    const int g = forced == 4 || forced == 16 ? forced : (np >= (1 << 16) ? 4 : 16);
     const int per_block = kBlock / g;
     const int blocks = std::max(1, std::min((np + per_block - 1) / per_block, 16384));
 #define SEARCH(GG, F) nn_grid_search_kernel<GG, F><<<blocks, kBlock, 0, st>>>(np, px, py, pz, gv, budget, idx, fb_count, fb_list, fb_T)
     if (grid_flat_scan(g)) {
-        if (g == 1) SEARCH(1, true);
-        else if (g == 4) SEARCH(4, true);
+        if (g == 4) SEARCH(4, true);
         else SEARCH(16, true);
     } else {
-        if (g == 1) SEARCH(1, false);
-        else if (g == 4) SEARCH(4, false);
+        if (g == 4) SEARCH(4, false);
         else SEARCH(16, false);
     }
 #undef SEARCH
@@ -542,24 +542,22 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
                                 hipStream_t st, const int *stop, int inline_nm)
 {
     // lanes per query as the unseeded search (launch_nn_grid_search): many queries a few lanes
-    // each, few queries 16 lanes each; ICP_GRID_GROUP overrides (1 | 4 | 16)
+    // each, few queries 16 lanes each; ICP_GRID_GROUP overrides (4 | 16)
     static const int forced = [] {
         const char *e = getenv("ICP_GRID_GROUP");
         return e ? atoi(e) : 0;
     }();
-    const int g = forced == 1 || forced == 4 || forced == 16 ? forced : (n >= (1 << 16) ? 4 : 16);
+    const int g = forced == 4 || forced == 16 ? forced : (n >= (1 << 16) ? 4 : 16);
     const int per_block = kBlock / g;
     const int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
 #define RESOLVE_ALL(GG, F)                                                                                       \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(nullptr, nullptr, nullptr, px, py, pz, m4, gv, budget, \
                                                              idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n)
     if (grid_flat_scan(g)) {
-        if (g == 1) RESOLVE_ALL(1, true);
-        else if (g == 4) RESOLVE_ALL(4, true);
+        if (g == 4) RESOLVE_ALL(4, true);
         else RESOLVE_ALL(16, true);
     } else {
-        if (g == 1) RESOLVE_ALL(1, false);
-        else if (g == 4) RESOLVE_ALL(4, false);
+        if (g == 4) RESOLVE_ALL(4, false);
         else RESOLVE_ALL(16, false);
     }
 #undef RESOLVE_ALL

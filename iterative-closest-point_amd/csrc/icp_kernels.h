@@ -114,7 +114,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
-                               hipStream_t st, const int *stop = nullptr);
+                               hipStream_t st, const int *stop = nullptr, const double4 *m4 = nullptr,
+                               unsigned *audit = nullptr);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
@@ -201,6 +202,10 @@ void launch_centred_moments(const double *px, const double *py, const double *pz
 // p' = p - mu in place (substract_col)
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,
                      hipStream_t st);
+// out = in - m (AoS; substract_col with a caller-given m, compute.cu:381-398)
+void launch_subtract_aos(const double *in, int n, const double m[3], double *out, hipStream_t st);
+// out3 += (sum idx, sum (j+1) idx[j], #{idx[j] == j}) mod 2^64 (test digest); a no-op if *done
+void launch_idx_digest(const int *idx, int n, const int *done, unsigned long long *out3, hipStream_t st);
 // partial [sum ||y||^2, sum ||p||^2] (y_p_norm)
 void launch_norms(const double *yx, const double *yy, const double *yz, const double *px,
                   const double *py, const double *pz, int n, double *partials, hipStream_t st);

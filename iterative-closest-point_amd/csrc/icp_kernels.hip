@@ -1299,7 +1299,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const double *__restrict__ py, const double *__restrict__ pz, int np, int nm, double cx,
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint,
-    const int *__restrict__ stop)
+    const int *__restrict__ stop, const double4 *__restrict__ m4, unsigned *__restrict__ audit)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
     const int j = blockIdx.x * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
@@ -1329,6 +1329,19 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         double T = bg + db + delta(Rc) + 0x1.0p-48 * Db;
         T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
         ok = sg > T;
+        if (audit && ok && sub == 0) {
+            // certificate audit (icp_set_cert_audit): the winner's filter error against its bound,
+            // |G^ - G64| / delta_b (G64 = fp64 G of the winner, in the same scaled units), and the
+            // certified margin (second - T) / (T - b) in units of the threshold's own width
+            const double4 mb = m4[id];
+            const double b0 = (mb.x - cx) * scale, b1 = (mb.y - cy) * scale, b2 = (mb.z - cz) * scale;
+            const double g64 = (b0 * b0 + b1 * b1 + b2 * b2) - 2.0 * ((ax * b0 + ay * b1) + az * b2);
+            const float ratio = (float)(fabs(bg - g64) / db);
+            const float margin = (float)fmax((sg - T) / (T - bg), 0.0);
+            atomicMax(audit, __float_as_uint(ratio));
+            atomicMin(audit + 1, __float_as_uint(margin));
+            atomicAdd(audit + 2, 1u);
+        }
     }
     ok = ok || !valid || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
     if (ok && valid && sub == 0) idx[j] = id;
@@ -1687,6 +1700,44 @@ __global__ __launch_bounds__(kBlock) void centre_aos_kernel(const double *__rest
         out[3 * (size_t)i] = in[3 * (size_t)i] - m0;
         out[3 * (size_t)i + 1] = in[3 * (size_t)i + 1] - m1;
         out[3 * (size_t)i + 2] = in[3 * (size_t)i + 2] - m2;
+    }
+}
+
+// substract_col (compute.cu:381-398): out[:, i] = in[:, i] - m for a caller-given 3-vector m
+// (AoS in and out; either may be mapped host memory)
+__global__ __launch_bounds__(kBlock) void subtract_aos_kernel(const double *__restrict__ in, int n, double m0,
+                                                             double m1, double m2, double *__restrict__ out)
+{
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        out[3 * (size_t)i] = in[3 * (size_t)i] - m0;
+        out[3 * (size_t)i + 1] = in[3 * (size_t)i + 1] - m1;
+        out[3 * (size_t)i + 2] = in[3 * (size_t)i + 2] - m2;
+    }
+}
+
+// Test instrumentation (icp_set_index_digest): (sum idx[j], sum (j+1) idx[j], #{idx[j] == j}) of
+// one search's correspondences, mod 2^64 -- integer sums, so independent of the summation order.
+__global__ __launch_bounds__(kBlock) void idx_digest_kernel(const int *__restrict__ idx, int n,
+                                                           const int *__restrict__ done,
+                                                           unsigned long long *__restrict__ out)
+{
+    if (done && *done) return;
+    unsigned long long a = 0, w = 0, id = 0;
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        const unsigned long long v = (unsigned long long)(long long)idx[i];
+        a += v;
+        w += v * (unsigned long long)(i + 1);
+        id += idx[i] == i;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        w += __shfl_xor(w, o, 64);
+        id += __shfl_xor(id, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(out, a);
+        atomicAdd(out + 1, w);
+        atomicAdd(out + 2, id);
     }
 }
 
@@ -2113,7 +2164,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
-                               hipStream_t st, const int *stop)
+                               hipStream_t st, const int *stop, const double4 *m4, unsigned *audit)
 {
     // (its fp64 certificate is heavy and every lane of a group repeats it: lanes only pay off
     // for very many splits; ICP_FIN16_LANES = 1 | 4 | 8 overrides, for experiments)
@@ -2126,7 +2177,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
 #define FIN16(SD, G)                                                                                         \
     nn_finalize_mfma16_kernel<SD, G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
                                                               pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
-                                                              idx, amb_count, amb_list, amb_hint, stop)
+                                                              idx, amb_count, amb_list, amb_hint, stop, m4, audit)
     if (seed16) {
         if (g == 8) FIN16(true, 8); else if (g == 4) FIN16(true, 4); else FIN16(true, 1);
     } else {
@@ -2239,6 +2290,18 @@ void launch_centred_moments(const double *px, const double *py, const double *pz
 {
     centred_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, sums,
                                                               n_total, partials);
+}
+
+void launch_subtract_aos(const double *in, int n, const double m[3], double *out, hipStream_t st)
+{
+    if (n <= 0) return;
+    subtract_aos_kernel<<<grid_for(n), kBlock, 0, st>>>(in, n, m[0], m[1], m[2], out);
+}
+
+void launch_idx_digest(const int *idx, int n, const int *done, unsigned long long *out3, hipStream_t st)
+{
+    if (n <= 0) return;
+    idx_digest_kernel<<<grid_for(n, 1024), kBlock, 0, st>>>(idx, n, done, out3);
 }
 
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,

@@ -56,6 +56,8 @@ EXPORTED = [
     "icp_compute_centroid", "icp_y_p_norm", "icp_err_compute", "icp_find_alignment",
     "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
     "icp_load_matrix", "icp_write_matrix", "icp_free", "icp_get_stats", "icp_reset_stats",
+    "icp_ensure_model", "icp_subtract_col", "icp_get_indices", "icp_set_index_digest",
+    "icp_get_index_digest", "icp_set_cert_audit",
 ]
 
 
@@ -73,7 +75,9 @@ class Result(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("nn_ms", C.c_double), ("nn_launches", C.c_longlong), ("nn_pairs", C.c_longlong),
                 ("ambiguous", C.c_longlong), ("level1_queued", C.c_longlong), ("level1_unrecovered", C.c_longlong), ("iter_ms", C.c_double), ("iterations", C.c_longlong),
-                ("grid_fallback", C.c_longlong)]
+                ("grid_fallback", C.c_longlong), ("allreduce_ms", C.c_double),
+                ("allreduce_calls", C.c_longlong), ("cert_max_err_ratio", C.c_double),
+                ("cert_min_margin", C.c_double), ("cert_audited", C.c_longlong)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
@@ -122,6 +126,12 @@ def lib() -> C.CDLL:
     L.icp_write_matrix.argtypes = [C.c_char_p, dp, sz]
     L.icp_free.argtypes = [vp]
     L.icp_free.restype = None
+    L.icp_ensure_model.argtypes = [vp, dp, sz, C.POINTER(C.c_int)]
+    L.icp_subtract_col.argtypes = [vp, dp, sz, dp, dp]
+    L.icp_get_indices.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.icp_set_index_digest.argtypes = [vp, sz]
+    L.icp_get_index_digest.argtypes = [vp, C.POINTER(C.c_uint64), sz]
+    L.icp_set_cert_audit.argtypes = [vp, C.c_int]
     L.icp_get_stats.argtypes = [vp, C.POINTER(Stats)]
     L.icp_reset_stats.argtypes = [vp]
     _lib = L
@@ -280,6 +290,13 @@ class Context:
         m = _cloud(m)
         self._check(lib().icp_set_model(self._h, _dp(m), m.shape[0]))
 
+    def ensure_model(self, m) -> bool:
+        """icp_ensure_model: upload unless the resident model has these exact contents."""
+        m = _cloud(m)
+        up = C.c_int(0)
+        self._check(lib().icp_ensure_model(self._h, _dp(m), m.shape[0], C.byref(up)))
+        return bool(up.value)
+
     def set_scene(self, p, np_total: int | None = None):
         p = _cloud(p)
         self._check(lib().icp_set_scene(self._h, _dp(p), p.shape[0], p.shape[0] if np_total is None else np_total))
@@ -309,6 +326,33 @@ class Context:
         self._check(lib().icp_closest_matrix(self._h, _dp(p), p.shape[0], _dp(y),
                                              idx.ctypes.data_as(C.POINTER(C.c_int32))))
         return y, idx
+
+    def subtract_col(self, xyz, m):
+        """substract_col_w (compute.cu:381-416): xyz - m for a caller-given 3-vector m."""
+        xyz = _cloud(xyz)
+        out = np.empty_like(xyz)
+        self._check(lib().icp_subtract_col(self._h, _dp(xyz), xyz.shape[0], _dp(_vec(m, 3)), _dp(out)))
+        return out
+
+    def get_indices(self) -> np.ndarray:
+        """Correspondences of the last search over the resident scene (np_local int32)."""
+        idx = np.empty(self._np_local, dtype=np.int32)
+        self._check(lib().icp_get_indices(self._h, idx.ctypes.data_as(C.POINTER(C.c_int32))))
+        return idx
+
+    def set_index_digest(self, cap: int):
+        self._check(lib().icp_set_index_digest(self._h, cap))
+        self._digest_cap = cap
+
+    def set_cert_audit(self, on: bool):
+        self._check(lib().icp_set_cert_audit(self._h, 1 if on else 0))
+
+    def index_digest(self, k: int | None = None) -> np.ndarray:
+        """(k, 3) uint64: per icp_run iteration (sum idx, sum (j+1) idx[j], #{idx[j] == j})."""
+        k = self._digest_cap if k is None else k
+        out = np.zeros((max(k, 1), 3), dtype=np.uint64)
+        self._check(lib().icp_get_index_digest(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64)), k))
+        return out[:k]
 
     def compute_centroid(self, xyz, centred: bool = True):
         xyz = _cloud(xyz)

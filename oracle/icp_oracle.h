@@ -49,6 +49,11 @@ void oracle_closest(const double *p, size_t np, const double *m, size_t nm, int 
 void oracle_closest_range(const double *p, size_t j0, size_t j1, const double *m, size_t nm,
                           int nn_mode, int32_t *idx, double *y);
 
+/* Same indices as oracle_closest_range(..., ORACLE_NN_SQUARED, ...) for finite inputs,
+ * evaluated W model points x 4 queries at a time (icp_oracle_fast.c); for large fixtures. */
+void oracle_closest_range_blocked(const double *p, size_t j0, size_t j1, const double *m, size_t nm,
+                                  int32_t *idx, double *y);
+
 /* src/cpu.cc:81-91 max_element_index — the reference's quirk: never updates `max`,
  * returns the LAST i in 1..3 with ev[i] > ev[0], else 0. */
 int oracle_max_element_index(const double ev[4]);

@@ -50,6 +50,7 @@ def lib() -> C.CDLL:
         sz = C.c_size_t
         L.oracle_closest.argtypes = [dp, sz, dp, sz, C.c_int, ip, dp]
         L.oracle_closest_range.argtypes = [dp, sz, sz, dp, sz, C.c_int, ip, dp]
+        L.oracle_closest_range_blocked.argtypes = [dp, sz, sz, dp, sz, ip, dp]
         L.oracle_max_element_index.argtypes = [dp]
         L.oracle_eig_sym4.argtypes = [dp, dp, dp]
         L.oracle_find_alignment.argtypes = [dp, dp, sz, C.POINTER(Alignment)]
@@ -83,6 +84,17 @@ def closest(p, m, nn_mode: int = NN_SQUARED, j0: int = 0, j1: int | None = None)
     y = np.zeros_like(p)
     lib().oracle_closest_range(_dp(p), j0, j1, _dp(m), m.shape[0], nn_mode,
                                idx.ctypes.data_as(C.POINTER(C.c_int32)), _dp(y))
+    return y[j0:j1], idx[j0:j1]
+
+
+def closest_blocked(p, m, j0: int = 0, j1: int | None = None):
+    """closest(p, m, NN_SQUARED, j0, j1), SIMD-blocked (icp_oracle_fast.c; finite inputs)."""
+    p = _cloud(p); m = _cloud(m)
+    j1 = p.shape[0] if j1 is None else j1
+    idx = np.zeros(p.shape[0], dtype=np.int32)
+    y = np.zeros_like(p)
+    lib().oracle_closest_range_blocked(_dp(p), j0, j1, _dp(m), m.shape[0],
+                                       idx.ctypes.data_as(C.POINTER(C.c_int32)), _dp(y))
     return y[j0:j1], idx[j0:j1]
 
 

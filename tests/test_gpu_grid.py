@@ -106,3 +106,66 @@ def test_grid_variant_at_c4_matches_fp64_and_rarely_falls_back(amd):
         _, ref = ctx.closest_matrix(p)
     np.testing.assert_array_equal(idx, ref)
     assert st["grid_fallback"] <= 16, st
+
+
+def icp_runs(amd, m, p, iters, variants=("grid", "fp64")):
+    out = {}
+    for name in variants:
+        mode, variant = (amd.NN_FP64, 0) if name == "fp64" else (amd.NN_CERTIFIED, CERTIFIED[name])
+        with amd.Context(0, mode) as ctx:
+            ctx.set_nn_variant(variant)
+            ctx.set_allow_unequal(m.shape[0] != p.shape[0])
+            ctx.set_model(m)
+            ctx.set_scene(p)
+            ctx.reset_stats()
+            res, errs = ctx.run(iters, -1.0)
+            out[name] = (res, errs, ctx.get_scene(), ctx.get_indices(), ctx.stats())
+    return out
+
+
+def assert_same_run(runs, ref="fp64"):
+    r0, e0, s0, i0, _ = runs[ref]
+    for name, (r, e, s, i, _) in runs.items():
+        assert r.iterations == r0.iterations, name
+        np.testing.assert_array_equal(e, e0, err_msg=name)
+        np.testing.assert_array_equal(s, s0, err_msg=name)
+        np.testing.assert_array_equal(i, i0, err_msg=name)
+
+
+def test_grid_variant_icp_run_hollow_cube_falls_back(amd):
+    """icp_run with the grid variant: iterations >= 2 take the seeded resolve
+    (launch_nn_grid_resolve_all).  On the hollow cube the scene's centre queries are tied
+    across faces, their boxes exceed the budget and go to nn_resolve (T = +inf); the run must
+    equal the fp64 brute force bit for bit."""
+    g = integer_lattice(40)
+    m = g[(g == 0).any(1) | (g == 39).any(1)]
+    k = 600
+    p = np.concatenate([np.column_stack([np.full(k, 19.5), np.full(k, 19.5), 19.5 + RNG.integers(-2, 3, k)]),
+                        m[RNG.integers(0, m.shape[0], m.shape[0] - k)] + RNG.normal(scale=0.05, size=(m.shape[0] - k, 3))])
+    runs = icp_runs(amd, m, p, 4)
+    assert_same_run(runs)
+    assert runs["grid"][4]["grid_fallback"] > 0, runs["grid"][4]
+
+
+def test_grid_variant_icp_run_clustered(amd):
+    a = RNG.normal(scale=0.01, size=(15000, 3))
+    b = RNG.normal(scale=0.01, size=(15000, 3)) + 100.0
+    m = np.round(np.concatenate([a, b]) * 4096) / 4096
+    p = np.round((m[RNG.permutation(m.shape[0])[:20000]] + [0.002, -0.001, 0.0005]) * 4096) / 4096
+    runs = icp_runs(amd, m, p, 5, ("grid", "mfma16", "valu", "fp64"))
+    assert_same_run(runs)
+
+
+def test_grid_variant_seeded_non_finite_scene_point(amd):
+    """A NaN scene point makes the whole iteration non-finite (as in the reference).  The
+    seeded grid resolve must still return the first-minimum rule's index for it (0: no
+    comparison holds), like every other path, instead of keeping its stale seed."""
+    m = RNG.normal(size=(5000, 3))
+    p = m[RNG.integers(0, 5000, 5000)] + RNG.normal(scale=0.01, size=(5000, 3))
+    p[17] = [np.nan, 0.0, 0.0]
+    runs = icp_runs(amd, m, p, 3, ("grid", "valu", "fp64"))
+    for name, (res, errs, scene, idx, _) in runs.items():
+        assert res.iterations == 3, name
+        assert np.isnan(errs).all(), name
+        assert (idx == 0).all(), name  # every query is NaN after the first transform
+    assert_same_run({k: (v[0], v[1], v[2], v[3], v[4]) for k, v in runs.items()})

@@ -149,3 +149,40 @@ def test_bunny_fixture_records_tie_sensitivity(golden):
     assert g["idx0_sqrt_vs_squared_mismatches"] >= 0
     for name in ("cow_tr1", "cow_tr2", "horse_tr1", "horse_tr2"):
         assert golden[name]["idx0_sqrt_vs_squared_mismatches"] == 0
+
+
+@pytest.mark.parametrize("n,nm", [(1, 1), (5, 7), (37, 13), (300, 1000), (129, 4099)])
+def test_closest_blocked_equals_scalar(oracle, n, nm):
+    """The SIMD-blocked form (icp_oracle_fast.c, used for the C4 fixture) returns the scalar
+    loop's indices: random clouds, exact duplicates (ties -> first index), ragged sizes."""
+    rng = np.random.default_rng(n * 7919 + nm)
+    p = rng.uniform(-1, 1, (n, 3))
+    m = rng.uniform(-1, 1, (nm, 3))
+    m[3 % nm::5] = m[0]                     # many exact ties with index 0
+    if nm > 20:
+        m[nm - 1] = m[nm // 2]              # a tie between lanes of different residue
+        p[: min(n, 4)] = m[nm // 2]         # distance exactly 0, twice
+    y1, i1 = oracle.closest(p, m)
+    y2, i2 = oracle.closest_blocked(p, m)
+    assert np.array_equal(i1, i2)
+    assert np.array_equal(y1, y2)
+    # a sub-range only touches its rows
+    j0, j1 = n // 3, n - n // 4
+    _, ir = oracle.closest_blocked(p, m, j0, j1)
+    assert np.array_equal(ir, i1[j0:j1])
+
+
+def test_c4_fixture_inputs_and_shape(icp_lib):
+    """tests/golden/c4_oracle.json was made on the bench's exact inputs (host-side generator,
+    no device work) and holds a full 30-iteration trajectory."""
+    import hashlib
+    import json
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c4_oracle.json")))
+    m, p = icp_lib.synthetic_pair(fx["n"], seed=fx["seed"])
+    assert hashlib.sha256(m.tobytes()).hexdigest() == fx["model_sha256"]
+    assert hashlib.sha256(p.tobytes()).hexdigest() == fx["scene_sha256"]
+    assert fx["n"] == 1 << 20 and fx["iters"] == 30 and len(fx["err"]) == 30 and len(fx["idx"]) == 30
+    e = np.array(fx["err"])
+    assert np.all(np.isfinite(e)) and np.all(np.diff(e) < 0)  # a converging registration
+    ident = [d["identity"] for d in fx["idx"]]
+    assert ident[-1] > ident[0]  # correspondences move toward the known identity pairing

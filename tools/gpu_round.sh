@@ -28,7 +28,7 @@ run() { # name timeout cmd...
 
 for s in $STEPS; do
     case $s in
-    test)  run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
+    test)  run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread --durations=15 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_mfma) run bench_mfma 300 python bench.py --variant mfma --no-cpu-baseline --no-cow ;;
@@ -94,6 +94,10 @@ for s in $STEPS; do
     gridr64) for g in 16 64 16 64; do ICP_GRID_RGROUP=$g run gridr64_$g 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1; cat $OUT/gridr64_$g.log >> $OUT/gridr64_all_$g.log; done ;;
     gseed) for v in 0 1 0 1; do ICP_GRID_SEED=$v run gseed_$v 300 python3 tools/nn_probe.py --variant mfma16 --reps 3 || exit 1; cat $OUT/gseed_$v.log >> $OUT/gseed_all_$v.log; done ;;
     configs) run configs 300 python tools/configs_probe.py ;;
+    calib) run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/calib1" -o fetch -- tools/hbm_calib &&
+           run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib2" -o write -- tools/hbm_calib ;;
+    test_new) run pytest_new 900 python -u -m pytest tests/test_gpu_c4c5.py tests/test_gpu_boundary.py tests/test_gpu_cert_stress.py \
+               tests/test_gpu_grid.py -m gpu -v -rf --timeout 300 --timeout-method thread --durations=15 ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;

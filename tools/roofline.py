@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Recompute every roofline figure bench.py reports from the committed profiles.
+
+    python tools/roofline.py [--tag r02a] [--n 1048576] [--world 1]
+
+Inputs (both written by tools/gpu_round.sh on the GPU box, then copied into profiles/):
+  profiles/<tag>_bench_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `bench.py --no-cases`
+  profiles/<tag>_pmc_traffic.json         tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE
+                                          passes of the same command (FETCH_SIZE doubled, gfx950)
+Without --tag: the newest tag that has both files.
+
+Per kernel: average duration, PMC bytes per launch, achieved GB/s and fraction of the 8 TB/s
+HBM peak, and -- where the kernel has a per-point algorithmic byte count (below) -- the
+algorithmic GB/s and the over-fetch ratio PMC / algorithmic.  For the O(N*M) NN filter:
+algorithmic TFLOP/s = 8 flop per (query, model) pair / average duration,
+against the 2.5 PF dense f16 MFMA peak of the unit it runs on, and the executed MFMA rate
+(32 flop per pair: v_mfma_f32_32x32x16_f16, K = 16) as the matrix-pipe utilisation.
+
+Algorithmic bytes per scene point (fp64 SoA clouds):
+  shifted_moments_kernel / gather_moments_kernel: idx 4 + m4[idx] 32 + p 24 + write Y 24 = 84
+  centred_moments_kernel: p 24 + Y 24 = 48
+  transform_err_kernel (icp_run form): p 24 + Y 24 + write p 24 + p32 16 + seed16 4 = 92
+  NN filter: SURVEY §8d compulsory 12 N + 12 M + 4 N (fp32 xyz in, int32 index out)
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROFILES = os.path.join(ROOT, "profiles")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense ~2.5 PF
+NN_KERNELS = ("nn_mfma16r_kernel<8>", "nn_mfma16r_kernel<4>", "nn_mfma16_kernel", "nn_mfma16_kernel<seeded>")
+BYTES_PER_POINT = {"shifted_moments_kernel": 84, "gather_moments_kernel": 84, "centred_moments_kernel": 48,
+                   "transform_err_kernel": 92}
+
+
+def _tag_key(tag):
+    """r01t < r01ei < r02a: round number, then suffix length, then suffix."""
+    import re
+    m = re.match(r"r(\d+)([a-z]*)", tag)
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, tag)
+
+
+def newest_tag():
+    tags = []
+    for f in glob.glob(os.path.join(PROFILES, "*_pmc_traffic.json")):
+        tag = os.path.basename(f)[: -len("_pmc_traffic.json")]
+        if os.path.exists(os.path.join(PROFILES, f"{tag}_bench_kernel_stats.csv")):
+            tags.append(tag)
+    return max(tags, key=_tag_key) if tags else None
+
+
+def kernel_times(path):
+    from pmc_summary import short
+    out = {}
+    for r in csv.DictReader(open(path)):
+        k = short(r["Name"])
+        out[k] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) * 1e-6}
+    return out
+
+
+def roofline(tag=None, n=1 << 20, world=1):
+    tag = tag or newest_tag()
+    if tag is None:
+        return None
+    times = kernel_times(os.path.join(PROFILES, f"{tag}_bench_kernel_stats.csv"))
+    pmc = json.load(open(os.path.join(PROFILES, f"{tag}_pmc_traffic.json")))["kernels"]
+    n_local = (n + world - 1) // world
+    out = {"tag": tag, "n_model": n, "n_scene_local": n_local, "kernels": {}}
+    for k, t in sorted(times.items(), key=lambda kv: -kv[1]["avg_ms"] * kv[1]["calls"]):
+        row = {"calls": t["calls"], "avg_ms": t["avg_ms"]}
+        p = pmc.get(k)
+        if p and t["avg_ms"] > 0:
+            row["pmc_bytes"] = p["traffic_bytes_per_launch"]
+            row["pmc_gbps"] = p["traffic_bytes_per_launch"] / (t["avg_ms"] * 1e-3) / 1e9
+            row["pmc_hbm_frac"] = row["pmc_gbps"] / HBM_PEAK_GBS
+        if k in BYTES_PER_POINT:
+            b = BYTES_PER_POINT[k] * n_local
+            row["algorithmic_bytes"] = b
+            row["algorithmic_gbps"] = b / (t["avg_ms"] * 1e-3) / 1e9
+            row["hbm_frac"] = row["algorithmic_gbps"] / HBM_PEAK_GBS
+            if "pmc_bytes" in row:
+                row["over_fetch"] = row["pmc_bytes"] / b
+        if k in NN_KERNELS:
+            pairs = float(n_local) * n
+            row["algorithmic_tflops"] = 8.0 * pairs / (t["avg_ms"] * 1e-3) / 1e12
+            row["frac_of_f16_mfma_peak"] = row["algorithmic_tflops"] / F16_MFMA_PEAK_TFLOPS
+            row["executed_mfma_tflops"] = 32.0 * pairs / (t["avg_ms"] * 1e-3) / 1e12
+            row["mfma_pipe_util"] = row["executed_mfma_tflops"] / F16_MFMA_PEAK_TFLOPS
+            cb = 16.0 * n_local + 12.0 * n
+            row["compulsory_bytes"] = cb
+            row["compulsory_gbps"] = cb / (t["avg_ms"] * 1e-3) / 1e9
+        out["kernels"][k] = row
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag")
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--world", type=int, default=1)
+    a = ap.parse_args()
+    r = roofline(a.tag, a.n, a.world)
+    if r is None:
+        sys.exit("no profiles/<tag>_pmc_traffic.json + <tag>_bench_kernel_stats.csv pair found")
+    print(json.dumps(r, indent=1))
+
+
+if __name__ == "__main__":
+    main()
