@@ -93,6 +93,7 @@ typedef struct icp_stats {
     double cert_max_err_ratio;
     double cert_min_margin;
     long long cert_audited;
+    long long persistent_runs; /* icp_run calls that ran as ONE launch (icp_set_run_mode)      */
 } icp_stats;
 
 /* ---- context ------------------------------------------------------------ */
@@ -139,6 +140,18 @@ int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded
 int icp_set_allow_unequal(icp_ctx *ctx, int allow);
 /* ICP_NN_VARIANT_* (default AUTO). */
 int icp_set_nn_variant(icp_ctx *ctx, int variant);
+/* How icp_run executes (results are bit-identical either way):
+ * LAUNCHES:   the device-resident loop of a few launches per iteration (any size, any rank count);
+ * PERSISTENT: the whole run in ONE launch of co-resident workgroups holding the model in LDS,
+ *             one grid barrier per iteration -- taken when the run is eligible: one rank without
+ *             a communicator, 4 <= np <= 4096, nm <= ~6,400 points, no index digest;
+ * AUTO:       PERSISTENT for eligible runs with the AUTO NN variant (an explicitly chosen NN
+ *             variant runs its own search cascade), else LAUNCHES.  The default.
+ * The environment variable ICP_RUN_MODE=launches|persistent overrides (A/B runs). */
+#define ICP_RUN_AUTO 0
+#define ICP_RUN_LAUNCHES 1
+#define ICP_RUN_PERSISTENT 2
+int icp_set_run_mode(icp_ctx *ctx, int mode);
 
 /* ---- the ICP loop: GPU::ICP::find_corresponding_opti (src/GPU/gpu.cc:52-83) -- */
 /* Runs up to max_iter iterations on the resident clouds; stops after the iteration

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -24,6 +25,62 @@
 #include "icp_kernels.h"
 
 using namespace icp;
+
+// The one-launch loop's model image: points in Morton order of their 10-bit quantised
+// coordinates (ties: original index), split into 64-point blocks with exact fp64 boxes, so
+// that a query scans only the blocks whose box is within its seed distance.  Layout (doubles):
+// x[nm] | y[nm] | z[nm] | blocks x (lo x, lo y, lo z, hi x, hi y, hi z) | int32 original
+// index per sorted position (packed two per double).
+std::vector<double> icp::persist_model_image(const double *m, size_t nm, size_t *blocks_out)
+{
+    double lo[3] = {m[0], m[1], m[2]}, hi[3] = {m[0], m[1], m[2]};
+    for (size_t j = 1; j < nm; ++j)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], m[3 * j + a]);
+            hi[a] = std::max(hi[a], m[3 * j + a]);
+        }
+    auto spread = [](uint64_t v) { // 10 bits -> every third bit
+        v &= 0x3ff;
+        v = (v | (v << 16)) & 0x30000ff;
+        v = (v | (v << 8)) & 0x300f00f;
+        v = (v | (v << 4)) & 0x30c30c3;
+        v = (v | (v << 2)) & 0x9249249;
+        return v;
+    };
+    std::vector<uint64_t> key(nm);
+    for (size_t j = 0; j < nm; ++j) {
+        uint64_t code = 0;
+        for (int a = 0; a < 3; ++a) {
+            const double w = hi[a] - lo[a];
+            const double t = w > 0 ? (m[3 * j + a] - lo[a]) / w * 1023.0 : 0.0;
+            code |= spread((uint64_t)std::min(1023.0, std::max(0.0, t))) << a;
+        }
+        key[j] = (code << 32) | (uint64_t)j; // (code, original index): a total order
+    }
+    std::sort(key.begin(), key.end());
+    const size_t nb = (nm + 63) / 64;
+    std::vector<double> img(3 * nm + 6 * nb + (nm + 1) / 2);
+    int32_t *orig = (int32_t *)(img.data() + 3 * nm + 6 * nb);
+    for (size_t k = 0; k < nm; ++k) {
+        const size_t j = (size_t)(key[k] & 0xffffffffu);
+        for (int a = 0; a < 3; ++a) img[a * nm + k] = m[3 * j + a];
+        orig[k] = (int32_t)j;
+    }
+    for (size_t b = 0; b < nb; ++b) {
+        double *box = img.data() + 3 * nm + 6 * b;
+        for (int a = 0; a < 3; ++a) {
+            box[a] = img[a * nm + 64 * b];
+            box[3 + a] = box[a];
+        }
+        for (size_t k = 64 * b + 1; k < std::min(nm, 64 * b + 64); ++k)
+            for (int a = 0; a < 3; ++a) {
+                box[a] = std::min(box[a], img[a * nm + k]);
+                box[3 + a] = std::max(box[3 + a], img[a * nm + k]);
+            }
+    }
+    *blocks_out = nb;
+    return img;
+}
 
 namespace {
 
@@ -123,6 +180,20 @@ struct icp_ctx {
     double *h_io = nullptr, *d_io = nullptr;
     size_t io_cap = 0, io_off = 0;
     bool io_pending = false; // a queued kernel may still read h_io
+
+    // one-launch registration of small clouds (icp_iter.hip, launch_icp_persistent)
+    int run_mode = ICP_RUN_AUTO;
+    int n_cu = 0;                    // compute units
+    size_t lds_per_cu = 0, lds_per_block = 0;
+    double *pers_part = nullptr;     // 2 x kBlock x kNumSums published partials
+    unsigned *pers_sync = nullptr;   // arrival counter, abort word (+ padding to 16 B)
+    size_t pers_part_cap = 0, pers_sync_cap = 0;
+    unsigned long long *pers_stamps = nullptr; // ICP_PERSIST_STAMPS=1: phase stamps
+    size_t pers_stamps_cap = 0;
+    // the model in Morton order for the one-launch NN (models <= kPersistMaxModel points):
+    // x[nm] | y[nm] | z[nm] | 64-point block boxes (lo xyz, hi xyz) | original index (int32)
+    double *pm_img = nullptr;
+    size_t pm_img_cap = 0, pm_blocks = 0;
 
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     icp_stats stats{};
@@ -372,9 +443,9 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         int *pi = (int *)(pb + (size_t)pl.splits * n);
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         launch_nn_fp64(q.x, q.y, q.z, (int)n, ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm,
-                       pl, pb, pi, ctx->st);
+                       pl, pb, pi, ctx->st, stop);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
-        launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st);
+        launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st, stop);
         LAUNCHCHK("nn_fp64");
     } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
         // exact grid search for every query; over-budget boxes -> fp64 brute force per query
@@ -574,6 +645,11 @@ static int ctx_init(icp_ctx *ctx)
     // timing-only events: no system-scope fence (an L2 writeback + invalidate per record);
     // data always reaches the host through a stream synchronisation or the mapped flags
     for (auto &e : ctx->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, ctx->device));
+    ctx->n_cu = prop.multiProcessorCount;
+    ctx->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
+    ctx->lds_per_block = prop.sharedMemPerBlock;
     return ensure_reduction_space(ctx);
 }
 
@@ -673,7 +749,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
-                    (void *)ctx->cert_audit})
+                    (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
+                    (void *)ctx->pers_stamps, (void *)ctx->pm_img})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -695,6 +772,13 @@ int icp_set_nn_variant(icp_ctx *ctx, int variant)
 {
     if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_GRID) return ICP_E_ARG;
     ctx->nn_variant = variant;
+    return ICP_OK;
+}
+
+int icp_set_run_mode(icp_ctx *ctx, int mode)
+{
+    if (!ctx || mode < ICP_RUN_AUTO || mode > ICP_RUN_PERSISTENT) return ICP_E_ARG;
+    ctx->run_mode = mode;
     return ICP_OK;
 }
 
@@ -778,6 +862,12 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_cid, ctx->g_count,
                       ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->st);
     LAUNCHCHK("grid_build");
+    std::vector<double> pm;
+    if (nm <= (size_t)kPersistMaxModel) { // the one-launch loop's Morton-ordered model image
+        pm = persist_model_image(m_xyz, nm, &ctx->pm_blocks);
+        TRY(grow(ctx, &ctx->pm_img, &ctx->pm_img_cap, pm.size()));
+        HIPCHK(hipMemcpyAsync(ctx->pm_img, pm.data(), sizeof(double) * pm.size(), hipMemcpyHostToDevice, ctx->st));
+    }
     HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
     ctx->nm = nm;
@@ -863,6 +953,122 @@ static int wait_flag(icp_ctx *ctx, const int *flag, int ticket)
     }
 }
 
+static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_result *res,
+                      std::chrono::steady_clock::time_point wall0);
+
+
+// Workgroups of the one-launch registration for this run, or 0 if it does not apply: one
+// rank, no communicator, n <= kRedSingle (the single-workgroup passes it reproduces bit for
+// bit), the model in LDS, >= 64 co-resident workgroups, no per-iteration instrumentation.
+static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *lds_out)
+{
+    static const int forced = [] { // ICP_RUN_MODE=launches|persistent (A/B runs)
+        const char *e = getenv("ICP_RUN_MODE");
+        if (!e) return -1;
+        return std::strcmp(e, "launches") == 0 ? ICP_RUN_LAUNCHES
+               : std::strcmp(e, "persistent") == 0 ? ICP_RUN_PERSISTENT : -1;
+    }();
+    const int mode = forced >= 0 ? forced : ctx->run_mode;
+    if (mode == ICP_RUN_LAUNCHES) return 0;
+    if (mode == ICP_RUN_AUTO && ctx->nn_variant != ICP_NN_VARIANT_AUTO) return 0; // explicit variants run their cascade
+    if (ctx->world != 1 || ctx->comm || ctx->host_reduce || ctx->digest_cap || max_iter < 1) return 0;
+    if (n < 4 || n > (size_t)kRedSingle || ctx->nm < 1 || ctx->nm > (size_t)kPersistMaxModel) return 0;
+    const size_t lds = 24 * ctx->nm + 48 * ctx->pm_blocks, statics = persistent_static_lds();
+    if (!ctx->pm_img) return 0;
+    if (lds + statics > ctx->lds_per_cu) return 0; // (gfx950: one workgroup may take the whole 160 KiB)
+    const int per_cu = (int)std::min<size_t>(2, ctx->lds_per_cu / (lds + statics)); // (<= 2: 199 VGPRs)
+    // residency margin: a quarter of the admissible slots left free (a barrier over a grid that
+    // is not fully resident would only time out, but it would be an error, not a slow run);
+    // 256 / 128 / 64 workgroups, so that every one owns the same number of virtual threads
+    const int slots = ctx->n_cu * per_cu * 3 / 4;
+    const int grid = slots >= kBlock ? kBlock : slots >= kBlock / 2 ? kBlock / 2 : kBlock / 4;
+    if (grid < 64) return 0;
+    *lds_out = lds;
+    return grid;
+}
+
+// icp_run as ONE launch (launch_icp_persistent): same results, bit for bit, as the loop below.
+static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, double threshold, double *err_trace,
+                          icp_result *res, std::chrono::steady_clock::time_point wall0)
+{
+    const size_t n = ctx->scene.n;
+    DevCloud &P = ctx->scene, &Y = ctx->Y;
+    TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n)); // (a fresh context has run no search yet)
+    TRY(grow(ctx, &ctx->pers_part, &ctx->pers_part_cap, (size_t)2 * kBlock * kNumSums));
+    static const bool stamps = getenv("ICP_PERSIST_STAMPS") != nullptr;
+    if (stamps) {
+        TRY(grow(ctx, &ctx->pers_stamps, &ctx->pers_stamps_cap, (size_t)2 * kPersistMaxStamps + 2 * kBlock));
+        HIPCHK(hipMemsetAsync(ctx->pers_stamps, 0, sizeof(unsigned long long) * (2 * kPersistMaxStamps + 2 * kBlock), ctx->st));
+    }
+    TRY(grow(ctx, &ctx->pers_sync, &ctx->pers_sync_cap, kPersistSyncWords));
+    HIPCHK(hipMemsetAsync(ctx->pers_sync, 0, kPersistSyncWords * sizeof(unsigned), ctx->st));
+    ctx->h_flags[3] = 0; // abort word (mapped host)
+    PersistArgs a{};
+    a.img = ctx->pm_img;
+    a.nblk = (int)ctx->pm_blocks;
+    a.nm = (int)ctx->nm;
+    a.n = (int)n;
+    a.px = P.x;
+    a.py = P.y;
+    a.pz = P.z;
+    a.yx = Y.x;
+    a.yy = Y.y;
+    a.yz = Y.z;
+    a.p32 = P.f;
+    a.idx = ctx->idx;
+    a.part = ctx->pers_part;
+    a.sync = ctx->pers_sync;
+    a.h_abort = ctx->d_flags + 3;
+    a.N = (double)ctx->np_total;
+    a.c0 = ctx->c[0];
+    a.c1 = ctx->c[1];
+    a.c2 = ctx->c[2];
+    a.threshold = threshold;
+    a.max_iter = max_iter;
+    a.err_trace = ctx->err_trace_dev;
+    a.s_glob = ctx->iter_state;
+    a.h_state = ctx->d_iter_mirror;
+    a.h_trace = ctx->d_trace;
+    a.stamps = stamps ? ctx->pers_stamps : nullptr;
+    static const int cull = [] { // ICP_PERSIST_NN=all: every model point for every query (A/B)
+        const char *e = getenv("ICP_PERSIST_NN");
+        return e && std::strcmp(e, "all") == 0 ? 0 : 1;
+    }();
+    a.cull = cull;
+    for (int k = 0; k < 3; ++k) a.m0[k] = ctx->model_host[k];
+    launch_icp_persistent(a, grid, lds, ctx->st);
+    LAUNCHCHK("icp_persistent");
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (stamps) { // phase durations of workgroup 0 (tags: 0 NN begin, 1 NN end, 2 published,
+                  // 3 barrier passed, 8 partials loaded, 4 folded, 5 Horn done, 6 transformed, 7 end)
+        std::vector<unsigned long long> h(2 * kPersistMaxStamps + 2 * kBlock);
+        HIPCHK(hipMemcpy(h.data(), ctx->pers_stamps, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+        double acc[9] = {0}, cntp[9] = {0};
+        for (int k = 1; k < kPersistMaxStamps && h[2 * k + 1]; ++k) {
+            const int tag = (int)h[2 * k];
+            acc[tag] += (double)(h[2 * k + 1] - h[2 * k - 1]) * 0.01; // 100 MHz -> us
+            cntp[tag] += 1;
+        }
+        fprintf(stderr, "[persist] grid %d lds %zu: us ending at tag (calls):", grid, lds);
+        for (int t = 0; t < 9; ++t) fprintf(stderr, " %d:%.2f(%g)", t, acc[t], cntp[t]);
+        double nmin = 1e30, nmax = 0, nsum = 0, bmin = 1e30, bmax = 0, bsum = 0;
+        for (int w = 0; w < grid; ++w) {
+            const double tn = h[2 * kPersistMaxStamps + 2 * w] * 0.01, tb = h[2 * kPersistMaxStamps + 2 * w + 1] * 0.01;
+            nmin = std::min(nmin, tn), nmax = std::max(nmax, tn), nsum += tn;
+            bmin = std::min(bmin, tb), bmax = std::max(bmax, tb), bsum += tb;
+        }
+        fprintf(stderr, " | per-wg NN min/mean/max %.1f/%.1f/%.1f barrier %.1f/%.1f/%.1f us\n", nmin, nsum / grid, nmax,
+                bmin, bsum / grid, bmax);
+    }
+    if (__atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE) != 0)
+        return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the one-launch loop timed out (workgroups not co-resident)");
+    ctx->seeds_valid = true;
+    const int iters = ctx->h_iter->iter;
+    ctx->stats.nn_pairs += (long long)iters * (long long)n * (long long)ctx->nm;
+    ctx->stats.persistent_runs += 1;
+    return finish_run(ctx, threshold, err_trace, res, wall0);
+}
+
 // The loop of GPU::ICP::find_corresponding_opti (gpu.cc:52-83), device-resident: every
 // iteration is enqueued without waiting on the previous one -- NN search, moments and their
 // all-reduces, the Horn solve (horn_step, the host's own code), transform + residual and its
@@ -918,6 +1124,11 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         ctx->iter_ev.push_back(e);
+    }
+    {
+        size_t lds = 0;
+        const int grid = persistent_grid(ctx, n, max_iter, &lds);
+        if (grid) return run_persistent(ctx, grid, lds, max_iter, threshold, err_trace, res, wall0);
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     if (ctx->digest_cap) HIPCHK(hipMemsetAsync(ctx->digest, 0, sizeof(unsigned long long) * 3 * ctx->digest_cap, ctx->st));
@@ -1038,7 +1249,14 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         stop = done != 0;
     }
     HIPCHK(hipStreamSynchronize(ctx->st)); // (the iterations queued behind the last one drain)
-    const IterState &hs = *ctx->h_iter;    // mirrored by the last recorded err_step
+    return finish_run(ctx, threshold, err_trace, res, wall0);
+}
+
+// The run's result from the mapped host mirror of the last recorded iteration (both loops).
+static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_result *res,
+                      std::chrono::steady_clock::time_point wall0)
+{
+    const IterState &hs = *ctx->h_iter; // mirrored by the last recorded err step
     icp_result r{};
     r.iterations = hs.iter;
     r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55) when no iteration ran

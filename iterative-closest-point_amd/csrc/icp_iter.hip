@@ -150,7 +150,539 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_small_kernel(
     if (threadIdx.x == 0) err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
 }
 
+// ---- a whole small registration in ONE launch --------------------------------------------------
+//
+// For a single-rank run of n <= kRedSingle scene points against a model that fits in LDS, the
+// classic loop is ~8 dependent launches per iteration (NN cascade, fused tail), each paying the
+// ~4-5 us launch floor for a few us of work.  This kernel runs the whole of icp_run instead:
+// G co-resident workgroups (one or two per CU), every one holding the model in LDS.
+//
+// Work split.  The classic single-workgroup passes (gather/centred/shifted moments, transform +
+// residual, each launched with one 256-thread workgroup for n <= kRedSingle) have thread t sum
+// the points t, t + 256, ... in order, then fold the 256 per-thread partials with
+// block_sum_store.  Here those 256 threads are VIRTUAL: workgroup b owns the virtual threads
+// v = b, b + G, ... and with them exactly their points.  It computes each owned virtual thread's
+// partial in the same order, publishes it, and after a grid barrier every workgroup folds the
+// 256 published partials with the same block_sum_store tree.  Every sum, hence every Horn solve,
+// transform and error, is therefore BIT-IDENTICAL to the launch-per-step loop, in every
+// workgroup (the Horn step runs redundantly in each, on identical sums).
+//
+// NN.  Each owned query scans the LDS model in fp64 in the reference's order (compute.cu:112-117)
+// and takes the lexicographic (D64, index) minimum -- the first minimum, the rule every NN path
+// returns (nn_exact_few_kernel's scan), so no certificate is needed.
+//
+// Per iteration: NN + moments of the owned points, ONE grid barrier (publish 17 sums + the
+// previous iteration's residual, fold), Horn, transform.  The error of iteration i is known at
+// iteration i+1's barrier, where the err test of gpu.cc:76-80 runs; if it stops the loop, the
+// state is the one after iteration i's transform (iteration i+1's NN results are never
+// committed), exactly where the reference breaks.  The first iteration takes the reference's
+// two passes (two barriers); after the last iteration one more barrier exchanges its residual.
+//
+// Hand-off (guide §6 Guideline 16, R1): partials are stored write-through (relaxed agent-scope
+// atomic stores = sc1), every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup
+// barrier, lane 0 adds to a monotonic arrival counter, polls it relaxed with s_sleep, and every
+// load of a partial is an agent-scope atomic load (sc1).  The partial buffer alternates with the
+// barrier's parity: a workgroup can publish barrier e+2's partials only after every workgroup
+// has arrived at e+1, i.e. finished reading e's.  Spins are bounded: a timeout (workgroups not
+// co-resident) sets an abort word that every waiting workgroup sees, and icp_run reports it.
+
+constexpr int kPersistVT = kBlock;  // virtual threads (the single-workgroup passes' threads)
+constexpr int kPersistMaxOwn = 64;  // owned points per workgroup (G >= 64, n <= kRedSingle)
+constexpr int kPersistK = kNumSums; // widest published partial: 17 moments + 1 residual
+constexpr unsigned kPersistSpinLimit = 1u << 20; // polls (~1 us each) before a barrier gives up
+
+static_assert(kRedSingle / kPersistVT * (kPersistVT / 64) <= kPersistMaxOwn, "owned points per workgroup");
+
+__device__ __forceinline__ void pub_store(double *p, double v)
+{
+    __hip_atomic_store((unsigned long long *)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid barrier number `e` (1-based); false if it timed out or another workgroup aborted.
+// Every thread calls it after its own payload stores.  Two-level arrival: workgroup b counts
+// into group b % 8 (a label: which workgroups share an XCD under the usual round-robin
+// dispatch; correctness does not depend on it), the last arrival of a group into the top
+// counter, and the last group releases every group's generation word, which the group's
+// workgroups poll (32 pollers per word instead of 256 on one counter).  All words are
+// agent-scope atomics (sc1), monotonic within the launch, zeroed before it.
+//   sync[0] top counter   sync[1] abort word   sync[kSyncGrp + 16 g] group g's counter
+//   sync[kSyncGen + 16 g] group g's generation (one 64-byte line each)
+constexpr int kSyncGroups = 8, kSyncGrp = 16, kSyncGen = kSyncGrp + 16 * kSyncGroups;
+__device__ bool persist_barrier(unsigned *sync, unsigned e, int *h_abort, int *s_ok)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned G = gridDim.x, b = blockIdx.x, g = b % kSyncGroups;
+        const unsigned ng = G < kSyncGroups ? G : kSyncGroups;
+        const unsigned gs = (G - g + kSyncGroups - 1) / kSyncGroups; // workgroups in group g
+        const unsigned old = __hip_atomic_fetch_add(sync + kSyncGrp + 16 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == gs * e) { // the group's last arrival
+            const unsigned top = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (top + 1 == ng * e) // the last group: release all
+                for (unsigned h = 0; h < ng; ++h)
+                    __hip_atomic_store(sync + kSyncGen + 16 * h, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        int ok = 1;
+        for (unsigned spin = 1; __hip_atomic_load(sync + kSyncGen + 16 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e;
+             ++spin) {
+            if ((spin & 63u) == 0u &&
+                (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || spin > kPersistSpinLimit)) {
+                ok = 0;
+                __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(h_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// block_sum_store<K>'s result, bit for bit, with cheaper cross-lane moves: its shuffle-down
+// tree needs, at each level, lane l's partner l + off only for the lanes that feed lane 0
+// (l < off), so off = 32 takes a bpermute, off = 16 a ds_swizzle (xor 16 within 32 lanes) and
+// off = 8..1 DPP row shifts (partners in the same 16-lane row).  Float addition is
+// commutative, so each pair sums the same two values as the shuffle tree.
+template <int OFF> __device__ __forceinline__ int lane_down(int v)
+{
+    if constexpr (OFF == 32) return __builtin_amdgcn_ds_bpermute((int)((threadIdx.x & 63) + 32) << 2, v);
+    else if constexpr (OFF == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);
+    else return __builtin_amdgcn_update_dpp(0, v, 0x100 | OFF, 0xF, 0xF, true);
+}
+template <int OFF> __device__ __forceinline__ double lane_down_d(double v)
+{
+    const long long x = __double_as_longlong(v);
+    const int lo = lane_down<OFF>((int)(unsigned)x), hi = lane_down<OFF>((int)(x >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int K> __device__ __forceinline__ void persist_block_sum(double (&a)[K], double *out)
+{
+    __shared__ double sh[kBlock / 64][K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += lane_down_d<32>(a[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += lane_down_d<16>(a[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += lane_down_d<8>(a[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += lane_down_d<4>(a[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += lane_down_d<2>(a[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] += lane_down_d<1>(a[k]);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
+    }
+}
+
+// In-kernel phase stamps (ICP_PERSIST_STAMPS=1): workgroup 0, thread 0, the 100 MHz realtime
+// counter at each phase boundary.
+__device__ __forceinline__ void persist_stamp(unsigned long long *stamps, int &ns, int tag)
+{
+    if (stamps && blockIdx.x == 0 && threadIdx.x == 0 && ns < kPersistMaxStamps) {
+        stamps[2 * ns] = (unsigned long long)tag;
+        stamps[2 * ns + 1] = __builtin_amdgcn_s_memrealtime();
+        ++ns;
+    }
+}
+
+// Fold the 256 published partials (row t = virtual thread t, kPersistK doubles, 144 B) with
+// block_sum_store<K>'s tree.  Thread t reads its row with 16-byte write-through-coherent (sc1)
+// buffer loads: every load of handed-off bytes bypasses this CU's L1 (Guideline 16, R1).
+template <int K>
+__device__ __forceinline__ void persist_fold(const double *part, double *sums, unsigned long long *stamps, int &ns)
+{
+    static_assert(kPersistK % 2 == 0, "rows are whole 16-byte granules");
+    constexpr int kGranules = (K + 1) / 2;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)part, (short)0, (int)(kPersistVT * kPersistK * sizeof(double)), 0x00020000);
+    const int base = (int)(threadIdx.x * kPersistK * sizeof(double));
+    double acc[2 * kGranules];
+#pragma unroll
+    for (int g = 0; g < kGranules; ++g) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, base + 16 * g, 0, 16 /* sc1 */);
+        acc[2 * g] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+        acc[2 * g + 1] = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
+    }
+    persist_stamp(stamps, ns, 8);
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = acc[k];
+    persist_block_sum<K>(a, sums);
+}
+
+__global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
+{
+    // the Morton-ordered model image (persist_model_image): x[nm] | y[nm] | z[nm] | boxes
+    extern __shared__ __attribute__((aligned(16))) double s_model[];
+    __shared__ double own_p[3][kPersistMaxOwn], own_y[3][kPersistMaxOwn], own_r[kPersistMaxOwn];
+    __shared__ double e_part[kPersistMaxOwn / 16];
+    __shared__ double sums[kPersistK];
+    __shared__ int own_i[kPersistMaxOwn], own_k[kPersistMaxOwn];
+    __shared__ int v_start[kPersistVT / 64 + 1];
+    __shared__ IterState st;
+    __shared__ int cnt[4];
+    __shared__ int s_ok;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int G = gridDim.x, b = blockIdx.x;
+    const int nm = a.nm, n = a.n;
+    const int nblk = a.nblk;
+    double *mxs = s_model, *mys = s_model + nm, *mzs = s_model + 2 * nm, *boxes = s_model + 3 * nm;
+    const int *orig = (const int *)(a.img + 3 * nm + 6 * nblk); // original index per sorted position
+    const int nv = (kPersistVT - b + G - 1) / G; // owned virtual threads v = b + lv G
+    for (int k = tid; k < 3 * nm + 6 * nblk; k += kBlock) s_model[k] = a.img[k];
+    if (tid == 0) {
+        int q = 0;
+        for (int lv = 0; lv < nv; ++lv) {
+            v_start[lv] = q;
+            for (int i = b + lv * G; i < n; i += kPersistVT) own_i[q++] = i;
+        }
+        v_start[nv] = q;
+        for (size_t w = 0; w < sizeof(IterState) / sizeof(int); ++w) ((int *)&st)[w] = 0;
+        for (int k = 0; k < 4; ++k) cnt[k] = 0;
+    }
+    __syncthreads();
+    const int nown = v_start[nv];
+    for (int q = tid; q < nown; q += kBlock) {
+        const int i = own_i[q];
+        own_p[0][q] = a.px[i];
+        own_p[1][q] = a.py[i];
+        own_p[2][q] = a.pz[i];
+    }
+    __syncthreads();
+
+    unsigned epoch = 0;
+    int nstamp = 0;
+    unsigned long long wg_nn = 0, wg_bar = 0; // this workgroup's NN / barrier-wait time (stamps)
+    persist_stamp(a.stamps, nstamp, 0);
+    // thread (lv, k): the k-th sum of owned virtual thread lv (k < 32, lv < nv)
+    const int my_lv = tid >> 5, my_k = tid & 31;
+    const bool summer = my_lv < nv;
+    const int my_v = b + my_lv * G;
+    double *const part0 = a.part, *const part1 = a.part + (size_t)kPersistVT * kPersistK;
+
+    // publish K values per owned virtual thread (produced by `term`), barrier, fold into sums[0..K)
+    // The k-th sum of owned virtual thread lv over its points, in point order, with the
+    // classic passes' per-point arithmetic: kind 0/1 adds (X_a - c_a), kind 2 adds
+    // (P_a - cp_a)(Y_b - cy_b), kind 3/4 adds ((X0-c0)^2 + (X1-c1)^2) + (X2-c2)^2 (X = Y for
+    // 3, P for 4).  The operands of all (<= 16) points are read from LDS first.
+    auto pick = [](int i, double x0, double x1, double x2) { return i == 0 ? x0 : i == 1 ? x1 : x2; };
+    auto vsum = [&](int lv, int kind, int ia, int ib, const double (&cp)[3], const double (&cy)[3]) -> double {
+        const int q0 = v_start[lv], cnt = v_start[lv + 1] - q0;
+        const double *ra = kind == 1 ? own_y[ia] : kind == 3 ? own_y[0] : own_p[kind == 4 ? 0 : ia];
+        const double *rb = kind == 2 ? own_y[ib] : kind == 3 ? own_y[1] : own_p[1];
+        const double *rc = kind == 3 ? own_y[2] : own_p[2];
+        // (centres by selection, not by a runtime index into a register array)
+        const double ca = kind == 1 ? pick(ia, cy[0], cy[1], cy[2])
+                          : kind == 3 ? cy[0] : pick(kind == 4 ? 0 : ia, cp[0], cp[1], cp[2]);
+        const double cb = kind == 2 ? pick(ib, cy[0], cy[1], cy[2]) : kind == 3 ? cy[1] : cp[1];
+        const double cc = kind == 3 ? cy[2] : cp[2];
+        constexpr int kMaxPts = kRedSingle / kPersistVT;
+        double A[kMaxPts], B[kMaxPts], C[kMaxPts];
+#pragma unroll
+        for (int r = 0; r < kMaxPts; ++r) {
+            const int q = q0 + min(r, max(cnt - 1, 0));
+            A[r] = ra[q];
+            B[r] = kind >= 2 ? rb[q] : 0.0;
+            C[r] = kind >= 3 ? rc[q] : 0.0;
+        }
+        double acc = 0.0;
+        if (kind <= 1) {
+#pragma unroll
+            for (int r = 0; r < kMaxPts; ++r)
+                if (r < cnt) acc += A[r] - ca;
+        } else if (kind == 2) {
+#pragma unroll
+            for (int r = 0; r < kMaxPts; ++r)
+                if (r < cnt) acc += (A[r] - ca) * (B[r] - cb);
+        } else {
+#pragma unroll
+            for (int r = 0; r < kMaxPts; ++r)
+                if (r < cnt) {
+                    const double x0 = A[r] - ca, x1 = B[r] - cb, x2 = C[r] - cc;
+                    acc += (x0 * x0 + x1 * x1) + x2 * x2;
+                }
+        }
+        return acc;
+    };
+
+    auto exchange = [&](int K, auto &&term) -> bool {
+        double *part = (epoch & 1u) ? part1 : part0;
+        if (summer && my_k < K) pub_store(part + (size_t)my_v * kPersistK + my_k, term(my_lv, my_k));
+        ++epoch;
+        persist_stamp(a.stamps, nstamp, 2);
+        const unsigned long long t_bar = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        if (!persist_barrier(a.sync, epoch, a.h_abort, &s_ok)) return false;
+        if (a.stamps && tid == 0) wg_bar += __builtin_amdgcn_s_memrealtime() - t_bar;
+        persist_stamp(a.stamps, nstamp, 3);
+        switch (K) { // per column: the classic pass's block_sum_store<K> tree
+        case 1: persist_fold<1>(part, sums, a.stamps, nstamp); break;
+        case 6: persist_fold<6>(part, sums, a.stamps, nstamp); break;
+        case 11: persist_fold<11>(part, sums, a.stamps, nstamp); break;
+        default: persist_fold<kPersistK>(part, sums, a.stamps, nstamp); break;
+        }
+        __syncthreads();
+        persist_stamp(a.stamps, nstamp, 4);
+        return true;
+    };
+
+    // NN of the owned queries, exact first minimum.  Wave w takes a contiguous share of them, 4
+    // at a time.  A query's seed distance r2 is its distance to the previous iteration's
+    // correspondence (own_y; +inf in the first iteration): every model point at least as close
+    // lies in a 64-point block whose box is within r2 (conservatively: r2 (1 + 2^-40) + 2^-900
+    // covers the rounding of both fp64 evaluations), and the seed itself is one of them, so the
+    // lexicographic (D64, original index) minimum over those blocks is the global one.  Lanes
+    // hold one point of each scanned block (sorted position k = 64 b + lane); a tie of D64
+    // compares original indices (global reads, rare).  Distances follow compute.cu:112-117.
+    auto nn_owned = [&](bool seeded) {
+        const int per = (nown + 3) >> 2;
+        const int q_lo = wave * per, q_hi = min(nown, q_lo + per);
+        for (int q0 = q_lo; q0 < q_hi; q0 += 4) {
+            double qx[4], qy[4], qz[4], bd[4];
+            int bk[4];
+            unsigned long long mlo[4], mhi[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = min(q0 + u, q_hi - 1);
+                qx[u] = own_p[0][q];
+                qy[u] = own_p[1][q];
+                qz[u] = own_p[2][q];
+                bd[u] = INFINITY;
+                bk[u] = 0x7fffffff;
+                auto box_d2 = [&](int j) { // squared distance from the query to block j's box
+                    if (j >= nblk) return (double)INFINITY;
+                    const double *bx = boxes + 6 * j;
+                    const double ex = fmax(bx[0] - qx[u], qx[u] - bx[3]), ey = fmax(bx[1] - qy[u], qy[u] - bx[4]),
+                                 ez = fmax(bx[2] - qz[u], qz[u] - bx[5]);
+                    const double fx = ex > 0.0 ? ex : 0.0, fy = ey > 0.0 ? ey : 0.0, fz = ez > 0.0 ? ez : 0.0;
+                    return (fx * fx + fy * fy) + fz * fz;
+                };
+                const double b0 = box_d2(lane), b1 = box_d2(lane + 64);
+                double r2 = INFINITY;
+                if (seeded) { // the previous correspondence
+                    const double dx = qx[u] - own_y[0][q], dy = qy[u] - own_y[1][q], dz = qz[u] - own_y[2][q];
+                    r2 = (dx * dx + dy * dy) + dz * dz;
+                } else { // the nearest point of the block with the nearest box
+                    double bb = fmin(b0, b1);
+                    int jb = b1 < b0 ? lane + 64 : lane;
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        const double ob = __shfl_xor(bb, o, 64);
+                        const int oj = __shfl_xor(jb, o, 64);
+                        const bool t = (ob < bb) | ((ob == bb) & (oj < jb));
+                        bb = t ? ob : bb;
+                        jb = t ? oj : jb;
+                    }
+                    const int k = min(64 * jb + lane, nm - 1); // (a valid point of block jb or of the last)
+                    const double dx = qx[u] - mxs[k], dy = qy[u] - mys[k], dz = qz[u] - mzs[k];
+                    r2 = (dx * dx + dy * dy) + dz * dz;
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) r2 = fmin(r2, __shfl_xor(r2, o, 64)); // (NaN only if all are)
+                }
+                if (!a.cull) r2 = INFINITY;
+                // every point with D64 <= r2 lies in a block whose box is within r2; the bound covers
+                // the rounding of both fp64 evaluations (+inf stays +inf, NaN stays NaN: no block)
+                const double lim = r2 * (1.0 + 0x1p-40) + 0x1p-900;
+                mlo[u] = __ballot(b0 <= lim);
+                mhi[u] = __ballot(b1 <= lim);
+            }
+            for (int half = 0; half < 2; ++half) {
+                unsigned long long all = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) all |= half ? mhi[u] : mlo[u];
+                while (all) { // wave-uniform: one scanned block per trip
+                    const int blk = __ffsll((long long)all) - 1 + 64 * half;
+                    all &= all - 1;
+                    const int k = 64 * blk + lane;
+                    const bool valid = k < nm;
+                    const int kk = valid ? k : nm - 1;
+                    const double mx = mxs[kk], my = mys[kk], mz = mzs[kk];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (!(((half ? mhi[u] : mlo[u]) >> (blk - 64 * half)) & 1ull)) continue; // (uniform)
+                        const double dx = qx[u] - mx, dy = qy[u] - my, dz = qz[u] - mz;
+                        const double e = (dx * dx + dy * dy) + dz * dz;
+                        bool take = valid & (e < bd[u]);
+                        if (valid & (e == bd[u]) & (bd[u] < INFINITY)) // a tie: the lower original index
+                            take = orig[min(k, nm - 1)] < orig[min(bk[u], nm - 1)];
+                        bd[u] = take ? e : bd[u];
+                        bk[u] = take ? k : bk[u];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int bo = bk[u] == 0x7fffffff ? 0x7fffffff : orig[min(bk[u], nm - 1)];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const double od = __shfl_xor(bd[u], o, 64);
+                    const int oo = __shfl_xor(bo, o, 64), ok = __shfl_xor(bk[u], o, 64);
+                    const bool take = (od < bd[u]) | ((od == bd[u]) & (oo < bo)); // (no short circuit: selects)
+                    bd[u] = take ? od : bd[u];
+                    bo = take ? oo : bo;
+                    bk[u] = take ? ok : bk[u];
+                }
+                if (lane == 0 && q0 + u < q_hi) {
+                    const int q = q0 + u;
+                    if (bo == 0x7fffffff) { // no comparison held (a NaN query): index 0, as the reference's scan
+                        own_k[q] = 0;
+                        own_y[0][q] = a.m0[0];
+                        own_y[1][q] = a.m0[1];
+                        own_y[2][q] = a.m0[2];
+                    } else {
+                        own_k[q] = bo;
+                        own_y[0][q] = mxs[bk[u]];
+                        own_y[1][q] = mys[bk[u]];
+                        own_y[2][q] = mzs[bk[u]];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    };
+
+    auto err_step = [&](double e) { // gpu.cc:71-80 (err_step_body), on this workgroup's state
+        if (tid == 0) {
+            const double err = (e + e) / a.N;
+            if (b == 0) {
+                a.err_trace[st.iter] = err;
+                a.h_trace[st.iter] = err;
+            }
+            st.iter += 1;
+            if (err < a.threshold || st.iter >= a.max_iter) st.done = 1;
+            if (b == 0) {
+                const int *src = (const int *)&st;
+                int *dst = (int *)a.h_state;
+                for (size_t k = 0; k < sizeof(IterState) / sizeof(int); ++k) dst[k] = src[k];
+            }
+        }
+        __syncthreads();
+    };
+
+    for (int it = 0;; ++it) {
+        persist_stamp(a.stamps, nstamp, 0);
+        const unsigned long long t_nn = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        nn_owned(it > 0);
+        if (a.stamps && tid == 0) wg_nn += __builtin_amdgcn_s_memrealtime() - t_nn;
+        persist_stamp(a.stamps, nstamp, 1);
+        if (it == 0) {
+            // gather_moments_kernel: sum p, sum y
+            const double zero[3] = {0.0, 0.0, 0.0}; // (x - 0.0 == x: the raw sums of gather_moments)
+            if (!exchange(6, [&](int lv, int k) { return vsum(lv, k < 3 ? 0 : 1, k < 3 ? k : k - 3, 0, zero, zero); }))
+                return;
+            const double mp[3] = {sums[kSumP] / a.N, sums[kSumP + 1] / a.N, sums[kSumP + 2] / a.N};
+            const double my[3] = {sums[kSumY] / a.N, sums[kSumY + 1] / a.N, sums[kSumY + 2] / a.N};
+            double keep[6];
+            for (int k = 0; k < 6; ++k) keep[k] = sums[k];
+            __syncthreads(); // (sums is rewritten by the next exchange)
+            // centred_moments_kernel: S, d_caps, sp around the means
+            if (!exchange(11, [&](int lv, int k) {
+                    return k < 9 ? vsum(lv, 2, k / 3, k % 3, mp, my) : vsum(lv, k == 9 ? 3 : 4, 0, 0, mp, my);
+                }))
+                return;
+            double S11[11];
+            for (int k = 0; k < 11; ++k) S11[k] = sums[k];
+            __syncthreads();
+            if (tid < 6) sums[tid] = keep[tid];
+            if (tid < 11) sums[kSumS + tid] = S11[tid];
+            __syncthreads();
+            if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 0, cnt, &st);
+        } else {
+            // shifted_moments_kernel + the previous iteration's residual (column 17)
+            const double cp[3] = {st.shift_p[0], st.shift_p[1], st.shift_p[2]};
+            const double cy[3] = {st.shift_y[0], st.shift_y[1], st.shift_y[2]};
+            if (!exchange(kPersistK, [&](int lv, int k) {
+                    if (k == kNumSums - 1) return e_part[lv];
+                    return k < 3    ? vsum(lv, 0, k, 0, cp, cy)
+                           : k < 6  ? vsum(lv, 1, k - 3, 0, cp, cy)
+                           : k < 15 ? vsum(lv, 2, (k - 6) / 3, (k - 6) % 3, cp, cy)
+                                    : vsum(lv, k == 15 ? 3 : 4, 0, 0, cp, cy);
+                }))
+                return;
+            err_step(sums[kNumSums - 1]); // iteration it-1's error (gpu.cc:76-80)
+            if (st.done) break;           // this iteration's NN is never committed
+            if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 1, cnt, &st);
+        }
+        __syncthreads();
+        persist_stamp(a.stamps, nstamp, 5);
+        // the iteration counts: its correspondences, then apply + residual (transform_err_kernel)
+        const Xform xf = st.xf;
+        for (int q = tid; q < nown; q += kBlock) {
+            const int i = own_i[q];
+            a.idx[i] = own_k[q];
+            a.yx[i] = own_y[0][q];
+            a.yy[i] = own_y[1][q];
+            a.yz[i] = own_y[2][q];
+            double q0, q1, q2;
+            transform_point(xf, own_p[0][q], own_p[1][q], own_p[2][q], q0, q1, q2);
+            own_r[q] = residual2(own_y[0][q], own_y[1][q], own_y[2][q], q0, q1, q2);
+            own_p[0][q] = q0;
+            own_p[1][q] = q1;
+            own_p[2][q] = q2;
+            a.px[i] = q0;
+            a.py[i] = q1;
+            a.pz[i] = q2;
+            if (a.p32) a.p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
+        }
+        __syncthreads();
+        if (tid < nv) {
+            double e = 0.0;
+            for (int q = v_start[tid]; q < v_start[tid + 1]; ++q) e += own_r[q];
+            e_part[tid] = e;
+        }
+        __syncthreads();
+        persist_stamp(a.stamps, nstamp, 6);
+        if (it + 1 == a.max_iter) { // the last residual: one more exchange
+            if (!exchange(1, [&](int lv, int) { return e_part[lv]; })) return;
+            err_step(sums[0]);
+            break;
+        }
+    }
+    persist_stamp(a.stamps, nstamp, 7);
+    if (a.stamps && tid == 0) { // per-workgroup totals after workgroup 0's phase stamps
+        a.stamps[2 * kPersistMaxStamps + 2 * b] = wg_nn;
+        a.stamps[2 * kPersistMaxStamps + 2 * b + 1] = wg_bar;
+    }
+    if (b == 0 && tid == 0) *a.s_glob = st;
+}
+
 } // namespace
+
+size_t persistent_static_lds()
+{
+    static const size_t bytes = [] {
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, (const void *)icp_persistent_kernel) != hipSuccess) {
+            (void)hipGetLastError();
+            return (size_t)16 * 1024; // (conservative)
+        }
+        return (size_t)fa.sharedSizeBytes;
+    }();
+    return bytes;
+}
+
+void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st)
+{
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void *)icp_persistent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kPersistLdsMax);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)attr;
+    icp_persistent_kernel<<<grid, kBlock, lds_bytes, st>>>(args);
+}
 
 void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,
                       IterState *st_dev, hipStream_t st)

@@ -124,9 +124,10 @@ void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *
 // fp64 brute force: partial (best d64, argbest) per (split, query), then merge.
 void launch_nn_fp64(const double *px, const double *py, const double *pz, int np,
                     const double *mx, const double *my, const double *mz, int nm,
-                    const NNPlan &plan, double *part_best, int *part_idx, hipStream_t st);
+                    const NNPlan &plan, double *part_best, int *part_idx, hipStream_t st,
+                    const int *stop = nullptr);
 void launch_nn_finalize64(const double *part_best, const int *part_idx, int splits, int np,
-                          int *idx, hipStream_t st);
+                          int *idx, hipStream_t st, const int *stop = nullptr);
 
 // ---- uniform grid over the model: exact resolver of queued queries (icp_grid.hip) ---
 constexpr long long kGridMaxCells = 1LL << 24;
@@ -269,6 +270,37 @@ void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, 
                                  const double c[3], int *amb_count, IterState *st_dev, double threshold,
                                  int max_iter, double *err_trace, int *hflag_dev, int ticket,
                                  IterState *h_state_dev, double *h_trace_dev, hipStream_t st);
+// A whole icp_run of a small single-rank registration in ONE launch (icp_iter.hip): `grid`
+// co-resident workgroups, the model in LDS (lds_bytes = 24 nm), one grid barrier per iteration;
+// bit-identical to the launch-per-step loop.  sync[0..1] (arrival counter, abort word) must be
+// zero at launch; *h_abort (mapped host) is set if a barrier timed out.
+constexpr size_t kPersistLdsMax = 160 * 1024 - 12 * 1024; // dynamic LDS (the statics take ~9 KiB)
+constexpr int kPersistMaxModel = (int)(kPersistLdsMax / 24);
+struct PersistArgs {
+    const double *img; // persist_model_image: Morton-ordered model, block boxes, original indices
+    int nblk, nm, n;
+    double *px, *py, *pz, *yx, *yy, *yz;
+    float4 *p32;
+    int *idx;
+    double *part;   // 2 x kBlock x kNumSums (alternating with the barrier's parity)
+    unsigned *sync; // kPersistSyncWords barrier words: top counter, abort word, per-group lines
+    int *h_abort;
+    double N, c0, c1, c2, threshold;
+    int max_iter;
+    double *err_trace; // device trace
+    IterState *s_glob; // the run's final state
+    IterState *h_state; // mapped host mirror of the last recorded iteration
+    double *h_trace;    // mapped host trace
+    unsigned long long *stamps; // nullable: (tag, realtime) pairs of workgroup 0's phases
+    int cull;                   // 1: scan only the blocks within the seed distance (0: all)
+    double m0[3];               // model point 0 (a NaN query's correspondence)
+};
+constexpr int kPersistMaxStamps = 1024;
+constexpr int kPersistSyncWords = 512; // barrier words (icp_iter.hip: persist_barrier)
+void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st);
+size_t persistent_static_lds(); // the kernel's static LDS bytes
+// (host) the kernel's model image; *blocks_out = 64-point blocks (icp_engine.hip)
+std::vector<double> persist_model_image(const double *m_xyz, size_t nm, size_t *blocks_out);
 // zero a run's IterState and the NN queue counters (amb_count[0..3])
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st);
 

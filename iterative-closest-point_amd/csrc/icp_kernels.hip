@@ -1543,9 +1543,10 @@ __global__ __launch_bounds__(kBlock) void nn_fp64_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     int np, const double *__restrict__ mx, const double *__restrict__ my,
     const double *__restrict__ mz, int nm, int chunk, double *__restrict__ part_best,
-    int *__restrict__ part_idx)
+    int *__restrict__ part_idx, const int *__restrict__ stop)
 {
     __shared__ D4 tile[kTile64];
+    if (stop && *stop) return; // an ICP iteration queued behind the converged one
     const int tid = threadIdx.x;
     const int split = blockIdx.y;
     const int m0 = split * chunk;
@@ -1615,8 +1616,10 @@ __global__ __launch_bounds__(kBlock) void nn_fp64_kernel(
 __global__ __launch_bounds__(kBlock) void nn_finalize64_kernel(const double *__restrict__ part_best,
                                                                const int *__restrict__ part_idx,
                                                                int splits, int np,
-                                                               int *__restrict__ idx)
+                                                               int *__restrict__ idx,
+                                                               const int *__restrict__ stop)
 {
+    if (stop && *stop) return; // (idx keeps the last counted iteration's correspondences)
     const int j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= np) return;
     double b = part_best[j];
@@ -2213,22 +2216,22 @@ void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm,
 
 void launch_nn_fp64(const double *px, const double *py, const double *pz, int np, const double *mx,
                     const double *my, const double *mz, int nm, const NNPlan &pl,
-                    double *part_best, int *part_idx, hipStream_t st)
+                    double *part_best, int *part_idx, hipStream_t st, const int *stop)
 {
     dim3 grid(pl.qblocks, pl.splits);
     if (pl.q_per_lane == 2)
         nn_fp64_kernel<2><<<grid, kBlock, 0, st>>>(px, py, pz, np, mx, my, mz, nm, pl.chunk,
-                                                   part_best, part_idx);
+                                                   part_best, part_idx, stop);
     else
         nn_fp64_kernel<1><<<grid, kBlock, 0, st>>>(px, py, pz, np, mx, my, mz, nm, pl.chunk,
-                                                   part_best, part_idx);
+                                                   part_best, part_idx, stop);
 }
 
 void launch_nn_finalize64(const double *part_best, const int *part_idx, int splits, int np,
-                          int *idx, hipStream_t st)
+                          int *idx, hipStream_t st, const int *stop)
 {
     nn_finalize64_kernel<<<(np + kBlock - 1) / kBlock, kBlock, 0, st>>>(part_best, part_idx,
-                                                                         splits, np, idx);
+                                                                         splits, np, idx, stop);
 }
 
 // up to kRedSingle points one workgroup does the whole pass (and writes the final sums

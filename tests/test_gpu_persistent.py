@@ -1,0 +1,164 @@
+"""The one-launch registration of small clouds (icp_set_run_mode, launch_icp_persistent).
+
+For a single-rank icp_run of n <= 4096 scene points against a model that fits in LDS, the
+engine runs the whole loop of GPU::ICP::find_corresponding_opti (src/GPU/gpu.cc:52-83) as ONE
+launch of co-resident workgroups with one grid barrier per iteration.  Its sums are built from
+the same per-thread partials and the same fold tree as the launch-per-step loop, so the two
+must agree BIT FOR BIT: error trace, (s, R, t), final cloud and correspondences -- on the
+bundled cow pair (converging and threshold-free runs), on random pairs whose sizes straddle
+the single-workgroup pass boundaries (4, 255, 256, 257, ..., 4096 points; models from 1 to
+6,000 points), with a NaN scene point, and in both NN modes.  The oracle trajectory is checked
+too (rtol 1e-9, tests/golden/traces.json).
+"""
+import numpy as np
+import pytest
+
+import datasets
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def amd(icp_lib):
+    if icp_lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    return icp_lib
+
+
+def run(amd, m, p, mode, iters, threshold=1e-5, nn_mode=0, variant=0):
+    with amd.Context(0, nn_mode) as ctx:
+        ctx.set_nn_variant(variant)
+        ctx.set_run_mode(mode)
+        ctx.set_allow_unequal(m.shape[0] != p.shape[0])
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        res, errs = ctx.run(iters, threshold)
+        out = (res.iterations, res.converged, res.err, res.s, tuple(res.R), tuple(res.t), errs,
+               ctx.get_scene(), ctx.get_indices(), ctx.stats()["persistent_runs"])
+    return out
+
+
+def assert_same(a, b):
+    assert a[:6] == b[:6] or (np.isnan(a[2]) and np.isnan(b[2])), (a[:6], b[:6])
+    np.testing.assert_array_equal(a[6], b[6])
+    np.testing.assert_array_equal(a[7], b[7])
+    np.testing.assert_array_equal(a[8], b[8])
+
+
+@pytest.mark.parametrize("scene,iters,threshold", [("cow_tr1", 20, 1e-5), ("cow_tr2", 20, 1e-5),
+                                                   ("cow_tr1", 1, -1.0), ("cow_tr1", 2, -1.0),
+                                                   ("cow_tr2", 15, -1.0)])
+@pytest.mark.parametrize("nn_mode", [0, 1])
+def test_cow_one_launch_matches_launch_loop(amd, golden, scene, iters, threshold, nn_mode):
+    m = amd.load_matrix(datasets.path("cow_ref"))
+    p = amd.load_matrix(datasets.path(scene))
+    one = run(amd, m, p, amd.RUN_PERSISTENT, iters, threshold, nn_mode)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, iters, threshold, nn_mode)
+    auto = run(amd, m, p, amd.RUN_AUTO, iters, threshold, nn_mode)
+    assert one[9] == 1 and loop[9] == 0 and auto[9] == 1  # the default takes the one launch
+    assert_same(one, loop)
+    assert_same(auto, loop)
+    if threshold > 0:
+        g = golden[scene]
+        assert one[0] == g["iterations"]
+        np.testing.assert_allclose(one[6], g["err"], rtol=1e-9)
+
+
+SIZES = [(4, 4), (7, 1), (100, 3000), (255, 255), (256, 256), (257, 600), (1000, 1000),
+         (2903, 50), (3000, 6000), (4095, 4096), (4096, 4096)]
+
+
+@pytest.mark.parametrize("n,nm", SIZES)
+def test_random_sizes_bitwise(amd, n, nm):
+    rng = np.random.default_rng(n * 7919 + nm)
+    m = rng.uniform(-1, 1, size=(nm, 3))
+    a = rng.uniform(0.05, 0.3)
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    k = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    rot = np.eye(3) + np.sin(a) * k + (1 - np.cos(a)) * k @ k
+    p = m[rng.integers(0, nm, n)] @ rot.T + rng.normal(scale=0.05, size=3) + rng.normal(scale=0.01, size=(n, 3))
+    one = run(amd, m, p, amd.RUN_PERSISTENT, 6, -1.0)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 6, -1.0)
+    assert one[9] == 1 and loop[9] == 0
+    assert one[0] == 6
+    assert_same(one, loop)
+
+
+def test_nan_scene_point(amd):
+    rng = np.random.default_rng(3)
+    m = rng.uniform(-1, 1, size=(500, 3))
+    p = m + 0.01
+    p[17, 1] = np.nan
+    one = run(amd, m, p, amd.RUN_PERSISTENT, 3, -1.0)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 3, -1.0)
+    assert one[9] == 1
+    assert one[8][17] == 0  # a NaN query's correspondence is index 0 (the reference's scan)
+    assert one[0] == loop[0] == 3
+    np.testing.assert_array_equal(one[6], loop[6])
+    np.testing.assert_array_equal(one[7], loop[7])
+    np.testing.assert_array_equal(one[8], loop[8])
+
+
+def test_ineligible_runs_take_the_launch_loop(amd):
+    rng = np.random.default_rng(4)
+    m = rng.uniform(-1, 1, size=(5000, 3))
+    p = rng.uniform(-1, 1, size=(4097, 3))  # n > 4096: beyond the single-workgroup passes
+    assert run(amd, m, p, amd.RUN_PERSISTENT, 2, -1.0)[9] == 0
+    m = rng.uniform(-1, 1, size=(9000, 3))  # model beyond LDS
+    assert run(amd, m, p[:3000], amd.RUN_PERSISTENT, 2, -1.0)[9] == 0
+    m = rng.uniform(-1, 1, size=(3000, 3))  # an explicit NN variant keeps its own cascade under AUTO
+    assert run(amd, m, p[:3000], amd.RUN_AUTO, 2, -1.0, variant=amd.VARIANT_GRID)[9] == 0
+
+
+def test_repeated_runs_and_per_operation_calls(amd):
+    """Two icp_run calls on one context continue from the resident scene; a closest_matrix
+    afterwards still answers from the resident model."""
+    m = amd.load_matrix(datasets.path("cow_ref"))
+    p = amd.load_matrix(datasets.path("cow_tr2"))
+    outs = {}
+    for mode in (amd.RUN_PERSISTENT, amd.RUN_LAUNCHES):
+        with amd.Context(0) as ctx:
+            ctx.set_run_mode(mode)
+            ctx.set_model(m)
+            ctx.set_scene(p)
+            r1, e1 = ctx.run(4, -1.0)
+            r2, e2 = ctx.run(5, 1e-5)
+            s = ctx.get_scene()
+            _, idx = ctx.closest_matrix(s)
+            outs[mode] = (e1, e2, r2.iterations, s, idx, ctx.stats()["persistent_runs"])
+    a, b = outs[amd.RUN_PERSISTENT], outs[amd.RUN_LAUNCHES]
+    assert a[5] == 2 and b[5] == 0
+    for x, y in zip(a[:5], b[:5]):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("case", ["lattice_ties", "duplicates", "far_scene", "planar"])
+def test_ties_and_degenerate_models_bitwise(amd, case):
+    """The one-launch NN scans only the model blocks within each query's seed distance and
+    breaks exact D64 ties by original index: lattice models with half-integer queries (many
+    equidistant points), duplicated model points, a scene far outside the model (every block
+    in range) and a planar model."""
+    rng = np.random.default_rng(["lattice_ties", "duplicates", "far_scene", "planar"].index(case) + 50)
+    if case == "lattice_ties":
+        g = np.arange(-7, 8, dtype=float)
+        m = np.stack(np.meshgrid(g, g, g[:8], indexing="ij"), axis=-1).reshape(-1, 3)
+        m = m[rng.permutation(m.shape[0])]
+        p = m[rng.integers(0, m.shape[0], 1500)] + 0.5  # equidistant from up to 8 lattice points
+    elif case == "duplicates":
+        base = rng.uniform(-1, 1, size=(700, 3))
+        m = np.concatenate([base, base[::-1], base[:300]])
+        m = m[rng.permutation(m.shape[0])]
+        p = base[rng.integers(0, 700, 2000)] + rng.normal(scale=1e-3, size=(2000, 3))
+    elif case == "far_scene":
+        m = rng.uniform(-1, 1, size=(3000, 3))
+        p = rng.uniform(-1, 1, size=(3000, 3)) + np.array([50.0, -20.0, 5.0])
+    else:
+        m = rng.uniform(-1, 1, size=(2500, 3))
+        m[:, 2] = 0.25
+        p = m[rng.integers(0, 2500, 2500)] + rng.normal(scale=0.02, size=(2500, 3))
+        p[:, 2] = 0.25 + 0.1
+    one = run(amd, m, p, amd.RUN_PERSISTENT, 5, -1.0)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 5, -1.0)
+    assert one[9] == 1 and one[0] == 5
+    assert_same(one, loop)

@@ -98,6 +98,11 @@ for s in $STEPS; do
            run calib_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/calib2" -o write -- tools/hbm_calib ;;
     test_new) run pytest_new 900 python -u -m pytest tests/test_gpu_c4c5.py tests/test_gpu_boundary.py tests/test_gpu_cert_stress.py \
                tests/test_gpu_grid.py -m gpu -v -rf --timeout 300 --timeout-method thread --durations=15 ;;
+    test_pers) run pytest_pers 300 python -u -m pytest tests/test_gpu_persistent.py -m gpu -v -rf --timeout 120 --timeout-method thread --durations=10 ;;
+    cowab) for m in launches persistent launches persistent; do ICP_RUN_MODE=$m run cowab_$m 300 ./iterative-closest-point_amd/build/icp-bench \
+               --ref "$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_ref"))')" \
+               --scene "$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_tr1"))')" \
+               --min-time 0.3 --only opti_gpu_loop || exit 1; cat $OUT/cowab_$m.log >> $OUT/cowab_all_$m.log; done ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
