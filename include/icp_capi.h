@@ -209,7 +209,10 @@ void icp_free(void *p);
 /* ---- instrumentation ----------------------------------------------------- */
 /* Correspondences of the last NN search over the resident scene (the last icp_run
  * iteration's compute_Y_w_opti, gpu.cc:69): idx_out[j] = model index of this rank's scene
- * point j (np_local entries).  ICP_E_NO_MODEL if no search has run since icp_set_scene. */
+ * point j (np_local entries).  ICP_E_NO_MODEL if no search has run since icp_set_scene.
+ * A run with an all-reduce (ranks > 1 or a communicator) tests the error one iteration late;
+ * when it stops on the threshold, the search of the iteration after the converged one has
+ * already run, and these are its correspondences (of the final cloud). */
 int icp_get_indices(icp_ctx *ctx, int32_t *idx_out);
 /* Test instrumentation: with cap > 0, every icp_run iteration k < cap records a digest of its
  * correspondence indices (this rank's shard, local j): (sum idx[j], sum (j+1) idx[j],
