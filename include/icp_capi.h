@@ -94,6 +94,8 @@ typedef struct icp_stats {
     double cert_min_margin;
     long long cert_audited;
     long long persistent_runs; /* icp_run calls that ran as ONE launch (icp_set_run_mode)      */
+    long long cpu_rule_ties;   /* ICP_NN_RULE_CPU_SQRT: near ties evaluated on the host       */
+    long long cpu_rule_changed; /* ... whose CPU-rule answer differs from the squared rule's   */
 } icp_stats;
 
 /* ---- context ------------------------------------------------------------ */
@@ -148,6 +150,17 @@ int icp_set_nn_variant(icp_ctx *ctx, int variant);
  * AUTO:       PERSISTENT for eligible runs with the AUTO NN variant (an explicitly chosen NN
  *             variant runs its own search cascade), else LAUNCHES.  The default.
  * The environment variable ICP_RUN_MODE=launches|persistent overrides (A/B runs). */
+/* Which distance the first minimum is taken over (default SQUARED):
+ * SQUARED:  (dx*dx + dy*dy) + dz*dz -- the reference's GPU path (compute.cu:112-117,137);
+ * CPU_SQRT: sqrt((pow(dx,2) + pow(dy,2)) + pow(dz,2)) with libm pow -- the reference's CPU path
+ *           (src/cpu.cc:17-22, the `icp` binary).  The two differ only at near ties (sqrt merges
+ *           squared distances an ulp apart; libm pow is not always x*x).  The device finds the
+ *           queries with a near tie and the host evaluates those candidates with libm (the run
+ *           then synchronises once per search; the one-launch loop is not used). */
+#define ICP_NN_RULE_SQUARED 0
+#define ICP_NN_RULE_CPU_SQRT 1
+int icp_set_nn_rule(icp_ctx *ctx, int rule);
+
 #define ICP_RUN_AUTO 0
 #define ICP_RUN_LAUNCHES 1
 #define ICP_RUN_PERSISTENT 2

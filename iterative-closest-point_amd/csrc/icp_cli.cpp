@@ -4,7 +4,11 @@
 //
 // Same positional contract, stderr lines ([load] / [ICP] / [output]), ./output.txt and
 // exit codes as the reference.  Both binaries run the HIP engine (there is no CPU
-// fallback in the product).  Options (after the positionals):
+// fallback in the product).  `icp` keeps the reference CPU path's NN rule (src/main.cc ->
+// cpu.cc:17-22: first minimum of sqrt(pow() sums), ICP_NN_RULE_CPU_SQRT) and `icp-gpu` the GPU
+// path's (compute.cu:112-117: squared distances); they differ only at near ties.
+// Options (after the positionals):
+//   --rule cpu|squared override the binary's NN rule
 //   --allow-unequal    run even when the clouds differ in size (reference: exit 255)
 //   --nn fp64|certified  NN arithmetic (default certified; identical results)
 //   --threshold X      convergence threshold (default 1e-5, src/cpu.hh:113)
@@ -39,6 +43,7 @@ int main(int argc, char **argv)
     const int max_iter = std::atoi(argv[3]);
     bool allow_unequal = false;
     int nn_mode = ICP_NN_CERTIFIED, device = 0;
+    int rule = std::strcmp(prog, "icp") == 0 ? ICP_NN_RULE_CPU_SQRT : ICP_NN_RULE_SQUARED;
     double threshold = 1e-5;
     const char *out = "output.txt";
     for (int a = 4; a < argc; ++a) {
@@ -46,6 +51,9 @@ int main(int argc, char **argv)
         else if (!std::strcmp(argv[a], "--nn") && a + 1 < argc) {
             ++a;
             nn_mode = !std::strcmp(argv[a], "fp64") ? ICP_NN_FP64 : ICP_NN_CERTIFIED;
+        } else if (!std::strcmp(argv[a], "--rule") && a + 1 < argc) {
+            ++a;
+            rule = !std::strcmp(argv[a], "cpu") ? ICP_NN_RULE_CPU_SQRT : ICP_NN_RULE_SQUARED;
         } else if (!std::strcmp(argv[a], "--threshold") && a + 1 < argc) threshold = std::atof(argv[++a]);
         else if (!std::strcmp(argv[a], "--out") && a + 1 < argc) out = argv[++a];
         else if (!std::strcmp(argv[a], "--device") && a + 1 < argc) device = std::atoi(argv[++a]);
@@ -76,6 +84,7 @@ int main(int argc, char **argv)
         return 3;
     }
     icp_set_allow_unequal(ctx, allow_unequal ? 1 : 0);
+    icp_set_nn_rule(ctx, rule);
     if ((rc = icp_set_model(ctx, m, nm)) != ICP_OK || (rc = icp_set_scene(ctx, p, np, np)) != ICP_OK) {
         std::fprintf(stderr, "[error] %s: %s\n", icp_strerror(rc), icp_last_error(ctx));
         return 3;

@@ -181,6 +181,12 @@ struct icp_ctx {
     size_t io_cap = 0, io_off = 0;
     bool io_pending = false; // a queued kernel may still read h_io
 
+    // ICP_NN_RULE_CPU_SQRT: the near-tie window of every search (launch_nn_cpu_rule_window)
+    int nn_rule = ICP_NN_RULE_SQUARED;
+    CpuRuleEntry *cr_entries = nullptr;
+    int *cr_count = nullptr;
+    size_t cr_cap = 0, cr_count_cap = 0;
+
     // one-launch registration of small clouds (icp_iter.hip, launch_icp_persistent)
     int run_mode = ICP_RUN_AUTO;
     int n_cu = 0;                    // compute units
@@ -568,6 +574,74 @@ int nn_search(icp_ctx *ctx, const DevCloud &q, size_t n)
     return n ? nn_counts_to_host(ctx) : ICP_OK;
 }
 
+// The reference CPU path's distance (src/cpu.cc:17-19): (pow(dx,2) + pow(dy,2)) + pow(dz,2),
+// then sqrt, with libm's pow -- called through a volatile pointer so that the compiler cannot
+// turn pow(x, 2.0) into x*x (libm's pow is not always correctly rounded; the reference, built
+// without optimisation, calls it: benchmark/callgrind.out.76685).
+static double (*volatile g_libm_pow)(double, double) = std::pow;
+static double cpu_rule_distance(const double q[3], const double *m)
+{
+    const double dx = q[0] - m[0], dy = q[1] - m[1], dz = q[2] - m[2];
+    const double t = (g_libm_pow(dx, 2.0) + g_libm_pow(dy, 2.0)) + g_libm_pow(dz, 2.0);
+    return std::sqrt(t);
+}
+
+// ICP_NN_RULE_CPU_SQRT: after a search has left the squared-rule first minimum in idx, find the
+// queries with another point inside their near-tie window on the device, evaluate the
+// reference's CPU arithmetic on the host for exactly those candidates (minCoeff's first
+// minimum, cpu.cc:22), and write the changed correspondences back.  Synchronises the stream.
+int cpu_rule_fixup(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop)
+{
+    if (ctx->nn_rule != ICP_NN_RULE_CPU_SQRT || n == 0) return ICP_OK;
+    TRY(grow(ctx, &ctx->cr_count, &ctx->cr_count_cap, 1));
+    size_t want = std::min<size_t>(n, 4096);
+    for (int pass = 0; pass < 2; ++pass) {
+        TRY(grow(ctx, &ctx->cr_entries, &ctx->cr_cap, want));
+        HIPCHK(hipMemsetAsync(ctx->cr_count, 0, sizeof(int), ctx->st));
+        launch_nn_cpu_rule_window((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), grid_budget(ctx), ctx->idx,
+                                  ctx->cr_count, ctx->cr_entries, (int)ctx->cr_cap, ctx->st, stop);
+        LAUNCHCHK("nn_cpu_rule_window");
+        int cnt = 0;
+        HIPCHK(hipMemcpyAsync(&cnt, ctx->cr_count, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        if ((size_t)cnt > ctx->cr_cap) { // more near ties than entries: once more with room for all
+            want = (size_t)cnt;
+            continue;
+        }
+        if (cnt == 0) return ICP_OK;
+        std::vector<CpuRuleEntry> h((size_t)cnt);
+        HIPCHK(hipMemcpy(h.data(), ctx->cr_entries, sizeof(CpuRuleEntry) * (size_t)cnt, hipMemcpyDeviceToHost));
+        const double *m = ctx->model_host.data();
+        std::vector<int> cand;
+        for (const CpuRuleEntry &e : h) {
+            cand.clear();
+            if (e.n >= 0) {
+                cand.assign(e.cand, e.cand + e.n);
+                std::sort(cand.begin(), cand.end());
+            } else { // a window the grid could not bound: every model point, in order
+                cand.resize(ctx->nm);
+                for (size_t k = 0; k < ctx->nm; ++k) cand[k] = (int)k;
+            }
+            int best = cand.empty() ? e.h : cand[0];
+            double bd = cand.empty() ? 0.0 : cpu_rule_distance(e.q, m + 3 * (size_t)best);
+            for (size_t c = 1; c < cand.size(); ++c) {
+                const double d = cpu_rule_distance(e.q, m + 3 * (size_t)cand[c]);
+                if (d < bd) { // minCoeff: strict, so the lowest index of the minimum
+                    bd = d;
+                    best = cand[c];
+                }
+            }
+            ctx->stats.cpu_rule_ties += 1;
+            if (best != e.h) {
+                ctx->stats.cpu_rule_changed += 1;
+                HIPCHK(hipMemcpy(ctx->idx + e.j, &best, sizeof(int), hipMemcpyHostToDevice));
+            }
+        }
+        return ICP_OK;
+    }
+    return fail(ctx, ICP_E_HIP, "cpu_rule_fixup: the near-tie list kept growing");
+}
+
 // after the stream has been synchronised (h_amb holds the last search's final counts): fold
 // the NN events and queue sizes into the stats
 void account_nn(icp_ctx *ctx, size_t n)
@@ -750,7 +824,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
-                    (void *)ctx->pers_stamps, (void *)ctx->pm_img})
+                    (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->cr_entries,
+                    (void *)ctx->cr_count})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -772,6 +847,13 @@ int icp_set_nn_variant(icp_ctx *ctx, int variant)
 {
     if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_GRID) return ICP_E_ARG;
     ctx->nn_variant = variant;
+    return ICP_OK;
+}
+
+int icp_set_nn_rule(icp_ctx *ctx, int rule)
+{
+    if (!ctx || (rule != ICP_NN_RULE_SQUARED && rule != ICP_NN_RULE_CPU_SQRT)) return ICP_E_ARG;
+    ctx->nn_rule = rule;
     return ICP_OK;
 }
 
@@ -972,6 +1054,7 @@ static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *l
     if (mode == ICP_RUN_LAUNCHES) return 0;
     if (mode == ICP_RUN_AUTO && ctx->nn_variant != ICP_NN_VARIANT_AUTO) return 0; // explicit variants run their cascade
     if (ctx->world != 1 || ctx->comm || ctx->host_reduce || ctx->digest_cap || max_iter < 1) return 0;
+    if (ctx->nn_rule != ICP_NN_RULE_SQUARED) return 0; // (the host resolves the CPU rule's near ties)
     if (n < 4 || n > (size_t)kRedSingle || ctx->nm < 1 || ctx->nm > (size_t)kPersistMaxModel) return 0;
     const size_t lds = 24 * ctx->nm + 48 * ctx->pm_blocks, statics = persistent_static_lds();
     if (!ctx->pm_img) return 0;
@@ -1169,6 +1252,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
                                 &sd->done)); // (run_init zeroed the counters)
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
+            TRY(cpu_rule_fixup(ctx, P, n, &sd->done)); // (ICP_NN_RULE_CPU_SQRT only: host near ties)
             ar_timed[slot] = false;
             if ((size_t)enqueued < ctx->digest_cap) {
                 launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st);
@@ -1317,11 +1401,13 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
     TRY(check_ready(ctx, false));
     if (!p_xyz && np) return ICP_E_ARG;
     // (an explicitly chosen NN variant always runs its own cascade, as the tests of it expect)
-    if (np && np <= kFewQueries && (ctx->nn_variant == ICP_NN_VARIANT_AUTO || ctx->nn_mode == ICP_NN_FP64))
+    if (np && np <= kFewQueries && (ctx->nn_variant == ICP_NN_VARIANT_AUTO || ctx->nn_mode == ICP_NN_FP64) &&
+        ctx->nn_rule == ICP_NN_RULE_SQUARED)
         return closest_few(ctx, p_xyz, np, y_xyz_out, idx_out);
     TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
     ctx->seeds_valid = false; // idx is about to hold other queries' correspondences
     TRY(nn_search(ctx, ctx->qa, np));
+    TRY(cpu_rule_fixup(ctx, ctx->qa, np, nullptr));
     if (np && y_xyz_out) {
         TRY(grow_cloud(ctx, ctx->qb, np, false));
         launch_gather_moments(ctx->idx, ctx->m4, ctx->qa.x,

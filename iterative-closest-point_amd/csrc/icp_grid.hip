@@ -563,4 +563,98 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
 #undef RESOLVE_ALL
 }
 
+// ---- the reference CPU path's rule (ICP_NN_RULE_CPU_SQRT) ------------------------------------
+// src/cpu.cc:17-22 takes the first minimum of sqrt((pow(dx,2) + pow(dy,2)) + pow(dz,2)) with libm
+// pow: per term within ~1 ulp of dx*dx, and sqrt can merge squared distances 1-2 ulp apart.  So
+// the CPU winner of query j lies among the points whose D64 is within 2^-44 (relative) of the
+// squared-rule winner h = idx[j], far beyond both effects.  One G-lane group per query scans the
+// complete grid box of that window and counts its points; a query with more than one (a near tie
+// under either rule) is written out for the host, which evaluates the reference's own
+// arithmetic with libm on exactly those candidates (icp_engine.hip, cpu_rule_fixup).  A box over
+// budget, or more than kCpuRuleMaxCand candidates, is written with n = -1: the host then
+// evaluates every model point for that query.
+namespace {
+template <int G>
+__global__ __launch_bounds__(kBlock) void nn_cpu_rule_window_kernel(
+    int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    const double4 *__restrict__ m4, GridView gv, int budget, const int *__restrict__ idx, int *__restrict__ count,
+    CpuRuleEntry *__restrict__ out, int max_entries, const int *__restrict__ stop)
+{
+    if (stop && *stop) return; // a frozen (converged) ICP iteration
+    const int sub = threadIdx.x & (G - 1);
+    const int groups = gridDim.x * (kBlock / G);
+    for (int j = (blockIdx.x * kBlock + threadIdx.x) / G; j < n; j += groups) { // (uniform per group)
+        const double q[3] = {px[j], py[j], pz[j]};
+        const int h = idx[j];
+        const double4 mh = m4[h];
+        const double best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
+        if (!(best == best && best < INFINITY)) continue; // NaN / inf: both rules give the scan's answer
+        // (+2^-1000: squares that underflow under one rule and not the other)
+        const double T = best * (1.0 + 0x1p-44) + 0x1p-1000;
+        int c0[3], c1[3];
+        const bool ok = complete_box(q, T, gv, budget, c0, c1);
+        int cnt = 0;
+        if (ok) {
+            const int ny = c1[1] - c0[1] + 1, nrows = ny * (c1[2] - c0[2] + 1);
+            for (int r = sub; r < nrows; r += G) {
+                const int row = ((c0[2] + r / ny) * gv.g[1] + c0[1] + r % ny) * gv.g[0];
+                for (int k = gv.start[row + c0[0]]; k < gv.start[row + c1[0] + 1]; ++k) {
+                    const double4 m = gv.pts[k];
+                    cnt += d64g(q[0], q[1], q[2], m.x, m.y, m.z) <= T;
+                }
+            }
+#pragma unroll
+            for (int o = G / 2; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, G);
+        }
+        if (ok && cnt <= 1) continue; // the winner alone in its window: the same under both rules
+        int e = 0;
+        if (sub == 0) e = atomicAdd(count, 1);
+        e = __shfl(e, 0, G);
+        if (e >= max_entries) continue; // (the host sees count > max_entries and rescans everything)
+        CpuRuleEntry *en = out + e;
+        if (sub == 0) {
+            en->j = j;
+            en->h = h;
+            en->q[0] = q[0];
+            en->q[1] = q[1];
+            en->q[2] = q[2];
+            en->n = ok && cnt <= kCpuRuleMaxCand ? cnt : -1;
+        }
+        if (ok && cnt <= kCpuRuleMaxCand) { // the candidates, in any order (the host sorts them)
+            int pos = 0;
+            const int ny = c1[1] - c0[1] + 1, nrows = ny * (c1[2] - c0[2] + 1);
+            for (int r = 0; r < nrows; ++r) { // (serial per group: a handful of cells, rarely taken)
+                const int row = ((c0[2] + r / ny) * gv.g[1] + c0[1] + r % ny) * gv.g[0];
+                const int k0 = gv.start[row + c0[0]], k1 = gv.start[row + c1[0] + 1];
+                for (int b = k0; b < k1; b += G) {
+                    const int k = b + sub;
+                    bool in = false;
+                    int mi = 0;
+                    if (k < k1) {
+                        const double4 m = gv.pts[k];
+                        in = d64g(q[0], q[1], q[2], m.x, m.y, m.z) <= T;
+                        mi = (int)m.w;
+                    }
+                    const unsigned long long bal = __ballot(in);
+                    const int lanebase = (threadIdx.x & 63) & ~(G - 1);
+                    const unsigned long long mine = (bal >> lanebase) & ((G == 64) ? ~0ull : ((1ull << G) - 1));
+                    if (in) en->cand[pos + __popcll(mine & ((1ull << sub) - 1))] = mi;
+                    pos += __popcll(mine);
+                }
+            }
+        }
+    }
+}
+} // namespace
+
+void launch_nn_cpu_rule_window(int n, const double *px, const double *py, const double *pz, const double4 *m4,
+                               const GridView &gv, int budget, const int *idx, int *count, CpuRuleEntry *out,
+                               int max_entries, hipStream_t st, const int *stop)
+{
+    constexpr int G = 16;
+    const int blocks = std::max(1, std::min((n + kBlock / G - 1) / (kBlock / G), 16384));
+    nn_cpu_rule_window_kernel<G><<<blocks, kBlock, 0, st>>>(n, px, py, pz, m4, gv, budget, idx, count, out,
+                                                            max_entries, stop);
+}
+
 } // namespace icp

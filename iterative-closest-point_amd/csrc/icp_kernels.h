@@ -172,6 +172,19 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const double *T_in, double *T_out, hipStream_t st, const int *stop = nullptr,
                             int inline_nm = 0);
 
+// The reference CPU rule's near ties (icp_grid.hip): queries whose squared-rule winner idx[j]
+// has another point within the window are appended to out[*count] (count zeroed by the caller).
+constexpr int kCpuRuleMaxCand = 26;
+struct CpuRuleEntry {
+    int j, h;                     // query, its squared-rule winner
+    int n;                        // candidates written to cand (-1: scan the whole model)
+    int cand[kCpuRuleMaxCand + 1];
+    double q[3];                  // the query
+};
+void launch_nn_cpu_rule_window(int n, const double *px, const double *py, const double *pz, const double4 *m4,
+                               const GridView &gv, int budget, const int *idx, int *count, CpuRuleEntry *out,
+                               int max_entries, hipStream_t st, const int *stop = nullptr);
+
 // Exact grid NN of all np queries (ICP_NN_VARIANT_GRID): idx, or fb_list (+ fb_T = +inf)
 // for the queries whose ring or box would exceed `budget` cells.
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,

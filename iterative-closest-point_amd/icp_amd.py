@@ -46,6 +46,8 @@ VARIANT_VALU = 1
 VARIANT_MFMA = 2
 VARIANT_MFMA16 = 3
 VARIANT_GRID = 4  # exact grid NN for every query
+RULE_SQUARED = 0    # icp_set_nn_rule: the reference GPU path's squared distance (default)
+RULE_CPU_SQRT = 1   # the reference CPU path's sqrt(pow) distance (src/cpu.cc:17-22)
 RUN_AUTO = 0        # icp_set_run_mode: one launch for eligible small runs, else the launch loop
 RUN_LAUNCHES = 1
 RUN_PERSISTENT = 2
@@ -60,7 +62,7 @@ EXPORTED = [
     "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
     "icp_load_matrix", "icp_write_matrix", "icp_free", "icp_get_stats", "icp_reset_stats",
     "icp_ensure_model", "icp_subtract_col", "icp_get_indices", "icp_set_index_digest",
-    "icp_get_index_digest", "icp_set_cert_audit", "icp_set_run_mode",
+    "icp_get_index_digest", "icp_set_cert_audit", "icp_set_run_mode", "icp_set_nn_rule",
 ]
 
 
@@ -81,7 +83,8 @@ class Stats(C.Structure):
                 ("grid_fallback", C.c_longlong), ("allreduce_ms", C.c_double),
                 ("allreduce_calls", C.c_longlong), ("cert_max_err_ratio", C.c_double),
                 ("cert_min_margin", C.c_double), ("cert_audited", C.c_longlong),
-                ("persistent_runs", C.c_longlong)]
+                ("persistent_runs", C.c_longlong), ("cpu_rule_ties", C.c_longlong),
+                ("cpu_rule_changed", C.c_longlong)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
@@ -117,6 +120,7 @@ def lib() -> C.CDLL:
     L.icp_set_allow_unequal.argtypes = [vp, C.c_int]
     L.icp_set_nn_variant.argtypes = [vp, C.c_int]
     L.icp_set_run_mode.argtypes = [vp, C.c_int]
+    L.icp_set_nn_rule.argtypes = [vp, C.c_int]
     L.icp_run.argtypes = [vp, C.c_int, C.c_double, dp, C.POINTER(Result)]
     L.icp_closest_matrix.argtypes = [vp, dp, sz, dp, C.POINTER(C.c_int32)]
     L.icp_compute_centroid.argtypes = [vp, dp, sz, dp, dp]
@@ -314,6 +318,10 @@ class Context:
 
     def set_nn_variant(self, variant: int):
         self._check(lib().icp_set_nn_variant(self._h, variant))
+
+    def set_nn_rule(self, rule: int):
+        """icp_set_nn_rule: RULE_SQUARED (GPU path) / RULE_CPU_SQRT (the reference CPU path)."""
+        self._check(lib().icp_set_nn_rule(self._h, rule))
 
     def set_run_mode(self, mode: int):
         """icp_set_run_mode: RUN_AUTO / RUN_LAUNCHES / RUN_PERSISTENT (bit-identical results)."""

@@ -186,3 +186,38 @@ def test_c4_fixture_inputs_and_shape(icp_lib):
     assert np.all(np.isfinite(e)) and np.all(np.diff(e) < 0)  # a converging registration
     ident = [d["identity"] for d in fx["idx"]]
     assert ident[-1] > ident[0]  # correspondences move toward the known identity pairing
+
+
+def test_oracle_cpu_rule_calls_libm_pow(oracle):
+    """The oracle's sqrt(pow) rule (cpu.cc:17-22) must call libm's pow, as the reference's
+    unoptimised build does, not gcc's x*x folding (oracle/Makefile: -fno-builtin-pow): on this
+    libm, pow(x, 2.0) != x*x for ~0.08% of inputs.  Pinned on bunny's three first-search near
+    ties against a pure-Python restatement through ctypes libm, and against the committed
+    CPU-rule fixture (tests/golden/make_cpu_rule.py)."""
+    import ctypes
+    import math
+    import datasets
+    libm = ctypes.CDLL("libm.so.6")
+    libm.pow.restype = ctypes.c_double
+    libm.pow.argtypes = [ctypes.c_double, ctypes.c_double]
+    rng = np.random.default_rng(0)
+    xs = rng.normal(size=20000)
+    assert sum(libm.pow(float(x), 2.0) != float(x) * float(x) for x in xs) > 0
+    m = oracle.load_matrix(datasets.path("bun000"))
+    p = oracle.load_matrix(datasets.path("bun045"))
+    ties = [8277, 15594, 20678]
+    _, got = oracle.closest(p[ties], m, oracle.NN_CPU_SQRT)
+    ref = []
+    for j in ties:
+        q = p[j]
+        best, bd = 0, None
+        for k in range(m.shape[0]):
+            d = math.sqrt((libm.pow(q[0] - m[k, 0], 2.0) + libm.pow(q[1] - m[k, 1], 2.0)) + libm.pow(q[2] - m[k, 2], 2.0))
+            if bd is None or d < bd:
+                best, bd = k, d
+        ref.append(best)
+    assert got.tolist() == ref
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "bun045_cpu_rule_idx0.npz"))["idx0"]
+    assert fx[ties].tolist() == ref
+    _, sq = oracle.closest(p[ties], m, oracle.NN_SQUARED)
+    assert (sq != got).all()  # each is a near tie the two rules break differently
