@@ -194,6 +194,9 @@ struct icp_ctx {
     double *pers_part = nullptr;     // 2 x kBlock x kNumSums published partials
     unsigned *pers_sync = nullptr;   // arrival counter, abort word (+ padding to 16 B)
     size_t pers_part_cap = 0, pers_sync_cap = 0;
+    bool pers_sync_valid = false;    // the barrier words hold pers_epoch_base barriers of grid pers_grid
+    unsigned pers_epoch_base = 0;
+    int pers_grid = 0;
     unsigned long long *pers_stamps = nullptr; // ICP_PERSIST_STAMPS=1: phase stamps
     size_t pers_stamps_cap = 0;
     // the model in Morton order for the one-launch NN (models <= kPersistMaxModel points):
@@ -311,8 +314,13 @@ int upload_cloud(icp_ctx *ctx, DevCloud &c, const double *xyz, size_t n, bool ma
         double *h, *d;
         TRY(io_take(ctx, 3 * n, &h, &d));
         std::memcpy(h, xyz, sizeof(double) * 3 * n);
-        launch_aos_to_soa(d, n, c.x, c.y, c.z, ctx->st);
         ctx->io_pending = true;
+        if (make_f32) {
+            launch_aos_to_soa_f32(d, n, c.x, c.y, c.z, ctx->c, c.f, ctx->st);
+            LAUNCHCHK("upload_cloud");
+            return ICP_OK;
+        }
+        launch_aos_to_soa(d, n, c.x, c.y, c.z, ctx->st);
     } else {
         TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * n));
         HIPCHK(hipMemcpyAsync(ctx->stage, xyz, sizeof(double) * 3 * n, hipMemcpyHostToDevice, ctx->st));
@@ -984,9 +992,11 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     if (np_total > (size_t)0x7fffffff) return fail(ctx, ICP_E_ARG, "scene too large");
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
-    TRY(upload_cloud(ctx, ctx->scene, p_xyz, np_local, true));
     TRY(grow_cloud(ctx, ctx->Y, np_local, false));
-    HIPCHK(hipStreamSynchronize(ctx->st));
+    TRY(upload_cloud(ctx, ctx->scene, p_xyz, np_local, true));
+    // a small cloud went through the mapped staging buffer (host-copied: the caller's array is
+    // free again), a large one through a pageable copy; either way the stream orders the rest
+    if (3 * np_local > kMappedIo) HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->np_total = np_total;
     ctx->has_scene = true;
     ctx->seeds_valid = false;
@@ -1084,8 +1094,16 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, doub
         HIPCHK(hipMemsetAsync(ctx->pers_stamps, 0, sizeof(unsigned long long) * (2 * kPersistMaxStamps + 2 * kBlock), ctx->st));
     }
     TRY(grow(ctx, &ctx->pers_sync, &ctx->pers_sync_cap, kPersistSyncWords));
-    HIPCHK(hipMemsetAsync(ctx->pers_sync, 0, kPersistSyncWords * sizeof(unsigned), ctx->st));
+    // the barrier words count on from the previous launch of the same grid (no memset launch);
+    // zeroed on the first launch, when the grid changes and after an aborted launch
+    if (!ctx->pers_sync_valid || ctx->pers_grid != grid) {
+        HIPCHK(hipMemsetAsync(ctx->pers_sync, 0, kPersistSyncWords * sizeof(unsigned), ctx->st));
+        ctx->pers_epoch_base = 0;
+        ctx->pers_grid = grid;
+    }
+    ctx->pers_sync_valid = false; // (until this launch has completed cleanly)
     ctx->h_flags[3] = 0; // abort word (mapped host)
+    ctx->h_flags[7] = 0; // barriers used (mapped host)
     PersistArgs a{};
     a.img = ctx->pm_img;
     a.nblk = (int)ctx->pm_blocks;
@@ -1118,6 +1136,8 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, doub
         return e && std::strcmp(e, "all") == 0 ? 0 : 1;
     }();
     a.cull = cull;
+    a.epoch_base = ctx->pers_epoch_base;
+    a.h_epochs = ctx->d_flags + 7;
     for (int k = 0; k < 3; ++k) a.m0[k] = ctx->model_host[k];
     launch_icp_persistent(a, grid, lds, ctx->st);
     LAUNCHCHK("icp_persistent");
@@ -1143,8 +1163,11 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, doub
         fprintf(stderr, " | per-wg NN min/mean/max %.1f/%.1f/%.1f barrier %.1f/%.1f/%.1f us\n", nmin, nsum / grid, nmax,
                 bmin, bsum / grid, bmax);
     }
-    if (__atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE) != 0)
+    if (__atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE) != 0) {
         return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the one-launch loop timed out (workgroups not co-resident)");
+    }
+    ctx->pers_epoch_base += (unsigned)__atomic_load_n(ctx->h_flags + 7, __ATOMIC_ACQUIRE);
+    ctx->pers_sync_valid = true;
     ctx->seeds_valid = true;
     const int iters = ctx->h_iter->iter;
     ctx->stats.nn_pairs += (long long)iters * (long long)n * (long long)ctx->nm;

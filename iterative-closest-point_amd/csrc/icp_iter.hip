@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
         ++epoch;
         persist_stamp(a.stamps, nstamp, 2);
         const unsigned long long t_bar = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-        if (!persist_barrier(a.sync, epoch, a.h_abort, &s_ok)) return false;
+        if (!persist_barrier(a.sync, a.epoch_base + epoch, a.h_abort, &s_ok)) return false;
         if (a.stamps && tid == 0) wg_bar += __builtin_amdgcn_s_memrealtime() - t_bar;
         persist_stamp(a.stamps, nstamp, 3);
         switch (K) { // per column: the classic pass's block_sum_store<K> tree
@@ -654,7 +654,11 @@ __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
         a.stamps[2 * kPersistMaxStamps + 2 * b] = wg_nn;
         a.stamps[2 * kPersistMaxStamps + 2 * b + 1] = wg_bar;
     }
-    if (b == 0 && tid == 0) *a.s_glob = st;
+    if (b == 0 && tid == 0) {
+        *a.s_glob = st;
+        // the barriers this launch used: the next launch continues the monotonic counters
+        __hip_atomic_store(a.h_epochs, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 } // namespace

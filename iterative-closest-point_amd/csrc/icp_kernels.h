@@ -64,6 +64,9 @@ void launch_aos_to_soa(const double *aos, size_t n, double *x, double *y, double
                        hipStream_t st);
 void launch_soa_to_aos(const double *x, const double *y, const double *z, size_t n, double *aos,
                        hipStream_t st);
+// both at once: SoA fp64 + the centred fp32 copy
+void launch_aos_to_soa_f32(const double *aos, size_t n, double *x, double *y, double *z, const double c[3],
+                           float4 *f, hipStream_t st);
 // f[j] = (float)(p_j - c) (xyz), w = 0
 void launch_make_f32(const double *x, const double *y, const double *z, size_t n, double cx,
                      double cy, double cz, float4 *f, hipStream_t st);
@@ -285,8 +288,9 @@ void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, 
                                  IterState *h_state_dev, double *h_trace_dev, hipStream_t st);
 // A whole icp_run of a small single-rank registration in ONE launch (icp_iter.hip): `grid`
 // co-resident workgroups, the model in LDS (lds_bytes = 24 nm), one grid barrier per iteration;
-// bit-identical to the launch-per-step loop.  sync[0..1] (arrival counter, abort word) must be
-// zero at launch; *h_abort (mapped host) is set if a barrier timed out.
+// bit-identical to the launch-per-step loop.  The sync words count barriers monotonically from
+// zero across launches of the same grid (epoch_base); *h_abort (mapped host) is set if a
+// barrier timed out.
 constexpr size_t kPersistLdsMax = 160 * 1024 - 12 * 1024; // dynamic LDS (the statics take ~9 KiB)
 constexpr int kPersistMaxModel = (int)(kPersistLdsMax / 24);
 struct PersistArgs {
@@ -307,6 +311,8 @@ struct PersistArgs {
     unsigned long long *stamps; // nullable: (tag, realtime) pairs of workgroup 0's phases
     int cull;                   // 1: scan only the blocks within the seed distance (0: all)
     double m0[3];               // model point 0 (a NaN query's correspondence)
+    unsigned epoch_base;        // barriers of earlier launches on the same sync words (monotonic)
+    int *h_epochs;              // mapped host: the barriers this launch used
 };
 constexpr int kPersistMaxStamps = 1024;
 constexpr int kPersistSyncWords = 512; // barrier words (icp_iter.hip: persist_barrier)

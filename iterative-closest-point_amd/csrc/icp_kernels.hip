@@ -104,6 +104,20 @@ __global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const double *__rest
     }
 }
 
+// aos_to_soa + make_f32 in one pass (a cloud upload: one launch instead of two)
+__global__ __launch_bounds__(kBlock) void aos_to_soa_f32_kernel(const double *__restrict__ aos, size_t n,
+                                                                double *x, double *y, double *z, double cx,
+                                                                double cy, double cz, float4 *f)
+{
+    for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
+        const double a = aos[3 * i], b = aos[3 * i + 1], c = aos[3 * i + 2];
+        x[i] = a;
+        y[i] = b;
+        z[i] = c;
+        f[i] = make_float4((float)(a - cx), (float)(b - cy), (float)(c - cz), 0.0f);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(const double *__restrict__ x,
                                                             const double *__restrict__ y,
                                                             const double *__restrict__ z,
@@ -1893,6 +1907,13 @@ void launch_soa_to_aos(const double *x, const double *y, const double *z, size_t
 {
     if (!n) return;
     soa_to_aos_kernel<<<grid_for(n), kBlock, 0, st>>>(x, y, z, n, aos);
+}
+
+void launch_aos_to_soa_f32(const double *aos, size_t n, double *x, double *y, double *z, const double c[3],
+                           float4 *f, hipStream_t st)
+{
+    if (!n) return;
+    aos_to_soa_f32_kernel<<<grid_for(n), kBlock, 0, st>>>(aos, n, x, y, z, c[0], c[1], c[2], f);
 }
 
 void launch_make_f32(const double *x, const double *y, const double *z, size_t n, double cx,
