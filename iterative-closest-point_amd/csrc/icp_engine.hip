@@ -194,6 +194,9 @@ struct icp_ctx {
     double *pers_part = nullptr;     // 2 x kBlock x kNumSums published partials
     unsigned *pers_sync = nullptr;   // arrival counter, abort word (+ padding to 16 B)
     size_t pers_part_cap = 0, pers_sync_cap = 0;
+    double *tail_part = nullptr;     // fused mid-size tail: published partials (18 x kTailMaxBlocks)
+    unsigned *tail_sync = nullptr;   // its barrier words
+    size_t tail_part_cap = 0, tail_sync_cap = 0;
     bool pers_sync_valid = false;    // the barrier words hold pers_epoch_base barriers of grid pers_grid
     unsigned pers_epoch_base = 0;
     int pers_grid = 0;
@@ -833,7 +836,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
                     (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->cr_entries,
-                    (void *)ctx->cr_count})
+                    (void *)ctx->cr_count, (void *)ctx->tail_part, (void *)ctx->tail_sync})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -1049,6 +1052,9 @@ static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_res
                       std::chrono::steady_clock::time_point wall0);
 
 
+// the run all-reduces its sums (ranks > 1 or a communicator): error test one iteration late
+static bool lag_run(const icp_ctx *ctx) { return ctx->comm != nullptr || ctx->world > 1; }
+
 // Workgroups of the one-launch registration for this run, or 0 if it does not apply: one
 // rank, no communicator, n <= kRedSingle (the single-workgroup passes it reproduces bit for
 // bit), the model in LDS, >= 64 co-resident workgroups, no per-iteration instrumentation.
@@ -1237,6 +1243,22 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         if (grid) return run_persistent(ctx, grid, lds, max_iter, threshold, err_trace, res, wall0);
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
+    // mid-size single-rank runs: iterations >= 2 end in ONE fused launch (moments ... error step)
+    static const int forced_mode = [] {
+        const char *e = getenv("ICP_RUN_MODE");
+        return e && std::strcmp(e, "launches") == 0 ? ICP_RUN_LAUNCHES : -1;
+    }();
+    const int tail_blocks = red_blocks(n);
+    const bool fused_tail = (forced_mode < 0 ? ctx->run_mode : forced_mode) != ICP_RUN_LAUNCHES && !lag_run(ctx) &&
+                            n > (size_t)kRedSingle && tail_blocks <= kTailMaxBlocks &&
+                            tail_blocks <= ctx->n_cu * 3 / 4;
+    unsigned tail_epoch = 0;
+    if (fused_tail) {
+        TRY(grow(ctx, &ctx->tail_part, &ctx->tail_part_cap, (size_t)18 * kTailMaxBlocks));
+        TRY(grow(ctx, &ctx->tail_sync, &ctx->tail_sync_cap, kPersistSyncWords));
+        HIPCHK(hipMemsetAsync(ctx->tail_sync, 0, kPersistSyncWords * sizeof(unsigned), ctx->st));
+        ctx->h_flags[11] = 0; // its barriers' abort word (mapped host)
+    }
     if (ctx->digest_cap) HIPCHK(hipMemsetAsync(ctx->digest, 0, sizeof(unsigned long long) * 3 * ctx->digest_cap, ctx->st));
     bool ar_timed[kRing] = {};
     IterState *sd = ctx->iter_state;
@@ -1299,6 +1321,48 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             // the previous Horn step left (its transformed centroid, its correspondence centroid)
             if (enqueued == 0) {
                 TRY(moments_phase(ctx, n));
+            } else if (fused_tail) {
+                // steps 2-6 in one launch of the same workgroups (bit-identical; see icp_iter.hip)
+                const int sl = enqueued % kRing;
+                slot_ticket[sl] = ++ctx->flag_ticket;
+                TailArgs ta{};
+                ta.idx = ctx->idx;
+                ta.m4 = ctx->m4;
+                ta.px = P.x;
+                ta.py = P.y;
+                ta.pz = P.z;
+                ta.n = (int)n;
+                ta.yx = Y.x;
+                ta.yy = Y.y;
+                ta.yz = Y.z;
+                ta.p32 = P.f;
+                ta.sa = sa;
+                ta.part17 = ctx->tail_part;
+                ta.part1 = ctx->tail_part + (size_t)17 * kTailMaxBlocks;
+                ta.sync = ctx->tail_sync;
+                ta.epoch_base = tail_epoch;
+                ta.h_abort = ctx->d_flags + 11;
+                ta.N = N;
+                ta.c0 = ctx->c[0];
+                ta.c1 = ctx->c[1];
+                ta.c2 = ctx->c[2];
+                ta.cnt = ctx->amb_count;
+                ta.s = sd;
+                ta.threshold = threshold;
+                ta.max_iter = max_iter;
+                ta.err_trace = ctx->err_trace_dev;
+                ta.hflag = ctx->d_flags + 4 * sl;
+                ta.ticket = slot_ticket[sl];
+                ta.h_state = ctx->d_iter_mirror;
+                ta.h_trace = ctx->d_trace;
+                static const bool split_err = getenv("ICP_TAIL_SPLIT_ERR") != nullptr; // (A/B)
+                ta.sums_out = split_err ? ctx->sums : nullptr;
+                launch_iteration_tail_grid(ta, tail_blocks, ctx->st);
+                LAUNCHCHK("iteration_tail_grid");
+                if (split_err) TRY(enqueue_err_step(enqueued));
+                tail_epoch += 2;
+                ++enqueued;
+                continue;
             } else {
                 launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
                                        red_target(ctx, n, ctx->sums), ctx->st);
@@ -1356,6 +1420,8 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         stop = done != 0;
     }
     HIPCHK(hipStreamSynchronize(ctx->st)); // (the iterations queued behind the last one drain)
+    if (fused_tail && __atomic_load_n(ctx->h_flags + 11, __ATOMIC_ACQUIRE) != 0)
+        return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the fused iteration tail timed out");
     return finish_run(ctx, threshold, err_trace, res, wall0);
 }
 

@@ -661,7 +661,128 @@ __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
     }
 }
 
+// ---- the rest of a mid-size iteration in ONE launch ----------------------------------------------
+//
+// After the NN search, an iteration of the launch loop for 4,096 < n on one rank is six short
+// launches: shifted moments, their reduce, the Horn step, transform + residual, its reduce and
+// the error step -- each a few us of work under a ~5 us launch (C3: 29 us of 164).  This kernel
+// runs them as one launch of the same workgroups: workgroup b is the classic passes' workgroup b
+// (red_blocks(n) of them, thread t the points b*256 + t, + stride), so its partials are the
+// classic partials; two grid barriers (persist_barrier, write-through partials) replace the
+// kernel boundaries, every workgroup folds the partials with reduce_kernel's tree and runs the
+// Horn step itself, and workgroup 0 alone writes the loop state, the NN statistics and the
+// error step's outputs.  Bit-identical to the six launches.  A frozen (converged) iteration
+// still takes both barriers, so every launch uses exactly two (the host counts them).
+__device__ __forceinline__ double pub_load(const double *p)
+{
+    return __longlong_as_double((long long)__hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// reduce_kernel<K>'s result from the published partials (rows of K doubles), into LDS out[0..K)
+template <int K> __device__ __forceinline__ void tail_fold(const double *part, int nblocks, double *out)
+{
+    __shared__ double sh[kBlock / 64][K];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += pub_load(part + (size_t)b * K + k);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        double r = sh[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
+        out[threadIdx.x] = r;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
+{
+    __shared__ IterState st;
+    __shared__ double loc[kNumSums], sums[kNumSums];
+    __shared__ int cnt0[4];
+    __shared__ int s_ok;
+    const int tid = threadIdx.x, b = blockIdx.x, nb = gridDim.x;
+    if (tid == 0) {
+        st = *a.s; // (read before the first barrier; only workgroup 0 writes it, after the last)
+        for (int k = 0; k < 4; ++k) cnt0[k] = 0;
+    }
+    __syncthreads();
+    const bool frozen = st.done != 0;
+    // shifted_moments_kernel
+    {
+        const double cp0 = st.shift_p[0], cp1 = st.shift_p[1], cp2 = st.shift_p[2];
+        const double cy0 = st.shift_y[0], cy1 = st.shift_y[1], cy2 = st.shift_y[2];
+        double m[17];
+#pragma unroll
+        for (int k = 0; k < 17; ++k) m[k] = 0.0;
+        if (!frozen)
+            for (int i = b * kBlock + tid; i < a.n; i += nb * kBlock)
+                shifted_moment_point(i, a.idx, a.m4, a.px, a.py, a.pz, a.yx, a.yy, a.yz, cp0, cp1, cp2, cy0, cy1, cy2, m);
+        block_sum_store<17>(m, loc);
+        __syncthreads();
+        if (tid < 17) pub_store(a.part17 + (size_t)b * 17 + tid, loc[tid]);
+    }
+    if (!persist_barrier(a.sync, a.epoch_base + 1, a.h_abort, &s_ok)) return;
+    tail_fold<17>(a.part17, nb, sums); // reduce_kernel<17>
+    // horn_step_kernel (workgroup 0 folds and clears the NN queue counters)
+    if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 1, b == 0 ? a.cnt : cnt0, &st);
+    __syncthreads();
+    // transform_err_kernel (icp_run form)
+    {
+        double e[1] = {0.0};
+        if (!st.done) {
+            const Xform xf = st.xf;
+            for (int i = b * kBlock + tid; i < a.n; i += nb * kBlock) {
+                double q0, q1, q2;
+                transform_point(xf, a.px[i], a.py[i], a.pz[i], q0, q1, q2);
+                e[0] += residual2(a.yx[i], a.yy[i], a.yz[i], q0, q1, q2);
+                a.px[i] = q0;
+                a.py[i] = q1;
+                a.pz[i] = q2;
+                if (a.p32) a.p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
+                if (a.sa.seed16)
+                    a.sa.seed16[i] = mfma16_seed_value(q0, q1, q2, a.yx[i], a.yy[i], a.yz[i], a.sa.c[0], a.sa.c[1],
+                                                       a.sa.c[2], a.sa.scale);
+            }
+        }
+        block_sum_store<1>(e, loc);
+        __syncthreads();
+        if (tid == 0) pub_store(a.part1 + b, loc[0]);
+    }
+    if (!persist_barrier(a.sync, a.epoch_base + 2, a.h_abort, &s_ok)) return;
+    tail_fold<1>(a.part1, nb, sums + kSumErr); // reduce_kernel<1>
+    // err_step_kernel, and the loop state back to memory
+    if (b == 0 && tid == 0) {
+        if (a.sums_out) { // (A/B: the error step as its own launch)
+            for (int k = 0; k < kNumSums; ++k) a.sums_out[k] = sums[k];
+        } else {
+            err_step_body(sums, a.N, a.threshold, a.max_iter, a.err_trace, &st, a.hflag, a.ticket, a.h_state, a.h_trace);
+        }
+        *a.s = st;
+    }
+}
+
 } // namespace
+
+void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t st)
+{
+    iteration_tail_grid_kernel<<<nblocks, kBlock, 0, st>>>(args);
+}
 
 size_t persistent_static_lds()
 {

@@ -320,6 +320,35 @@ void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, 
 size_t persistent_static_lds(); // the kernel's static LDS bytes
 // (host) the kernel's model image; *blocks_out = 64-point blocks (icp_engine.hip)
 std::vector<double> persist_model_image(const double *m_xyz, size_t nm, size_t *blocks_out);
+// Iterations >= 2 of a single-rank run with 4,096 < n: shifted moments, reduce, Horn step,
+// transform + residual, reduce and error step in ONE launch of red_blocks(n) co-resident
+// workgroups with two grid barriers (icp_iter.hip); bit-identical to the six launches.
+struct TailArgs {
+    const int *idx;
+    const double4 *m4;
+    double *px, *py, *pz;
+    int n;
+    double *yx, *yy, *yz;
+    float4 *p32;
+    SeedArgs sa;
+    double *part17, *part1; // published partials: red_blocks(n) x 17, red_blocks(n)
+    unsigned *sync;         // kPersistSyncWords barrier words, counting from zero within a run
+    unsigned epoch_base;    // barriers of the run's earlier launches (two each)
+    int *h_abort;           // mapped host: set if a barrier timed out
+    double N, c0, c1, c2;
+    int *cnt;               // the NN queue counters (folded into the statistics, then zeroed)
+    IterState *s;
+    double threshold;
+    int max_iter;
+    double *err_trace;
+    int *hflag;
+    int ticket;
+    IterState *h_state;
+    double *h_trace;
+    double *sums_out; // non-null: write the reduced sums there and leave the error step to a launch
+};
+constexpr int kTailMaxBlocks = 192; // red_blocks(n) <= this (n <= 49,152): co-resident with room
+void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t st);
 // zero a run's IterState and the NN queue counters (amb_count[0..3])
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st);
 

@@ -487,7 +487,7 @@ __device__ __forceinline__ double seed_shift(unsigned seed)
     return -(hi + lo) * 16384.0;
 }
 
-constexpr double kF16QueryClamp = 32000.0;
+// (kF16QueryClamp: icp_device.h)
 constexpr int kTile16 = 512; // model points per LDS tile of the f16 filter (16 KiB), x2 buffers
 // s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8])
 constexpr int kVmcnt0 = 0x0F70;                   // vmcnt(0)
@@ -1249,31 +1249,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     }
 }
 
-// Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
-// s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see
-// nn_finalize_mfma16_kernel), rounded outward by 2^-20 and split into f16 hi/lo of -s0 / 2^14.
-// seed of query p (unscaled fp64) from a model point m: packed f16 (hi | lo << 16) of -s0 / 2^14
-__device__ __forceinline__ unsigned mfma16_seed_value(double p0, double p1, double p2, double m0, double m1,
-                                                      double m2, double cx, double cy, double cz, double scale)
-{
-    const double a0 = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double a1 = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double a2 = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
-    const double b0 = (m0 - cx) * scale, b1 = (m1 - cy) * scale, b2 = (m2 - cz) * scale;
-    const double bb = b0 * b0 + b1 * b1 + b2 * b2;
-    const double G = bb - 2.0 * (a0 * b0 + a1 * b1 + a2 * b2);
-    const double u = 0x1.0p-24;
-    const double A = sqrt(a0 * a0 + a1 * a1 + a2 * a2), R = sqrt(bb);
-    const double span = R * R + 2.0 * A * R;
-    const double ds = 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * (fabs(G) + 1e-3 * span) +
-                      4.0 * u * (A + R) + 1e-3;
-    double s0 = G + 4.0 * ds + 1.0;
-    s0 += fabs(s0) * 0x1.0p-20;
-    const double x = fmin(fmax(-s0 / 16384.0, -65000.0), 65000.0);
-    const _Float16 hi = (_Float16)x;
-    const _Float16 lo = (_Float16)(x - (double)hi);
-    return (unsigned)__builtin_bit_cast(unsigned short, hi) | ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
-}
+// (mfma16_seed_value: icp_device.h, shared with the fused iteration tail of icp_iter.hip)
 
 __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,

@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("ICP_AMD_LIB", os.path.join(_HERE, "build", "libicp_hip.so"))
+LIB_PATH = os.environ.get("ICP_AMD_LIB") or os.path.join(_HERE, "build", "libicp_hip.so")
 
 ICP_OK = 0
 ICP_E_ARG = -1

@@ -162,3 +162,34 @@ def test_ties_and_degenerate_models_bitwise(amd, case):
     loop = run(amd, m, p, amd.RUN_LAUNCHES, 5, -1.0)
     assert one[9] == 1 and one[0] == 5
     assert_same(one, loop)
+
+
+# ---- the fused iteration tail of mid-size runs (4,096 < n <= 49,152): one launch for moments,
+# reduce, Horn, transform, reduce and error step, bit-identical to the six launches ----------
+
+
+@pytest.mark.parametrize("pair,iters,threshold,nn_mode,variant", [
+    (("horse_ref", "horse_tr1"), 50, 1e-5, 0, 0),   # C3 as bench.py runs it
+    (("horse_ref", "horse_tr2"), 20, 1e-5, 0, 0),   # converges at 8
+    (("bun000", "bun045"), 50, 1e-5, 0, 0),         # C2 (allow_unequal)
+    (("bun000", "bun045"), 6, -1.0, 1, 0),          # fp64 NN
+    (("horse_ref", "horse_tr1"), 6, -1.0, 0, 4),    # grid variant
+])
+def test_fused_tail_matches_launches(amd, pair, iters, threshold, nn_mode, variant):
+    m = amd.load_matrix(datasets.path(pair[0]))
+    p = amd.load_matrix(datasets.path(pair[1]))
+    fused = run(amd, m, p, amd.RUN_AUTO, iters, threshold, nn_mode, variant)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, iters, threshold, nn_mode, variant)
+    assert fused[9] == loop[9] == 0  # (not the one-launch registration: n > 4,096)
+    assert_same(fused, loop)
+
+
+@pytest.mark.parametrize("n,nm", [(4097, 4097), (8192, 3000), (12345, 20000), (49152, 49152)])
+def test_fused_tail_random_sizes(amd, n, nm):
+    rng = np.random.default_rng(n + 3 * nm)
+    m = rng.normal(size=(nm, 3))
+    p = m[rng.integers(0, nm, n)] @ np.array([[0.99, -0.1, 0.0], [0.1, 0.99, 0.0], [0.0, 0.0, 1.0]]).T + 0.03
+    fused = run(amd, m, p, amd.RUN_AUTO, 7, -1.0)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 7, -1.0)
+    assert fused[0] == 7
+    assert_same(fused, loop)
