@@ -206,14 +206,16 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
 def baseline_configs(device, reps=3):
     """BASELINE.json configs C2 (bun000 vs bun045, allow_unequal) and C3 (horse_ref vs horse_tr1):
     complete 50-iteration registrations (reference semantics, threshold 1e-5; neither converges
-    within 50) on this GPU with the default NN path, and with the exact grid variant beside it
-    (the same trajectory bit for bit)."""
+    within 50) on this GPU with the default path -- one launch per registration
+    (icp_persistent_mid_kernel: culled exact fp64 NN) -- and beside it the launch loop with the
+    brute-force f16 MFMA filter and the exact grid variant (the same trajectory bit for bit)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import datasets
 
-    def registration(m, p, unequal, variant):
+    def registration(m, p, unequal, variant, mode=icp_amd.RUN_AUTO):
         with icp_amd.Context(device) as ctx:
             ctx.set_nn_variant(variant)
+            ctx.set_run_mode(mode)
             ctx.set_allow_unequal(unequal)
             ctx.set_model(m)
             ctx.set_scene(p)
@@ -231,11 +233,15 @@ def baseline_configs(device, reps=3):
         m = icp_amd.load_matrix(datasets.path(ref))
         p = icp_amd.load_matrix(datasets.path(scene))
         res, errs, dt, st = registration(m, p, unequal, icp_amd.VARIANT_AUTO)
+        lres, lerrs, ldt, lst = registration(m, p, unequal, icp_amd.VARIANT_AUTO, icp_amd.RUN_LAUNCHES)
         gres, gerrs, gdt, _ = registration(m, p, unequal, icp_amd.VARIANT_GRID)
         out[name] = {"n_model": int(m.shape[0]), "n_scene": int(p.shape[0]), "iterations": res.iterations,
                      "ms_per_registration": dt * 1e3, "iterations_per_s": res.iterations / dt,
-                     "nn_filter_ms": st["nn_ms"] / max(st["nn_launches"], 1),
+                     "path": "one launch per registration" if st["persistent_runs"] else "launch loop",
                      "final_err": float(errs[res.iterations - 1]),
+                     "launch_loop": {"iterations_per_s": lres.iterations / ldt, "ms_per_registration": ldt * 1e3,
+                                     "nn_filter_ms": lst["nn_ms"] / max(lst["nn_launches"], 1),
+                                     "same_trajectory": bool(np.array_equal(lerrs, errs))},
                      "grid_variant": {"iterations_per_s": gres.iterations / gdt, "ms_per_registration": gdt * 1e3,
                                       "same_trajectory": bool(np.array_equal(gerrs, errs))}}
     return out

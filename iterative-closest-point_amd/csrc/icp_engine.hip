@@ -26,43 +26,51 @@
 
 using namespace icp;
 
-// The one-launch loop's model image: points in Morton order of their 10-bit quantised
-// coordinates (ties: original index), split into 64-point blocks with exact fp64 boxes, so
-// that a query scans only the blocks whose box is within its seed distance.  Layout (doubles):
-// x[nm] | y[nm] | z[nm] | blocks x (lo x, lo y, lo z, hi x, hi y, hi z) | int32 original
-// index per sorted position (packed two per double).
+// The one-launch loops' model image: points in the order of a kd split -- a range of more
+// than 1,024 points splits at a multiple of 1,024, one of more than 64 at a multiple of 64, one
+// of more than 16 at a multiple of 16, each at about its middle along the widest axis of its
+// box (nth_element; ties: original index) -- so that every 16-point block, 64-point tile and
+// 1,024-point superblock is a kd cell and their boxes barely overlap.  Layout (doubles):
+// x[nm] | y[nm] | z[nm] | 64-point blocks x (lo x, lo y, lo z, hi x, hi y, hi z) | int32
+// original index per sorted position (packed two per double) | superblocks (16 consecutive
+// blocks) x their boxes, the same six doubles | the 64-point blocks' then the 16-point blocks'
+// boxes as six floats each, rounded outward (the mid-size kernel's LDS copy).
 std::vector<double> icp::persist_model_image(const double *m, size_t nm, size_t *blocks_out)
 {
-    double lo[3] = {m[0], m[1], m[2]}, hi[3] = {m[0], m[1], m[2]};
-    for (size_t j = 1; j < nm; ++j)
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], m[3 * j + a]);
-            hi[a] = std::max(hi[a], m[3 * j + a]);
-        }
-    auto spread = [](uint64_t v) { // 10 bits -> every third bit
-        v &= 0x3ff;
-        v = (v | (v << 16)) & 0x30000ff;
-        v = (v | (v << 8)) & 0x300f00f;
-        v = (v | (v << 4)) & 0x30c30c3;
-        v = (v | (v << 2)) & 0x9249249;
-        return v;
-    };
-    std::vector<uint64_t> key(nm);
-    for (size_t j = 0; j < nm; ++j) {
-        uint64_t code = 0;
-        for (int a = 0; a < 3; ++a) {
-            const double w = hi[a] - lo[a];
-            const double t = w > 0 ? (m[3 * j + a] - lo[a]) / w * 1023.0 : 0.0;
-            code |= spread((uint64_t)std::min(1023.0, std::max(0.0, t))) << a;
-        }
-        key[j] = (code << 32) | (uint64_t)j; // (code, original index): a total order
+    std::vector<uint32_t> ord(nm);
+    for (size_t j = 0; j < nm; ++j) ord[j] = (uint32_t)j;
+    std::vector<std::pair<size_t, size_t>> stack{{0, nm}};
+    while (!stack.empty()) {
+        const auto [lo, hi] = stack.back();
+        stack.pop_back();
+        const size_t cnt = hi - lo;
+        const size_t unit = cnt > 1024 ? 1024 : cnt > 64 ? 64 : cnt > 16 ? 16 : 0;
+        if (!unit) continue;
+        double bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = lo; k < hi; ++k)
+            for (int a = 0; a < 3; ++a) {
+                bl[a] = std::min(bl[a], m[3 * ord[k] + a]);
+                bh[a] = std::max(bh[a], m[3 * ord[k] + a]);
+            }
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+            if (bh[a] - bl[a] > bh[ax] - bl[ax]) ax = a;
+        const size_t units = (cnt + unit - 1) / unit, mid = lo + unit * ((units + 1) / 2);
+        if (mid >= hi) continue; // (one unit: a leaf at this level, split below)
+        std::nth_element(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, [&](uint32_t x, uint32_t y) {
+            const double vx = m[3 * x + ax], vy = m[3 * y + ax];
+            return vx < vy || (vx == vy && x < y);
+        });
+        stack.push_back({lo, mid});
+        stack.push_back({mid, hi});
     }
-    std::sort(key.begin(), key.end());
     const size_t nb = (nm + 63) / 64;
-    std::vector<double> img(3 * nm + 6 * nb + (nm + 1) / 2);
+    const size_t nsb = (nb + 15) / 16, nb16 = (nm + 15) / 16;
+    const size_t nf32 = 6 * (nb + nb16);
+    std::vector<double> img(3 * nm + 6 * nb + (nm + 1) / 2 + 6 * nsb + (nf32 + 1) / 2);
     int32_t *orig = (int32_t *)(img.data() + 3 * nm + 6 * nb);
     for (size_t k = 0; k < nm; ++k) {
-        const size_t j = (size_t)(key[k] & 0xffffffffu);
+        const size_t j = ord[k];
         for (int a = 0; a < 3; ++a) img[a * nm + k] = m[3 * j + a];
         orig[k] = (int32_t)j;
     }
@@ -78,6 +86,44 @@ std::vector<double> icp::persist_model_image(const double *m, size_t nm, size_t 
                 box[3 + a] = std::max(box[3 + a], img[a * nm + k]);
             }
     }
+    double *sbox = img.data() + 3 * nm + 6 * nb + (nm + 1) / 2;
+    for (size_t s = 0; s < nsb; ++s) {
+        const double *first = img.data() + 3 * nm + 6 * (16 * s);
+        for (int a = 0; a < 6; ++a) sbox[6 * s + a] = first[a];
+        for (size_t b = 16 * s + 1; b < std::min(nb, 16 * s + 16); ++b) {
+            const double *box = img.data() + 3 * nm + 6 * b;
+            for (int a = 0; a < 3; ++a) {
+                sbox[6 * s + a] = std::min(sbox[6 * s + a], box[a]);
+                sbox[6 * s + 3 + a] = std::max(sbox[6 * s + 3 + a], box[3 + a]);
+            }
+        }
+    }
+    // fp32 boxes rounded outward: each contains its exact box, so its distance is a lower bound
+    float *f32 = (float *)(sbox + 6 * nsb);
+    auto down = [](double v) {
+        float f = (float)v;
+        return (double)f > v ? std::nextafter(f, -INFINITY) : f;
+    };
+    auto up = [](double v) {
+        float f = (float)v;
+        return (double)f < v ? std::nextafter(f, INFINITY) : f;
+    };
+    for (size_t b = 0; b < nb; ++b)
+        for (int a = 0; a < 3; ++a) {
+            f32[6 * b + a] = down(img[3 * nm + 6 * b + a]);
+            f32[6 * b + 3 + a] = up(img[3 * nm + 6 * b + 3 + a]);
+        }
+    float *f16b = f32 + 6 * nb;
+    for (size_t b = 0; b < nb16; ++b)
+        for (int a = 0; a < 3; ++a) {
+            double lo = img[a * nm + 16 * b], hi = lo;
+            for (size_t k = 16 * b + 1; k < std::min(nm, 16 * b + 16); ++k) {
+                lo = std::min(lo, img[a * nm + k]);
+                hi = std::max(hi, img[a * nm + k]);
+            }
+            f16b[6 * b + a] = down(lo);
+            f16b[6 * b + 3 + a] = up(hi);
+        }
     *blocks_out = nb;
     return img;
 }
@@ -196,6 +242,12 @@ struct icp_ctx {
     size_t pers_part_cap = 0, pers_sync_cap = 0;
     double *tail_part = nullptr;     // fused mid-size tail: published partials (18 x kTailMaxBlocks)
     unsigned *tail_sync = nullptr;   // its barrier words
+    double *mid_q4 = nullptr;        // mid-size one-launch loop: published queries (4 per point)
+    int *mid_res = nullptr;          // and their correspondences
+    int *mid_perm = nullptr;         // its search order (each point's row)
+    char *mid_cnt = nullptr;         // the order's scratch (radix sort)
+    double m_lo[3] = {0, 0, 0}, m_hi[3] = {0, 0, 0}; // the model's box
+    size_t mid_q4_cap = 0, mid_res_cap = 0, mid_perm_cap = 0, mid_cnt_cap = 0;
     size_t tail_part_cap = 0, tail_sync_cap = 0;
     bool pers_sync_valid = false;    // the barrier words hold pers_epoch_base barriers of grid pers_grid
     unsigned pers_epoch_base = 0;
@@ -836,7 +888,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
                     (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->cr_entries,
-                    (void *)ctx->cr_count, (void *)ctx->tail_part, (void *)ctx->tail_sync})
+                    (void *)ctx->cr_count, (void *)ctx->tail_part, (void *)ctx->tail_sync,
+                    (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -956,10 +1009,19 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
                       ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->st);
     LAUNCHCHK("grid_build");
     std::vector<double> pm;
-    if (nm <= (size_t)kPersistMaxModel) { // the one-launch loop's Morton-ordered model image
+    if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel)) { // the one-launch loops' model image
         pm = persist_model_image(m_xyz, nm, &ctx->pm_blocks);
         TRY(grow(ctx, &ctx->pm_img, &ctx->pm_img_cap, pm.size()));
         HIPCHK(hipMemcpyAsync(ctx->pm_img, pm.data(), sizeof(double) * pm.size(), hipMemcpyHostToDevice, ctx->st));
+        for (int k = 0; k < 3; ++k) { // the model's box (the mid-size loop's search order)
+            ctx->m_lo[k] = INFINITY;
+            ctx->m_hi[k] = -INFINITY;
+        }
+        for (size_t j = 0; j < nm; ++j)
+            for (int k = 0; k < 3; ++k) {
+                ctx->m_lo[k] = std::min(ctx->m_lo[k], m_xyz[3 * j + k]);
+                ctx->m_hi[k] = std::max(ctx->m_hi[k], m_xyz[3 * j + k]);
+            }
     }
     HIPCHK(hipStreamSynchronize(ctx->st));
     ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
@@ -1056,10 +1118,14 @@ static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_res
 static bool lag_run(const icp_ctx *ctx) { return ctx->comm != nullptr || ctx->world > 1; }
 
 // Workgroups of the one-launch registration for this run, or 0 if it does not apply: one
-// rank, no communicator, n <= kRedSingle (the single-workgroup passes it reproduces bit for
-// bit), the model in LDS, >= 64 co-resident workgroups, no per-iteration instrumentation.
-static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *lds_out)
+// rank, no communicator, no per-iteration instrumentation, and either
+//  - n <= kRedSingle (the single-workgroup passes it reproduces bit for bit), the model in
+//    LDS, >= 64 co-resident workgroups (icp_persistent_kernel), or
+//  - kRedSingle < n <= kTailMaxBlocks * 256, red_blocks(n) workgroups co-resident with a
+//    quarter of the CUs to spare, nm <= kPersistMidMaxModel (icp_persistent_mid_kernel; *mid_out).
+static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *lds_out, bool *mid_out)
 {
+    *mid_out = false;
     static const int forced = [] { // ICP_RUN_MODE=launches|persistent (A/B runs)
         const char *e = getenv("ICP_RUN_MODE");
         if (!e) return -1;
@@ -1071,7 +1137,27 @@ static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *l
     if (mode == ICP_RUN_AUTO && ctx->nn_variant != ICP_NN_VARIANT_AUTO) return 0; // explicit variants run their cascade
     if (ctx->world != 1 || ctx->comm || ctx->host_reduce || ctx->digest_cap || max_iter < 1) return 0;
     if (ctx->nn_rule != ICP_NN_RULE_SQUARED) return 0; // (the host resolves the CPU rule's near ties)
-    if (n < 4 || n > (size_t)kRedSingle || ctx->nm < 1 || ctx->nm > (size_t)kPersistMaxModel) return 0;
+    if (n > (size_t)kRedSingle) {
+        static const bool mid_off = [] { // ICP_PERSIST_MID=0: mid-size runs keep the launch loop (A/B)
+            const char *e = getenv("ICP_PERSIST_MID");
+            return e && std::strcmp(e, "0") == 0;
+        }();
+        if (mid_off || n > (size_t)kTailMaxBlocks * kBlock || ctx->nm < 1 || ctx->nm > (size_t)kPersistMidMaxModel ||
+            !ctx->pm_img)
+            return 0;
+        // the classic red_blocks(n) workgroups, widened to the whole co-resident grid: the extra
+        // ones own no point and only search (their partial rows are +0.0, which leaves
+        // reduce_kernel's tree bit for bit unchanged)
+        const int classic = red_blocks(n), wide = std::min(kTailMaxBlocks, ctx->n_cu * 3 / 4);
+        const int grid = std::max(classic, wide);
+        if (grid > ctx->n_cu * 3 / 4 || grid > kTailMaxBlocks || (size_t)classic * kBlock < n) return 0;
+        const size_t lds = 24 * (ctx->pm_blocks + (ctx->nm + 15) / 16);
+        if (lds > kPersistMidLdsMax || lds + persistent_mid_static_lds() > ctx->lds_per_cu) return 0;
+        *lds_out = lds;
+        *mid_out = true;
+        return grid;
+    }
+    if (n < 4 || ctx->nm < 1 || ctx->nm > (size_t)kPersistMaxModel) return 0;
     const size_t lds = 24 * ctx->nm + 48 * ctx->pm_blocks, statics = persistent_static_lds();
     if (!ctx->pm_img) return 0;
     if (lds + statics > ctx->lds_per_cu) return 0; // (gfx950: one workgroup may take the whole 160 KiB)
@@ -1087,17 +1173,19 @@ static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *l
 }
 
 // icp_run as ONE launch (launch_icp_persistent): same results, bit for bit, as the loop below.
-static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, double threshold, double *err_trace,
-                          icp_result *res, std::chrono::steady_clock::time_point wall0)
+static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_iter, double threshold,
+                          double *err_trace, icp_result *res, std::chrono::steady_clock::time_point wall0)
 {
+    static_assert(2 * kTailMaxBlocks <= 2 * kBlock, "pers_part holds the mid kernel's rows");
     const size_t n = ctx->scene.n;
     DevCloud &P = ctx->scene, &Y = ctx->Y;
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n)); // (a fresh context has run no search yet)
     TRY(grow(ctx, &ctx->pers_part, &ctx->pers_part_cap, (size_t)2 * kBlock * kNumSums));
     static const bool stamps = getenv("ICP_PERSIST_STAMPS") != nullptr;
     if (stamps) {
-        TRY(grow(ctx, &ctx->pers_stamps, &ctx->pers_stamps_cap, (size_t)2 * kPersistMaxStamps + 2 * kBlock));
-        HIPCHK(hipMemsetAsync(ctx->pers_stamps, 0, sizeof(unsigned long long) * (2 * kPersistMaxStamps + 2 * kBlock), ctx->st));
+        const size_t ns = (size_t)2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock;
+        TRY(grow(ctx, &ctx->pers_stamps, &ctx->pers_stamps_cap, ns));
+        HIPCHK(hipMemsetAsync(ctx->pers_stamps, 0, sizeof(unsigned long long) * ns, ctx->st));
     }
     TRY(grow(ctx, &ctx->pers_sync, &ctx->pers_sync_cap, kPersistSyncWords));
     // the barrier words count on from the previous launch of the same grid (no memset launch);
@@ -1145,12 +1233,36 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, doub
     a.epoch_base = ctx->pers_epoch_base;
     a.h_epochs = ctx->d_flags + 7;
     for (int k = 0; k < 3; ++k) a.m0[k] = ctx->model_host[k];
-    launch_icp_persistent(a, grid, lds, ctx->st);
+    if (mid) {
+        // the first search seeds the kernel's culled scan: one pass of the exact cascade (the
+        // resident correspondences if they pair this scene already), so that even a far first
+        // iteration admits only the blocks within each query's exact NN distance
+        if (!ctx->seeds_valid) {
+            launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
+            TRY(nn_search_begin(ctx, P, n, false, nullptr, nullptr, false, false, &ctx->iter_state->done));
+        }
+        TRY(grow(ctx, &ctx->mid_q4, &ctx->mid_q4_cap, 4 * n));
+        TRY(grow(ctx, &ctx->mid_res, &ctx->mid_res_cap, n));
+        TRY(grow(ctx, &ctx->mid_perm, &ctx->mid_perm_cap, n));
+        const size_t ob = mid_order_scratch_bytes((int)n);
+        TRY(grow(ctx, (char **)&ctx->mid_cnt, &ctx->mid_cnt_cap, ob));
+        if (launch_mid_order(P.x, P.y, P.z, (int)n, ctx->m_lo, ctx->m_hi, ctx->mid_cnt, ob, ctx->mid_perm, ctx->st))
+            return fail(ctx, ICP_E_HIP, "icp_run: the mid-size search order (radix sort) failed");
+        LAUNCHCHK("mid_order");
+        a.perm = ctx->mid_perm;
+        a.seed_idx = ctx->idx;
+        a.m4 = ctx->m4;
+        a.q4 = ctx->mid_q4;
+        a.res = ctx->mid_res;
+        launch_icp_persistent_mid(a, grid, lds, ctx->st);
+    } else {
+        launch_icp_persistent(a, grid, lds, ctx->st);
+    }
     LAUNCHCHK("icp_persistent");
     HIPCHK(hipStreamSynchronize(ctx->st));
     if (stamps) { // phase durations of workgroup 0 (tags: 0 NN begin, 1 NN end, 2 published,
                   // 3 barrier passed, 8 partials loaded, 4 folded, 5 Horn done, 6 transformed, 7 end)
-        std::vector<unsigned long long> h(2 * kPersistMaxStamps + 2 * kBlock);
+        std::vector<unsigned long long> h(2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock);
         HIPCHK(hipMemcpy(h.data(), ctx->pers_stamps, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
         double acc[9] = {0}, cntp[9] = {0};
         for (int k = 1; k < kPersistMaxStamps && h[2 * k + 1]; ++k) {
@@ -1168,6 +1280,18 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, int max_iter, doub
         }
         fprintf(stderr, " | per-wg NN min/mean/max %.1f/%.1f/%.1f barrier %.1f/%.1f/%.1f us\n", nmin, nsum / grid, nmax,
                 bmin, bsum / grid, bmax);
+        if (mid) { // per workgroup: NN us (all iterations, first), superblocks / tile rounds / blocks per query
+            const unsigned long long *w = h.data() + 2 * kPersistMaxStamps + 2 * kBlock;
+            double mx[5] = {0}, sm[5] = {0};
+            for (int g = 0; g < grid; ++g) {
+                const double q = std::max<double>(1.0, (double)w[8 * g + 5]);
+                const double v[5] = {w[8 * g] * 0.01, w[8 * g + 1] * 0.01, w[8 * g + 2] / q, w[8 * g + 3] / q, w[8 * g + 4] / q};
+                for (int k = 0; k < 5; ++k) mx[k] = std::max(mx[k], v[k]), sm[k] += v[k];
+            }
+            fprintf(stderr, "[persist-mid] per wg mean/max: NN %.1f/%.1f us (first %.1f/%.1f) | per query (batch counts /4): "
+                            "superblocks %.2f/%.2f tile rounds %.2f/%.2f blocks %.2f/%.2f\n",
+                    sm[0] / grid, mx[0], sm[1] / grid, mx[1], sm[2] / grid, mx[2], sm[3] / grid, mx[3], sm[4] / grid, mx[4]);
+        }
     }
     if (__atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE) != 0) {
         return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the one-launch loop timed out (workgroups not co-resident)");
@@ -1239,8 +1363,9 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
     }
     {
         size_t lds = 0;
-        const int grid = persistent_grid(ctx, n, max_iter, &lds);
-        if (grid) return run_persistent(ctx, grid, lds, max_iter, threshold, err_trace, res, wall0);
+        bool mid = false;
+        const int grid = persistent_grid(ctx, n, max_iter, &lds, &mid);
+        if (grid) return run_persistent(ctx, grid, lds, mid, max_iter, threshold, err_trace, res, wall0);
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     // mid-size single-rank runs: iterations >= 2 end in ONE fused launch (moments ... error step)
@@ -1254,7 +1379,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
                             tail_blocks <= ctx->n_cu * 3 / 4;
     unsigned tail_epoch = 0;
     if (fused_tail) {
-        TRY(grow(ctx, &ctx->tail_part, &ctx->tail_part_cap, (size_t)18 * kTailMaxBlocks));
+        TRY(grow(ctx, &ctx->tail_part, &ctx->tail_part_cap, (size_t)19 * kTailMaxBlocks));
         TRY(grow(ctx, &ctx->tail_sync, &ctx->tail_sync_cap, kPersistSyncWords));
         HIPCHK(hipMemsetAsync(ctx->tail_sync, 0, kPersistSyncWords * sizeof(unsigned), ctx->st));
         ctx->h_flags[11] = 0; // its barriers' abort word (mapped host)
@@ -1338,7 +1463,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
                 ta.p32 = P.f;
                 ta.sa = sa;
                 ta.part17 = ctx->tail_part;
-                ta.part1 = ctx->tail_part + (size_t)17 * kTailMaxBlocks;
+                ta.part1 = ctx->tail_part + (size_t)18 * kTailMaxBlocks;
                 ta.sync = ctx->tail_sync;
                 ta.epoch_base = tail_epoch;
                 ta.h_abort = ctx->d_flags + 11;

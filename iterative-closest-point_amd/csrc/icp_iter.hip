@@ -679,8 +679,33 @@ __device__ __forceinline__ double pub_load(const double *p)
                                                              __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// reduce_kernel<K>'s result from the published partials (rows of K doubles), into LDS out[0..K)
-template <int K> __device__ __forceinline__ void tail_fold(const double *part, int nblocks, double *out)
+// Row b (K of its S doubles) of the published partials, with write-through-coherent (sc1)
+// loads issued together: 16-byte buffer loads when the row is 16-byte aligned (S even), else
+// agent-scope atomic loads.
+template <int K, int S> __device__ __forceinline__ void load_row(const double *part, int nblocks, int b, double (&v)[K])
+{
+    if constexpr (S % 2 == 0) {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)part, (short)0, (int)((size_t)nblocks * S * sizeof(double)), 0x00020000);
+        const int base = (int)((size_t)b * S * sizeof(double));
+        constexpr int G = (K + 1) / 2;
+        decltype(__builtin_amdgcn_raw_buffer_load_b128(rsrc, 0, 0, 0)) g[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, base + 16 * j, 0, 16 /* sc1 */);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const auto &q = g[k / 2];
+            const unsigned lo = (k & 1) ? q[2] : q[0], hi = (k & 1) ? q[3] : q[1];
+            v[k] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = pub_load(part + (size_t)b * S + k);
+    }
+}
+
+// reduce_kernel<K>'s result from the published partials (rows of S >= K doubles), into LDS out[0..K)
+template <int K, int S = K> __device__ __forceinline__ void tail_fold(const double *part, int nblocks, double *out)
 {
     __shared__ double sh[kBlock / 64][K];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -688,8 +713,10 @@ template <int K> __device__ __forceinline__ void tail_fold(const double *part, i
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = 0.0;
     for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+        double v[K];
+        load_row<K, S>(part, nblocks, b, v);
 #pragma unroll
-        for (int k = 0; k < K; ++k) a[k] += pub_load(part + (size_t)b * K + k);
+        for (int k = 0; k < K; ++k) a[k] += v[k];
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -735,10 +762,10 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
                 shifted_moment_point(i, a.idx, a.m4, a.px, a.py, a.pz, a.yx, a.yy, a.yz, cp0, cp1, cp2, cy0, cy1, cy2, m);
         block_sum_store<17>(m, loc);
         __syncthreads();
-        if (tid < 17) pub_store(a.part17 + (size_t)b * 17 + tid, loc[tid]);
+        if (tid < 17) pub_store(a.part17 + (size_t)b * 18 + tid, loc[tid]); // (18: 16-byte rows)
     }
     if (!persist_barrier(a.sync, a.epoch_base + 1, a.h_abort, &s_ok)) return;
-    tail_fold<17>(a.part17, nb, sums); // reduce_kernel<17>
+    tail_fold<17, 18>(a.part17, nb, sums); // reduce_kernel<17>
     // horn_step_kernel (workgroup 0 folds and clears the NN queue counters)
     if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 1, b == 0 ? a.cnt : cnt0, &st);
     __syncthreads();
@@ -777,11 +804,536 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
     }
 }
 
+// ---- a whole mid-size registration in ONE launch ------------------------------------------------
+//
+// For a single-rank run of 4,096 < n <= 49,152 scene points against a model of <= 65,536 points
+// (C2, C3), the launch loop is still ~10 launches per iteration: the f16 filter and its
+// finalize/resolve cascade, then the fused tail.  This kernel runs the whole of icp_run as one
+// launch of min(192, 3/4 of the CUs) co-resident 512-thread workgroups.
+//
+// Bit-identity.  Thread t < 256 of workgroup b < red_blocks(n) = ceil(n / 256) owns point
+// i = 256 b + t, so each classic per-thread partial is one point's terms and each workgroup's
+// 256-thread sum tree is the classic workgroup's partial; the workgroups beyond the classic grid
+// own no point and publish +0.0 rows, which leave reduce_kernel's tree unchanged bit for bit.
+// Partials cross the grid through write-through stores and persist_barrier (as above) and every
+// workgroup folds them with reduce_kernel's tree: every sum, Horn solve, transform and error is
+// BIT-IDENTICAL to the launch loop.
+//
+// Per iteration, three grid barriers: (1) the NN of every point by the whole grid; (2) the one-
+// pass moments (the first iteration: the reference's two passes, two barriers), then Horn and
+// commit + transform in every workgroup; (3) the residual, then the error test right after its
+// transform as in the loop (gpu.cc:71-80) -- nothing is computed past the iteration that stops.
+//
+// NN.  Each owner publishes its point and seed distance (row my_pos of a.q4, in the search order
+// of launch_mid_order: stably sorted by a 32^3 Morton cell, so that a batch's four queries lie
+// close together whatever order the cloud came in) and wave w of the grid takes the 4-query
+// batches w, w + W, ... of that order: every wave samples the whole scene, so no workgroup waits
+// on a costly region of its own.  The search is an exact fp64 first minimum over the model
+// image (global memory, L2 resident: <= 1.6 MB, in kd order) with a three-level box hierarchy:
+// superblocks of 1,024 points (<= 64, one per lane, exact boxes in registers), tiles of 64 and
+// blocks of 16 points (boxes rounded outward to fp32, in LDS).  A query's seed distance r2 is its
+// distance to its previous correspondence (first iteration: from one pass of the exact cascade
+// before the launch, icp_run); every model point at least as close lies in a block whose box is
+// within r2 (1 + 2^-40) + 2^-900 -- the small kernel's bound; an outward-rounded box only admits
+// more -- and the seed point is one of them, so the lexicographic (D64, original index) minimum
+// over the admitted blocks is the global one.  Lane 16 u + j tests tile j of an admitted
+// superblock for query u; lane 16 i + 4 u + b block b of the i-th admitted tile for query u; lane
+// 16 u + j scans point j of each admitted block (four blocks' gathers in flight together) for
+// query u.  Distances follow compute.cu:112-117.
+constexpr int kMidSb = 16;     // 64-point tiles per superblock
+constexpr int kMidThreads = 512;
+
+// squared distance from q to the box (lo x, lo y, lo z, hi x, hi y, hi z) -- the small kernel's
+template <typename T> __device__ __forceinline__ double box_dist2(const T *bx, double qx, double qy, double qz)
+{
+    const double ex = fmax((double)bx[0] - qx, qx - (double)bx[3]), ey = fmax((double)bx[1] - qy, qy - (double)bx[4]),
+                 ez = fmax((double)bx[2] - qz, qz - (double)bx[5]);
+    const double fx = ex > 0.0 ? ex : 0.0, fy = ey > 0.0 ? ey : 0.0, fz = ez > 0.0 ? ez : 0.0;
+    return (fx * fx + fy * fy) + fz * fz;
+}
+
+template <typename T> __device__ __forceinline__ T pick4(int u, T a0, T a1, T a2, T a3)
+{
+    return u == 0 ? a0 : u == 1 ? a1 : u == 2 ? a2 : a3;
+}
+
+// argmin of (d, j) over the lane group of width W (xor tree): the lowest j among the smallest d
+template <int W> __device__ __forceinline__ int group_argmin(double d, int j)
+{
+#pragma unroll
+    for (int o = W / 2; o >= 1; o >>= 1) {
+        const double od = __shfl_xor(d, o, 64);
+        const int oj = __shfl_xor(j, o, 64);
+        const bool t = (od < d) | ((od == d) & (oj < j));
+        d = t ? od : d;
+        j = t ? oj : j;
+    }
+    return j;
+}
+
+// block_sum_store<K> (the classic 256-thread tree) inside a 512-thread workgroup: waves 4..7
+// take part in the synchronisation only
+template <int K> __device__ __forceinline__ void classic_sum(double (&a)[K], double *out)
+{
+    __shared__ double sh[kBlock / 64][K];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += __shfl_down(a[k], off, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0 && wave < kBlock / 64)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        out[k] = ((sh[0][k] + sh[1][k]) + sh[2][k]) + sh[3][k];
+    }
+}
+
+// tail_fold<K, S> (reduce_kernel's tree) inside a 512-thread workgroup
+template <int K, int S> __device__ __forceinline__ void classic_fold(const double *part, int nblocks, double *out)
+{
+    __shared__ double sh[kBlock / 64][K];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.0;
+    if (threadIdx.x < kBlock)
+        for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+            double v[K];
+            load_row<K, S>(part, nblocks, b, v);
+#pragma unroll
+            for (int k = 0; k < K; ++k) a[k] += v[k];
+        }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    }
+    if (lane == 0 && wave < kBlock / 64) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        double r = sh[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
+        out[threadIdx.x] = r;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void pub_store_i(int *p, int v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int pub_load_i(const int *p)
+{
+    return __hip_atomic_load((int *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(PersistArgs a)
+{
+    // tile boxes (ntile x 6 floats) | block boxes (nb16 x 6 floats), outward-rounded fp32
+    extern __shared__ __attribute__((aligned(16))) float s_box32[];
+    __shared__ IterState st;
+    __shared__ double loc[kPersistK], sums[kPersistK];
+    __shared__ int cnt0[4];
+    __shared__ int s_ok;
+    __shared__ unsigned s_cnt[3]; // (stamps only) admitted superblocks, tile rounds, blocks scanned
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int b = blockIdx.x, nb = gridDim.x;
+    const int n = a.n, nm = a.nm, ntile = a.nblk, nsb = (ntile + kMidSb - 1) / kMidSb, nb16 = (nm + 15) / 16;
+    const double *__restrict__ mxg = a.img, *__restrict__ myg = a.img + nm, *__restrict__ mzg = a.img + 2 * nm;
+    const int *__restrict__ orig = (const int *)(a.img + 3 * nm + 6 * ntile);
+    const double *__restrict__ sboxes = a.img + 3 * nm + 6 * ntile + (nm + 1) / 2;
+    const float *__restrict__ box32g = (const float *)(sboxes + 6 * nsb);
+    const float *tbox = s_box32, *bbox = s_box32 + 6 * ntile;
+    for (int k = tid; k < 6 * (ntile + nb16); k += kMidThreads) s_box32[k] = box32g[k];
+    const int i = b * kBlock + tid; // this thread's point (threads < 256: the classic passes' thread)
+    const bool own = tid < kBlock && i < n;
+    double p0 = own ? a.px[i] : 0.0, p1 = own ? a.py[i] : 0.0, p2 = own ? a.pz[i] : 0.0;
+    double y0 = 0.0, y1 = 0.0, y2 = 0.0;
+    if (own) { // the first search is seeded by an exact pass already made (icp_run)
+        const double4 m = a.m4[a.seed_idx[i]];
+        y0 = m.x;
+        y1 = m.y;
+        y2 = m.z;
+    }
+    if (tid == 0) {
+        for (size_t w = 0; w < sizeof(IterState) / sizeof(int); ++w) ((int *)&st)[w] = 0;
+        for (int k = 0; k < 4; ++k) cnt0[k] = 0;
+        for (int k = 0; k < 3; ++k) s_cnt[k] = 0;
+    }
+    // this lane's superblock box (lane < nsb), for every query of the run
+    double sbx[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) sbx[k] = lane < nsb ? sboxes[6 * lane + k] : 0.0;
+    __syncthreads();
+
+    unsigned epoch = 0;
+    int nstamp = 0;
+    persist_stamp(a.stamps, nstamp, 0);
+    double *const part0 = a.part, *const part1 = a.part + (size_t)kTailMaxBlocks * kPersistK;
+    auto barrier = [&]() -> bool {
+        ++epoch;
+        return persist_barrier(a.sync, a.epoch_base + epoch, a.h_abort, &s_ok);
+    };
+    // publish loc[0..K) (this workgroup's partials), barrier, fold the grid's rows into sums[0..K)
+    auto exchange = [&](int K) -> bool {
+        double *part = (epoch & 1u) ? part1 : part0;
+        if (tid < K) pub_store(part + (size_t)b * kPersistK + tid, loc[tid]);
+        persist_stamp(a.stamps, nstamp, 2);
+        if (!barrier()) return false;
+        persist_stamp(a.stamps, nstamp, 3);
+        switch (K) { // per column: reduce_kernel<K>'s tree
+        case 1: classic_fold<1, kPersistK>(part, nb, sums); break;
+        case 6: classic_fold<6, kPersistK>(part, nb, sums); break;
+        case 11: classic_fold<11, kPersistK>(part, nb, sums); break;
+        default: classic_fold<kPersistK - 1, kPersistK>(part, nb, sums); break;
+        }
+        persist_stamp(a.stamps, nstamp, 4);
+        return true;
+    };
+    // the owned point's search input for any wave of the grid: position and seed distance
+    // (rows in the search order: the owned point's row is my_pos = a.perm[i])
+    const int my_pos = own ? a.perm[i] : 0;
+    auto publish_query = [&]() {
+        if (own) {
+            const double dx = p0 - y0, dy = p1 - y1, dz = p2 - y2;
+            double *q = a.q4 + 4 * (size_t)my_pos;
+            pub_store(q, p0);
+            pub_store(q + 1, p1);
+            pub_store(q + 2, p2);
+            pub_store(q + 3, (dx * dx + dy * dy) + dz * dz); // (the scan's own arithmetic: the seed is admitted)
+        }
+    };
+    const __amdgpu_buffer_rsrc_t q4r =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.q4, (short)0, (int)((size_t)n * 32), 0x00020000);
+
+    // NN of the queries q0 .. q0 + nq4 - 1 (the wave's lanes work together); results to a.res
+    const int lu = lane >> 4, lj = lane & 15;           // scan layout: query u, point j of a block
+    const int li = lane >> 4, lu2 = (lane >> 2) & 3, lb = lane & 3; // block test: tile i, query u, block b
+    auto nn_batch = [&](int q0, int nq4) {
+        double qx[4], qy[4], qz[4], lim[4];
+        {
+            decltype(__builtin_amdgcn_raw_buffer_load_b128(q4r, 0, 0, 0)) g[8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { // (a repeated query past the end: same result, not stored)
+                const int off = 32 * (q0 + min(u, nq4 - 1));
+                g[2 * u] = __builtin_amdgcn_raw_buffer_load_b128(q4r, off, 0, 16 /* sc1 */);
+                g[2 * u + 1] = __builtin_amdgcn_raw_buffer_load_b128(q4r, off + 16, 0, 16);
+            }
+            auto dbl = [](unsigned lo, unsigned hi) {
+                return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            };
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                qx[u] = dbl(g[2 * u][0], g[2 * u][1]);
+                qy[u] = dbl(g[2 * u][2], g[2 * u][3]);
+                qz[u] = dbl(g[2 * u + 1][0], g[2 * u + 1][1]);
+                const double r2 = a.cull ? dbl(g[2 * u + 1][2], g[2 * u + 1][3]) : (double)INFINITY;
+                lim[u] = r2 * (1.0 + 0x1p-40) + 0x1p-900;
+            }
+        }
+        unsigned long long sm[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sm[u] = __ballot(lane < nsb && box_dist2(sbx, qx[u], qy[u], qz[u]) <= lim[u]);
+        unsigned long long S = sm[0] | sm[1] | sm[2] | sm[3];
+        // per-lane views of the batch
+        const double sqx = pick4(lu, qx[0], qx[1], qx[2], qx[3]), sqy = pick4(lu, qy[0], qy[1], qy[2], qy[3]),
+                     sqz = pick4(lu, qz[0], qz[1], qz[2], qz[3]), slim = pick4(lu, lim[0], lim[1], lim[2], lim[3]);
+        const unsigned long long ssm = pick4(lu, sm[0], sm[1], sm[2], sm[3]);
+        const double tqx = pick4(lu2, qx[0], qx[1], qx[2], qx[3]), tqy = pick4(lu2, qy[0], qy[1], qy[2], qy[3]),
+                     tqz = pick4(lu2, qz[0], qz[1], qz[2], qz[3]), tlim = pick4(lu2, lim[0], lim[1], lim[2], lim[3]);
+        double bd = INFINITY;
+        int bk = 0x7fffffff;
+        unsigned c_sb = 0, c_tr = 0, c_bl = 0;
+        while (S) { // wave-uniform: one admitted superblock per trip
+            const int s = __ffsll((long long)S) - 1;
+            S &= S - 1;
+            ++c_sb;
+            const int t = kMidSb * s + lj;
+            const unsigned long long tm =
+                __ballot(((ssm >> s) & 1ull) && t < ntile && box_dist2(tbox + 6 * t, sqx, sqy, sqz) <= slim);
+            unsigned T = (unsigned)((tm | (tm >> 16) | (tm >> 32) | (tm >> 48)) & 0xffffull);
+            while (T) { // up to four admitted tiles per trip
+                ++c_tr;
+                int tj[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    tj[r] = T ? __ffs((int)T) - 1 : -1;
+                    T &= T - 1;
+                }
+                const int mj = pick4(li, tj[0], tj[1], tj[2], tj[3]);
+                const int bl = 4 * (kMidSb * s + mj) + lb;
+                const bool hit = mj >= 0 && ((tm >> (16 * lu2 + mj)) & 1ull) && bl < nb16 &&
+                                 box_dist2(bbox + 6 * bl, tqx, tqy, tqz) <= tlim;
+                const unsigned long long bm = __ballot(hit); // bit 16 i + 4 u + b
+                const unsigned long long any = bm | (bm >> 4) | (bm >> 8) | (bm >> 12);
+                unsigned A = (unsigned)((any & 0xf) | ((any >> 12) & 0xf0) | ((any >> 24) & 0xf00) | ((any >> 36) & 0xf000));
+                while (A) { // up to four admitted blocks per trip (their gathers in flight together):
+                            // lane 16 u + j scans point j of each for query u
+                    int kc[4];
+                    bool valid[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int ib = A ? __ffs((int)A) - 1 : -1;
+                        A &= A - 1;
+                        c_bl += ib >= 0;
+                        const int r = ib >> 2, bsel = ib & 3;
+                        const int blk = 4 * (kMidSb * s + pick4(r & 3, tj[0], tj[1], tj[2], tj[3])) + bsel;
+                        const int k = 16 * blk + lj;
+                        valid[g] = ib >= 0 && k < nm && ((bm >> (16 * r + 4 * lu + bsel)) & 1ull);
+                        kc[g] = ib >= 0 && k < nm ? k : nm - 1;
+                    }
+                    double mx[4], my[4], mz[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        mx[g] = mxg[kc[g]];
+                        my[g] = myg[kc[g]];
+                        mz[g] = mzg[kc[g]];
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const double dx = sqx - mx[g], dy = sqy - my[g], dz = sqz - mz[g];
+                        const double e = (dx * dx + dy * dy) + dz * dz; // compute.cu:112-117
+                        bool take = valid[g] & (e < bd);
+                        if (valid[g] & (e == bd) & (bd < INFINITY)) // a tie: the lower original index
+                            take = orig[kc[g]] < orig[min(bk, nm - 1)];
+                        bd = take ? e : bd;
+                        bk = take ? kc[g] : bk;
+                    }
+                }
+            }
+        }
+        // (D64, original index) minimum over the 16 lanes of each query: first by (D64, sorted
+        // position); only if another lane holds a different point at the same D64 (a tie across
+        // lanes, rare) by the original indices
+        double rd = bd;
+        int rk = bk;
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) {
+            const double od = __shfl_xor(rd, o, 64);
+            const int ok = __shfl_xor(rk, o, 64);
+            const bool take = (od < rd) | ((od == rd) & (ok < rk));
+            rd = take ? od : rd;
+            rk = take ? ok : rk;
+        }
+        if (__ballot((bd == rd) & (bk != rk) & (rd < INFINITY))) {
+            rd = bd;
+            rk = bk;
+            int ro = bk == 0x7fffffff ? 0x7fffffff : orig[min(bk, nm - 1)];
+#pragma unroll
+            for (int o = 8; o >= 1; o >>= 1) {
+                const double od = __shfl_xor(rd, o, 64);
+                const int oo = __shfl_xor(ro, o, 64), ok = __shfl_xor(rk, o, 64);
+                const bool take = (od < rd) | ((od == rd) & (oo < ro));
+                rd = take ? od : rd;
+                ro = take ? oo : ro;
+                rk = take ? ok : rk;
+            }
+        }
+        if (lj == 0 && lu < nq4) pub_store_i(a.res + q0 + lu, rk == 0x7fffffff ? -1 : rk);
+        if (a.stamps && lane == 0) {
+            atomicAdd(&s_cnt[0], c_sb);
+            atomicAdd(&s_cnt[1], c_tr);
+            atomicAdd(&s_cnt[2], c_bl);
+        }
+    };
+
+    // The grid's NN, spread: wave w of the grid takes the 4-query batches w, w + W, w + 2W, ...
+    // (W waves), so that every wave samples the whole scene and no workgroup waits on a costly
+    // region of its own.
+    const int ntask = (n + 3) / 4, nwaves = nb * (kMidThreads / 64), gw = b * (kMidThreads / 64) + (tid >> 6);
+    auto nn = [&](int) -> bool {
+        for (int v = gw; v < ntask; v += nwaves) nn_batch(4 * v, min(4, n - 4 * v));
+        return barrier();
+    };
+
+    auto err_step = [&](double e) { // gpu.cc:71-80 (err_step_body), on this workgroup's state
+        if (tid == 0) {
+            const double err = (e + e) / a.N;
+            if (b == 0) {
+                a.err_trace[st.iter] = err;
+                a.h_trace[st.iter] = err;
+            }
+            st.iter += 1;
+            if (err < a.threshold || st.iter >= a.max_iter) st.done = 1;
+            if (b == 0) {
+                const int *src = (const int *)&st;
+                int *dst = (int *)a.h_state;
+                for (size_t k = 0; k < sizeof(IterState) / sizeof(int); ++k) dst[k] = src[k];
+            }
+        }
+        __syncthreads();
+    };
+
+    unsigned long long wg_nn = 0, wg_nn0 = 0;
+    publish_query();
+    if (!barrier()) return;
+    for (int it = 0;; ++it) {
+        persist_stamp(a.stamps, nstamp, 0);
+        const unsigned long long t_nn = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        if (!nn(it)) return;
+        if (a.stamps && tid == 0) {
+            const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_nn;
+            wg_nn += dt;
+            if (it == 0) wg_nn0 = dt;
+        }
+        const int nk = own ? pub_load_i(a.res + my_pos) : -1;
+        const int no = nk >= 0 ? orig[nk] : 0;
+        const double n0 = nk >= 0 ? mxg[nk] : a.m0[0], n1 = nk >= 0 ? myg[nk] : a.m0[1],
+                     n2 = nk >= 0 ? mzg[nk] : a.m0[2];
+        persist_stamp(a.stamps, nstamp, 1);
+        if (it == 0) {
+            { // gather_moments_kernel: sum p, sum y
+                double t[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+                if (own) {
+                    t[0] += p0;
+                    t[1] += p1;
+                    t[2] += p2;
+                    t[3] += n0;
+                    t[4] += n1;
+                    t[5] += n2;
+                }
+                classic_sum<6>(t, loc);
+                if (!exchange(6)) return;
+            }
+            const double mpx = sums[kSumP] / a.N, mpy = sums[kSumP + 1] / a.N, mpz = sums[kSumP + 2] / a.N;
+            const double myx = sums[kSumY] / a.N, myy = sums[kSumY + 1] / a.N, myz = sums[kSumY + 2] / a.N;
+            double keep[6];
+            for (int k = 0; k < 6; ++k) keep[k] = sums[k];
+            { // centred_moments_kernel: S, d_caps, sp around the means
+                double t[11];
+#pragma unroll
+                for (int k = 0; k < 11; ++k) t[k] = 0.0;
+                if (own) {
+                    const double q0 = p0 - mpx, q1 = p1 - mpy, q2 = p2 - mpz;
+                    const double w0 = n0 - myx, w1 = n1 - myy, w2 = n2 - myz;
+                    t[0] += q0 * w0;
+                    t[1] += q0 * w1;
+                    t[2] += q0 * w2;
+                    t[3] += q1 * w0;
+                    t[4] += q1 * w1;
+                    t[5] += q1 * w2;
+                    t[6] += q2 * w0;
+                    t[7] += q2 * w1;
+                    t[8] += q2 * w2;
+                    t[9] += (w0 * w0 + w1 * w1) + w2 * w2;
+                    t[10] += (q0 * q0 + q1 * q1) + q2 * q2;
+                }
+                classic_sum<11>(t, loc);
+                if (!exchange(11)) return;
+            }
+            double S11[11];
+            for (int k = 0; k < 11; ++k) S11[k] = sums[k];
+            __syncthreads();
+            if (tid < 6) sums[tid] = keep[tid];
+            if (tid < 11) sums[kSumS + tid] = S11[tid];
+            __syncthreads();
+            if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 0, cnt0, &st);
+        } else { // shifted_moments_kernel
+            const double cp0 = st.shift_p[0], cp1 = st.shift_p[1], cp2 = st.shift_p[2];
+            const double cy0 = st.shift_y[0], cy1 = st.shift_y[1], cy2 = st.shift_y[2];
+            double m[17];
+#pragma unroll
+            for (int k = 0; k < 17; ++k) m[k] = 0.0;
+            if (own) {
+                const double q0 = p0 - cp0, q1 = p1 - cp1, q2 = p2 - cp2;
+                const double w0 = n0 - cy0, w1 = n1 - cy1, w2 = n2 - cy2;
+                m[0] += q0;
+                m[1] += q1;
+                m[2] += q2;
+                m[3] += w0;
+                m[4] += w1;
+                m[5] += w2;
+                m[6] += q0 * w0;
+                m[7] += q0 * w1;
+                m[8] += q0 * w2;
+                m[9] += q1 * w0;
+                m[10] += q1 * w1;
+                m[11] += q1 * w2;
+                m[12] += q2 * w0;
+                m[13] += q2 * w1;
+                m[14] += q2 * w2;
+                m[15] += (w0 * w0 + w1 * w1) + w2 * w2;
+                m[16] += (q0 * q0 + q1 * q1) + q2 * q2;
+            }
+            classic_sum<17>(m, loc);
+            if (!exchange(17)) return;
+            if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 1, cnt0, &st);
+        }
+        __syncthreads();
+        persist_stamp(a.stamps, nstamp, 5);
+        // the iteration's correspondences, then apply + residual (transform_err_kernel) and the
+        // next search's input
+        {
+            const Xform xf = st.xf;
+            double e[1] = {0.0};
+            y0 = n0;
+            y1 = n1;
+            y2 = n2;
+            if (own) {
+                a.idx[i] = nk >= 0 ? no : 0;
+                a.yx[i] = y0;
+                a.yy[i] = y1;
+                a.yz[i] = y2;
+                double q0, q1, q2;
+                transform_point(xf, p0, p1, p2, q0, q1, q2);
+                e[0] += residual2(y0, y1, y2, q0, q1, q2);
+                p0 = q0;
+                p1 = q1;
+                p2 = q2;
+                a.px[i] = q0;
+                a.py[i] = q1;
+                a.pz[i] = q2;
+                if (a.p32) a.p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
+            }
+            publish_query();
+            __syncthreads(); // (loc is rewritten below)
+            classic_sum<1>(e, loc);
+        }
+        persist_stamp(a.stamps, nstamp, 6);
+        if (!exchange(1)) return; // the residual: err_step right after its transform (gpu.cc:71-80)
+        err_step(sums[0]);
+        if (st.done) break;
+    }
+    persist_stamp(a.stamps, nstamp, 7);
+    if (a.stamps && tid == 0) { // per-workgroup: NN time (all, first), the scan counts
+        unsigned long long *w = a.stamps + 2 * kPersistMaxStamps + 2 * kBlock + 8 * b;
+        w[0] = wg_nn;
+        w[1] = wg_nn0;
+        w[2] = s_cnt[0];
+        w[3] = s_cnt[1];
+        w[4] = s_cnt[2];
+        w[5] = (unsigned long long)max(0, min(kBlock, n - b * kBlock));
+    }
+    if (b == 0 && tid == 0) {
+        *a.s_glob = st;
+        __hip_atomic_store(a.h_epochs, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 } // namespace
 
 void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t st)
 {
     iteration_tail_grid_kernel<<<nblocks, kBlock, 0, st>>>(args);
+}
+
+void launch_icp_persistent_mid(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st)
+{
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void *)icp_persistent_mid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kPersistMidLdsMax);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)attr;
+    icp_persistent_mid_kernel<<<grid, kMidThreads, lds_bytes, st>>>(args);
 }
 
 size_t persistent_static_lds()
@@ -791,6 +1343,19 @@ size_t persistent_static_lds()
         if (hipFuncGetAttributes(&fa, (const void *)icp_persistent_kernel) != hipSuccess) {
             (void)hipGetLastError();
             return (size_t)16 * 1024; // (conservative)
+        }
+        return (size_t)fa.sharedSizeBytes;
+    }();
+    return bytes;
+}
+
+size_t persistent_mid_static_lds()
+{
+    static const size_t bytes = [] {
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, (const void *)icp_persistent_mid_kernel) != hipSuccess) {
+            (void)hipGetLastError();
+            return (size_t)32 * 1024; // (conservative)
         }
         return (size_t)fa.sharedSizeBytes;
     }();

@@ -313,12 +313,30 @@ struct PersistArgs {
     double m0[3];               // model point 0 (a NaN query's correspondence)
     unsigned epoch_base;        // barriers of earlier launches on the same sync words (monotonic)
     int *h_epochs;              // mapped host: the barriers this launch used
+    const int *seed_idx;        // (mid-size kernel) exact correspondences seeding the first search
+    const double4 *m4;          // the model as double4 rows (with seed_idx)
+    double *q4;                 // (mid-size kernel) n x (x, y, z, seed distance): the published queries
+    int *res;                   // (mid-size kernel) n: their correspondences (sorted positions)
+    const int *perm;            // (mid-size kernel) n: each point's row in the search order (launch_mid_order)
 };
+// pos[q] = query q's place when the queries are sorted, stably, by their cell of a 32^3 grid over
+// the box [lo, hi] (Morton order of the cells) (icp_order.hip); scratch: mid_order_scratch_bytes(n)
+size_t mid_order_scratch_bytes(int n);
+int launch_mid_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
+                     const double hi[3], void *scratch, size_t bytes, int *pos, hipStream_t st);
 constexpr int kPersistMaxStamps = 1024;
 constexpr int kPersistSyncWords = 512; // barrier words (icp_iter.hip: persist_barrier)
 void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st);
+// The same for 4,096 < n <= kTailMaxBlocks * 256 (icp_persistent_mid_kernel): grid = red_blocks(n)
+// workgroups of 512 threads, the model image in global memory (nm <= kPersistMidMaxModel: <= 64
+// superblocks of 16 tiles), its fp32 tile and block boxes in LDS (lds_bytes = 24 (tiles +
+// ceil(nm / 16))), part = 2 x kTailMaxBlocks x kNumSums.
+constexpr int kPersistMidMaxModel = 64 * 16 * 64;
+constexpr size_t kPersistMidLdsMax = 24 * (kPersistMidMaxModel / 64 + kPersistMidMaxModel / 16);
+void launch_icp_persistent_mid(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st);
+size_t persistent_mid_static_lds();
 size_t persistent_static_lds(); // the kernel's static LDS bytes
-// (host) the kernel's model image; *blocks_out = 64-point blocks (icp_engine.hip)
+// (host) the kernels' model image; *blocks_out = 64-point blocks (icp_engine.hip)
 std::vector<double> persist_model_image(const double *m_xyz, size_t nm, size_t *blocks_out);
 // Iterations >= 2 of a single-rank run with 4,096 < n: shifted moments, reduce, Horn step,
 // transform + residual, reduce and error step in ONE launch of red_blocks(n) co-resident
@@ -331,7 +349,7 @@ struct TailArgs {
     double *yx, *yy, *yz;
     float4 *p32;
     SeedArgs sa;
-    double *part17, *part1; // published partials: red_blocks(n) x 17, red_blocks(n)
+    double *part17, *part1; // published partials: red_blocks(n) rows of 18 (17 used), red_blocks(n)
     unsigned *sync;         // kPersistSyncWords barrier words, counting from zero within a run
     unsigned epoch_base;    // barriers of the run's earlier launches (two each)
     int *h_abort;           // mapped host: set if a barrier timed out

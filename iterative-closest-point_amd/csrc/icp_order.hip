@@ -1,0 +1,83 @@
+// icp_order.hip — the mid-size one-launch loop's search order (icp_iter.hip,
+// icp_persistent_mid_kernel): the scene's queries sorted by the Morton cell of a 32^3 grid over
+// the model's box that holds them, stably (file order within a cell), so that the four queries
+// of a search batch lie close together whatever order the cloud came in.  The order only decides
+// which queries share a batch; every result is the exact first minimum regardless.
+#include <hip/hip_runtime.h>
+#include <hipcub/device/device_radix_sort.hpp>
+
+#include "icp_kernels.h"
+
+namespace icp {
+namespace {
+
+struct OrderBox {
+    double lo[3], sc[3];
+};
+
+__device__ __forceinline__ unsigned order_key(double x, double y, double z, const OrderBox &bx)
+{
+    auto cell = [](double v, double l, double s) {
+        const double t = (v - l) * s;
+        return !(t > 0.0) ? 0u : t >= 31.0 ? 31u : (unsigned)t; // (NaN: cell 0; outside: border cells)
+    };
+    auto spread = [](unsigned v) { // 5 bits -> every third bit
+        v = (v | (v << 8)) & 0x0300f00fu;
+        v = (v | (v << 4)) & 0x030c30c3u;
+        v = (v | (v << 2)) & 0x09249249u;
+        return v;
+    };
+    return spread(cell(x, bx.lo[0], bx.sc[0])) | (spread(cell(y, bx.lo[1], bx.sc[1])) << 1) |
+           (spread(cell(z, bx.lo[2], bx.sc[2])) << 2);
+}
+
+__global__ __launch_bounds__(kBlock) void order_keys_kernel(const double *__restrict__ px, const double *__restrict__ py,
+                                                          const double *__restrict__ pz, int n, OrderBox bx,
+                                                          unsigned *__restrict__ key, int *__restrict__ val)
+{
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q < n) {
+        key[q] = order_key(px[q], py[q], pz[q], bx);
+        val[q] = q;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void order_pos_kernel(const int *__restrict__ sorted, int n, int *__restrict__ pos)
+{
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < n) pos[sorted[k]] = k;
+}
+
+constexpr int kOrderBits = 15;
+
+} // namespace
+
+size_t mid_order_scratch_bytes(int n)
+{
+    size_t temp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned *)nullptr, (unsigned *)nullptr,
+                                             (const int *)nullptr, (int *)nullptr, n, 0, kOrderBits);
+    return 4 * (size_t)n * sizeof(int) + ((temp + 255) & ~(size_t)255);
+}
+
+int launch_mid_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
+                     const double hi[3], void *scratch, size_t bytes, int *pos, hipStream_t st)
+{
+    OrderBox bx;
+    for (int k = 0; k < 3; ++k) {
+        bx.lo[k] = lo[k];
+        bx.sc[k] = hi[k] > lo[k] ? 32.0 / (hi[k] - lo[k]) : 0.0;
+    }
+    unsigned *k0 = (unsigned *)scratch, *k1 = k0 + n;
+    int *v0 = (int *)(k1 + n), *v1 = v0 + n;
+    void *temp = v1 + n;
+    size_t temp_bytes = bytes - 4 * (size_t)n * sizeof(int);
+    const int g = (n + kBlock - 1) / kBlock;
+    order_keys_kernel<<<g, kBlock, 0, st>>>(px, py, pz, n, bx, k0, v0);
+    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, v1, n, 0, kOrderBits, st) != hipSuccess)
+        return -1;
+    order_pos_kernel<<<g, kBlock, 0, st>>>(v1, n, pos);
+    return 0;
+}
+
+} // namespace icp

@@ -103,10 +103,12 @@ def test_nan_scene_point(amd):
 def test_ineligible_runs_take_the_launch_loop(amd):
     rng = np.random.default_rng(4)
     m = rng.uniform(-1, 1, size=(5000, 3))
-    p = rng.uniform(-1, 1, size=(4097, 3))  # n > 4096: beyond the single-workgroup passes
+    p = rng.uniform(-1, 1, size=(49153, 3))  # n > 192 x 256: beyond the co-resident classic grid
     assert run(amd, m, p, amd.RUN_PERSISTENT, 2, -1.0)[9] == 0
-    m = rng.uniform(-1, 1, size=(9000, 3))  # model beyond LDS
+    m = rng.uniform(-1, 1, size=(9000, 3))  # model beyond LDS (small kernel)
     assert run(amd, m, p[:3000], amd.RUN_PERSISTENT, 2, -1.0)[9] == 0
+    m = rng.uniform(-1, 1, size=(65537, 3))  # model beyond 64 superblocks (mid-size kernel)
+    assert run(amd, m, p[:5000], amd.RUN_PERSISTENT, 2, -1.0)[9] == 0
     m = rng.uniform(-1, 1, size=(3000, 3))  # an explicit NN variant keeps its own cascade under AUTO
     assert run(amd, m, p[:3000], amd.RUN_AUTO, 2, -1.0, variant=amd.VARIANT_GRID)[9] == 0
 
@@ -165,14 +167,15 @@ def test_ties_and_degenerate_models_bitwise(amd, case):
 
 
 # ---- the fused iteration tail of mid-size runs (4,096 < n <= 49,152): one launch for moments,
-# reduce, Horn, transform, reduce and error step, bit-identical to the six launches ----------
+# reduce, Horn, transform, reduce and error step, bit-identical to the six launches.  (Under
+# AUTO an explicit NN variant keeps the launch loop, whose iterations end in the fused tail.) --
 
 
 @pytest.mark.parametrize("pair,iters,threshold,nn_mode,variant", [
-    (("horse_ref", "horse_tr1"), 50, 1e-5, 0, 0),   # C3 as bench.py runs it
-    (("horse_ref", "horse_tr2"), 20, 1e-5, 0, 0),   # converges at 8
-    (("bun000", "bun045"), 50, 1e-5, 0, 0),         # C2 (allow_unequal)
-    (("bun000", "bun045"), 6, -1.0, 1, 0),          # fp64 NN
+    (("horse_ref", "horse_tr1"), 50, 1e-5, 0, 3),   # C3 with the default cascade's f16 filter
+    (("horse_ref", "horse_tr2"), 20, 1e-5, 0, 3),   # converges at 8
+    (("bun000", "bun045"), 50, 1e-5, 0, 3),         # C2 (allow_unequal)
+    (("bun000", "bun045"), 6, -1.0, 1, 3),          # fp64 NN
     (("horse_ref", "horse_tr1"), 6, -1.0, 0, 4),    # grid variant
 ])
 def test_fused_tail_matches_launches(amd, pair, iters, threshold, nn_mode, variant):
@@ -189,7 +192,112 @@ def test_fused_tail_random_sizes(amd, n, nm):
     rng = np.random.default_rng(n + 3 * nm)
     m = rng.normal(size=(nm, 3))
     p = m[rng.integers(0, nm, n)] @ np.array([[0.99, -0.1, 0.0], [0.1, 0.99, 0.0], [0.0, 0.0, 1.0]]).T + 0.03
-    fused = run(amd, m, p, amd.RUN_AUTO, 7, -1.0)
+    fused = run(amd, m, p, amd.RUN_AUTO, 7, -1.0, variant=amd.VARIANT_MFMA16)
     loop = run(amd, m, p, amd.RUN_LAUNCHES, 7, -1.0)
-    assert fused[0] == 7
+    assert fused[9] == 0 and fused[0] == 7
     assert_same(fused, loop)
+
+
+# ---- the one-launch registration of mid-size runs (icp_persistent_mid_kernel): 4,096 < n <=
+# 49,152 scene points, models up to 65,536 points in global memory; bit-identical to the loop --
+
+
+@pytest.mark.parametrize("pair,iters,threshold,nn_mode", [
+    (("horse_ref", "horse_tr1"), 50, 1e-5, 0),   # C3 as bench.py runs it
+    (("horse_ref", "horse_tr2"), 20, 1e-5, 0),   # converges at 8
+    (("bun000", "bun045"), 50, 1e-5, 0),         # C2 (allow_unequal)
+    (("bun000", "bun045"), 6, -1.0, 1),          # fp64 NN mode in the loop
+    (("horse_ref", "horse_tr1"), 1, -1.0, 0),    # one iteration: the first pass and the last residual
+    (("horse_ref", "horse_tr1"), 2, -1.0, 0),
+])
+def test_mid_one_launch_matches_launch_loop(amd, golden, pair, iters, threshold, nn_mode):
+    m = amd.load_matrix(datasets.path(pair[0]))
+    p = amd.load_matrix(datasets.path(pair[1]))
+    one = run(amd, m, p, amd.RUN_AUTO, iters, threshold, nn_mode)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, iters, threshold, nn_mode)
+    assert one[9] == 1 and loop[9] == 0  # the default takes the one launch
+    assert_same(one, loop)
+    if threshold > 0 and pair[1] in golden:
+        g = golden[pair[1]]
+        assert one[0] == g["iterations"]
+        np.testing.assert_allclose(one[6], g["err"], rtol=1e-9)
+
+
+MID_SIZES = [(4097, 4097), (4097, 1), (5000, 64), (8192, 3000), (12345, 20000), (30000, 65536),
+             (40000, 40000), (49152, 49152)]
+
+
+@pytest.mark.parametrize("n,nm", MID_SIZES)
+def test_mid_random_sizes_bitwise(amd, n, nm):
+    rng = np.random.default_rng(n * 31 + nm)
+    m = rng.uniform(-1, 1, size=(nm, 3))
+    a = rng.uniform(0.05, 0.3)
+    axis = rng.normal(size=3)
+    axis /= np.linalg.norm(axis)
+    k = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+    rot = np.eye(3) + np.sin(a) * k + (1 - np.cos(a)) * k @ k
+    p = m[rng.integers(0, nm, n)] @ rot.T + rng.normal(scale=0.05, size=3) + rng.normal(scale=0.01, size=(n, 3))
+    one = run(amd, m, p, amd.RUN_PERSISTENT, 6, -1.0)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 6, -1.0)
+    assert one[9] == 1 and loop[9] == 0
+    assert one[0] == 6
+    assert_same(one, loop)
+
+
+@pytest.mark.parametrize("case", ["lattice_ties", "duplicates", "far_scene", "planar", "nan_point"])
+def test_mid_ties_and_degenerate_models_bitwise(amd, case):
+    """The mid-size kernel's culled scan (superblocks, then blocks) on the small kernel's hard
+    cases at 4,096 < n: exact ties broken by original index, duplicated points, a scene far
+    outside the model, a planar model and a NaN scene point (index 0)."""
+    rng = np.random.default_rng(["lattice_ties", "duplicates", "far_scene", "planar", "nan_point"].index(case) + 90)
+    if case == "lattice_ties":
+        g = np.arange(-12, 13, dtype=float)
+        m = np.stack(np.meshgrid(g, g, g[:12], indexing="ij"), axis=-1).reshape(-1, 3)
+        m = m[rng.permutation(m.shape[0])]
+        p = m[rng.integers(0, m.shape[0], 9000)] + 0.5  # equidistant from up to 8 lattice points
+    elif case == "duplicates":
+        base = rng.uniform(-1, 1, size=(3000, 3))
+        m = np.concatenate([base, base[::-1], base[:1000]])
+        m = m[rng.permutation(m.shape[0])]
+        p = base[rng.integers(0, 3000, 8000)] + rng.normal(scale=1e-3, size=(8000, 3))
+    elif case == "far_scene":
+        m = rng.uniform(-1, 1, size=(6000, 3))
+        p = rng.uniform(-1, 1, size=(6000, 3)) + np.array([50.0, -20.0, 5.0])
+    elif case == "planar":
+        m = rng.uniform(-1, 1, size=(20000, 3))
+        m[:, 2] = 0.25
+        p = m[rng.integers(0, 20000, 20000)] + rng.normal(scale=0.02, size=(20000, 3))
+        p[:, 2] = 0.25 + 0.1
+    else:
+        m = rng.uniform(-1, 1, size=(10000, 3))
+        p = m + 0.01
+        p[4321, 1] = np.nan
+    one = run(amd, m, p, amd.RUN_PERSISTENT, 4, -1.0)
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 4, -1.0)
+    assert one[9] == 1 and one[0] == 4
+    if case == "nan_point":
+        assert one[8][4321] == 0  # a NaN query's correspondence is index 0 (the reference's scan)
+        for x, y in zip(one[6:9], loop[6:9]):
+            np.testing.assert_array_equal(x, y)
+    else:
+        assert_same(one, loop)
+
+
+def test_mid_repeated_runs_and_per_operation_calls(amd):
+    m = amd.load_matrix(datasets.path("horse_ref"))
+    p = amd.load_matrix(datasets.path("horse_tr2"))
+    outs = {}
+    for mode in (amd.RUN_PERSISTENT, amd.RUN_LAUNCHES):
+        with amd.Context(0) as ctx:
+            ctx.set_run_mode(mode)
+            ctx.set_model(m)
+            ctx.set_scene(p)
+            r1, e1 = ctx.run(3, -1.0)
+            r2, e2 = ctx.run(10, 1e-5)
+            s = ctx.get_scene()
+            _, idx = ctx.closest_matrix(s)
+            outs[mode] = (e1, e2, r2.iterations, s, idx, ctx.stats()["persistent_runs"])
+    a, b = outs[amd.RUN_PERSISTENT], outs[amd.RUN_LAUNCHES]
+    assert a[5] == 2 and b[5] == 0
+    for x, y in zip(a[:5], b[:5]):
+        np.testing.assert_array_equal(x, y)

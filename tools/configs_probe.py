@@ -19,7 +19,8 @@ import datasets  # noqa: E402
 
 CONFIGS = {"C2_bunny": ("bun000", "bun045", True), "C3_horse": ("horse_ref", "horse_tr1", False),
            "C1_cow_gpu": ("cow_ref", "cow_tr1", False)}
-VARIANTS = {"auto": 0, "valu": 1, "mfma": 2, "mfma16": 3, "grid": 4}
+VARIANTS = {"auto": 0, "valu": 1, "mfma": 2, "mfma16": 3, "grid": 4,
+            "loop": 0}  # loop: the default NN cascade in the launch loop (icp_set_run_mode LAUNCHES)
 
 
 def main():
@@ -42,6 +43,8 @@ def main():
         for v in a.variants:
             with icp_amd.Context(0, icp_amd.NN_CERTIFIED) as ctx:
                 ctx.set_nn_variant(VARIANTS[v])
+                if v == "loop":
+                    ctx.set_run_mode(icp_amd.RUN_LAUNCHES)
                 ctx.set_allow_unequal(unequal)
                 ctx.set_model(m)
                 ctx.set_scene(p)
@@ -59,6 +62,7 @@ def main():
                               "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1),
                               "queued_per_iter": st["level1_queued"] / max(st["iterations"], 1),
                               "fallback_per_iter": st["grid_fallback"] / max(st["iterations"], 1),
+                              "persistent_runs": st["persistent_runs"],
                               "final_err": float(errs[res.iterations - 1])}), flush=True)
 
 

@@ -103,6 +103,8 @@ for s in $STEPS; do
                --ref "$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_ref"))')" \
                --scene "$(python3 -c 'import sys; sys.path.insert(0, "tests"); import datasets; print(datasets.path("cow_tr1"))')" \
                --min-time 0.3 --only opti_gpu_loop || exit 1; cat $OUT/cowab_$m.log >> $OUT/cowab_all_$m.log; done ;;
+    midab) run midab 300 python tools/configs_probe.py --configs C2_bunny C3_horse syn20000 --variants auto loop --reps 5 &&
+           ICP_PERSIST_STAMPS=1 run midstamps 120 python tools/configs_probe.py --configs C3_horse C2_bunny --variants auto --reps 1 ;;
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
