@@ -1288,9 +1288,19 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
                 const double v[5] = {w[8 * g] * 0.01, w[8 * g + 1] * 0.01, w[8 * g + 2] / q, w[8 * g + 3] / q, w[8 * g + 4] / q};
                 for (int k = 0; k < 5; ++k) mx[k] = std::max(mx[k], v[k]), sm[k] += v[k];
             }
-            fprintf(stderr, "[persist-mid] per wg mean/max: NN %.1f/%.1f us (first %.1f/%.1f) | per query (batch counts /4): "
-                            "superblocks %.2f/%.2f tile rounds %.2f/%.2f blocks %.2f/%.2f\n",
-                    sm[0] / grid, mx[0], sm[1] / grid, mx[1], sm[2] / grid, mx[2], sm[3] / grid, mx[3], sm[4] / grid, mx[4]);
+            double tph[4] = {0, 0, 0, 0}, cnt[3] = {0, 0, 0};
+            for (int g = 0; g < grid; ++g) {
+                tph[0] += (double)(w[8 * g + 6] & 0xffffffffu) * 0.01;
+                tph[1] += (double)(w[8 * g + 6] >> 32) * 0.01;
+                tph[2] += (double)(w[8 * g + 7] & 0xffffffffu) * 0.01;
+                tph[3] += (double)(w[8 * g + 7] >> 32) * 0.01;
+                for (int k = 0; k < 3; ++k) cnt[k] += (double)w[8 * g + 2 + k];
+            }
+            const double nbat = (double)((ctx->scene.n + 3) / 4) * std::max(1, ctx->h_iter->iter);
+            fprintf(stderr, "[persist-mid] per wg NN mean/max %.1f/%.1f us (first %.1f/%.1f) | per batch: superblocks %.2f "
+                            "tile rounds %.2f blocks %.2f | per batch us: query loads %.2f tests %.2f gathers %.2f reduce+store %.2f\n",
+                    sm[0] / grid, mx[0], sm[1] / grid, mx[1], cnt[0] / nbat, cnt[1] / nbat, cnt[2] / nbat, tph[0] / nbat,
+                    tph[1] / nbat, tph[2] / nbat, tph[3] / nbat);
         }
     }
     if (__atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE) != 0) {

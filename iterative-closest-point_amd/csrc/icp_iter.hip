@@ -943,6 +943,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     __shared__ int cnt0[4];
     __shared__ int s_ok;
     __shared__ unsigned s_cnt[3]; // (stamps only) admitted superblocks, tile rounds, blocks scanned
+    __shared__ unsigned long long s_tph[4]; // (stamps only) wave time: query loads, superblock/tile tests, scans, reduce
     const int tid = threadIdx.x, lane = tid & 63;
     const int b = blockIdx.x, nb = gridDim.x;
     const int n = a.n, nm = a.nm, ntile = a.nblk, nsb = (ntile + kMidSb - 1) / kMidSb, nb16 = (nm + 15) / 16;
@@ -966,6 +967,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
         for (size_t w = 0; w < sizeof(IterState) / sizeof(int); ++w) ((int *)&st)[w] = 0;
         for (int k = 0; k < 4; ++k) cnt0[k] = 0;
         for (int k = 0; k < 3; ++k) s_cnt[k] = 0;
+        for (int k = 0; k < 4; ++k) s_tph[k] = 0;
     }
     // this lane's superblock box (lane < nsb), for every query of the run
     double sbx[6];
@@ -1017,6 +1019,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     const int lu = lane >> 4, lj = lane & 15;           // scan layout: query u, point j of a block
     const int li = lane >> 4, lu2 = (lane >> 2) & 3, lb = lane & 3; // block test: tile i, query u, block b
     auto nn_batch = [&](int q0, int nq4) {
+        unsigned long long tp0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, tsc = 0;
         double qx[4], qy[4], qz[4], lim[4];
         {
             decltype(__builtin_amdgcn_raw_buffer_load_b128(q4r, 0, 0, 0)) g[8];
@@ -1037,6 +1040,11 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
                 const double r2 = a.cull ? dbl(g[2 * u + 1][2], g[2 * u + 1][3]) : (double)INFINITY;
                 lim[u] = r2 * (1.0 + 0x1p-40) + 0x1p-900;
             }
+        }
+        unsigned long long tp1 = 0;
+        if (a.stamps) {
+            __builtin_amdgcn_s_waitcnt(0);
+            tp1 = __builtin_amdgcn_s_memrealtime();
         }
         unsigned long long sm[4];
 #pragma unroll
@@ -1089,12 +1097,17 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
                         valid[g] = ib >= 0 && k < nm && ((bm >> (16 * r + 4 * lu + bsel)) & 1ull);
                         kc[g] = ib >= 0 && k < nm ? k : nm - 1;
                     }
+                    const unsigned long long ts0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
                     double mx[4], my[4], mz[4];
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
                         mx[g] = mxg[kc[g]];
                         my[g] = myg[kc[g]];
                         mz[g] = mzg[kc[g]];
+                    }
+                    if (a.stamps) {
+                        __builtin_amdgcn_s_waitcnt(0);
+                        tsc += __builtin_amdgcn_s_memrealtime() - ts0;
                     }
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
@@ -1109,6 +1122,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
                 }
             }
         }
+        const unsigned long long tp2 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
         // (D64, original index) minimum over the 16 lanes of each query: first by (D64, sorted
         // position); only if another lane holds a different point at the same D64 (a tie across
         // lanes, rare) by the original indices
@@ -1141,6 +1155,12 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
             atomicAdd(&s_cnt[0], c_sb);
             atomicAdd(&s_cnt[1], c_tr);
             atomicAdd(&s_cnt[2], c_bl);
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long tp3 = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&s_tph[0], tp1 - tp0);
+            atomicAdd(&s_tph[1], tp2 - tp1 - tsc);
+            atomicAdd(&s_tph[2], tsc);
+            atomicAdd(&s_tph[3], tp3 - tp2);
         }
     };
 
@@ -1310,6 +1330,8 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
         w[3] = s_cnt[1];
         w[4] = s_cnt[2];
         w[5] = (unsigned long long)max(0, min(kBlock, n - b * kBlock));
+        w[6] = s_tph[0] | (s_tph[1] << 32); // (100 MHz ticks summed over the waves; < 2^32 each)
+        w[7] = s_tph[2] | (s_tph[3] << 32);
     }
     if (b == 0 && tid == 0) {
         *a.s_glob = st;
