@@ -144,9 +144,11 @@ int icp_set_allow_unequal(icp_ctx *ctx, int allow);
 int icp_set_nn_variant(icp_ctx *ctx, int variant);
 /* How icp_run executes (results are bit-identical either way):
  * LAUNCHES:   the device-resident loop of a few launches per iteration (any size, any rank count);
- * PERSISTENT: the whole run in ONE launch of co-resident workgroups holding the model in LDS,
- *             one grid barrier per iteration -- taken when the run is eligible: one rank without
- *             a communicator, 4 <= np <= 4096, nm <= ~6,400 points, no index digest;
+ * PERSISTENT: the whole run in ONE launch of co-resident workgroups -- taken when the run is
+ *             eligible: one rank without a communicator, the squared NN rule, no index digest,
+ *             and either 4 <= np <= 4096 with nm <= ~6,400 points (the model in LDS, one grid
+ *             barrier per iteration) or 4096 < np <= 49,152 with nm <= 65,536 (the model in
+ *             global memory, its block boxes in LDS, three grid barriers per iteration);
  * AUTO:       PERSISTENT for eligible runs with the AUTO NN variant (an explicitly chosen NN
  *             variant runs its own search cascade), else LAUNCHES.  The default.
  * The environment variable ICP_RUN_MODE=launches|persistent overrides (A/B runs). */
