@@ -96,6 +96,8 @@ typedef struct icp_stats {
     long long persistent_runs; /* icp_run calls that ran as ONE launch (icp_set_run_mode)      */
     long long cpu_rule_ties;   /* ICP_NN_RULE_CPU_SQRT: near ties evaluated on the host       */
     long long cpu_rule_changed; /* ... whose CPU-rule answer differs from the squared rule's   */
+    long long persistent_fallbacks; /* one-launch runs that found their grid not co-resident at
+                                       the first barrier and ran the launch loop instead         */
 } icp_stats;
 
 /* ---- context ------------------------------------------------------------ */

@@ -1173,6 +1173,9 @@ static int persistent_grid(const icp_ctx *ctx, size_t n, int max_iter, size_t *l
 }
 
 // icp_run as ONE launch (launch_icp_persistent): same results, bit for bit, as the loop below.
+// kPersistFallback: the launch gave up at its first grid barrier, before writing any state
+// (some workgroups were not co-resident); the caller runs the launch loop instead.
+constexpr int kPersistFallback = 1;
 static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_iter, double threshold,
                           double *err_trace, icp_result *res, std::chrono::steady_clock::time_point wall0)
 {
@@ -1232,6 +1235,10 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
     a.cull = cull;
     a.epoch_base = ctx->pers_epoch_base;
     a.h_epochs = ctx->d_flags + 7;
+    { // tests: ICP_PERSIST_TEST_ABORT=1 makes the first barrier fail as if a workgroup never came
+        const char *e = getenv("ICP_PERSIST_TEST_ABORT");
+        a.test_abort = e && e[0] == '1';
+    }
     for (int k = 0; k < 3; ++k) a.m0[k] = ctx->model_host[k];
     if (mid) {
         // the first search seeds the kernel's culled scan: one pass of the exact cascade (the
@@ -1303,9 +1310,13 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
                     tph[1] / nbat, tph[2] / nbat, tph[3] / nbat);
         }
     }
-    if (__atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE) != 0) {
-        return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the one-launch loop timed out (workgroups not co-resident)");
+    const int aborted = __atomic_load_n(ctx->h_flags + 3, __ATOMIC_ACQUIRE);
+    if (aborted == 1) { // at the first barrier: not co-resident, nothing written -> the launch loop
+        ctx->stats.persistent_fallbacks += 1;
+        return kPersistFallback;
     }
+    if (aborted != 0)
+        return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the one-launch loop timed out (workgroups not co-resident)");
     ctx->pers_epoch_base += (unsigned)__atomic_load_n(ctx->h_flags + 7, __ATOMIC_ACQUIRE);
     ctx->pers_sync_valid = true;
     ctx->seeds_valid = true;
@@ -1375,7 +1386,10 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         size_t lds = 0;
         bool mid = false;
         const int grid = persistent_grid(ctx, n, max_iter, &lds, &mid);
-        if (grid) return run_persistent(ctx, grid, lds, mid, max_iter, threshold, err_trace, res, wall0);
+        if (grid) {
+            const int r = run_persistent(ctx, grid, lds, mid, max_iter, threshold, err_trace, res, wall0);
+            if (r != kPersistFallback) return r;
+        }
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     // mid-size single-rank runs: iterations >= 2 end in ONE fused launch (moments ... error step)

@@ -190,6 +190,9 @@ constexpr int kPersistVT = kBlock;  // virtual threads (the single-workgroup pas
 constexpr int kPersistMaxOwn = 64;  // owned points per workgroup (G >= 64, n <= kRedSingle)
 constexpr int kPersistK = kNumSums; // widest published partial: 17 moments + 1 residual
 constexpr unsigned kPersistSpinLimit = 1u << 20; // polls (~1 us each) before a barrier gives up
+// The first barrier of a launch gives up sooner: if some workgroups are not co-resident (another
+// persistent kernel holds CUs), nothing has been written yet, so icp_run takes the launch loop.
+constexpr unsigned kPersistFirstSpinLimit = 1u << 14;
 
 static_assert(kRedSingle / kPersistVT * (kPersistVT / 64) <= kPersistMaxOwn, "owned points per workgroup");
 
@@ -200,6 +203,8 @@ __device__ __forceinline__ void pub_store(double *p, double v)
 }
 
 // Grid barrier number `e` (1-based); false if it timed out or another workgroup aborted.
+// *h_abort (mapped host) records why: 1 at the launch's first barrier (`first`: no state written
+// yet), 2 at a later one.  `force` (tests: icp_persist_test_abort) aborts the first barrier at once.
 // Every thread calls it after its own payload stores.  Two-level arrival: workgroup b counts
 // into group b % 8 (a label: which workgroups share an XCD under the usual round-robin
 // dispatch; correctness does not depend on it), the last arrival of a group into the top
@@ -209,11 +214,17 @@ __device__ __forceinline__ void pub_store(double *p, double v)
 //   sync[0] top counter   sync[1] abort word   sync[kSyncGrp + 16 g] group g's counter
 //   sync[kSyncGen + 16 g] group g's generation (one 64-byte line each)
 constexpr int kSyncGroups = 8, kSyncGrp = 16, kSyncGen = kSyncGrp + 16 * kSyncGroups;
-__device__ bool persist_barrier(unsigned *sync, unsigned e, int *h_abort, int *s_ok)
+__device__ bool persist_barrier(unsigned *sync, unsigned e, int *h_abort, int *s_ok, bool first = false,
+                                bool force = false)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's write-through stores have landed
     __syncthreads();
-    if (threadIdx.x == 0) {
+    const unsigned limit = first ? kPersistFirstSpinLimit : kPersistSpinLimit;
+    if (threadIdx.x == 0 && force && blockIdx.x == 0) {
+        __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(h_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *s_ok = 0;
+    } else if (threadIdx.x == 0) {
         const unsigned G = gridDim.x, b = blockIdx.x, g = b % kSyncGroups;
         const unsigned ng = G < kSyncGroups ? G : kSyncGroups;
         const unsigned gs = (G - g + kSyncGroups - 1) / kSyncGroups; // workgroups in group g
@@ -228,10 +239,10 @@ __device__ bool persist_barrier(unsigned *sync, unsigned e, int *h_abort, int *s
         for (unsigned spin = 1; __hip_atomic_load(sync + kSyncGen + 16 * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e;
              ++spin) {
             if ((spin & 63u) == 0u &&
-                (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || spin > kPersistSpinLimit)) {
+                (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || spin > limit)) {
                 ok = 0;
                 __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(h_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(h_abort, first ? 1 : 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -423,7 +434,8 @@ __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
         ++epoch;
         persist_stamp(a.stamps, nstamp, 2);
         const unsigned long long t_bar = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-        if (!persist_barrier(a.sync, a.epoch_base + epoch, a.h_abort, &s_ok)) return false;
+        if (!persist_barrier(a.sync, a.epoch_base + epoch, a.h_abort, &s_ok, epoch == 1, epoch == 1 && a.test_abort))
+            return false;
         if (a.stamps && tid == 0) wg_bar += __builtin_amdgcn_s_memrealtime() - t_bar;
         persist_stamp(a.stamps, nstamp, 3);
         switch (K) { // per column: the classic pass's block_sum_store<K> tree
@@ -981,7 +993,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     double *const part0 = a.part, *const part1 = a.part + (size_t)kTailMaxBlocks * kPersistK;
     auto barrier = [&]() -> bool {
         ++epoch;
-        return persist_barrier(a.sync, a.epoch_base + epoch, a.h_abort, &s_ok);
+        return persist_barrier(a.sync, a.epoch_base + epoch, a.h_abort, &s_ok, epoch == 1, epoch == 1 && a.test_abort);
     };
     // publish loc[0..K) (this workgroup's partials), barrier, fold the grid's rows into sums[0..K)
     auto exchange = [&](int K) -> bool {

@@ -318,6 +318,7 @@ struct PersistArgs {
     double *q4;                 // (mid-size kernel) n x (x, y, z, seed distance): the published queries
     int *res;                   // (mid-size kernel) n: their correspondences (sorted positions)
     const int *perm;            // (mid-size kernel) n: each point's row in the search order (launch_mid_order)
+    int test_abort;             // tests: abort at the first barrier, as if not co-resident
 };
 // pos[q] = query q's place when the queries are sorted, stably, by their cell of a 32^3 grid over
 // the box [lo, hi] (Morton order of the cells) (icp_order.hip); scratch: mid_order_scratch_bytes(n)

@@ -84,7 +84,7 @@ class Stats(C.Structure):
                 ("allreduce_calls", C.c_longlong), ("cert_max_err_ratio", C.c_double),
                 ("cert_min_margin", C.c_double), ("cert_audited", C.c_longlong),
                 ("persistent_runs", C.c_longlong), ("cpu_rule_ties", C.c_longlong),
-                ("cpu_rule_changed", C.c_longlong)]
+                ("cpu_rule_changed", C.c_longlong), ("persistent_fallbacks", C.c_longlong)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)

@@ -301,3 +301,32 @@ def test_mid_repeated_runs_and_per_operation_calls(amd):
     assert a[5] == 2 and b[5] == 0
     for x, y in zip(a[:5], b[:5]):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("pair", [("cow_ref", "cow_tr1"), ("horse_ref", "horse_tr2")])
+def test_first_barrier_abort_falls_back_to_the_launch_loop(amd, pair, monkeypatch):
+    """A one-launch run whose grid is not co-resident (another persistent kernel holding CUs)
+    gives up at its first grid barrier, before it writes any state, and icp_run takes the launch
+    loop: the same results, counted in persistent_fallbacks.  ICP_PERSIST_TEST_ABORT=1 makes the
+    first barrier fail at once; a later run on the same context takes the one launch again (its
+    barrier words were reset)."""
+    m = amd.load_matrix(datasets.path(pair[0]))
+    p = amd.load_matrix(datasets.path(pair[1]))
+    loop = run(amd, m, p, amd.RUN_LAUNCHES, 20, 1e-5)
+    with amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        monkeypatch.setenv("ICP_PERSIST_TEST_ABORT", "1")
+        res, errs = ctx.run(20, 1e-5)
+        st = ctx.stats()
+        assert st["persistent_runs"] == 0 and st["persistent_fallbacks"] == 1
+        assert res.iterations == loop[0]
+        np.testing.assert_array_equal(errs, loop[6])
+        np.testing.assert_array_equal(ctx.get_scene(), loop[7])
+        np.testing.assert_array_equal(ctx.get_indices(), loop[8])
+        monkeypatch.delenv("ICP_PERSIST_TEST_ABORT")
+        ctx.set_scene(p)
+        res2, errs2 = ctx.run(20, 1e-5)
+        assert ctx.stats()["persistent_runs"] == 1
+        np.testing.assert_array_equal(errs2, loop[6])
+        np.testing.assert_array_equal(ctx.get_scene(), loop[7])
