@@ -1079,6 +1079,8 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
             const unsigned long long tm =
                 __ballot(((ssm >> s) & 1ull) && t < ntile && box_dist2(tbox + 6 * t, sqx, sqy, sqz) <= slim);
             unsigned T = (unsigned)((tm | (tm >> 16) | (tm >> 32) | (tm >> 48)) & 0xffffull);
+            // the superblock's admitted blocks (bit 4 tile + b): A for the wave, lm for this lane's query
+            unsigned long long A = 0, lm = 0;
             while (T) { // up to four admitted tiles per trip
                 ++c_tr;
                 int tj[4];
@@ -1092,43 +1094,66 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
                 const bool hit = mj >= 0 && ((tm >> (16 * lu2 + mj)) & 1ull) && bl < nb16 &&
                                  box_dist2(bbox + 6 * bl, tqx, tqy, tqz) <= tlim;
                 const unsigned long long bm = __ballot(hit); // bit 16 i + 4 u + b
-                const unsigned long long any = bm | (bm >> 4) | (bm >> 8) | (bm >> 12);
-                unsigned A = (unsigned)((any & 0xf) | ((any >> 12) & 0xf0) | ((any >> 24) & 0xf00) | ((any >> 36) & 0xf000));
-                while (A) { // up to four admitted blocks per trip (their gathers in flight together):
-                            // lane 16 u + j scans point j of each for query u
-                    int kc[4];
-                    bool valid[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (tj[r] < 0) break; // (uniform)
+                    const unsigned long long g = bm >> (16 * r);
+                    A |= ((g | (g >> 4) | (g >> 8) | (g >> 12)) & 0xfull) << (4 * tj[r]);
+                    lm |= ((g >> (4 * lu)) & 0xfull) << (4 * tj[r]);
+                }
+            }
+            while (A) { // up to four admitted blocks per trip (their gathers in flight together):
+                        // lane 16 u + j scans point j of each for query u
+                int kc[4];
+                bool valid[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int ib = A ? __ffsll((long long)A) - 1 : -1;
+                    A &= A - 1;
+                    c_bl += ib >= 0;
+                    const int k = 16 * (4 * kMidSb * s + ib) + lj;
+                    valid[g] = ib >= 0 && k < nm && ((lm >> ib) & 1ull);
+                    kc[g] = valid[g] ? k : nm - 1;
+                }
+                const unsigned long long ts0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+                double mx[4], my[4], mz[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    mx[g] = mxg[kc[g]];
+                    my[g] = myg[kc[g]];
+                    mz[g] = mzg[kc[g]];
+                }
+                if (a.stamps) {
+                    __builtin_amdgcn_s_waitcnt(0);
+                    tsc += __builtin_amdgcn_s_memrealtime() - ts0;
+                }
+                double e[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const double dx = sqx - mx[g], dy = sqy - my[g], dz = sqz - mz[g];
+                    e[g] = (dx * dx + dy * dy) + dz * dz; // compute.cu:112-117
+                }
+                // strict improvements in order; an exact tie with the running best (from before
+                // the trip or within it) sends the whole trip down the ordered path again
+                const double bd0 = bd;
+                const int bk0 = bk;
+                bool eq = false;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    eq |= valid[g] & (e[g] == bd);
+                    const bool take = valid[g] & (e[g] < bd);
+                    bd = take ? e[g] : bd;
+                    bk = take ? kc[g] : bk;
+                }
+                if (__builtin_expect(__ballot(eq) != 0, 0)) { // (uniform, rare)
+                    bd = bd0;
+                    bk = bk0;
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
-                        const int ib = A ? __ffs((int)A) - 1 : -1;
-                        A &= A - 1;
-                        c_bl += ib >= 0;
-                        const int r = ib >> 2, bsel = ib & 3;
-                        const int blk = 4 * (kMidSb * s + pick4(r & 3, tj[0], tj[1], tj[2], tj[3])) + bsel;
-                        const int k = 16 * blk + lj;
-                        valid[g] = ib >= 0 && k < nm && ((bm >> (16 * r + 4 * lu + bsel)) & 1ull);
-                        kc[g] = ib >= 0 && k < nm ? k : nm - 1;
-                    }
-                    const unsigned long long ts0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-                    double mx[4], my[4], mz[4];
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        mx[g] = mxg[kc[g]];
-                        my[g] = myg[kc[g]];
-                        mz[g] = mzg[kc[g]];
-                    }
-                    if (a.stamps) {
-                        __builtin_amdgcn_s_waitcnt(0);
-                        tsc += __builtin_amdgcn_s_memrealtime() - ts0;
-                    }
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const double dx = sqx - mx[g], dy = sqy - my[g], dz = sqz - mz[g];
-                        const double e = (dx * dx + dy * dy) + dz * dz; // compute.cu:112-117
-                        bool take = valid[g] & (e < bd);
-                        if (valid[g] & (e == bd) & (bd < INFINITY)) // a tie: the lower original index
+                        bool take = valid[g] & (e[g] < bd);
+                        if (valid[g] & (e[g] == bd) & (bd < INFINITY)) // a tie: the lower original index
                             take = orig[kc[g]] < orig[min(bk, nm - 1)];
-                        bd = take ? e : bd;
+                        bd = take ? e[g] : bd;
                         bk = take ? kc[g] : bk;
                     }
                 }
