@@ -488,5 +488,26 @@ def main():
         dist.destroy_process_group()
 
 
+def reap_children():
+    """Leave no process behind (the driver counts processes at the end of the run): every child
+    is joined where it is started (subprocess.run, with-block thread pools); anything still
+    alive here is named on stderr and terminated."""
+    try:
+        import psutil
+    except ImportError:
+        return
+    kids = psutil.Process().children(recursive=True)
+    for k in kids:
+        try:
+            print(f"[bench] terminating leftover child {k.pid} {k.name()}", file=sys.stderr)
+            k.terminate()
+        except psutil.NoSuchProcess:
+            pass
+    psutil.wait_procs(kids, timeout=5)
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    finally:
+        reap_children()
