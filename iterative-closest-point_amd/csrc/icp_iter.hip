@@ -1058,14 +1058,30 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
             __builtin_amdgcn_s_waitcnt(0);
             tp1 = __builtin_amdgcn_s_memrealtime();
         }
-        unsigned long long sm[4];
+        // superblocks: one test against the batch's box (every query inside it, the largest bound):
+        // fp64 rounding is monotone, so this admits every superblock a single query would
+        unsigned long long S;
+        {
+            const double bq[6] = {fmin(fmin(qx[0], qx[1]), fmin(qx[2], qx[3])), fmin(fmin(qy[0], qy[1]), fmin(qy[2], qy[3])),
+                                  fmin(fmin(qz[0], qz[1]), fmin(qz[2], qz[3])), fmax(fmax(qx[0], qx[1]), fmax(qx[2], qx[3])),
+                                  fmax(fmax(qy[0], qy[1]), fmax(qy[2], qy[3])), fmax(fmax(qz[0], qz[1]), fmax(qz[2], qz[3]))};
+            const double lmax = fmax(fmax(lim[0], lim[1]), fmax(lim[2], lim[3]));
+            double d2 = 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) sm[u] = __ballot(lane < nsb && box_dist2(sbx, qx[u], qy[u], qz[u]) <= lim[u]);
-        unsigned long long S = sm[0] | sm[1] | sm[2] | sm[3];
+            for (int k = 0; k < 3; ++k) {
+                const double g = fmax(sbx[k] - bq[3 + k], bq[k] - sbx[3 + k]);
+                const double f = g > 0.0 ? g : 0.0;
+                d2 = k == 0 ? f * f : d2 + f * f;
+            }
+            // (a NaN query makes the batch box NaN: no superblock, as for its own test; its
+            // neighbours in the batch then search all superblocks -- never fewer)
+            const bool nanq = !(bq[0] == bq[0] && bq[1] == bq[1] && bq[2] == bq[2] && bq[3] == bq[3] &&
+                                bq[4] == bq[4] && bq[5] == bq[5]);
+            S = __ballot(lane < nsb && (nanq || d2 <= lmax));
+        }
         // per-lane views of the batch
         const double sqx = pick4(lu, qx[0], qx[1], qx[2], qx[3]), sqy = pick4(lu, qy[0], qy[1], qy[2], qy[3]),
                      sqz = pick4(lu, qz[0], qz[1], qz[2], qz[3]), slim = pick4(lu, lim[0], lim[1], lim[2], lim[3]);
-        const unsigned long long ssm = pick4(lu, sm[0], sm[1], sm[2], sm[3]);
         const double tqx = pick4(lu2, qx[0], qx[1], qx[2], qx[3]), tqy = pick4(lu2, qy[0], qy[1], qy[2], qy[3]),
                      tqz = pick4(lu2, qz[0], qz[1], qz[2], qz[3]), tlim = pick4(lu2, lim[0], lim[1], lim[2], lim[3]);
         double bd = INFINITY;
@@ -1076,8 +1092,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
             S &= S - 1;
             ++c_sb;
             const int t = kMidSb * s + lj;
-            const unsigned long long tm =
-                __ballot(((ssm >> s) & 1ull) && t < ntile && box_dist2(tbox + 6 * t, sqx, sqy, sqz) <= slim);
+            const unsigned long long tm = __ballot(t < ntile && box_dist2(tbox + 6 * t, sqx, sqy, sqz) <= slim);
             unsigned T = (unsigned)((tm | (tm >> 16) | (tm >> 32) | (tm >> 48)) & 0xffffull);
             // the superblock's admitted blocks (bit 4 tile + b): A for the wave, lm for this lane's query
             unsigned long long A = 0, lm = 0;
