@@ -1186,7 +1186,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
     TRY(grow(ctx, &ctx->pers_part, &ctx->pers_part_cap, (size_t)2 * kBlock * kNumSums));
     static const bool stamps = getenv("ICP_PERSIST_STAMPS") != nullptr;
     if (stamps) {
-        const size_t ns = (size_t)2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock;
+        const size_t ns = (size_t)2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock + 2 * kBlock;
         TRY(grow(ctx, &ctx->pers_stamps, &ctx->pers_stamps_cap, ns));
         HIPCHK(hipMemsetAsync(ctx->pers_stamps, 0, sizeof(unsigned long long) * ns, ctx->st));
     }
@@ -1269,7 +1269,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
     HIPCHK(hipStreamSynchronize(ctx->st));
     if (stamps) { // phase durations of workgroup 0 (tags: 0 NN begin, 1 NN end, 2 published,
                   // 3 barrier passed, 8 partials loaded, 4 folded, 5 Horn done, 6 transformed, 7 end)
-        std::vector<unsigned long long> h(2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock);
+        std::vector<unsigned long long> h(2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock + 2 * kBlock);
         HIPCHK(hipMemcpy(h.data(), ctx->pers_stamps, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
         double acc[9] = {0}, cntp[9] = {0};
         for (int k = 1; k < kPersistMaxStamps && h[2 * k + 1]; ++k) {
@@ -1304,6 +1304,14 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
                 for (int k = 0; k < 3; ++k) cnt[k] += (double)w[8 * g + 2 + k];
             }
             const double nbat = (double)((ctx->scene.n + 3) / 4) * std::max(1, ctx->h_iter->iter);
+            double wsum = 0, wmax = 0; // per-wave busy time, summed over the iterations (max: of one iteration)
+            for (int g = 0; g < grid; ++g) {
+                wsum += (double)w[8 * kBlock + 2 * g] * 0.01;
+                wmax = std::max(wmax, (double)w[8 * kBlock + 2 * g + 1] * 0.01);
+            }
+            const int iters = std::max(1, ctx->h_iter->iter);
+            fprintf(stderr, "[persist-mid] wave busy per NN: mean %.1f us, slowest wave of any NN %.1f us\n",
+                    wsum / (grid * 8.0 * iters), wmax);
             fprintf(stderr, "[persist-mid] per wg NN mean/max %.1f/%.1f us (first %.1f/%.1f) | per batch: superblocks %.2f "
                             "tile rounds %.2f blocks %.2f | per batch us: query loads %.2f tests %.2f gathers %.2f reduce+store %.2f\n",
                     sm[0] / grid, mx[0], sm[1] / grid, mx[1], cnt[0] / nbat, cnt[1] / nbat, cnt[2] / nbat, tph[0] / nbat,

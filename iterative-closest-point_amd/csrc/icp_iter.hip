@@ -853,6 +853,7 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
 // 16 u + j scans point j of each admitted block (four blocks' gathers in flight together) for
 // query u.  Distances follow compute.cu:112-117.
 constexpr int kMidSb = 16;     // 64-point tiles per superblock
+static_assert(kTailMaxBlocks <= kBlock, "the stamps buffer holds kBlock workgroups' timers");
 constexpr int kMidThreads = 512;
 
 // squared distance from q to the box (lo x, lo y, lo z, hi x, hi y, hi z) -- the small kernel's
@@ -956,6 +957,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     __shared__ int s_ok;
     __shared__ unsigned s_cnt[3]; // (stamps only) admitted superblocks, tile rounds, blocks scanned
     __shared__ unsigned long long s_tph[4]; // (stamps only) wave time: query loads, superblock/tile tests, scans, reduce
+    __shared__ unsigned long long s_wbusy[2]; // (stamps only) this workgroup's waves: sum, max of the per-iteration busy time
     const int tid = threadIdx.x, lane = tid & 63;
     const int b = blockIdx.x, nb = gridDim.x;
     const int n = a.n, nm = a.nm, ntile = a.nblk, nsb = (ntile + kMidSb - 1) / kMidSb, nb16 = (nm + 15) / 16;
@@ -980,6 +982,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
         for (int k = 0; k < 4; ++k) cnt0[k] = 0;
         for (int k = 0; k < 3; ++k) s_cnt[k] = 0;
         for (int k = 0; k < 4; ++k) s_tph[k] = 0;
+        s_wbusy[0] = s_wbusy[1] = 0;
     }
     // this lane's superblock box (lane < nsb), for every query of the run
     double sbx[6];
@@ -1221,7 +1224,13 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     // region of its own.
     const int ntask = (n + 3) / 4, nwaves = nb * (kMidThreads / 64), gw = b * (kMidThreads / 64) + (tid >> 6);
     auto nn = [&](int) -> bool {
+        const unsigned long long tb0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
         for (int v = gw; v < ntask; v += nwaves) nn_batch(4 * v, min(4, n - 4 * v));
+        if (a.stamps && lane == 0) {
+            const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - tb0;
+            atomicAdd(&s_wbusy[0], dt);
+            atomicMax(&s_wbusy[1], dt);
+        }
         return barrier();
     };
 
@@ -1384,6 +1393,10 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
         w[5] = (unsigned long long)max(0, min(kBlock, n - b * kBlock));
         w[6] = s_tph[0] | (s_tph[1] << 32); // (100 MHz ticks summed over the waves; < 2^32 each)
         w[7] = s_tph[2] | (s_tph[3] << 32);
+        // (after the 8 x kBlock per-workgroup words: 2 x kBlock more, allocated by run_persistent)
+        unsigned long long *wb = a.stamps + 2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock;
+        wb[2 * b] = s_wbusy[0];
+        wb[2 * b + 1] = s_wbusy[1];
     }
     if (b == 0 && tid == 0) {
         *a.s_glob = st;
