@@ -247,6 +247,7 @@ struct icp_ctx {
     int *mid_perm = nullptr;         // its search order (each point's row)
     char *mid_cnt = nullptr;         // the order's scratch (radix sort)
     double m_lo[3] = {0, 0, 0}, m_hi[3] = {0, 0, 0}; // the model's box
+    double pm_seed_big = 0.0;        // PersistArgs::seed_big for this model
     size_t mid_q4_cap = 0, mid_res_cap = 0, mid_perm_cap = 0, mid_cnt_cap = 0;
     size_t tail_part_cap = 0, tail_sync_cap = 0;
     bool pers_sync_valid = false;    // the barrier words hold pers_epoch_base barriers of grid pers_grid
@@ -1013,6 +1014,24 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         pm = persist_model_image(m_xyz, nm, &ctx->pm_blocks);
         TRY(grow(ctx, &ctx->pm_img, &ctx->pm_img_cap, pm.size()));
         HIPCHK(hipMemcpyAsync(ctx->pm_img, pm.data(), sizeof(double) * pm.size(), hipMemcpyHostToDevice, ctx->st));
+        { // the mid-size search's stale-seed scale: a move beyond 2 diagonals of a median 16-point block
+            const size_t nb16 = (nm + 15) / 16;
+            std::vector<double> d2(nb16);
+            for (size_t b = 0; b < nb16; ++b) {
+                double acc = 0.0;
+                for (int k = 0; k < 3; ++k) {
+                    double lo = pm[k * nm + 16 * b], hi = lo;
+                    for (size_t j = 16 * b + 1; j < std::min(nm, 16 * b + 16); ++j) {
+                        lo = std::min(lo, pm[k * nm + j]);
+                        hi = std::max(hi, pm[k * nm + j]);
+                    }
+                    acc += (hi - lo) * (hi - lo);
+                }
+                d2[b] = acc;
+            }
+            std::nth_element(d2.begin(), d2.begin() + nb16 / 2, d2.end());
+            ctx->pm_seed_big = 4.0 * d2[nb16 / 2];
+        }
         for (int k = 0; k < 3; ++k) { // the model's box (the mid-size loop's search order)
             ctx->m_lo[k] = INFINITY;
             ctx->m_hi[k] = -INFINITY;
@@ -1257,6 +1276,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
             return fail(ctx, ICP_E_HIP, "icp_run: the mid-size search order (radix sort) failed");
         LAUNCHCHK("mid_order");
         a.perm = ctx->mid_perm;
+        a.seed_big = ctx->pm_seed_big;
         a.seed_idx = ctx->idx;
         a.m4 = ctx->m4;
         a.q4 = ctx->mid_q4;
@@ -1276,6 +1296,12 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
             const int tag = (int)h[2 * k];
             acc[tag] += (double)(h[2 * k + 1] - h[2 * k - 1]) * 0.01; // 100 MHz -> us
             cntp[tag] += 1;
+        }
+        if (mid) { // workgroup 0's NN phase (tag 0 -> 1, its barrier wait included) per iteration
+            fprintf(stderr, "[persist-mid] NN per iteration (us):");
+            for (int k = 1; k < kPersistMaxStamps && h[2 * k + 1]; ++k)
+                if (h[2 * k] == 1 && h[2 * k - 2] == 0) fprintf(stderr, " %.0f", (double)(h[2 * k + 1] - h[2 * k - 1]) * 0.01);
+            fprintf(stderr, "\n");
         }
         fprintf(stderr, "[persist] grid %d lds %zu: us ending at tag (calls):", grid, lds);
         for (int t = 0; t < 9; ++t) fprintf(stderr, " %d:%.2f(%g)", t, acc[t], cntp[t]);

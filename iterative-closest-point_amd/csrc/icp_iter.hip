@@ -1017,14 +1017,17 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     // the owned point's search input for any wave of the grid: position and seed distance
     // (rows in the search order: the owned point's row is my_pos = a.perm[i])
     const int my_pos = own ? a.perm[i] : 0;
-    auto publish_query = [&]() {
+    // `stale`: the point moved farther than the model's block scale since its correspondence was
+    // found (right after the first alignment, typically), flagged in the seed's sign bit
+    auto publish_query = [&](bool stale) {
         if (own) {
             const double dx = p0 - y0, dy = p1 - y1, dz = p2 - y2;
+            const double r2 = (dx * dx + dy * dy) + dz * dz; // (the scan's own arithmetic: the seed is admitted)
             double *q = a.q4 + 4 * (size_t)my_pos;
             pub_store(q, p0);
             pub_store(q + 1, p1);
             pub_store(q + 2, p2);
-            pub_store(q + 3, (dx * dx + dy * dy) + dz * dz); // (the scan's own arithmetic: the seed is admitted)
+            pub_store(q + 3, stale ? -r2 : r2);
         }
     };
     const __amdgpu_buffer_rsrc_t q4r =
@@ -1047,13 +1050,52 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
             auto dbl = [](unsigned lo, unsigned hi) {
                 return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
             };
+            double r2[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 qx[u] = dbl(g[2 * u][0], g[2 * u][1]);
                 qy[u] = dbl(g[2 * u][2], g[2 * u][3]);
                 qz[u] = dbl(g[2 * u + 1][0], g[2 * u + 1][1]);
-                const double r2 = a.cull ? dbl(g[2 * u + 1][2], g[2 * u + 1][3]) : (double)INFINITY;
-                lim[u] = r2 * (1.0 + 0x1p-40) + 0x1p-900;
+                r2[u] = dbl(g[2 * u + 1][2], g[2 * u + 1][3]);
+            }
+            const bool stale = signbit(r2[0]) || signbit(r2[1]) || signbit(r2[2]) || signbit(r2[3]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r2[u] = fabs(r2[u]);
+            // A stale seed (the query moved beyond the model's block scale since its correspondence
+            // was found, e.g. right after the first alignment) would admit a large part of the
+            // model: descend to the nearest-box superblock, tile and block and take the smaller
+            // distance (both are D64 of actual model points, so either admits its own block).
+            if (__builtin_expect(stale, 0)) { // (uniform)
+                int sbest[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) // lanes over superblocks, one query at a time
+                    sbest[u] = group_argmin<64>(lane < nsb ? box_dist2(sbx, qx[u], qy[u], qz[u]) : (double)INFINITY, lane);
+                // lane 16 u + j: tile j of query u's superblock, then block j < 4 of its tile,
+                // then point j of its block
+                const double dqx = pick4(lu, qx[0], qx[1], qx[2], qx[3]), dqy = pick4(lu, qy[0], qy[1], qy[2], qy[3]),
+                             dqz = pick4(lu, qz[0], qz[1], qz[2], qz[3]);
+                const int ds = pick4(lu, sbest[0], sbest[1], sbest[2], sbest[3]);
+                const int t = kMidSb * ds + lj;
+                const int tb = kMidSb * ds +
+                               group_argmin<16>(t < ntile ? box_dist2(tbox + 6 * t, dqx, dqy, dqz) : (double)INFINITY, lj);
+                const int bl = 4 * tb + (lj & 3);
+                const int bb = 4 * tb + group_argmin<16>(lj < 4 && bl < nb16 ? box_dist2(bbox + 6 * bl, dqx, dqy, dqz)
+                                                                            : (double)INFINITY, lj);
+                const int k = min(16 * bb + lj, nm - 1);
+                const double dx = dqx - mxg[k], dy = dqy - myg[k], dz = dqz - mzg[k];
+                double d = (dx * dx + dy * dy) + dz * dz; // compute.cu:112-117
+#pragma unroll
+                for (int o = 8; o >= 1; o >>= 1) d = fmin(d, __shfl_xor(d, o, 64));
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double du = __shfl(d, 16 * u, 64);
+                    r2[u] = du < r2[u] ? du : r2[u]; // (a NaN stays NaN: no comparison holds)
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double r = a.cull ? r2[u] : (double)INFINITY;
+                lim[u] = r * (1.0 + 0x1p-40) + 0x1p-900;
             }
         }
         unsigned long long tp1 = 0;
@@ -1253,7 +1295,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     };
 
     unsigned long long wg_nn = 0, wg_nn0 = 0;
-    publish_query();
+    publish_query(false);
     if (!barrier()) return;
     for (int it = 0;; ++it) {
         persist_stamp(a.stamps, nstamp, 0);
@@ -1354,6 +1396,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
         {
             const Xform xf = st.xf;
             double e[1] = {0.0};
+            bool moved = false;
             y0 = n0;
             y1 = n1;
             y2 = n2;
@@ -1365,6 +1408,8 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
                 double q0, q1, q2;
                 transform_point(xf, p0, p1, p2, q0, q1, q2);
                 e[0] += residual2(y0, y1, y2, q0, q1, q2);
+                const double m0 = q0 - p0, m1 = q1 - p1, m2 = q2 - p2;
+                moved = (m0 * m0 + m1 * m1) + m2 * m2 > a.seed_big;
                 p0 = q0;
                 p1 = q1;
                 p2 = q2;
@@ -1373,7 +1418,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
                 a.pz[i] = q2;
                 if (a.p32) a.p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
             }
-            publish_query();
+            publish_query(moved);
             __syncthreads(); // (loc is rewritten below)
             classic_sum<1>(e, loc);
         }

@@ -319,6 +319,7 @@ struct PersistArgs {
     int *res;                   // (mid-size kernel) n: their correspondences (sorted positions)
     const int *perm;            // (mid-size kernel) n: each point's row in the search order (launch_mid_order)
     int test_abort;             // tests: abort at the first barrier, as if not co-resident
+    double seed_big;            // (mid-size kernel) a query that moved farther (squared) gets a descent seed too
 };
 // pos[q] = query q's place when the queries are sorted, stably, by their cell of a 32^3 grid over
 // the box [lo, hi] (Morton order of the cells) (icp_order.hip); scratch: mid_order_scratch_bytes(n)
