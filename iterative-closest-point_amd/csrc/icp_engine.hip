@@ -1260,10 +1260,14 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
     }
     for (int k = 0; k < 3; ++k) a.m0[k] = ctx->model_host[k];
     if (mid) {
-        // the first search seeds the kernel's culled scan: one pass of the exact cascade (the
-        // resident correspondences if they pair this scene already), so that even a far first
-        // iteration admits only the blocks within each query's exact NN distance
-        if (!ctx->seeds_valid) {
+        // the first search is seeded by the resident correspondences if they pair this scene
+        // already; else every query descends to its nearest-box block (ICP_MID_PREPASS=1: one
+        // pass of the exact cascade instead, for A/B runs)
+        static const bool prepass = [] {
+            const char *e = getenv("ICP_MID_PREPASS");
+            return e && e[0] == '1';
+        }();
+        if (!ctx->seeds_valid && prepass) {
             launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
             TRY(nn_search_begin(ctx, P, n, false, nullptr, nullptr, false, false, &ctx->iter_state->done));
         }
@@ -1277,7 +1281,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
         LAUNCHCHK("mid_order");
         a.perm = ctx->mid_perm;
         a.seed_big = ctx->pm_seed_big;
-        a.seed_idx = ctx->idx;
+        a.seed_idx = ctx->seeds_valid || prepass ? ctx->idx : nullptr;
         a.m4 = ctx->m4;
         a.q4 = ctx->mid_q4;
         a.res = ctx->mid_res;

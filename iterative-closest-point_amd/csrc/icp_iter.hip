@@ -971,7 +971,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     const bool own = tid < kBlock && i < n;
     double p0 = own ? a.px[i] : 0.0, p1 = own ? a.py[i] : 0.0, p2 = own ? a.pz[i] : 0.0;
     double y0 = 0.0, y1 = 0.0, y2 = 0.0;
-    if (own) { // the first search is seeded by an exact pass already made (icp_run)
+    if (own && a.seed_idx) { // the first search seeded by the resident correspondences (icp_run)
         const double4 m = a.m4[a.seed_idx[i]];
         y0 = m.x;
         y1 = m.y;
@@ -1022,7 +1022,8 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     auto publish_query = [&](bool stale) {
         if (own) {
             const double dx = p0 - y0, dy = p1 - y1, dz = p2 - y2;
-            const double r2 = (dx * dx + dy * dy) + dz * dz; // (the scan's own arithmetic: the seed is admitted)
+            // (the scan's own arithmetic: the seed is admitted; no correspondence yet: +inf)
+            const double r2 = a.seed_idx || epoch > 0 ? (dx * dx + dy * dy) + dz * dz : (double)INFINITY;
             double *q = a.q4 + 4 * (size_t)my_pos;
             pub_store(q, p0);
             pub_store(q + 1, p1);
@@ -1295,7 +1296,7 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     };
 
     unsigned long long wg_nn = 0, wg_nn0 = 0;
-    publish_query(false);
+    publish_query(!a.seed_idx); // (without resident correspondences the first search descends)
     if (!barrier()) return;
     for (int it = 0;; ++it) {
         persist_stamp(a.stamps, nstamp, 0);
