@@ -330,3 +330,34 @@ def test_first_barrier_abort_falls_back_to_the_launch_loop(amd, pair, monkeypatc
         assert ctx.stats()["persistent_runs"] == 1
         np.testing.assert_array_equal(errs2, loop[6])
         np.testing.assert_array_equal(ctx.get_scene(), loop[7])
+
+
+def test_randomised_bitwise_fuzz(amd):
+    """tools/persist_fuzz.py, a short run: random sizes over both one-launch kernels' ranges,
+    uniform / surface / clustered / lattice (exact ties) / duplicated models, small to far
+    motions, fixed or converging runs -- every case one launch and bit-identical to the loop
+    (6,000 cases of it: profiles/r02bg_persist_fuzz/)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "persist_fuzz", os.path.join(os.path.dirname(__file__), "..", "tools", "persist_fuzz.py"))
+    fz = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fz)
+    rng = np.random.default_rng(2024)
+    kinds = ["uniform", "surface", "clusters", "lattice", "duplicates"]
+    for c in range(60):
+        small = c % 3 == 0
+        n = int(rng.integers(4, 4097)) if small else int(rng.integers(4097, 49153))
+        nm = int(rng.integers(1, 6001)) if small else int(rng.integers(16, 65537))
+        kind = kinds[c % len(kinds)]
+        m = fz.model(rng, kind, nm)
+        p = fz.rigid(rng, m[rng.integers(0, nm, n)] + rng.normal(scale=0.01, size=(n, 3)), [0.2, 1.0, 10.0][c % 3])
+        if kind == "lattice":
+            p = np.round(p * 2) / 2 + 0.5
+        iters, thr = int(rng.integers(1, 9)), (-1.0 if c % 2 else 1e-6)
+        one = fz.run(m, p, amd.RUN_PERSISTENT, iters, thr)
+        loop = fz.run(m, p, amd.RUN_LAUNCHES, iters, thr)
+        assert one[4] == 1 and loop[4] == 0, (c, n, nm, kind)
+        assert one[0] == loop[0], (c, n, nm, kind)
+        for x, y in zip(one[1:4], loop[1:4]):
+            np.testing.assert_array_equal(x, y, err_msg=f"case {c}: n={n} nm={nm} {kind}")
