@@ -1704,7 +1704,20 @@ int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3]
     if (!ctx || !mu || (!xyz && n) || n == 0) return ICP_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
-    if (3 * n <= kMappedIo) { // small: sum and centre straight from / into mapped host memory
+    if (n <= (size_t)kRedSingle) { // one launch on mapped host memory (icp_iter.hip)
+        double *hin, *din; // one region: input, the centred output, the three sums
+        TRY(io_take(ctx, 6 * n + 4, &hin, &din));
+        double *hout = hin + 3 * n, *dout = din + 3 * n, *hsum = hin + 6 * n, *dsum = din + 6 * n;
+        std::memcpy(hin, xyz, sizeof(double) * 3 * n);
+        launch_small_centroid(din, (int)n, (double)n, dsum, centred_out ? dout : nullptr, ctx->st);
+        LAUNCHCHK("centroid");
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        for (int k = 0; k < 3; ++k) mu[k] = hsum[k] / (double)n; // rowwise().mean()
+        if (centred_out) std::memcpy(centred_out, hout, sizeof(double) * 3 * n);
+        return ICP_OK;
+    }
+    if (3 * n <= kMappedIo) { // mid-size: sum and centre straight from / into mapped host memory
         double *hin, *din; // one region: input, then the centred output (<= the buffer's 2 x kMappedIo)
         TRY(io_take(ctx, (centred_out ? 6 : 3) * n, &hin, &din));
         double *hout = hin + 3 * n, *dout = din + 3 * n;
@@ -1783,6 +1796,23 @@ int icp_err_compute(icp_ctx *ctx, const double *y_xyz, double *p_xyz, size_t n, 
     if (!ctx || !sR || !t || !err || ((!y_xyz || !p_xyz) && n)) return ICP_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
+    if (n && n <= (size_t)kRedSingle) { // one launch on mapped host memory (icp_iter.hip)
+        double *h, *d; // y, p, the sum
+        TRY(io_take(ctx, 6 * n + 2, &h, &d));
+        std::memcpy(h, y_xyz, sizeof(double) * 3 * n);
+        std::memcpy(h + 3 * n, p_xyz, sizeof(double) * 3 * n);
+        Xform xf;
+        std::memcpy(xf.sR, sR, sizeof(xf.sR));
+        std::memcpy(xf.t, t, sizeof(xf.t));
+        std::memcpy(xf.c, ctx->c, sizeof(xf.c));
+        launch_small_err(d, d + 3 * n, (int)n, xf, in_place ? 1 : 0, d + 6 * n, ctx->st);
+        LAUNCHCHK("err_compute");
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        *err = h[6 * n];
+        if (in_place) std::memcpy(p_xyz, h + 3 * n, sizeof(double) * 3 * n);
+        return ICP_OK;
+    }
     TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
     TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
     Xform xf;
@@ -1806,6 +1836,22 @@ int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, s
     if (!ctx || !s || !R || !t || !err || !p_xyz || !y_xyz || n == 0) return ICP_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
+    if (n <= (size_t)kRedSingle) { // one launch on mapped host memory, Horn on the device (icp_iter.hip)
+        double *h, *d; // p, y, the results
+        TRY(io_take(ctx, 6 * n + 32, &h, &d));
+        std::memcpy(h, p_xyz, sizeof(double) * 3 * n);
+        std::memcpy(h + 3 * n, y_xyz, sizeof(double) * 3 * n);
+        launch_small_alignment(d, d + 3 * n, (int)n, d + 6 * n, ctx->st);
+        LAUNCHCHK("find_alignment");
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->io_pending = false;
+        const double *o = h + 6 * n;
+        *s = o[18];
+        for (int k = 0; k < 9; ++k) R[k] = o[19 + k];
+        for (int k = 0; k < 3; ++k) t[k] = o[28 + k];
+        *err = o[kSumErr];
+        return ICP_OK;
+    }
     TRY(upload_cloud(ctx, ctx->qb, p_xyz, n, false));
     TRY(upload_cloud(ctx, ctx->qa, y_xyz, n, false));
     launch_sum3(ctx->qb.x, ctx->qb.y, ctx->qb.z, (int)n, red_target(ctx, n, ctx->sums + kSumP), ctx->st);

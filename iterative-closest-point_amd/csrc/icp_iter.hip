@@ -150,6 +150,134 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_small_kernel(
     if (threadIdx.x == 0) err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
 }
 
+// ---- per-operation calls on small clouds (n <= kRedSingle): one launch each ---------------------
+//
+// icp_compute_centroid, icp_err_compute and icp_find_alignment on <= 4,096 points ran a chain of
+// single-workgroup passes around mapped copies (sum, centre / upload, transform + residual /
+// sums, centred moments, host Horn, transform + residual).  Each is ONE workgroup here, reading
+// and writing the caller's AoS data in mapped host memory, with the same per-thread order and
+// the same block_sum_store trees (bit-identical sums), and for find_alignment the Horn solve of
+// icp_horn.h on thread 0, as the device-resident loop runs it.
+
+__global__ __launch_bounds__(kBlock) void small_centroid_kernel(const double *__restrict__ in, int n, double n_total,
+                                                              double *__restrict__ sums_out, double *__restrict__ out)
+{
+    __shared__ double s3[3];
+    double a[3] = {0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < n; i += kBlock) { // sum3_kernel, stride 3
+        a[0] += in[3 * (size_t)i];
+        a[1] += in[3 * (size_t)i + 1];
+        a[2] += in[3 * (size_t)i + 2];
+    }
+    block_sum_store<3>(a, s3);
+    __syncthreads();
+    if (threadIdx.x < 3) sums_out[threadIdx.x] = s3[threadIdx.x];
+    if (out) { // centre_aos_kernel
+        const double m0 = s3[0] / n_total, m1 = s3[1] / n_total, m2 = s3[2] / n_total;
+        for (int i = threadIdx.x; i < n; i += kBlock) {
+            out[3 * (size_t)i] = in[3 * (size_t)i] - m0;
+            out[3 * (size_t)i + 1] = in[3 * (size_t)i + 1] - m1;
+            out[3 * (size_t)i + 2] = in[3 * (size_t)i + 2] - m2;
+        }
+    }
+}
+
+// transform_err_kernel on AoS: e = sum ||y - (sR p + t)||^2, p <- sR p + t if write_p
+__device__ __forceinline__ double small_transform_err(const double *__restrict__ y, double *__restrict__ p, int n,
+                                                      const Xform &xf, int write_p)
+{
+    __shared__ double s1[1];
+    double a[1] = {0.0};
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+        double q0, q1, q2;
+        transform_point(xf, p[3 * (size_t)i], p[3 * (size_t)i + 1], p[3 * (size_t)i + 2], q0, q1, q2);
+        a[0] += residual2(y[3 * (size_t)i], y[3 * (size_t)i + 1], y[3 * (size_t)i + 2], q0, q1, q2);
+        if (write_p) {
+            p[3 * (size_t)i] = q0;
+            p[3 * (size_t)i + 1] = q1;
+            p[3 * (size_t)i + 2] = q2;
+        }
+    }
+    block_sum_store<1>(a, s1);
+    __syncthreads();
+    return s1[0];
+}
+
+__global__ __launch_bounds__(kBlock) void small_err_kernel(const double *__restrict__ y, double *__restrict__ p, int n,
+                                                         Xform xf, int write_p, double *__restrict__ err_out)
+{
+    const double e = small_transform_err(y, p, n, xf, write_p);
+    if (threadIdx.x == 0) err_out[0] = e;
+}
+
+// out: [0..17) the sums of gpu.cc:95-151 (kSumP, kSumY, kSumS, kSumDcaps, kSumSp), [17] err,
+// [18] s, [19..28) R, [28..31) t
+__global__ __launch_bounds__(kBlock) void small_alignment_kernel(const double *__restrict__ p, const double *__restrict__ y,
+                                                               int n, double *__restrict__ out)
+{
+    __shared__ double sums[kNumSums];
+    __shared__ Xform xf;
+    const double N = (double)n;
+    { // sum3_kernel over p, then over y (two passes, as the classic launches)
+        double a[3] = {0.0, 0.0, 0.0};
+        for (int i = threadIdx.x; i < n; i += kBlock) {
+            a[0] += p[3 * (size_t)i];
+            a[1] += p[3 * (size_t)i + 1];
+            a[2] += p[3 * (size_t)i + 2];
+        }
+        block_sum_store<3>(a, sums + kSumP);
+        __syncthreads();
+        double b[3] = {0.0, 0.0, 0.0};
+        for (int i = threadIdx.x; i < n; i += kBlock) {
+            b[0] += y[3 * (size_t)i];
+            b[1] += y[3 * (size_t)i + 1];
+            b[2] += y[3 * (size_t)i + 2];
+        }
+        block_sum_store<3>(b, sums + kSumY);
+        __syncthreads();
+    }
+    { // centred_moments_kernel
+        const double mpx = sums[kSumP] / N, mpy = sums[kSumP + 1] / N, mpz = sums[kSumP + 2] / N;
+        const double myx = sums[kSumY] / N, myy = sums[kSumY + 1] / N, myz = sums[kSumY + 2] / N;
+        double a[11];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) a[k] = 0.0;
+        for (int i = threadIdx.x; i < n; i += kBlock) {
+            const double p0 = p[3 * (size_t)i] - mpx, p1 = p[3 * (size_t)i + 1] - mpy, p2 = p[3 * (size_t)i + 2] - mpz;
+            const double y0 = y[3 * (size_t)i] - myx, y1 = y[3 * (size_t)i + 1] - myy, y2 = y[3 * (size_t)i + 2] - myz;
+            a[0] += p0 * y0;
+            a[1] += p0 * y1;
+            a[2] += p0 * y2;
+            a[3] += p1 * y0;
+            a[4] += p1 * y1;
+            a[5] += p1 * y2;
+            a[6] += p2 * y0;
+            a[7] += p2 * y1;
+            a[8] += p2 * y2;
+            a[9] += (y0 * y0 + y1 * y1) + y2 * y2;
+            a[10] += (p0 * p0 + p1 * p1) + p2 * p2;
+        }
+        block_sum_store<11>(a, sums + kSumS);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { // the host's Horn solve (gpu.cc:106-146), icp_find_alignment's own formulas
+        const double mu_p[3] = {sums[kSumP] / N, sums[kSumP + 1] / N, sums[kSumP + 2] / N};
+        const double mu_y[3] = {sums[kSumY] / N, sums[kSumY + 1] / N, sums[kSumY + 2] / N};
+        double sc, R[9], t[3];
+        horn_solve(sums + kSumS, mu_p, mu_y, sums[kSumDcaps], sums[kSumSp], &sc, R, t);
+        for (int k = 0; k < 9; ++k) xf.sR[k] = sc * R[k];
+        for (int k = 0; k < 3; ++k) xf.t[k] = t[k];
+        for (int k = 0; k < 3; ++k) xf.c[k] = 0.0;
+        out[18] = sc;
+        for (int k = 0; k < 9; ++k) out[19 + k] = R[k];
+        for (int k = 0; k < 3; ++k) out[28 + k] = t[k];
+    }
+    __syncthreads();
+    const double e = small_transform_err(y, (double *)p, n, xf, 0); // (write_p = 0: p is only read)
+    if (threadIdx.x < kSumErr) out[threadIdx.x] = sums[threadIdx.x];
+    if (threadIdx.x == 0) out[kSumErr] = e;
+}
+
 // ---- a whole small registration in ONE launch --------------------------------------------------
 //
 // For a single-rank run of n <= kRedSingle scene points against a model that fits in LDS, the
@@ -1505,6 +1633,22 @@ void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, 
     }();
     (void)attr;
     icp_persistent_kernel<<<grid, kBlock, lds_bytes, st>>>(args);
+}
+
+void launch_small_centroid(const double *in_aos, int n, double n_total, double *sums_out, double *out_aos, hipStream_t st)
+{
+    small_centroid_kernel<<<1, kBlock, 0, st>>>(in_aos, n, n_total, sums_out, out_aos);
+}
+
+void launch_small_err(const double *y_aos, double *p_aos, int n, const Xform &xf, int write_p, double *err_out,
+                      hipStream_t st)
+{
+    small_err_kernel<<<1, kBlock, 0, st>>>(y_aos, p_aos, n, xf, write_p, err_out);
+}
+
+void launch_small_alignment(const double *p_aos, const double *y_aos, int n, double *out, hipStream_t st)
+{
+    small_alignment_kernel<<<1, kBlock, 0, st>>>(p_aos, y_aos, n, out);
 }
 
 void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,

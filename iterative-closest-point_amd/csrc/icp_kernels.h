@@ -369,6 +369,15 @@ struct TailArgs {
 };
 constexpr int kTailMaxBlocks = 192; // red_blocks(n) <= this (n <= 49,152): co-resident with room
 void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t st);
+// Per-operation calls on n <= kRedSingle points, ONE workgroup each on AoS data (mapped host
+// memory), bit-identical to the chains of single-workgroup passes (icp_iter.hip):
+// centroid: sums_out[3] = sum of the points, out (nullable) = in - sums / n_total;
+// err: *err_out = sum ||y - (sR p + t)||^2, p <- sR p + t if write_p;
+// alignment: out[31] = the 17 sums, err, s, R (9), t (3) of find_alignment (Horn on the device)
+void launch_small_centroid(const double *in_aos, int n, double n_total, double *sums_out, double *out_aos, hipStream_t st);
+void launch_small_err(const double *y_aos, double *p_aos, int n, const Xform &xf, int write_p, double *err_out,
+                      hipStream_t st);
+void launch_small_alignment(const double *p_aos, const double *y_aos, int n, double *out, hipStream_t st);
 // zero a run's IterState and the NN queue counters (amb_count[0..3])
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st);
 
