@@ -192,6 +192,8 @@ struct icp_ctx {
     IterState *d_iter_mirror = nullptr; // its device address
     double *h_trace = nullptr, *d_trace = nullptr; // mapped host error trace
     size_t trace_cap = 0;
+    int *h_sig = nullptr, *d_sig = nullptr; // mapped completion word of the per-operation calls
+    int sig_ticket = 0;
     double *h_few = nullptr;         // mapped host staging of the few-query path: q (3 x kFewQueries),
     double *d_few = nullptr;         //   y (3 x kFewQueries), idx (kFewQueries ints); device address
     int *h_flags = nullptr;          // mapped host (done, iter, ticket, -) per in-flight iteration
@@ -897,6 +899,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->h_iter) (void)hipHostFree(ctx->h_iter);
     if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
     if (ctx->h_few) (void)hipHostFree(ctx->h_few);
+    if (ctx->h_sig) (void)hipHostFree(ctx->h_sig);
     if (ctx->h_trace) (void)hipHostFree(ctx->h_trace);
     if (ctx->h_io) (void)hipHostFree(ctx->h_io);
     for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
@@ -1651,6 +1654,23 @@ static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_res
 // by the automatic variant choice (and the fp64 mode).
 constexpr size_t kFewQueries = 32;
 
+// The end of a per-operation call's work on the stream, without the runtime's synchronisation:
+// a one-thread kernel stores a ticket into mapped host memory and the host spins on it
+// (wait_flag: it still reports a failed stream).  Saves ~5-10 us per call, which is what the
+// per-point API's thousands of calls (compute_distance_w_naive) pay.
+static int sync_by_flag(icp_ctx *ctx)
+{
+    if (!ctx->h_sig) {
+        HIPCHK(hipHostMalloc((void **)&ctx->h_sig, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(ctx->h_sig, 0, 64);
+        HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_sig, ctx->h_sig, 0));
+    }
+    const int ticket = ++ctx->sig_ticket;
+    launch_signal(ctx->d_sig, ticket, ctx->st);
+    LAUNCHCHK("signal");
+    return wait_flag(ctx, ctx->h_sig, ticket);
+}
+
 static int closest_few(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_xyz_out, int32_t *idx_out)
 {
     if (!ctx->h_few) {
@@ -1664,9 +1684,32 @@ static int closest_few(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
     launch_nn_exact_few(ctx->d_few, (int)np, ctx->m4, (int)ctx->nm, (int *)(ctx->d_few + 6 * kFewQueries),
                         ctx->d_few + 3 * kFewQueries, ctx->st);
     LAUNCHCHK("nn_exact_few");
-    HIPCHK(hipStreamSynchronize(ctx->st));
+    TRY(sync_by_flag(ctx));
     if (y_xyz_out) std::memcpy(y_xyz_out, hy, sizeof(double) * 3 * np);
     if (idx_out) std::memcpy(idx_out, hi, sizeof(int32_t) * np);
+    ctx->stats.nn_pairs += (long long)np * (long long)ctx->nm;
+    return ICP_OK;
+}
+
+// A model image that fits in LDS, and a query count the mapped buffer holds: one launch
+// (launch_nn_lds), queries and results through mapped host memory.
+static int closest_lds(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_xyz_out, int32_t *idx_out)
+{
+    double *h, *d; // queries, y, idx
+    TRY(io_take(ctx, 6 * np + (np + 1) / 2, &h, &d));
+    std::memcpy(h, p_xyz, sizeof(double) * 3 * np);
+    static const int cull = [] { // ICP_PERSIST_NN=all: every model point for every query (A/B)
+        const char *e = getenv("ICP_PERSIST_NN");
+        return e && std::strcmp(e, "all") == 0 ? 0 : 1;
+    }();
+    const size_t lds = 24 * ctx->nm + 48 * ctx->pm_blocks;
+    launch_nn_lds(ctx->pm_img, (int)ctx->nm, (int)ctx->pm_blocks, d, (int)np, cull, ctx->model_host.data(),
+                  (int *)(d + 6 * np), d + 3 * np, lds, ctx->st);
+    LAUNCHCHK("nn_lds");
+    TRY(sync_by_flag(ctx));
+    ctx->io_pending = false;
+    if (y_xyz_out) std::memcpy(y_xyz_out, h + 3 * np, sizeof(double) * 3 * np);
+    if (idx_out) std::memcpy(idx_out, h + 6 * np, sizeof(int32_t) * np);
     ctx->stats.nn_pairs += (long long)np * (long long)ctx->nm;
     return ICP_OK;
 }
@@ -1677,9 +1720,12 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
     TRY(check_ready(ctx, false));
     if (!p_xyz && np) return ICP_E_ARG;
     // (an explicitly chosen NN variant always runs its own cascade, as the tests of it expect)
-    if (np && np <= kFewQueries && (ctx->nn_variant == ICP_NN_VARIANT_AUTO || ctx->nn_mode == ICP_NN_FP64) &&
-        ctx->nn_rule == ICP_NN_RULE_SQUARED)
-        return closest_few(ctx, p_xyz, np, y_xyz_out, idx_out);
+    const bool auto_rule = (ctx->nn_variant == ICP_NN_VARIANT_AUTO || ctx->nn_mode == ICP_NN_FP64) &&
+                           ctx->nn_rule == ICP_NN_RULE_SQUARED;
+    if (np && np <= kFewQueries && auto_rule) return closest_few(ctx, p_xyz, np, y_xyz_out, idx_out);
+    if (np && auto_rule && ctx->pm_img && ctx->nm <= (size_t)kPersistMaxModel && 3 * np <= kMappedIo &&
+        24 * ctx->nm + 48 * ctx->pm_blocks + 4096 <= ctx->lds_per_cu)
+        return closest_lds(ctx, p_xyz, np, y_xyz_out, idx_out);
     TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
     ctx->seeds_valid = false; // idx is about to hold other queries' correspondences
     TRY(nn_search(ctx, ctx->qa, np));
@@ -1711,7 +1757,7 @@ int icp_compute_centroid(icp_ctx *ctx, const double *xyz, size_t n, double mu[3]
         std::memcpy(hin, xyz, sizeof(double) * 3 * n);
         launch_small_centroid(din, (int)n, (double)n, dsum, centred_out ? dout : nullptr, ctx->st);
         LAUNCHCHK("centroid");
-        HIPCHK(hipStreamSynchronize(ctx->st));
+        TRY(sync_by_flag(ctx));
         ctx->io_pending = false;
         for (int k = 0; k < 3; ++k) mu[k] = hsum[k] / (double)n; // rowwise().mean()
         if (centred_out) std::memcpy(centred_out, hout, sizeof(double) * 3 * n);
@@ -1760,7 +1806,7 @@ int icp_subtract_col(icp_ctx *ctx, const double *xyz, size_t n, const double m[3
         std::memcpy(hin, xyz, sizeof(double) * 3 * n);
         launch_subtract_aos(din, (int)n, m, din + 3 * n, ctx->st);
         LAUNCHCHK("subtract_col");
-        HIPCHK(hipStreamSynchronize(ctx->st));
+        TRY(sync_by_flag(ctx));
         ctx->io_pending = false;
         std::memcpy(out, hin + 3 * n, sizeof(double) * 3 * n);
         return ICP_OK;
@@ -1807,7 +1853,7 @@ int icp_err_compute(icp_ctx *ctx, const double *y_xyz, double *p_xyz, size_t n, 
         std::memcpy(xf.c, ctx->c, sizeof(xf.c));
         launch_small_err(d, d + 3 * n, (int)n, xf, in_place ? 1 : 0, d + 6 * n, ctx->st);
         LAUNCHCHK("err_compute");
-        HIPCHK(hipStreamSynchronize(ctx->st));
+        TRY(sync_by_flag(ctx));
         ctx->io_pending = false;
         *err = h[6 * n];
         if (in_place) std::memcpy(p_xyz, h + 3 * n, sizeof(double) * 3 * n);
@@ -1843,7 +1889,7 @@ int icp_find_alignment(icp_ctx *ctx, const double *p_xyz, const double *y_xyz, s
         std::memcpy(h + 3 * n, y_xyz, sizeof(double) * 3 * n);
         launch_small_alignment(d, d + 3 * n, (int)n, d + 6 * n, ctx->st);
         LAUNCHCHK("find_alignment");
-        HIPCHK(hipStreamSynchronize(ctx->st));
+        TRY(sync_by_flag(ctx));
         ctx->io_pending = false;
         const double *o = h + 6 * n;
         *s = o[18];

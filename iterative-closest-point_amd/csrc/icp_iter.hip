@@ -460,6 +460,146 @@ __device__ __forceinline__ void persist_fold(const double *part, double *sums, u
     persist_block_sum<K>(a, sums);
 }
 
+// The small one-launch loop's exact search of 4 queries against the model image in LDS: x | y | z
+// (nm each, image order) | 64-point block boxes (nblk <= 128); orig: original index per image
+// position (global).  seeded: r2s[u] is query u's seed distance (a D64 to an actual model point);
+// else the nearest point of the block with the nearest box.  Every model point at least as close
+// lies in a block whose box is within the seed distance (conservatively: r2 (1 + 2^-40) + 2^-900
+// covers the rounding of both fp64 evaluations), and the seed point is one of them, so the
+// lexicographic (D64, original index) minimum over those blocks is the global one.  Lanes hold
+// one point of each scanned block (image position k = 64 b + lane); a D64 tie compares original
+// indices (global reads, rare).  Distances follow compute.cu:112-117.  On return every lane
+// holds each query's image position rk[u] and original index ro[u] (0x7fffffff: no comparison
+// held, a NaN query).
+__device__ __forceinline__ void lds_nn4(const double *mxs, const double *mys, const double *mzs, const double *boxes,
+                                        const int *orig, int nm, int nblk, int cull, const double (&qx)[4],
+                                        const double (&qy)[4], const double (&qz)[4], bool seeded,
+                                        const double (&r2s)[4], int (&rk)[4], int (&ro)[4])
+{
+    const int lane = threadIdx.x & 63;
+    double bd[4];
+    int bk[4];
+    unsigned long long mlo[4], mhi[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        bd[u] = INFINITY;
+        bk[u] = 0x7fffffff;
+        auto box_d2 = [&](int j) { // squared distance from the query to block j's box
+            if (j >= nblk) return (double)INFINITY;
+            const double *bx = boxes + 6 * j;
+            const double ex = fmax(bx[0] - qx[u], qx[u] - bx[3]), ey = fmax(bx[1] - qy[u], qy[u] - bx[4]),
+                         ez = fmax(bx[2] - qz[u], qz[u] - bx[5]);
+            const double fx = ex > 0.0 ? ex : 0.0, fy = ey > 0.0 ? ey : 0.0, fz = ez > 0.0 ? ez : 0.0;
+            return (fx * fx + fy * fy) + fz * fz;
+        };
+        const double b0 = box_d2(lane), b1 = box_d2(lane + 64);
+        double r2 = INFINITY;
+        if (seeded) {
+            r2 = r2s[u];
+        } else { // the nearest point of the block with the nearest box
+            double bb = fmin(b0, b1);
+            int jb = b1 < b0 ? lane + 64 : lane;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const double ob = __shfl_xor(bb, o, 64);
+                const int oj = __shfl_xor(jb, o, 64);
+                const bool t = (ob < bb) | ((ob == bb) & (oj < jb));
+                bb = t ? ob : bb;
+                jb = t ? oj : jb;
+            }
+            const int k = min(64 * jb + lane, nm - 1); // (a valid point of block jb or of the last)
+            const double dx = qx[u] - mxs[k], dy = qy[u] - mys[k], dz = qz[u] - mzs[k];
+            r2 = (dx * dx + dy * dy) + dz * dz;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) r2 = fmin(r2, __shfl_xor(r2, o, 64)); // (NaN only if all are)
+        }
+        if (!cull) r2 = INFINITY;
+        // (+inf stays +inf, NaN stays NaN: no block)
+        const double lim = r2 * (1.0 + 0x1p-40) + 0x1p-900;
+        mlo[u] = __ballot(b0 <= lim);
+        mhi[u] = __ballot(b1 <= lim);
+    }
+    for (int half = 0; half < 2; ++half) {
+        unsigned long long all = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) all |= half ? mhi[u] : mlo[u];
+        while (all) { // wave-uniform: one scanned block per trip
+            const int blk = __ffsll((long long)all) - 1 + 64 * half;
+            all &= all - 1;
+            const int k = 64 * blk + lane;
+            const bool valid = k < nm;
+            const int kk = valid ? k : nm - 1;
+            const double mx = mxs[kk], my = mys[kk], mz = mzs[kk];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!(((half ? mhi[u] : mlo[u]) >> (blk - 64 * half)) & 1ull)) continue; // (uniform)
+                const double dx = qx[u] - mx, dy = qy[u] - my, dz = qz[u] - mz;
+                const double e = (dx * dx + dy * dy) + dz * dz;
+                bool take = valid & (e < bd[u]);
+                if (valid & (e == bd[u]) & (bd[u] < INFINITY)) // a tie: the lower original index
+                    take = orig[min(k, nm - 1)] < orig[min(bk[u], nm - 1)];
+                bd[u] = take ? e : bd[u];
+                bk[u] = take ? k : bk[u];
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        int bo = bk[u] == 0x7fffffff ? 0x7fffffff : orig[min(bk[u], nm - 1)];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const double od = __shfl_xor(bd[u], o, 64);
+            const int oo = __shfl_xor(bo, o, 64), ok = __shfl_xor(bk[u], o, 64);
+            const bool take = (od < bd[u]) | ((od == bd[u]) & (oo < bo)); // (no short circuit: selects)
+            bd[u] = take ? od : bd[u];
+            bo = take ? oo : bo;
+            bk[u] = take ? ok : bk[u];
+        }
+        rk[u] = bk[u];
+        ro[u] = bo;
+    }
+}
+
+// icp_closest_matrix when the model image fits in LDS: ONE launch, every workgroup holding the
+// image and searching 32 of the queries (AoS, mapped host memory) with lds_nn4; idx and y = m[idx]
+// (AoS) straight into mapped host memory.  The first minimum, as every NN path returns it.
+constexpr int kLdsNNQueries = 32;
+__global__ __launch_bounds__(kBlock) void nn_lds_kernel(const double *__restrict__ img, int nm, int nblk,
+                                                      const double *__restrict__ q_aos, int nq, int cull, double m00,
+                                                      double m01, double m02, int *__restrict__ idx_out,
+                                                      double *__restrict__ y_aos)
+{
+    extern __shared__ __attribute__((aligned(16))) double s_model[];
+    const double *mxs = s_model, *mys = s_model + nm, *mzs = s_model + 2 * nm, *boxes = s_model + 3 * nm;
+    const int *orig = (const int *)(img + 3 * nm + 6 * nblk);
+    for (int k = threadIdx.x; k < 3 * nm + 6 * nblk; k += kBlock) s_model[k] = img[k];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qb = blockIdx.x * kLdsNNQueries + wave * (kLdsNNQueries / 4), qe = min(nq, qb + kLdsNNQueries / 4);
+    for (int q0 = qb; q0 < qe; q0 += 4) {
+        double qx[4], qy[4], qz[4], r2s[4] = {0.0, 0.0, 0.0, 0.0};
+        int rk[4], ro[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = min(q0 + u, qe - 1);
+            qx[u] = q_aos[3 * (size_t)q];
+            qy[u] = q_aos[3 * (size_t)q + 1];
+            qz[u] = q_aos[3 * (size_t)q + 2];
+        }
+        lds_nn4(mxs, mys, mzs, boxes, orig, nm, nblk, cull, qx, qy, qz, false, r2s, rk, ro);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (lane == u && q0 + u < qe) {
+                const int q = q0 + u;
+                const bool none = ro[u] == 0x7fffffff; // (a NaN query: index 0, the reference's scan)
+                idx_out[q] = none ? 0 : ro[u];
+                y_aos[3 * (size_t)q] = none ? m00 : mxs[rk[u]];
+                y_aos[3 * (size_t)q + 1] = none ? m01 : mys[rk[u]];
+                y_aos[3 * (size_t)q + 2] = none ? m02 : mzs[rk[u]];
+            }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
 {
     // the Morton-ordered model image (persist_model_image): x[nm] | y[nm] | z[nm] | boxes
@@ -589,102 +729,32 @@ __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
         const int per = (nown + 3) >> 2;
         const int q_lo = wave * per, q_hi = min(nown, q_lo + per);
         for (int q0 = q_lo; q0 < q_hi; q0 += 4) {
-            double qx[4], qy[4], qz[4], bd[4];
-            int bk[4];
-            unsigned long long mlo[4], mhi[4];
+            double qx[4], qy[4], qz[4], r2s[4];
+            int rk[4], ro[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int q = min(q0 + u, q_hi - 1);
                 qx[u] = own_p[0][q];
                 qy[u] = own_p[1][q];
                 qz[u] = own_p[2][q];
-                bd[u] = INFINITY;
-                bk[u] = 0x7fffffff;
-                auto box_d2 = [&](int j) { // squared distance from the query to block j's box
-                    if (j >= nblk) return (double)INFINITY;
-                    const double *bx = boxes + 6 * j;
-                    const double ex = fmax(bx[0] - qx[u], qx[u] - bx[3]), ey = fmax(bx[1] - qy[u], qy[u] - bx[4]),
-                                 ez = fmax(bx[2] - qz[u], qz[u] - bx[5]);
-                    const double fx = ex > 0.0 ? ex : 0.0, fy = ey > 0.0 ? ey : 0.0, fz = ez > 0.0 ? ez : 0.0;
-                    return (fx * fx + fy * fy) + fz * fz;
-                };
-                const double b0 = box_d2(lane), b1 = box_d2(lane + 64);
-                double r2 = INFINITY;
-                if (seeded) { // the previous correspondence
-                    const double dx = qx[u] - own_y[0][q], dy = qy[u] - own_y[1][q], dz = qz[u] - own_y[2][q];
-                    r2 = (dx * dx + dy * dy) + dz * dz;
-                } else { // the nearest point of the block with the nearest box
-                    double bb = fmin(b0, b1);
-                    int jb = b1 < b0 ? lane + 64 : lane;
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) {
-                        const double ob = __shfl_xor(bb, o, 64);
-                        const int oj = __shfl_xor(jb, o, 64);
-                        const bool t = (ob < bb) | ((ob == bb) & (oj < jb));
-                        bb = t ? ob : bb;
-                        jb = t ? oj : jb;
-                    }
-                    const int k = min(64 * jb + lane, nm - 1); // (a valid point of block jb or of the last)
-                    const double dx = qx[u] - mxs[k], dy = qy[u] - mys[k], dz = qz[u] - mzs[k];
-                    r2 = (dx * dx + dy * dy) + dz * dz;
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) r2 = fmin(r2, __shfl_xor(r2, o, 64)); // (NaN only if all are)
-                }
-                if (!a.cull) r2 = INFINITY;
-                // every point with D64 <= r2 lies in a block whose box is within r2; the bound covers
-                // the rounding of both fp64 evaluations (+inf stays +inf, NaN stays NaN: no block)
-                const double lim = r2 * (1.0 + 0x1p-40) + 0x1p-900;
-                mlo[u] = __ballot(b0 <= lim);
-                mhi[u] = __ballot(b1 <= lim);
+                const double dx = qx[u] - own_y[0][q], dy = qy[u] - own_y[1][q], dz = qz[u] - own_y[2][q];
+                r2s[u] = (dx * dx + dy * dy) + dz * dz; // (the previous correspondence; unused unseeded)
             }
-            for (int half = 0; half < 2; ++half) {
-                unsigned long long all = 0;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) all |= half ? mhi[u] : mlo[u];
-                while (all) { // wave-uniform: one scanned block per trip
-                    const int blk = __ffsll((long long)all) - 1 + 64 * half;
-                    all &= all - 1;
-                    const int k = 64 * blk + lane;
-                    const bool valid = k < nm;
-                    const int kk = valid ? k : nm - 1;
-                    const double mx = mxs[kk], my = mys[kk], mz = mzs[kk];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (!(((half ? mhi[u] : mlo[u]) >> (blk - 64 * half)) & 1ull)) continue; // (uniform)
-                        const double dx = qx[u] - mx, dy = qy[u] - my, dz = qz[u] - mz;
-                        const double e = (dx * dx + dy * dy) + dz * dz;
-                        bool take = valid & (e < bd[u]);
-                        if (valid & (e == bd[u]) & (bd[u] < INFINITY)) // a tie: the lower original index
-                            take = orig[min(k, nm - 1)] < orig[min(bk[u], nm - 1)];
-                        bd[u] = take ? e : bd[u];
-                        bk[u] = take ? k : bk[u];
-                    }
-                }
-            }
+            lds_nn4(mxs, mys, mzs, boxes, orig, nm, nblk, a.cull, qx, qy, qz, seeded, r2s, rk, ro);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                int bo = bk[u] == 0x7fffffff ? 0x7fffffff : orig[min(bk[u], nm - 1)];
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
-                    const double od = __shfl_xor(bd[u], o, 64);
-                    const int oo = __shfl_xor(bo, o, 64), ok = __shfl_xor(bk[u], o, 64);
-                    const bool take = (od < bd[u]) | ((od == bd[u]) & (oo < bo)); // (no short circuit: selects)
-                    bd[u] = take ? od : bd[u];
-                    bo = take ? oo : bo;
-                    bk[u] = take ? ok : bk[u];
-                }
                 if (lane == 0 && q0 + u < q_hi) {
                     const int q = q0 + u;
-                    if (bo == 0x7fffffff) { // no comparison held (a NaN query): index 0, as the reference's scan
+                    if (ro[u] == 0x7fffffff) { // no comparison held (a NaN query): index 0, as the reference's scan
                         own_k[q] = 0;
                         own_y[0][q] = a.m0[0];
                         own_y[1][q] = a.m0[1];
                         own_y[2][q] = a.m0[2];
                     } else {
-                        own_k[q] = bo;
-                        own_y[0][q] = mxs[bk[u]];
-                        own_y[1][q] = mys[bk[u]];
-                        own_y[2][q] = mzs[bk[u]];
+                        own_k[q] = ro[u];
+                        own_y[0][q] = mxs[rk[u]];
+                        own_y[1][q] = mys[rk[u]];
+                        own_y[2][q] = mzs[rk[u]];
                     }
                 }
             }
@@ -1633,6 +1703,29 @@ void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, 
     }();
     (void)attr;
     icp_persistent_kernel<<<grid, kBlock, lds_bytes, st>>>(args);
+}
+
+void launch_nn_lds(const double *img, int nm, int nblk, const double *q_aos, int nq, int cull, const double m0[3],
+                   int *idx_out, double *y_aos, size_t lds_bytes, hipStream_t st)
+{
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void *)nn_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kPersistLdsMax);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)attr;
+    const int g = (nq + kLdsNNQueries - 1) / kLdsNNQueries;
+    nn_lds_kernel<<<g, kBlock, lds_bytes, st>>>(img, nm, nblk, q_aos, nq, cull, m0[0], m0[1], m0[2], idx_out, y_aos);
+}
+
+__global__ void signal_kernel(int *flag, int ticket)
+{
+    __hip_atomic_store(flag, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_signal(int *flag_dev, int ticket, hipStream_t st)
+{
+    signal_kernel<<<1, 1, 0, st>>>(flag_dev, ticket);
 }
 
 void launch_small_centroid(const double *in_aos, int n, double n_total, double *sums_out, double *out_aos, hipStream_t st)

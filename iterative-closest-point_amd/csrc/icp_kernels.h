@@ -369,6 +369,13 @@ struct TailArgs {
 };
 constexpr int kTailMaxBlocks = 192; // red_blocks(n) <= this (n <= 49,152): co-resident with room
 void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t st);
+// one thread: *flag = ticket (system scope, release) once the stream's earlier work is done
+void launch_signal(int *flag_dev, int ticket, hipStream_t st);
+// icp_closest_matrix against a model image that fits in LDS (lds_bytes = 24 nm + 48 nblk): ONE
+// launch, 32 queries (AoS) per workgroup, idx and y = m[idx] (AoS) out -- all three may be mapped
+// host memory; the first minimum of D64, as every NN path
+void launch_nn_lds(const double *img, int nm, int nblk, const double *q_aos, int nq, int cull, const double m0[3],
+                   int *idx_out, double *y_aos, size_t lds_bytes, hipStream_t st);
 // Per-operation calls on n <= kRedSingle points, ONE workgroup each on AoS data (mapped host
 // memory), bit-identical to the chains of single-workgroup passes (icp_iter.hip):
 // centroid: sums_out[3] = sum of the points, out (nullable) = in - sums / n_total;
