@@ -1293,7 +1293,20 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
         launch_icp_persistent(a, grid, lds, ctx->st);
     }
     LAUNCHCHK("icp_persistent");
-    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (stamps) { // (the timers of every workgroup: the whole grid must have finished)
+        HIPCHK(hipStreamSynchronize(ctx->st));
+    } else { // workgroup 0's last store (h_flags[7] = barriers used, a release after the run's
+             // mirrored state); an aborted launch never writes it and ends with the stream
+        for (unsigned spin = 1; __atomic_load_n(ctx->h_flags + 7, __ATOMIC_ACQUIRE) == 0; ++spin) {
+            if ((spin & 1023u) == 0) {
+                const hipError_t q = hipStreamQuery(ctx->st);
+                if (q == hipErrorNotReady) continue;
+                if (q != hipSuccess) return fail(ctx, ICP_E_HIP, std::string("icp_run: ") + hipGetErrorString(q));
+                break; // (finished: aborted, or the word landed just now)
+            }
+            __builtin_ia32_pause();
+        }
+    }
     if (stamps) { // phase durations of workgroup 0 (tags: 0 NN begin, 1 NN end, 2 published,
                   // 3 barrier passed, 8 partials loaded, 4 folded, 5 Horn done, 6 transformed, 7 end)
         std::vector<unsigned long long> h(2 * kPersistMaxStamps + 2 * kBlock + 8 * kBlock + 2 * kBlock);

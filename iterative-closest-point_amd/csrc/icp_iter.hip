@@ -867,7 +867,8 @@ __global__ __launch_bounds__(kBlock) void icp_persistent_kernel(PersistArgs a)
     if (b == 0 && tid == 0) {
         *a.s_glob = st;
         // the barriers this launch used: the next launch continues the monotonic counters
-        __hip_atomic_store(a.h_epochs, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // (release: the run's mirrored state and trace before it -- the host waits on this word)
+        __hip_atomic_store(a.h_epochs, (int)epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1644,7 +1645,8 @@ __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(Persist
     }
     if (b == 0 && tid == 0) {
         *a.s_glob = st;
-        __hip_atomic_store(a.h_epochs, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // (release: the run's mirrored state and trace before it -- the host waits on this word)
+        __hip_atomic_store(a.h_epochs, (int)epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
