@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--cases", type=int, default=200)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-seconds", type=float, default=400.0)
+    ap.add_argument("--only", type=int, default=-1, help="run just this case (the others' data is still drawn)")
+    ap.add_argument("--dump", default="", help="with --only: save the case's clouds and both runs' indices (.npz)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     t0 = time.time()
@@ -82,12 +84,17 @@ def main():
             p = np.round(p * 2) / 2 + 0.5 * (rng.random() < 0.5)  # many exact half-integer ties
         iters = int(rng.integers(1, 12))
         thr = -1.0 if rng.random() < 0.5 else 1e-6
+        if a.only >= 0 and c != a.only:
+            continue
         one = run(m, p, icp_amd.RUN_PERSISTENT, iters, thr)
         loop = run(m, p, icp_amd.RUN_LAUNCHES, iters, thr)
-        ok = (one[4] == 1 and loop[4] == 0 and one[0] == loop[0] and np.array_equal(one[1], loop[1])
-              and np.array_equal(one[2], loop[2]) and np.array_equal(one[3], loop[3]))
+        ok = (one[4] == 1 and loop[4] == 0 and one[0] == loop[0] and np.array_equal(one[1], loop[1], equal_nan=True)
+              and np.array_equal(one[2], loop[2], equal_nan=True) and np.array_equal(one[3], loop[3]))
         done += 1
         fails += not ok
+        if a.dump:
+            np.savez(a.dump, m=m, p=p, iters=iters, thr=thr, one_err=one[1], loop_err=loop[1], one_idx=one[3],
+                     loop_idx=loop[3], one_p=one[2], loop_p=loop[2])
         rec = {"case": c, "n": n, "nm": nm, "kind": kind, "iters": iters, "thr": thr, "ran": one[0],
                "one_launch": one[4], "bitwise": ok}
         print(json.dumps(rec), flush=True)
