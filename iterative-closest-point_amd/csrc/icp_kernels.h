@@ -329,10 +329,12 @@ int launch_mid_order(const double *px, const double *py, const double *pz, int n
 constexpr int kPersistMaxStamps = 1024;
 constexpr int kPersistSyncWords = 512; // barrier words (icp_iter.hip: persist_barrier)
 void launch_icp_persistent(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st);
-// The same for 4,096 < n <= kTailMaxBlocks * 256 (icp_persistent_mid_kernel): grid = red_blocks(n)
-// workgroups of 512 threads, the model image in global memory (nm <= kPersistMidMaxModel: <= 64
-// superblocks of 16 tiles), its fp32 tile and block boxes in LDS (lds_bytes = 24 (tiles +
-// ceil(nm / 16))), part = 2 x kTailMaxBlocks x kNumSums.
+// The same for 4,096 < n <= kTailMaxBlocks * 256 (icp_persistent_mid_kernel): grid =
+// max(red_blocks(n), min(kTailMaxBlocks, 3/4 of the CUs)) workgroups of 512 threads (the ones past
+// red_blocks(n) own no point and only search), the model image in global memory (nm <=
+// kPersistMidMaxModel: <= 64 superblocks of 16 tiles), its fp32 tile and block boxes in LDS
+// (lds_bytes = 24 (tiles + ceil(nm / 16))), part = 2 x kTailMaxBlocks x kNumSums; q4 / res / perm:
+// the published queries, their correspondences and the search order (launch_mid_order).
 constexpr int kPersistMidMaxModel = 64 * 16 * 64;
 constexpr size_t kPersistMidLdsMax = 24 * (kPersistMidMaxModel / 64 + kPersistMidMaxModel / 16);
 void launch_icp_persistent_mid(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st);
