@@ -259,6 +259,36 @@ def test_surface_ops_match_oracle(amd, oracle):
         np.testing.assert_array_equal(p_new, op)  # per-point transform bitwise = oracle
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 255, 256, 257, 2903, 4095, 4096, 4097, 10000])
+def test_surface_ops_across_the_single_workgroup_boundary(amd, oracle, n):
+    """The per-operation calls take one launch on mapped memory up to 4,096 points and the
+    multi-workgroup passes above: both against the oracle on random clouds of every size class,
+    the per-point transform bitwise.  (find_alignment from 3 points: with 1 point the scale is
+    0 / 0 on every path, with 2 the rotation about their line is undetermined.)"""
+    rng = np.random.default_rng(n)
+    p = rng.normal(size=(n, 3)) * 3.0 + 1.0
+    y = p @ np.array([[0.96, -0.28, 0.0], [0.28, 0.96, 0.0], [0.0, 0.0, 1.0]]).T + 0.3 + rng.normal(scale=0.01, size=(n, 3))
+    al = oracle.find_alignment(p, y)
+    with amd.Context(0, 0) as ctx:
+        mu, centred = ctx.compute_centroid(p)
+        np.testing.assert_allclose(mu, p.mean(axis=0), rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(centred, p - mu, atol=0)
+        if n >= 3:
+            s, R, t, e = ctx.find_alignment(p, y)
+            assert s == pytest.approx(al.s, rel=1e-10)
+            np.testing.assert_allclose(R, np.array(al.R).reshape(3, 3), atol=1e-10)
+            np.testing.assert_allclose(t, np.array(al.t), atol=1e-9)
+            assert e == pytest.approx(al.err, rel=1e-8, abs=1e-12)
+        sc, R0, t0 = 1.01, [0.96, -0.28, 0.0, 0.28, 0.96, 0.0, 0.0, 0.0, 1.0], [0.1, -0.2, 0.3]
+        sR = (sc * np.array(R0)).reshape(9)
+        e1, p_same = ctx.err_compute(y, p, False, sR, t0)
+        np.testing.assert_array_equal(p_same, p)
+        e2, p_new = ctx.err_compute(y, p, True, sR, t0)
+        oe, op = oracle.err_compute(p, y, sc, R0, t0)
+        assert e1 == e2 and e2 == pytest.approx(oe, rel=1e-11, abs=1e-12)
+        np.testing.assert_array_equal(p_new, op)  # per-point transform bitwise = oracle
+
+
 def test_reference_shaped_icp_class(amd, golden_traces):
     m, p = load(amd, "cow_ref"), load(amd, "cow_tr1")
     icp = amd.ICP(m, p, 20)
