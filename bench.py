@@ -483,6 +483,10 @@ def main():
             if "all_cores" in out["cpu_baseline"]:
                 out["gpu_vs_cpu_all_cores"] = out["value"] / out["cpu_baseline"]["all_cores"]["value"]
         print(json.dumps(out), flush=True)
+    if dist is not None:
+        # rank 0 spent its CPU-baseline time above: every rank reaches the RCCL communicator's
+        # destroy together rather than some destroying while a peer is still inside the job
+        dist.barrier()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
