@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — ICP iterations/s on MI355X (BASELINE.json metric, config C4).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n POINTS] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--points N] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Workload (BASELINE.json configs[3]): synthetic 2^20-point model uniform in
@@ -288,7 +288,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1 << 20)
+    # (--points under torchrun: its own parser takes a bare "--n" for an ambiguous prefix of
+    # --nnodes / --nproc-per-node and stops)
+    ap.add_argument("--points", "--n", dest="n", type=int, default=1 << 20)
     ap.add_argument("--nn", choices=["certified", "fp64"], default="certified")
     ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16", "grid"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -411,7 +413,8 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic (mt19937_64 seed 42, uniform [-1,1]^3; scene = 5deg rotation + translation)",
-            "config": {"workload": f"C4 synthetic {args.n}-pt model vs rigid-transformed copy, fixed iterations",
+            "config": {"workload": f"{ {1 << 20: 'C4', 1 << 23: 'C5'}.get(args.n, 'custom')} synthetic "
+                                   f"{args.n}-pt model vs rigid-transformed copy, fixed iterations",
                        "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
                        "parallelism": f"scene-sharded x{world}, model replicated, "
                                       + ("gloo host all-reduce (rehearsal)" if os.environ.get("ICP_BENCH_HOST_REDUCE") == "1" and world > 1
