@@ -361,3 +361,37 @@ def test_randomised_bitwise_fuzz(amd):
         assert one[0] == loop[0], (c, n, nm, kind)
         for x, y in zip(one[1:4], loop[1:4]):
             np.testing.assert_array_equal(x, y, err_msg=f"case {c}: n={n} nm={nm} {kind}")
+
+
+def test_scale_fuzz_certified_equals_fp64(amd):
+    """tools/scale_fuzz.py, a short run: the default cascade of the launch loop (f16 MFMA filter,
+    certificate, grid resolver, fp64 fallback) against the fp64 brute force at 2^15..2^19 points,
+    every model shape of persist_fuzz, rescaled and offset clouds; unseeded and seeded iterations
+    bit for bit (error trace, final cloud, per-iteration correspondence digests).  Longer runs:
+    profiles/r02s3g/."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "scale_fuzz", os.path.join(os.path.dirname(__file__), "..", "tools", "scale_fuzz.py"))
+    sf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sf)
+    rng = np.random.default_rng(77)
+    kinds = ["uniform", "surface", "clusters", "lattice", "duplicates"]
+    queued = 0
+    for c in range(10):
+        n, nm = int(2 ** rng.uniform(15, 18)), int(2 ** rng.uniform(15, 18))
+        kind = kinds[c % len(kinds)]
+        m = sf.model(rng, kind, nm)
+        p = sf.rigid(rng, m[rng.integers(0, nm, n)] + rng.normal(scale=0.01, size=(n, 3)), [0.2, 1.0, 10.0][c % 3])
+        if kind == "lattice":
+            p = np.round(p * 2) / 2 + 0.5
+        else:
+            sc, off = 10.0 ** rng.uniform(-3, 3), rng.normal(size=3) * 100.0
+            m, p = m * sc + off * sc, p * sc + off * sc
+        cert = sf.run(m, p, amd.NN_CERTIFIED, 3)
+        ref = sf.run(m, p, amd.NN_FP64, 3)
+        assert cert[0] == ref[0] == 3, (c, n, nm, kind)
+        for x, y in zip(cert[1:4], ref[1:4]):
+            np.testing.assert_array_equal(x, y, err_msg=f"case {c}: n={n} nm={nm} {kind}")
+        queued += cert[4]["level1_queued"]
+    assert queued > 0  # the grid resolver took part
