@@ -7,7 +7,7 @@ Each case runs a fixed number of ICP iterations (the first unseeded, the rest se
 modes and must agree bit for bit: error trace, final cloud and every iteration's
 correspondence digest.
 
-    python tools/scale_fuzz.py --cases 40 --seed 1 [--max-seconds 400]
+    python tools/scale_fuzz.py --cases 40 --seed 1 [--max-seconds 400] [--log2 15 19]
 """
 import argparse
 import json
@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--cases", type=int, default=40)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--max-seconds", type=float, default=400.0)
+    ap.add_argument("--log2", type=float, nargs=2, default=[15.0, 19.0], metavar=("LO", "HI"),
+                    help="cloud sizes 2^U(LO, HI) (20 20: C4-size clouds)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     t0 = time.time()
@@ -48,8 +50,8 @@ def main():
     for c in range(a.cases):
         if time.time() - t0 > a.max_seconds:
             break
-        n = int(2 ** rng.uniform(15, 19))
-        nm = int(2 ** rng.uniform(15, 19))
+        n = int(2 ** rng.uniform(*a.log2))
+        nm = int(2 ** rng.uniform(*a.log2))
         kind = kinds[int(rng.integers(0, len(kinds)))]
         m = model(rng, kind, nm)
         p = m[rng.integers(0, nm, n)] + rng.normal(scale=rng.choice([0.0, 1e-3, 0.02]), size=(n, 3))
