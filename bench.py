@@ -132,6 +132,35 @@ def cpu_baseline(m, p, sample=4096, seed=0):
     return out
 
 
+def rank_record(rank, info, filter_ms, allreduce_ms, n_local, iterations):
+    """One rank's entry of the line's per_rank: its level-1 filter time and per-iteration
+    all-reduce latency (HIP events on the engine stream), and what it ran on -- its RCCL
+    communicator's ncclCommCount / ncclCommUserRank (null / its own rank without RCCL) and the
+    PCI bus id of its device (icp_get_comm_info)."""
+    return {"rank": rank, "filter_ms": filter_ms, "allreduce_ms_per_iter": allreduce_ms,
+            "n_scene_local": n_local, "iterations": iterations, "comm_count": info["comm_count"],
+            "comm_rank": info["comm_rank"], "pci_bus_id": info["pci_bus_id"]}
+
+
+def check_devices(per_rank, world, rccl):
+    """None if the ranks are what the line claims, else why not.  With RCCL every rank must
+    sit in one communicator of `world` ranks, at its own rank, on its own GPU (N distinct PCI
+    bus ids); without RCCL (1 rank, or the gloo rehearsal of several ranks on one GPU) only the
+    ranks themselves are checked."""
+    ranks = sorted(r["rank"] for r in per_rank)
+    if ranks != list(range(world)):
+        return f"per_rank holds ranks {ranks}, expected 0..{world - 1}"
+    if not rccl:
+        return None
+    bad = [r["rank"] for r in per_rank if r["comm_count"] != world or r["comm_rank"] != r["rank"]]
+    if bad:
+        return f"ranks {bad} are not rank r of a {world}-rank RCCL communicator"
+    buses = [r["pci_bus_id"] for r in per_rank]
+    if len(set(buses)) != world:
+        return f"{world} RCCL ranks on {len(set(buses))} distinct GPUs ({sorted(buses)})"
+    return None
+
+
 def _cow_paths():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import datasets
@@ -365,11 +394,13 @@ def main():
 
     nn_avg_ms = st["nn_ms"] / max(st["nn_launches"], 1)
     ar_ms = st["allreduce_ms"] / st["allreduce_calls"] if st["allreduce_calls"] else None
-    per_rank = [(rank, nn_avg_ms, ar_ms, c)]
+    host_reduce = world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1"
+    per_rank = [rank_record(rank, ctx.comm_info(), nn_avg_ms, ar_ms, c, st["iterations"])]
     if dist is not None:
         got = [None] * world
         dist.all_gather_object(got, per_rank[0])
         per_rank = got
+    device_error = check_devices(per_rank, world, rccl=(world > 1 and not host_reduce) or args.rccl)
     pairs = c * args.n
     # algorithmic flop against the peak of the unit the kernel runs on
     flops = FLOP_PER_PAIR * pairs
@@ -434,8 +465,7 @@ def main():
                                             f"pairs = {c} local queries x {args.n} model points",
                          "pairs_per_s": pairs / nn_s if nn_s > 0 else 0.0,
                          "nn_hbm": nn_hbm},
-            "per_rank": [{"rank": r, "filter_ms": f, "allreduce_ms_per_iter": a, "n_scene_local": cc}
-                         for r, f, a, cc in per_rank],
+            "per_rank": per_rank,
             "mfma_uncertified_per_iter": st["level1_queued"] / max(st["iterations"], 1),
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
@@ -485,6 +515,8 @@ def main():
             out["gpu_vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             if "all_cores" in out["cpu_baseline"]:
                 out["gpu_vs_cpu_all_cores"] = out["value"] / out["cpu_baseline"]["all_cores"]["value"]
+        if device_error:
+            out["device_error"] = device_error
         print(json.dumps(out), flush=True)
     if dist is not None:
         # rank 0 spent its CPU-baseline time above: every rank reaches the RCCL communicator's
@@ -493,6 +525,11 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+    if device_error:
+        # the line was printed (with device_error) for the record, but the run did not measure
+        # what it claims: N ranks of RCCL on N distinct GPUs
+        print(f"[bench] {device_error}", file=sys.stderr)
+        sys.exit(3)
 
 
 def reap_children():

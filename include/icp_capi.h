@@ -54,12 +54,17 @@ extern "C" {
  * GRID:   no brute-force filter: exact fp64 search on the model grid for every query
  *         (same first-minimum rule, same results); O(N) instead of
  *         O(N*M) for clouds whose nearest neighbours are local.
- * AUTO:   MFMA16 when both clouds have >= 65536 points, else VALU. */
+ * BUNDLE: MFMA16 behind an exact MFMA bound per (query, 32-point kd bundle of the model):
+ *         every query is tested against every bundle (N x M/32 bound evaluations, 32 x 32 per
+ *         instruction) and only the bundles that may hold a point as close as the query's
+ *         seed run the pair test (icp_bundle.hip).  Same results.
+ * AUTO:   MFMA16 when both clouds have >= 8192 points, else VALU. */
 #define ICP_NN_VARIANT_AUTO 0
 #define ICP_NN_VARIANT_VALU 1
 #define ICP_NN_VARIANT_MFMA 2
 #define ICP_NN_VARIANT_MFMA16 3
 #define ICP_NN_VARIANT_GRID 4
+#define ICP_NN_VARIANT_BUNDLE 5
 
 typedef struct icp_ctx icp_ctx;
 
@@ -243,6 +248,18 @@ int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap);
 
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out);
 int icp_reset_stats(icp_ctx *ctx);
+/* Instrumentation of the bundle filter (ICP_NN_VARIANT_BUNDLE): with enable = 1 its searches
+ * count, from zero, (out[0]) the 32-bundle blocks whose joint bound test fired in a wave,
+ * (out[1]) the 32-query groups with a bundle V <= 0 in them, (out[2]) the pair tests run
+ * (one f16 MFMA of 32 queries x 32 points each) -- the executed work behind the roofline;
+ * 0 = off (the default; no counting). */
+int icp_set_bundle_counters(icp_ctx *ctx, int enable);
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[3]);
+/* Who this context talks to (evidence for multi-GPU runs): *comm_count / *comm_rank =
+ * ncclCommCount / ncclCommUserRank of its RCCL communicator, or -1 / the context's rank when
+ * it has none (plain or host all-reduce contexts); bus_id (nullable, len >= 16) = the PCI bus
+ * id of its HIP device (hipDeviceGetPCIBusId), NUL-terminated. */
+int icp_get_comm_info(icp_ctx *ctx, int *comm_count, int *comm_rank, char *bus_id, int len);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,489 @@
+// icp_bundle.hip — the bundle-bound level-1 filter (ICP_NN_VARIANT_BUNDLE; the default for
+// large clouds): the f16 MFMA filter of icp_kernels.hip, with an exact MFMA bound per
+// (query, bundle of 32 model points) in front of the pair test.
+//
+// The reference's search (compute_Y_w_opti, src/GPU/compute.cu:154-245) evaluates every
+// (query, model point) pair.  Here every query is still tested against every model point's
+// BUNDLE: the model is stored in kd order (icp_bundle_kd_order), so 32 consecutive points form
+// a compact bundle b with centre c_b and radius r_b, and one v_mfma_f32_32x32x16_f16 evaluates
+// for 32 queries x 32 bundles
+//     V = |q - c|^2 - (d + r)^2  =  [q, 1, |q|^2 - d^2, d] . [-2c, |c|^2 - r^2, 1, -2r]
+// where d is the query's seed distance (its previous correspondence, or the grid seed).  V > 0
+// proves that no point of the bundle is as close as the seed, so the bundle cannot hold the
+// first minimum (nor tie with it): only the bundles with V <= 0 run the f16 pair test of
+// nn_mfma16r_kernel, which tracks (best, second, block) exactly as there.  The certificate,
+// the grid resolver and the fp64 fallback downstream are unchanged, so the returned indices
+// are the same fp64 first minimum bit for bit ("bundle bound").
+//
+// Soundness (scaled, centred units; S = 2^e, u = 2^-24; proof in DESIGN.md §3.1):
+//  * d' = (sqrt(D64(p, m_seed)) S (1 + 2^-40) + e_q)(1 + 2^-20) + 2^-20, e_q = 2^-20 |a|_1 +
+//    2^-22 >= |q^ - Q| (the f16 hi/lo split of the query), so every m with D64(p, m) <=
+//    D64(p, m_seed) has |Q - M| <= d' - e_q;
+//  * r' >= max_i |M_i - c^| over the bundle's points, c^ = the centre as the MFMA sees it;
+//  * the MFMA's sum differs from |q^ - c^|^2 - (d' + r')^2 by less than the margins
+//    mu_q = 2^-16 (|q^|^2 + d'^2) + 2^-4 and mu_c = 2^-16 (|c^|^2 + r'^2) + 2^-4 folded into
+//    the (|q|^2 - d^2) and (|c|^2 - r^2) operands (accumulation <= 24u sum|p| by the measured
+//    model of DESIGN.md §3.1, dropped lo x lo products <= 2^-22 each side, hi/lo representation
+//    of the composite operands, subnormal lo parts <= 2^-7 absolute): V^ > 0 => V > 0.
+// Queries outside the operand range (|a_k| > 8192 or d' > 11000) get V^ <= 0 for every bundle
+// (all bundles searched: the pair filter alone decides, as in nn_mfma16r_kernel).
+#include "icp_kernels.h"
+#include "icp_device.h"
+#include "icp_mfma16.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <type_traits>
+#include <vector>
+
+namespace icp {
+namespace {
+
+inline int bgrid(size_t n) { return (int)std::min<size_t>((n + kBlock - 1) / kBlock, 2048); }
+
+constexpr int kBundle = 32;                           // model points per bundle (= one pair block)
+constexpr int kBTile = 256;                           // bundles per LDS tile (8 KiB), x2 buffers
+constexpr int kBBlocksPerTile = kBTile / 32;          // 8 bundle blocks of 32 bundles
+constexpr int kBDmaPerWave = kBBlocksPerTile / 4;     // 2 wave-instructions per tile
+constexpr int kBVmcntDma = 0x0F70 | kBDmaPerWave;     // vmcnt(2): one tile's DMA may stay in flight
+constexpr int kBQG = 8;                               // 32-query groups per wave
+constexpr double kBQueryMax = 8192.0;                 // |a_k| range of the bundle operand
+constexpr double kBSeedMax = 11000.0;                 // d' range of the bundle operand
+
+// Query side of the bundle MFMA (see the file header): lane half h of query a (scaled,
+// clamped), seed distance d' (already inflated).  Slots: h = 0: qx hi, lo, hi, qy hi, lo, hi,
+// qz hi, lo; h = 1: qz hi, W hi, W lo, 4096, 4096, d hi, d lo, d hi, with
+// W = (|q^|^2 - d'^2 - mu_q) / 4096.  kBqForced: V^ <= 0 for every bundle (a query outside the
+// operand range); kBqNever: V^ > 0 for every bundle (a slot past the last query).
+enum { kBqNormal = 0, kBqForced = 1, kBqNever = 2 };
+__device__ __forceinline__ half8_t bundle_query_frag(const double a[3], double dq, int mode, int h)
+{
+    _Float16 xh, xl, yh, yl, zh, zl;
+    split_f16(a[0], xh, xl);
+    split_f16(a[1], yh, yl);
+    split_f16(a[2], zh, zl);
+    half8_t b;
+    if (h == 0) {
+        b[0] = xh; b[1] = xl; b[2] = xh; b[3] = yh;
+        b[4] = yl; b[5] = yh; b[6] = zh; b[7] = zl;
+        return b;
+    }
+    const double q0 = (double)xh + (double)xl, q1 = (double)yh + (double)yl, q2 = (double)zh + (double)zl;
+    const double qq = (q0 * q0 + q1 * q1) + q2 * q2;
+    const double mu = 0x1.0p-16 * (qq + dq * dq) + 0x1.0p-4;
+    _Float16 wh, wl, dh, dl;
+    split_f16((qq - dq * dq - mu) / 4096.0, wh, wl);
+    split_f16(dq, dh, dl);
+    if (mode != kBqNormal) { // forced: V^ < -6.7e7 for every bundle; never (no query): V^ > 6.7e7
+        wh = mode == kBqForced ? (_Float16)-65504.0f : (_Float16)65504.0f;
+        wl = (_Float16)0.0f;
+        dh = (_Float16)0.0f;
+        dl = (_Float16)0.0f;
+    }
+    b[0] = zh; b[1] = wh; b[2] = wl; b[3] = (_Float16)4096.0f;
+    b[4] = (_Float16)4096.0f; b[5] = dh; b[6] = dl; b[7] = dh;
+    return b;
+}
+
+// Seeded f16 filter behind the bundle bound.  Per wave 8 groups of 32 queries (256); the
+// queries of a workgroup are consecutive in `order` (a spatial order of the scene), so that
+// their bundles with V^ <= 0 coincide.  Per 32-bundle block: one bundle MFMA per group into
+// ONE joint v_min3 tree (carried, two MFMAs behind, as nn_mfma16r_kernel); when it is <= 0 the
+// trigger path re-issues the block's bundle MFMAs, collects per group the bundles with a
+// V^ <= 0 lane, and runs for each the pair MFMA (pair image in kd order, 1 KiB per bundle,
+// from L2) and the med3/min tracking of nn_mfma16r_kernel.  The groups' pair operands wait in
+// LDS for that path and for the index recovery (their VGPRs would cost the third wave).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_bundle_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, int np,
+    const int *__restrict__ order, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx,
+    double cy, double cz, double scale, const unsigned *__restrict__ seed16, const half8_t *__restrict__ bimg,
+    int nb_pad, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int nm, int chunk,
+    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx,
+    const int *__restrict__ stop, unsigned long long *__restrict__ counters)
+{
+    if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
+    constexpr int QG = kBQG;
+    unsigned n_blocks = 0, n_groups = 0, n_pairs = 0; // (counters: wave-uniform tallies)
+    __shared__ half8_t tiles[2][kBTile * 2];        // 2 x 8 KiB
+    __shared__ half8_t s_bq[4][QG][64];             // 32 KiB: the pair operands
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int split = blockIdx.y;
+    const int b0 = split * chunk;
+    const int b1 = min(b0 + chunk, nb_pad);
+    const int sbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
+
+    half8_t bb[QG];
+    float best[QG], second[QG];
+    int bblk[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int s = sbase + q * 32;
+        double a[3] = {0.0, 0.0, 0.0};
+        unsigned sd = 0u;
+        double dq = 0.0;
+        int mode = kBqNever;
+        if (s < np) {
+            const int j = order ? order[s] : s;
+            const double p0 = px[j], p1 = py[j], p2 = pz[j];
+            a[0] = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[1] = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+            a[2] = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+            sd = seed16[j];
+            // the seed distance in the reference's fp64 arithmetic (compute.cu:112-117)
+            const double4 m = m4[prev[j]];
+            const double dx = p0 - m.x, dy = p1 - m.y, dz = p2 - m.z;
+            const double D = (dx * dx + dy * dy) + dz * dz;
+            const double eq = 0x1.0p-20 * ((fabs(a[0]) + fabs(a[1])) + fabs(a[2])) + 0x1.0p-22;
+            dq = (sqrt(D) * scale * (1.0 + 0x1.0p-40) + 1e-300 + eq) * (1.0 + 0x1.0p-20) + 0x1.0p-20;
+            mode = fabs(a[0]) <= kBQueryMax && fabs(a[1]) <= kBQueryMax && fabs(a[2]) <= kBQueryMax && dq <= kBSeedMax
+                       ? kBqNormal
+                       : kBqForced;
+        }
+        s_bq[wave][q][lane] = query_frag(a, h, sd);
+        bb[q] = bundle_query_frag(a, dq, mode, h);
+        best[q] = 0.0f; // seeded: "nothing below s0'"
+        second[q] = 0.0f;
+        bblk[q] = 0;
+    }
+    const f32x16_t zero = {};
+
+    auto issue_tile = [&](int tb, int buf) {
+#pragma unroll
+        for (int i = 0; i < kBDmaPerWave; ++i) {
+            const int blk = wave + 4 * i;
+            __builtin_amdgcn_global_load_lds((const void *)(bimg + ((size_t)(tb >> 5) + blk) * 64 + lane),
+                                             (__attribute__((address_space(3))) void *)&tiles[buf][blk * 64],
+                                             16, 0, 0);
+        }
+    };
+    // the rare path: which bundles of this 32-bundle block may hold a point at least as close
+    // as some query's seed, and the pair test against each of them
+    auto update = [&](const half8_t &a8, int bblock) {
+        ++n_blocks;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bb[q], zero, 0, 0, 0);
+            unsigned mask = 0u;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const unsigned long long bl = __ballot(d[r] <= 0.0f);
+                const int row = (r & 3) + 8 * (r >> 2);
+                mask |= ((unsigned)bl != 0u ? 1u << row : 0u) | ((unsigned)(bl >> 32) != 0u ? 1u << (row + 4) : 0u);
+            }
+            if (!mask) continue;
+            ++n_groups;
+            n_pairs += __builtin_popcount(mask);
+            const half8_t bqv = s_bq[wave][q][lane];
+            while (mask) {
+                const int b = __builtin_ctz(mask);
+                mask &= mask - 1u;
+                const int blk = bblock * 32 + b; // pair block = bundle (kd order)
+                const half8_t ap = pimg[(size_t)blk * 64 + lane];
+                const f32x16_t dd = __builtin_amdgcn_mfma_f32_32x32x16_f16(ap, bqv, zero, 0, 0, 0);
+                if (!__any(min16v(dd) < second[q])) continue;
+                const float prevb = best[q];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], dd[r]);
+                    best[q] = fminf(best[q], dd[r]);
+                }
+                bblk[q] = best[q] < prevb ? blk : bblk[q];
+            }
+        }
+    };
+    // one 32-bundle block: d0, d1 = its q0, q1 results (issued one step earlier); issues the
+    // next block's q0, q1 MFMAs into dn0, dn1 unless LAST (nn_mfma16r_kernel's pipeline)
+    auto step = [&](const half8_t &a8, const half8_t &an, f32x16_t &d0, f32x16_t &d1, f32x16_t &dn0,
+                    f32x16_t &dn1, int bblock, auto last_tag) {
+        constexpr bool LAST = decltype(last_tag)::value;
+        float u, v;
+        f32x16_t dm2 = d0, dm1 = d1;
+#pragma unroll
+        for (int k = 2; k < QG; ++k) {
+            const f32x16_t dk = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bb[k], zero, 0, 0, 0);
+            if (k == 2) tree16(dm2, u, v);
+            else tree18(dm2, u, v);
+            dm2 = dm1;
+            dm1 = dk;
+        }
+        if (!LAST) dn0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bb[0], zero, 0, 0, 0);
+        tree18(dm2, u, v);
+        if (!LAST) dn1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(an, bb[1], zero, 0, 0, 0);
+        tree18(dm1, u, v);
+        const bool need = fminf(u, v) <= 0.0f;
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+#pragma unroll
+        for (int k = 3; k < QG; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        }
+        if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
+        if (__builtin_expect(__any(need), 0)) update(a8, bblock);
+    };
+    using More = std::integral_constant<bool, false>;
+    using Last = std::integral_constant<bool, true>;
+
+    issue_tile(b0, 0);
+    int it = 0;
+    for (int t0 = b0; t0 < b1; t0 += kBTile, ++it) {
+        const int cur = it & 1;
+        if (t0 + kBTile < b1) {
+            issue_tile(t0 + kBTile, cur ^ 1);
+            __builtin_amdgcn_s_waitcnt(kBVmcntDma);
+        } else {
+            __builtin_amdgcn_s_waitcnt(kVmcnt0);
+        }
+        __builtin_amdgcn_s_barrier();
+        const half8_t *tile = tiles[cur];
+        const int blk0 = t0 >> 5;
+        half8_t a0 = tile[lane], a1 = tile[64 + lane];
+        f32x16_t dA0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[0], zero, 0, 0, 0);
+        f32x16_t dA1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[1], zero, 0, 0, 0), dB0, dB1;
+#pragma unroll
+        for (int b = 0; b < kBBlocksPerTile - 2; b += 2) {
+            step(a0, a1, dA0, dA1, dB0, dB1, blk0 + b, More{});
+            a0 = tile[(b + 2) * 64 + lane];
+            step(a1, a0, dB0, dB1, dA0, dA1, blk0 + b + 1, More{});
+            a1 = tile[(b + 3) * 64 + lane];
+        }
+        step(a0, a1, dA0, dA1, dB0, dB1, blk0 + kBBlocksPerTile - 2, More{});
+        step(a1, a0, dB0, dB1, dA0, dA1, blk0 + kBBlocksPerTile - 1, Last{});
+        __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+        __builtin_amdgcn_s_barrier();
+    }
+
+    if (counters && lane == 0) { // icp_set_bundle_counters: the executed work of this wave
+        atomicAdd(counters, (unsigned long long)n_blocks);
+        atomicAdd(counters + 1, (unsigned long long)n_groups);
+        atomicAdd(counters + 2, (unsigned long long)n_pairs);
+    }
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const float b = best[q];
+        const float s2 = second[q];
+        const int blk = bblk[q];
+        const half8_t bqv = s_bq[wave][q][lane];
+        // index recovery (nn_mfma16r_kernel): re-run the pair MFMA on each distinct winning
+        // block; the lowest row with d == best (ties never certify: second would equal best)
+        int found = -1;
+        bool done = !(b < 0.0f);
+        for (int guard = 0; guard < 64; ++guard) {
+            const unsigned long long pend = __ballot(!done);
+            if (pend == 0ull) break;
+            const int lead = __ffsll((long long)pend) - 1;
+            const int rb = __shfl(blk, lead, 64);
+            const half8_t a8 = pimg[(size_t)rb * 64 + lane];
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bqv, zero, 0, 0, 0);
+            if (!done && blk == rb) {
+#pragma unroll
+                for (int r = 15; r >= 0; --r) {
+                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    found = (d[r] == b) ? rb * 32 + row : found;
+                }
+                done = true;
+            }
+        }
+        float bb2 = b, ss = s2;
+        int id = found;
+        {
+            const float ob = __shfl_xor(bb2, 32, 64), os = __shfl_xor(ss, 32, 64);
+            const int oi = __shfl_xor(id, 32, 64);
+            if (ob < bb2) {
+                ss = fminf(bb2, os);
+                bb2 = ob;
+                id = oi;
+            } else {
+                ss = fminf(ss, ob);
+                if (ob == bb2 && oi >= 0 && (id < 0 || oi < id)) id = oi;
+            }
+        }
+        const int s = sbase + q * 32;
+        if (h == 0 && s < np) {
+            const int j = order ? order[s] : s;
+            const size_t o = (size_t)split * np + j;
+            part_best[o] = bb2;
+            part_second[o] = ss;
+            part_idx[o] = id >= 0 ? kd_orig[id] : -1; // kd position -> original index (padding: nm)
+        }
+    }
+}
+
+// The model's kd-ordered images: pair image (build_mimage16_kernel's format, kd order, padding
+// points past nm) and the original index of every kd position (nm for padding).
+__global__ __launch_bounds__(kBlock) void build_pair_image_kd_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz, int nm,
+    const int *__restrict__ kd, int nm_b, double cx, double cy, double cz, double scale, half8_t *__restrict__ img,
+    int *__restrict__ kd_orig)
+{
+    for (int P = blockIdx.x * kBlock + threadIdx.x; P < nm_b; P += gridDim.x * kBlock) {
+        half8_t lo8 = {}, hi8 = {};
+        const int o = P < nm ? kd[P] : nm;
+        if (P < nm) {
+            const double b0 = (mx[o] - cx) * scale, b1 = (my[o] - cy) * scale, b2 = (mz[o] - cz) * scale;
+            const double mm = b0 * b0 + b1 * b1 + b2 * b2;
+            _Float16 xh, xl, yh, yl, zh, zl, mh, ml;
+            split_f16(b0, xh, xl);
+            split_f16(b1, yh, yl);
+            split_f16(b2, zh, zl);
+            split_f16(mm / 4096.0, mh, ml);
+            lo8[0] = xh; lo8[1] = xl; lo8[2] = xh; lo8[3] = yh;
+            lo8[4] = yl; lo8[5] = yh; lo8[6] = zh; lo8[7] = zl;
+            hi8[0] = zh; hi8[1] = mh; hi8[2] = ml; hi8[3] = xl;
+            hi8[4] = yl; hi8[5] = zl; hi8[6] = (_Float16)16384.0f; hi8[7] = (_Float16)16384.0f;
+        } else {
+            hi8[1] = (_Float16)65504.0f;
+            hi8[6] = (_Float16)16384.0f;
+            hi8[7] = (_Float16)16384.0f;
+        }
+        const int blk = P >> 5, i = P & 31;
+        img[(size_t)blk * 64 + i] = lo8;
+        img[(size_t)blk * 64 + 32 + i] = hi8;
+        kd_orig[P] = o;
+    }
+}
+
+// Bundle image: bundle b = kd positions [32 b, 32 b + 32); lane half h of row i of its
+// 32-bundle block holds slots 8h..8h+7: -2cx hi, hi, lo, -2cy hi, hi, lo, -2cz hi, hi |
+// -2cz lo, 4096, 4096, W hi, W lo, -2r hi, hi, lo with W = (|c^|^2 - r'^2 - mu_c) / 4096.
+// Padding bundles (no real point): W = +65504 (V^ > 0 for every in-range query).
+__global__ __launch_bounds__(kBlock) void build_bundle_image_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz, int nm,
+    const int *__restrict__ kd, int nb_pad, double cx, double cy, double cz, double scale,
+    half8_t *__restrict__ img, float *__restrict__ radius)
+{
+    for (int b = blockIdx.x * kBlock + threadIdx.x; b < nb_pad; b += gridDim.x * kBlock) {
+        half8_t lo8 = {}, hi8 = {};
+        const int k0 = b * kBundle, k1 = min(k0 + kBundle, nm);
+        float rad = -1.0f;
+        if (k0 < nm) {
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int k = k0; k < k1; ++k) {
+                const int o = kd[k];
+                const double v[3] = {(mx[o] - cx) * scale, (my[o] - cy) * scale, (mz[o] - cz) * scale};
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = fmin(lo[a], v[a]);
+                    hi[a] = fmax(hi[a], v[a]);
+                }
+            }
+            _Float16 ch[3], cl[3];
+            double c[3];
+            for (int a = 0; a < 3; ++a) {
+                split_f16(0.5 * (lo[a] + hi[a]), ch[a], cl[a]);
+                c[a] = (double)ch[a] + (double)cl[a];
+            }
+            double r2 = 0.0, mmax = 0.0;
+            for (int k = k0; k < k1; ++k) {
+                const int o = kd[k];
+                const double v0 = (mx[o] - cx) * scale, v1 = (my[o] - cy) * scale, v2 = (mz[o] - cz) * scale;
+                const double e0 = v0 - c[0], e1 = v1 - c[1], e2 = v2 - c[2];
+                r2 = fmax(r2, (e0 * e0 + e1 * e1) + e2 * e2);
+                mmax = fmax(mmax, fabs(v0) + fabs(v1) + fabs(v2));
+            }
+            // r' >= max |M_i - c^| over the exact scaled points (M~_i rounds (m - c) once)
+            const double r = (sqrt(r2) + 0x1.0p-50 * mmax) * (1.0 + 0x1.0p-40) + 1e-30;
+            const double cc = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+            const double mu = 0x1.0p-16 * (cc + r * r) + 0x1.0p-4;
+            _Float16 wh, wl, rh, rl;
+            split_f16((cc - r * r - mu) / 4096.0, wh, wl);
+            split_f16(r, rh, rl);
+            const _Float16 m2 = (_Float16)-2.0f;
+            lo8[0] = m2 * ch[0]; lo8[1] = m2 * ch[0]; lo8[2] = m2 * cl[0]; lo8[3] = m2 * ch[1];
+            lo8[4] = m2 * ch[1]; lo8[5] = m2 * cl[1]; lo8[6] = m2 * ch[2]; lo8[7] = m2 * ch[2];
+            hi8[0] = m2 * cl[2]; hi8[1] = (_Float16)4096.0f; hi8[2] = (_Float16)4096.0f; hi8[3] = wh;
+            hi8[4] = wl; hi8[5] = m2 * rh; hi8[6] = m2 * rh; hi8[7] = m2 * rl;
+            if (!(r <= 15000.0)) { // (cannot happen for a model in [-2^12, 2^12)^3) search it always
+                hi8[3] = (_Float16)-65504.0f;
+                hi8[4] = (_Float16)0.0f;
+            }
+            rad = (float)r;
+        } else {
+            hi8[3] = (_Float16)65504.0f;
+        }
+        const int g = b >> 5, i = b & 31;
+        img[(size_t)g * 64 + i] = lo8;
+        img[(size_t)g * 64 + 32 + i] = hi8;
+        if (radius) radius[b] = rad;
+    }
+}
+
+} // namespace
+
+int bundle_pad(size_t nm) // bundles, padded to whole LDS tiles
+{
+    const size_t nb = (nm + kBundle - 1) / kBundle;
+    return (int)((nb + kBTile - 1) / kBTile * kBTile);
+}
+
+// kd order of the model for the bundle filter: a range of more than 1,024 points splits at a
+// multiple of 1,024, one of more than 32 at a multiple of 32, each near its middle along the
+// widest axis of its box (nth_element; ties by original index), so that every 32-point bundle
+// and every 1,024-point block of 32 bundles is a kd cell.
+std::vector<int> bundle_kd_order(const double *m, size_t nm)
+{
+    std::vector<int> ord(nm);
+    for (size_t j = 0; j < nm; ++j) ord[j] = (int)j;
+    std::vector<std::pair<size_t, size_t>> stack{{0, nm}};
+    while (!stack.empty()) {
+        const auto [lo, hi] = stack.back();
+        stack.pop_back();
+        const size_t cnt = hi - lo;
+        const size_t unit = cnt > 1024 ? 1024 : cnt > (size_t)kBundle ? (size_t)kBundle : 0;
+        if (!unit) continue;
+        double bl[3] = {INFINITY, INFINITY, INFINITY}, bh[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = lo; k < hi; ++k)
+            for (int a = 0; a < 3; ++a) {
+                bl[a] = std::min(bl[a], m[3 * (size_t)ord[k] + a]);
+                bh[a] = std::max(bh[a], m[3 * (size_t)ord[k] + a]);
+            }
+        int ax = 0;
+        for (int a = 1; a < 3; ++a)
+            if (bh[a] - bl[a] > bh[ax] - bl[ax]) ax = a;
+        const size_t units = (cnt + unit - 1) / unit, mid = lo + unit * ((units + 1) / 2);
+        if (mid >= hi) continue;
+        std::nth_element(ord.begin() + lo, ord.begin() + mid, ord.begin() + hi, [&](int x, int y) {
+            const double vx = m[3 * (size_t)x + ax], vy = m[3 * (size_t)y + ax];
+            return vx < vy || (vx == vy && x < y);
+        });
+        stack.push_back({lo, mid});
+        stack.push_back({mid, hi});
+    }
+    return ord;
+}
+
+void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
+                                int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
+                                float *radius, hipStream_t st)
+{
+    const int nm_b = nb_pad * kBundle;
+    build_pair_image_kd_kernel<<<bgrid(nm_b), kBlock, 0, st>>>(mx, my, mz, nm, kd, nm_b, c[0], c[1], c[2], scale,
+                                                                  (half8_t *)pimg, kd_orig);
+    build_bundle_image_kernel<<<bgrid(nb_pad), kBlock, 0, st>>>(mx, my, mz, nm, kd, nb_pad, c[0], c[1], c[2],
+                                                                   scale, (half8_t *)bimg, radius);
+}
+
+NNPlan plan_nn_bundle(size_t np, int nb_pad)
+{
+    NNPlan pl = make_nn_plan(np, (size_t)nb_pad, kBTile, kBQG, 4 * kBQG * 32, (const void *)nn_bundle_kernel);
+    pl.kernel = 100;
+    return pl;
+}
+
+void launch_nn_bundle(const double *px, const double *py, const double *pz, int np, const int *order,
+                      const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
+                      const void *bimg, int nb_pad, const void *pimg, const int *kd_orig, int nm, const NNPlan &pl,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st, const int *stop,
+                      unsigned long long *counters)
+{
+    dim3 grid(pl.qblocks, pl.splits);
+    nn_bundle_kernel<<<grid, kBlock, 0, st>>>(px, py, pz, np, order, prev, m4, c[0], c[1], c[2], scale, seed16,
+                                              (const half8_t *)bimg, nb_pad, (const half8_t *)pimg, kd_orig, nm,
+                                              pl.chunk, part_best, part_second, part_idx, stop, counters);
+}
+
+} // namespace icp

@@ -159,7 +159,10 @@ struct icp_ctx {
     size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0, mimg16_cap = 0, mms16_cap = 0;
     int nn_variant = ICP_NN_VARIANT_AUTO;
     double c[3] = {0, 0, 0}; // centring point = model centroid
-    std::vector<double> model_host; // the last model uploaded (icp_ensure_model compares against it)
+    // host copy of the model (AoS): kept when the one-launch paths can take it (small models),
+    // downloaded on demand for the CPU rule's host fix-up, else empty (0.2 GB at 2^23 points)
+    std::vector<double> model_host;
+    unsigned long long model_hash = 0; // of the last model uploaded (icp_ensure_model compares it)
     double rm = 0.0;         // max |centred fp32 model coordinate|
     bool has_model = false;
 
@@ -233,7 +236,8 @@ struct icp_ctx {
     int nn_rule = ICP_NN_RULE_SQUARED;
     CpuRuleEntry *cr_entries = nullptr;
     int *cr_count = nullptr;
-    size_t cr_cap = 0, cr_count_cap = 0;
+    int *cr_fix = nullptr; // the fix-up's (query, index) pairs
+    size_t cr_cap = 0, cr_count_cap = 0, cr_fix_cap = 0;
 
     // one-launch registration of small clouds (icp_iter.hip, launch_icp_persistent)
     int run_mode = ICP_RUN_AUTO;
@@ -261,6 +265,20 @@ struct icp_ctx {
     // x[nm] | y[nm] | z[nm] | 64-point block boxes (lo xyz, hi xyz) | original index (int32)
     double *pm_img = nullptr;
     size_t pm_img_cap = 0, pm_blocks = 0;
+    // bundle-bound filter (icp_bundle.hip): the model's kd-ordered bundle and pair images, built
+    // per model of >= kBundleMinModel points; the query order of the scene it searches
+    char *b_img = nullptr, *b_pimg = nullptr; // 1 KiB per 32 bundles; 1 KiB per bundle
+    int *b_kd_orig = nullptr;                 // original index per kd position (nm: padding)
+    float *b_radius = nullptr;                // per bundle (scaled units)
+    int *b_kd = nullptr;                      // the kd order (upload staging)
+    int nb_pad = 0;                           // bundles (whole LDS tiles)
+    size_t b_img_cap = 0, b_pimg_cap = 0, b_kd_orig_cap = 0, b_radius_cap = 0, b_kd_cap = 0;
+    int *q_order = nullptr;                   // the bundle filter's query order (launch_query_order)
+    char *q_order_tmp = nullptr;
+    size_t q_order_cap = 0, q_order_tmp_cap = 0;
+    const double *q_order_src = nullptr;      // the cloud q_order was computed for (its x array)
+    size_t q_order_n = 0;
+    unsigned long long *b_counters = nullptr; // icp_set_bundle_counters: the filter's executed work
 
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     icp_stats stats{};
@@ -340,12 +358,15 @@ void free_cloud(DevCloud &c)
 
 // Clouds up to this many doubles (3 x 64k points, 1.5 MiB) move through the mapped buffer.
 constexpr size_t kMappedIo = 3 * 65536;
+constexpr int kBundleMinModel = 8192; // models from this size get the bundle filter's images
 
 // `count` (<= 2 x kMappedIo) doubles of the mapped buffer: host pointer (*h) and device pointer
 // (*d).  When the buffer is used up it is recycled from the start, after a sync if a kernel
 // may still read it.
 int io_take(icp_ctx *ctx, size_t count, double **h, double **d)
 {
+    if (count > 2 * kMappedIo) // callers gate on this; a larger region would run past the buffer
+        return fail(ctx, ICP_E_ARG, "io_take: " + std::to_string(count) + " doubles exceed the mapped buffer");
     if (ctx->io_off + count > ctx->io_cap) {
         if (ctx->io_pending) HIPCHK(hipStreamSynchronize(ctx->st));
         ctx->io_pending = false;
@@ -410,6 +431,43 @@ int download_cloud(icp_ctx *ctx, const DevCloud &c, size_t n, double *xyz)
     return ICP_OK;
 }
 
+// The model's host copy (AoS), downloaded once if set_model did not keep it.
+int model_host_copy(icp_ctx *ctx, const double **out)
+{
+    if (ctx->model_host.size() != 3 * ctx->nm) {
+        ctx->model_host.resize(3 * ctx->nm);
+        TRY(download_cloud(ctx, ctx->model, ctx->nm, ctx->model_host.data()));
+    }
+    *out = ctx->model_host.data();
+    return ICP_OK;
+}
+
+// 64-bit content hash of a model array (icp_ensure_model): two multiply-xorshift lanes over
+// the 8-byte words, folded with the length
+unsigned long long model_digest(const double *xyz, size_t count)
+{
+    unsigned long long a = 0x9e3779b97f4a7c15ull ^ count, b = 0xc2b2ae3d27d4eb4full;
+    size_t k = 0;
+    for (; k + 1 < count; k += 2) {
+        unsigned long long w0, w1;
+        std::memcpy(&w0, xyz + k, 8);
+        std::memcpy(&w1, xyz + k + 1, 8);
+        a = (a ^ w0) * 0xff51afd7ed558ccdull;
+        a ^= a >> 32;
+        b = (b ^ w1) * 0xc4ceb9fe1a85ec53ull;
+        b ^= b >> 29;
+    }
+    if (k < count) {
+        unsigned long long w;
+        std::memcpy(&w, xyz + k, 8);
+        a = (a ^ w) * 0xff51afd7ed558ccdull;
+    }
+    unsigned long long h = a ^ (b * 0x9e3779b97f4a7c15ull);
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    return h ^ (h >> 33);
+}
+
 int ensure_reduction_space(icp_ctx *ctx)
 {
     if (ctx->partials) return ICP_OK;
@@ -453,6 +511,7 @@ int level1_kind(const icp_ctx *ctx, size_t n)
 {
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return 1;
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA16) return 2;
+    if (ctx->nn_variant == ICP_NN_VARIANT_BUNDLE) return ctx->nb_pad > 0 ? 3 : 2;
     if (ctx->nn_variant == ICP_NN_VARIANT_VALU || ctx->nn_variant == ICP_NN_VARIANT_GRID) return 0;
     // measured crossover (tools/configs_probe.py, 50-iteration registrations of synthetic n x n
     // pairs): VALU wins at 4,096 (2.4 vs 8.9 ms), the f16 MFMA filter from 8,192 (3.3 vs 3.7
@@ -487,6 +546,33 @@ static int grid_budget(const icp_ctx *ctx)
     }();
     if (forced) return forced;
     return (int)std::min<size_t>(std::max<size_t>(kGridBudget, ctx->nm / 4), (size_t)1 << 16);
+}
+
+// The bundle filter's processing order of the n queries in q (a Morton order over the model's
+// box, launch_query_order): computed once per cloud -- an icp_run's scene moves rigidly, so its
+// first order stays spatially coherent -- and again after set_scene / closest_matrix uploads.
+// ICP_BUNDLE_ORDER=0: file order (A/B).
+int query_order(icp_ctx *ctx, const DevCloud &q, size_t n, const int **order)
+{
+    static const bool off = [] {
+        const char *e = getenv("ICP_BUNDLE_ORDER");
+        return e && atoi(e) == 0;
+    }();
+    *order = nullptr;
+    if (off) return ICP_OK;
+    if (ctx->q_order_src != q.x || ctx->q_order_n != n) {
+        TRY(grow(ctx, &ctx->q_order, &ctx->q_order_cap, n));
+        const size_t bytes = query_order_scratch_bytes((int)n);
+        TRY(grow(ctx, &ctx->q_order_tmp, &ctx->q_order_tmp_cap, bytes));
+        if (launch_query_order(q.x, q.y, q.z, (int)n, ctx->m_lo, ctx->m_hi, ctx->q_order_tmp, bytes, ctx->q_order,
+                               ctx->st) != 0)
+            return fail(ctx, ICP_E_HIP, "query_order: radix sort failed");
+        LAUNCHCHK("query_order");
+        ctx->q_order_src = q.x;
+        ctx->q_order_n = n;
+    }
+    *order = ctx->q_order;
+    return ICP_OK;
 }
 
 constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger model: nn_resolve, 256 per query)
@@ -535,7 +621,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                           ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st,
                           stop);
         LAUNCHCHK("nn_grid_search");
-    } else if (const int l1 = level1_kind(ctx, n)) {
+    } else if (int l1 = level1_kind(ctx, n)) {
         // level 1: MFMA expanded-form filter over every query.  An unseeded f16 search is
         // seeded from the model grid first (a near point per query; ICP_GRID_SEED=0 disables):
         // the full N x M pass then runs the seeded kernel, 35.9 -> ~28 ms at C4
@@ -543,14 +629,18 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             const char *e = getenv("ICP_GRID_SEED");
             return !(e && atoi(e) == 0);
         }();
-        const bool gseed = l1 == 2 && !seeded && grid_seed && ctx->g_pts;
+        // (the bundle bound needs every query's seed: without the grid, the full f16 pass)
+        if (l1 == 3 && !seeded && !(grid_seed && ctx->g_pts)) l1 = 2;
+        const bool gseed = l1 >= 2 && !seeded && grid_seed && ctx->g_pts;
         if (gseed) {
             launch_nn_grid_seed((int)n, q.x, q.y, q.z, grid_view(ctx), (int)ctx->nm, ctx->idx, ctx->st);
             LAUNCHCHK("nn_grid_seed");
             seeds_ready = false; // the seeds come from these candidates, below
         }
-        const bool sd = (seeded || gseed) && l1 == 2;
-        const NNPlan pl = l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd) : plan_nn_mfma(n, ctx->nm_pad);
+        const bool sd = (seeded || gseed) && l1 >= 2;
+        const NNPlan pl = l1 == 3   ? plan_nn_bundle(n, ctx->nb_pad)
+                          : l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd)
+                                    : plan_nn_mfma(n, ctx->nm_pad);
         if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
             launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->m4, ctx->c, ctx->scale16, ctx->seed16,
@@ -566,14 +656,20 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
+        const int *order = nullptr;
+        if (l1 == 3) TRY(query_order(ctx, q, n, &order));
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
-        if (l1 == 2)
+        if (l1 == 3)
+            launch_nn_bundle(q.x, q.y, q.z, (int)n, order, ctx->idx, ctx->m4, ctx->c, ctx->scale16, seeds, ctx->b_img,
+                             ctx->nb_pad, ctx->b_pimg, ctx->b_kd_orig, (int)ctx->nm, pl, pb, ps, pi, ctx->st, stop,
+                             ctx->b_counters);
+        else if (l1 == 2)
             launch_nn_mfma16(q.x, q.y, q.z, (int)n, ctx->c, ctx->scale16, seeds, ctx->mimg16, (int)ctx->nm_pad,
                              pl, pb, ps, pi, ctx->st, stop);
         else
             launch_nn_mfma(q.f, (int)n, ctx->mperm, (int)ctx->nm_pad, pl, pb, ps, pi, ctx->st);
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
-        if (l1 == 2)
+        if (l1 >= 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
                                       ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit);
@@ -676,9 +772,13 @@ int cpu_rule_fixup(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop)
         }
         if (cnt == 0) return ICP_OK;
         std::vector<CpuRuleEntry> h((size_t)cnt);
-        HIPCHK(hipMemcpy(h.data(), ctx->cr_entries, sizeof(CpuRuleEntry) * (size_t)cnt, hipMemcpyDeviceToHost));
-        const double *m = ctx->model_host.data();
+        HIPCHK(hipMemcpyAsync(h.data(), ctx->cr_entries, sizeof(CpuRuleEntry) * (size_t)cnt,
+                              hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        const double *m = nullptr;
+        TRY(model_host_copy(ctx, &m));
         std::vector<int> cand;
+        std::vector<int> changed; // (j, best) pairs, sent in one copy and scattered on ctx->st
         for (const CpuRuleEntry &e : h) {
             cand.clear();
             if (e.n >= 0) {
@@ -700,8 +800,18 @@ int cpu_rule_fixup(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop)
             ctx->stats.cpu_rule_ties += 1;
             if (best != e.h) {
                 ctx->stats.cpu_rule_changed += 1;
-                HIPCHK(hipMemcpy(ctx->idx + e.j, &best, sizeof(int), hipMemcpyHostToDevice));
+                changed.push_back(e.j);
+                changed.push_back(best);
             }
+        }
+        if (!changed.empty()) {
+            const size_t npairs = changed.size() / 2;
+            TRY(grow(ctx, &ctx->cr_fix, &ctx->cr_fix_cap, changed.size()));
+            HIPCHK(hipMemcpyAsync(ctx->cr_fix, changed.data(), sizeof(int) * changed.size(), hipMemcpyHostToDevice,
+                                  ctx->st));
+            launch_scatter_pairs(ctx->cr_fix, (int)npairs, ctx->idx, ctx->st);
+            LAUNCHCHK("scatter_pairs");
+            HIPCHK(hipStreamSynchronize(ctx->st)); // `changed` is pageable and local
         }
         return ICP_OK;
     }
@@ -869,6 +979,48 @@ int icp_ctx_create_sharded(int device, int nn_mode, int rank, int world_size, ic
     return ICP_OK;
 }
 
+int icp_set_bundle_counters(icp_ctx *ctx, int enable)
+{
+    if (!ctx) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (!enable) {
+        if (ctx->b_counters) HIPCHK(hipFree(ctx->b_counters));
+        ctx->b_counters = nullptr;
+        return ICP_OK;
+    }
+    if (!ctx->b_counters) HIPCHK(hipMalloc((void **)&ctx->b_counters, 4 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, 4 * sizeof(unsigned long long), ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    return ICP_OK;
+}
+
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[3])
+{
+    if (!ctx || !out) return ICP_E_ARG;
+    out[0] = out[1] = out[2] = 0;
+    if (!ctx->b_counters) return ICP_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    unsigned long long v[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(v, ctx->b_counters, sizeof(v), hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    for (int k = 0; k < 3; ++k) out[k] = v[k];
+    return ICP_OK;
+}
+
+int icp_get_comm_info(icp_ctx *ctx, int *comm_count, int *comm_rank, char *bus_id, int len)
+{
+    if (!ctx || !comm_count || !comm_rank || (bus_id && len < 16)) return ICP_E_ARG;
+    *comm_count = -1;
+    *comm_rank = ctx->rank;
+    if (ctx->comm) {
+        RCCLCHK(ncclCommCount(ctx->comm, comm_count));
+        RCCLCHK(ncclCommUserRank(ctx->comm, comm_rank));
+    }
+    if (bus_id) HIPCHK(hipDeviceGetPCIBusId(bus_id, len, ctx->device));
+    return ICP_OK;
+}
+
 void icp_ctx_destroy(icp_ctx *ctx)
 {
     if (!ctx) return;
@@ -890,8 +1042,9 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
-                    (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->cr_entries,
-                    (void *)ctx->cr_count, (void *)ctx->tail_part, (void *)ctx->tail_sync,
+                    (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->b_img, (void *)ctx->b_pimg, (void *)ctx->b_kd_orig,
+                    (void *)ctx->b_radius, (void *)ctx->b_kd, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters, (void *)ctx->cr_entries,
+                    (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
@@ -913,7 +1066,7 @@ const char *icp_last_error(const icp_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int icp_set_nn_variant(icp_ctx *ctx, int variant)
 {
-    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_GRID) return ICP_E_ARG;
+    if (!ctx || variant < ICP_NN_VARIANT_AUTO || variant > ICP_NN_VARIANT_BUNDLE) return ICP_E_ARG;
     ctx->nn_variant = variant;
     return ICP_OK;
 }
@@ -1035,18 +1188,38 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
             std::nth_element(d2.begin(), d2.begin() + nb16 / 2, d2.end());
             ctx->pm_seed_big = 4.0 * d2[nb16 / 2];
         }
-        for (int k = 0; k < 3; ++k) { // the model's box (the mid-size loop's search order)
-            ctx->m_lo[k] = INFINITY;
-            ctx->m_hi[k] = -INFINITY;
+    }
+    for (int k = 0; k < 3; ++k) { // the model's box (the query orders: mid-size loop, bundle filter)
+        ctx->m_lo[k] = INFINITY;
+        ctx->m_hi[k] = -INFINITY;
+    }
+    for (size_t j = 0; j < nm; ++j)
+        for (int k = 0; k < 3; ++k) {
+            ctx->m_lo[k] = std::min(ctx->m_lo[k], m_xyz[3 * j + k]);
+            ctx->m_hi[k] = std::max(ctx->m_hi[k], m_xyz[3 * j + k]);
         }
-        for (size_t j = 0; j < nm; ++j)
-            for (int k = 0; k < 3; ++k) {
-                ctx->m_lo[k] = std::min(ctx->m_lo[k], m_xyz[3 * j + k]);
-                ctx->m_hi[k] = std::max(ctx->m_hi[k], m_xyz[3 * j + k]);
-            }
+    ctx->nb_pad = 0;
+    if (nm >= (size_t)kBundleMinModel) { // the bundle filter's kd images (icp_bundle.hip)
+        const std::vector<int> kd = bundle_kd_order(m_xyz, nm);
+        const int nb_pad = bundle_pad(nm);
+        TRY(grow(ctx, &ctx->b_kd, &ctx->b_kd_cap, nm));
+        TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, (size_t)nb_pad * 32));
+        TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, (size_t)nb_pad * 1024));
+        TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, (size_t)nb_pad * 32));
+        TRY(grow(ctx, &ctx->b_radius, &ctx->b_radius_cap, (size_t)nb_pad));
+        HIPCHK(hipMemcpyAsync(ctx->b_kd, kd.data(), sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
+        launch_build_bundle_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
+                                   ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_radius, ctx->st);
+        LAUNCHCHK("build_bundle_images");
+        HIPCHK(hipStreamSynchronize(ctx->st)); // (kd is freed on return)
+        ctx->nb_pad = nb_pad;
     }
     HIPCHK(hipStreamSynchronize(ctx->st));
-    ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
+    if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel) || ctx->nn_rule == ICP_NN_RULE_CPU_SQRT)
+        ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
+    else
+        std::vector<double>().swap(ctx->model_host);
+    ctx->model_hash = model_digest(m_xyz, 3 * nm);
     ctx->nm = nm;
     ctx->nm_pad = nm_pad;
     ctx->has_model = true;
@@ -1065,9 +1238,13 @@ int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded
 {
     if (!ctx || !m_xyz || nm == 0) return ICP_E_ARG;
     if (uploaded) *uploaded = 0;
-    if (ctx->has_model && ctx->nm == nm && ctx->model_host.size() == 3 * nm &&
-        std::memcmp(ctx->model_host.data(), m_xyz, sizeof(double) * 3 * nm) == 0)
-        return ICP_OK;
+    if (ctx->has_model && ctx->nm == nm) {
+        // the kept copy compares exactly; a large model by its content hash
+        const bool same = ctx->model_host.size() == 3 * nm
+                              ? std::memcmp(ctx->model_host.data(), m_xyz, sizeof(double) * 3 * nm) == 0
+                              : model_digest(m_xyz, 3 * nm) == ctx->model_hash;
+        if (same) return ICP_OK;
+    }
     TRY(icp_set_model(ctx, m_xyz, nm));
     if (uploaded) *uploaded = 1;
     return ICP_OK;
@@ -1087,6 +1264,7 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     ctx->np_total = np_total;
     ctx->has_scene = true;
     ctx->seeds_valid = false;
+    ctx->q_order_src = nullptr; // new contents: a new query order
     return ICP_OK;
 }
 
@@ -1421,7 +1599,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_flags, ctx->h_flags, 0));
     }
     // seeded f16 searches: each transform writes the next search's seeds (no seed kernel)
-    const bool fuse_seeds = ctx->nn_mode == ICP_NN_CERTIFIED && level1_kind(ctx, n) == 2;
+    const bool fuse_seeds = ctx->nn_mode == ICP_NN_CERTIFIED && level1_kind(ctx, n) >= 2;
     SeedArgs sa;
     if (fuse_seeds) {
         TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
@@ -1736,11 +1914,13 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
     const bool auto_rule = (ctx->nn_variant == ICP_NN_VARIANT_AUTO || ctx->nn_mode == ICP_NN_FP64) &&
                            ctx->nn_rule == ICP_NN_RULE_SQUARED;
     if (np && np <= kFewQueries && auto_rule) return closest_few(ctx, p_xyz, np, y_xyz_out, idx_out);
-    if (np && auto_rule && ctx->pm_img && ctx->nm <= (size_t)kPersistMaxModel && 3 * np <= kMappedIo &&
-        24 * ctx->nm + 48 * ctx->pm_blocks + 4096 <= ctx->lds_per_cu)
+    // (closest_lds takes queries, y and the int32 indices from the mapped buffer: 6.5 doubles a query)
+    if (np && auto_rule && ctx->pm_img && ctx->nm <= (size_t)kPersistMaxModel &&
+        6 * np + (np + 1) / 2 <= 2 * kMappedIo && 24 * ctx->nm + 48 * ctx->pm_blocks + 4096 <= ctx->lds_per_cu)
         return closest_lds(ctx, p_xyz, np, y_xyz_out, idx_out);
     TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
     ctx->seeds_valid = false; // idx is about to hold other queries' correspondences
+    ctx->q_order_src = nullptr;
     TRY(nn_search(ctx, ctx->qa, np));
     TRY(cpu_rule_fixup(ctx, ctx->qa, np, nullptr));
     if (np && y_xyz_out) {
@@ -1987,7 +2167,10 @@ int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap)
 static int cert_audit_reset(icp_ctx *ctx)
 {
     const unsigned init[3] = {0u, 0x7f800000u, 0u}; // max ratio 0, min margin +inf, count 0
-    HIPCHK(hipMemcpy(ctx->cert_audit, init, sizeof(init), hipMemcpyHostToDevice));
+    // on the engine stream (non-blocking: the null-stream hipMemcpy is not ordered against it),
+    // then waited for, since `init` lives on this frame
+    HIPCHK(hipMemcpyAsync(ctx->cert_audit, init, sizeof(init), hipMemcpyHostToDevice, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
 }
 
@@ -2030,6 +2213,7 @@ int icp_get_stats(const icp_ctx *ctx, icp_stats *out)
 int icp_reset_stats(icp_ctx *ctx)
 {
     if (!ctx) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
     if (ctx->cert_audit) TRY(cert_audit_reset(ctx));
     ctx->stats = icp_stats{};
     return ICP_OK;

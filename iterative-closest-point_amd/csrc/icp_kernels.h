@@ -119,6 +119,35 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop = nullptr, const double4 *m4 = nullptr,
                                unsigned *audit = nullptr);
+// A split plan for `kernel` (make_plan): np queries in workgroups of queries_per_lane_block,
+// the model axis (nm rows, tiles of `tile`) split to fill >= 4 rounds of resident workgroups.
+NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel);
+// Bundle-bound f16 filter (icp_bundle.hip).  The model in kd order (bundle_kd_order): bundles
+// of 32 consecutive points, bundle_pad(nm) of them (whole 256-bundle LDS tiles); images built
+// once per model: bimg (1 KiB per 32 bundles), pimg (the f16 pair image in kd order, 1 KiB
+// per bundle), kd_orig (original index per kd position, nm for padding), radius (nullable,
+// per bundle, scaled units; -1 for padding).
+int bundle_pad(size_t nm);
+std::vector<int> bundle_kd_order(const double *m_xyz, size_t nm);
+void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
+                                int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
+                                float *radius, hipStream_t st);
+NNPlan plan_nn_bundle(size_t np, int nb_pad);
+// Seeded search (prev: each query's seed index, seed16 its f16 shift): partial (best, second,
+// original index) per (split, query) in the format of launch_nn_mfma16 (same finalize).
+// order (nullable): the queries' processing order (launch_query_order).
+void launch_nn_bundle(const double *px, const double *py, const double *pz, int np, const int *order,
+                      const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
+                      const void *bimg, int nb_pad, const void *pimg, const int *kd_orig, int nm, const NNPlan &pl,
+                      float *part_best, float *part_second, int *part_idx, hipStream_t st, const int *stop = nullptr,
+                      unsigned long long *counters = nullptr);
+// counters (nullable) += per launch: (32-bundle blocks whose joint test fired, per wave; groups
+// with a bundle V^ <= 0 in such a block; pair tests run = (group, bundle) pairs)
+// order[k] = the query processed k-th: the queries sorted by the Morton code of their cell in a
+// 1024^3 grid over the box [lo, hi] (icp_order.hip); scratch: query_order_scratch_bytes(n)
+size_t query_order_scratch_bytes(int n);
+int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
+                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
@@ -204,6 +233,8 @@ void launch_gather_moments(const int *idx, const double4 *m4, const double *px, 
                            double *partials, hipStream_t st);
 // *out = (double)*cnt (a device count joining an all-reduced vector of sums)
 void launch_count_to_double(const int *cnt, double *out, hipStream_t st);
+// dst[pairs[2i]] = pairs[2i + 1] for i < n (the CPU rule's host fix-ups)
+void launch_scatter_pairs(const int *pairs, int n, int *dst, hipStream_t st);
 void launch_make_aos4(const double *x, const double *y, const double *z, int n, double4 *m4,
                       hipStream_t st);
 // partial [sum p (3)] of one cloud

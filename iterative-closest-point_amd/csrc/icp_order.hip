@@ -1,4 +1,5 @@
-// icp_order.hip — the mid-size one-launch loop's search order (icp_iter.hip,
+// icp_order.hip — query orders: the bundle filter's (launch_query_order, a 30-bit Morton
+// order over the model's box) and the mid-size one-launch loop's search order (icp_iter.hip,
 // icp_persistent_mid_kernel): the scene's queries sorted by the Morton cell of a 32^3 grid over
 // the model's box that holds them, stably (file order within a cell), so that the four queries
 // of a search batch lie close together whatever order the cloud came in.  The order only decides
@@ -50,7 +51,59 @@ __global__ __launch_bounds__(kBlock) void order_pos_kernel(const int *__restrict
 
 constexpr int kOrderBits = 15;
 
+// 10 bits per axis (1024^3 cells) -> 30-bit Morton key
+__global__ __launch_bounds__(kBlock) void query_keys_kernel(const double *__restrict__ px, const double *__restrict__ py,
+                                                          const double *__restrict__ pz, int n, OrderBox bx,
+                                                          unsigned *__restrict__ key, int *__restrict__ val)
+{
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= n) return;
+    auto cell = [](double v, double l, double s) {
+        const double t = (v - l) * s;
+        return !(t > 0.0) ? 0u : t >= 1023.0 ? 1023u : (unsigned)t;
+    };
+    auto spread = [](unsigned v) { // 10 bits -> every third bit
+        v = (v | (v << 16)) & 0x030000ffu;
+        v = (v | (v << 8)) & 0x0300f00fu;
+        v = (v | (v << 4)) & 0x030c30c3u;
+        v = (v | (v << 2)) & 0x09249249u;
+        return v;
+    };
+    key[q] = spread(cell(px[q], bx.lo[0], bx.sc[0])) | (spread(cell(py[q], bx.lo[1], bx.sc[1])) << 1) |
+             (spread(cell(pz[q], bx.lo[2], bx.sc[2])) << 2);
+    val[q] = q;
+}
+
+constexpr int kQueryOrderBits = 30;
+
 } // namespace
+
+size_t query_order_scratch_bytes(int n)
+{
+    size_t temp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned *)nullptr, (unsigned *)nullptr,
+                                             (const int *)nullptr, (int *)nullptr, n, 0, kQueryOrderBits);
+    return 3 * (size_t)n * sizeof(int) + ((temp + 255) & ~(size_t)255);
+}
+
+int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
+                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st)
+{
+    OrderBox bx;
+    for (int k = 0; k < 3; ++k) {
+        bx.lo[k] = lo[k];
+        bx.sc[k] = hi[k] > lo[k] ? 1024.0 / (hi[k] - lo[k]) : 0.0;
+    }
+    unsigned *k0 = (unsigned *)scratch, *k1 = k0 + n;
+    int *v0 = (int *)(k1 + n);
+    void *temp = v0 + n;
+    size_t temp_bytes = bytes - 3 * (size_t)n * sizeof(int);
+    query_keys_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(px, py, pz, n, bx, k0, v0);
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, order, n, 0, kQueryOrderBits, st) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
 
 size_t mid_order_scratch_bytes(int n)
 {

@@ -46,6 +46,7 @@ VARIANT_VALU = 1
 VARIANT_MFMA = 2
 VARIANT_MFMA16 = 3
 VARIANT_GRID = 4  # exact grid NN for every query
+VARIANT_BUNDLE = 5  # f16 pair filter behind the per-(query, 32-point bundle) MFMA bound
 RULE_SQUARED = 0    # icp_set_nn_rule: the reference GPU path's squared distance (default)
 RULE_CPU_SQRT = 1   # the reference CPU path's sqrt(pow) distance (src/cpu.cc:17-22)
 RUN_AUTO = 0        # icp_set_run_mode: one launch for eligible small runs, else the launch loop
@@ -63,6 +64,7 @@ EXPORTED = [
     "icp_load_matrix", "icp_write_matrix", "icp_free", "icp_get_stats", "icp_reset_stats",
     "icp_ensure_model", "icp_subtract_col", "icp_get_indices", "icp_set_index_digest",
     "icp_get_index_digest", "icp_set_cert_audit", "icp_set_run_mode", "icp_set_nn_rule",
+    "icp_get_comm_info", "icp_set_bundle_counters", "icp_get_bundle_counters",
 ]
 
 
@@ -143,6 +145,9 @@ def lib() -> C.CDLL:
     L.icp_set_cert_audit.argtypes = [vp, C.c_int]
     L.icp_get_stats.argtypes = [vp, C.POINTER(Stats)]
     L.icp_reset_stats.argtypes = [vp]
+    L.icp_set_bundle_counters.argtypes = [vp, C.c_int]
+    L.icp_get_bundle_counters.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.icp_get_comm_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]
     _lib = L
     return L
 
@@ -405,6 +410,24 @@ class Context:
 
     def reset_stats(self):
         self._check(lib().icp_reset_stats(self._h))
+
+    def set_bundle_counters(self, on: bool):
+        self._check(lib().icp_set_bundle_counters(self._h, 1 if on else 0))
+
+    def bundle_counters(self) -> dict:
+        """The bundle filter's executed work since set_bundle_counters(True)."""
+        out = (C.c_uint64 * 3)()
+        self._check(lib().icp_get_bundle_counters(self._h, out))
+        return {"block_triggers": int(out[0]), "group_triggers": int(out[1]), "pair_tests": int(out[2])}
+
+    def comm_info(self) -> dict:
+        """RCCL communicator size / rank (None / this rank without one) and the PCI bus id of
+        this context's device: what a multi-GPU run really ran on."""
+        cnt, rk = C.c_int(0), C.c_int(0)
+        bus = C.create_string_buffer(64)
+        self._check(lib().icp_get_comm_info(self._h, C.byref(cnt), C.byref(rk), bus, 64))
+        return {"comm_count": cnt.value if cnt.value >= 0 else None, "comm_rank": rk.value,
+                "pci_bus_id": bus.value.decode()}
 
 
 # ---------------------------------------------------------------------------------

@@ -7,7 +7,7 @@ split over processes (the per-query answers do not depend on the split); checked
 against oracle_icp itself on cow before the long bunny run.  Writes tests/golden/cpu_rule.json
 and tests/golden/bun045_cpu_rule_idx0.npz.
 
-    python tests/golden/make_cpu_rule.py        (~3 min on 8 cores)
+    python tests/golden/make_cpu_rule.py        (~15 min on 8 cores)
 """
 import json
 import os
@@ -76,9 +76,9 @@ def main():
     m = O.load_matrix(datasets.path("bun000"))
     p = O.load_matrix(datasets.path("bun045"))
     with ProcessPoolExecutor(8, initializer=_init, initargs=(m,)) as pool:
-        mine, fin, idx0 = icp_cpu_rule(m, p, 10, -1.0, pool)
+        mine, fin, idx0 = icp_cpu_rule(m, p, 50, -1.0, pool)  # BASELINE C2: 50 iterations
     _, sq0 = O.closest_blocked(p, m)
-    res["bunny"] = dict(model="bun000", scene="bun045", max_iter=10, threshold=-1.0, allow_unequal=True, **mine,
+    res["bunny"] = dict(model="bun000", scene="bun045", max_iter=50, threshold=-1.0, allow_unequal=True, **mine,
                         final_sum=fin.sum(axis=0).tolist(), final_head=fin[:4].tolist(),
                         final_tail=fin[-4:].tolist(),
                         idx0_differs_from_squared=np.nonzero(idx0 != sq0)[0].tolist())

@@ -95,3 +95,36 @@ def test_reference_call_sequence_replay(icp_lib, golden, cfg):
     np.testing.assert_allclose(final.sum(axis=0), out["final_sum"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(final[0], out["final_head"], rtol=0, atol=1e-9)
     np.testing.assert_allclose(final[-1], out["final_tail"], rtol=0, atol=1e-9)
+
+
+def test_comm_info(icp_lib):
+    """icp_get_comm_info: what bench.py's per_rank records for every rank of a multi-GPU line."""
+    with icp_lib.Context(0) as c:
+        info = c.comm_info()
+        assert info["comm_count"] is None and info["comm_rank"] == 0
+        bus = info["pci_bus_id"]
+        assert len(bus) >= 7 and ":" in bus  # e.g. 0000:05:00.0
+    with icp_lib.Context(0, icp_lib.NN_CERTIFIED, rank=0, world_size=1, rccl_id=icp_lib.rccl_unique_id()) as c:
+        info = c.comm_info()
+        assert info["comm_count"] == 1 and info["comm_rank"] == 0 and info["pci_bus_id"] == bus
+
+
+def test_closest_matrix_mapped_buffer_limit(icp_lib):
+    """Queries up to the mapped buffer's size take the one-launch LDS search of a small model
+    (closest_lds: 6.5 doubles per query); 65,536 queries against cow need more than the buffer
+    holds and must take the staged path -- both bitwise equal to the cascade."""
+    m = icp_lib.load_matrix(datasets.path("cow_ref"))
+    rng = np.random.default_rng(9)
+    lo, hi = m.min(axis=0), m.max(axis=0)
+    for n in (60000, 60494, 60495, 65536):
+        p = rng.uniform(lo, hi, size=(n, 3))
+        with icp_lib.Context(0) as c:
+            c.set_model(m)
+            y, idx = c.closest_matrix(p)
+        with icp_lib.Context(0) as c:
+            c.set_nn_variant(icp_lib.VARIANT_VALU)  # an explicit variant: the cascade
+            c.set_model(m)
+            y2, idx2 = c.closest_matrix(p)
+        assert np.array_equal(idx, idx2), n
+        assert np.array_equal(y, y2), n
+        assert np.array_equal(y, m[idx]), n

@@ -63,12 +63,14 @@ def test_c4_trajectory_matches_oracle(amd):
 
     runs = {"default": run_c4(amd, m, p, amd.NN_CERTIFIED, amd.VARIANT_AUTO, iters),
             "fp64": run_c4(amd, m, p, amd.NN_FP64, amd.VARIANT_AUTO, iters),
-            "grid": run_c4(amd, m, p, amd.NN_CERTIFIED, amd.VARIANT_GRID, iters)}
+            "grid": run_c4(amd, m, p, amd.NN_CERTIFIED, amd.VARIANT_GRID, iters),
+            "bundle": run_c4(amd, m, p, amd.NN_CERTIFIED, amd.VARIANT_BUNDLE, iters),
+            "mfma16": run_c4(amd, m, p, amd.NN_CERTIFIED, amd.VARIANT_MFMA16, iters)}
     res, errs, dig, out, st = runs["default"]
     assert res.iterations == iters
     # the default path is the f16 MFMA filter and its certificate sent queries onward
     assert st["level1_queued"] > 0
-    for name in ("fp64", "grid"):
+    for name in ("fp64", "grid", "bundle", "mfma16"):
         r2, e2, d2, o2, _ = runs[name]
         assert np.array_equal(e2, errs), name
         assert np.array_equal(d2, dig), name

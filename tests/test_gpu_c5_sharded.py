@@ -1,0 +1,157 @@
+"""C5 at full size through the engine's own sharded protocol (BASELINE.json configs[4]: the
+2^23-point synthetic pair on 8 GPUs), rehearsed on one GPU.
+
+Eight virtual ranks are eight threads, each with its own context and stream on device 0
+(icp_ctx_create_sharded), holding the whole 2^23-point model and its scene shard
+icp_shard_range(2^23, r, 8) with np_total = 2^23.  Their per-iteration sums are combined by a
+host all-reduce in fixed rank order, which is what ncclAllReduce computes across the 8 cards;
+everything else -- the shard's search against the full model, the 18-sum shifted moments, the
+residual riding on the next iteration's all-reduce and its lagged error test
+(src/GPU/gpu.cc:52-83 restated per rank) -- is the code an 8-GPU run executes.
+
+Three iterations as bench.py's C5 runs them: two (the unseeded first, then a seeded one),
+then one more run whose search is seeded from the second iteration's correspondences.
+Asserted:
+  * all 8 ranks take bitwise-identical (err, s, R, t);
+  * the concatenated shard clouds equal a single-context 2^23 run (err rtol 1e-11, cloud atol
+    1e-11 x extent), its per-iteration correspondence digests exactly (the global digest
+    (sum idx, sum (j+1) idx[j]) is recombined from the shards' local ones), and the last
+    search's indices element for element;
+  * 256 sampled queries per rank, always including the shard's first and last query, equal
+    the oracle's brute force over all 2^23 model points (src/cpu.cc:5-27, squared rule).
+
+Int audit at 2^23 (the sizes this test is the only one to reach): model padding nm_pad and the
+f16 image offsets ((size_t)block * 64), the split partial offsets ((size_t)split * np + j) and
+the digest's (j + 1) * idx products (64-bit) are all computed in 64-bit or stay below 2^31.
+"""
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 1 << 23
+W = 8
+MASK = (1 << 64) - 1
+
+
+class HostAllReduce:
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world, timeout=300)
+        self.bufs = [None] * world
+
+    def for_rank(self, r):
+        def reduce(buf):
+            self.bufs[r] = buf.copy()
+            self.bar.wait()
+            acc = self.bufs[0].copy()
+            for k in range(1, self.world):  # fixed rank order: identical on every rank
+                acc += self.bufs[k]
+            self.bar.wait()
+            buf[:] = acc
+        return reduce
+
+
+def run_protocol(ctx):
+    ctx.set_index_digest(2)
+    r1, e1 = ctx.run(2, -1.0)
+    d1 = ctx.index_digest(2)
+    s2 = ctx.get_scene()
+    ctx.set_index_digest(1)
+    r2, e2 = ctx.run(1, -1.0)  # seeded from the second iteration's correspondences
+    d2 = ctx.index_digest(1)
+    return dict(err=np.concatenate([e1, e2]), res=r2, dig=np.concatenate([d1, d2]), s2=s2,
+                idx=ctx.get_indices(), s3=ctx.get_scene(), stats=ctx.stats())
+
+
+@pytest.fixture(scope="module")
+def c5(icp_lib):
+    amd = icp_lib
+    if amd.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    m, p = amd.synthetic_pair(N, seed=42)
+
+    with amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        single = run_protocol(ctx)
+
+    red = HostAllReduce(W)
+    ranks = [None] * W
+    errors = []
+
+    def worker(r):
+        try:
+            b, c = amd.shard_range(N, r, W)
+            with amd.Context(0, rank=r, world_size=W, host_allreduce=red.for_rank(r)) as ctx:
+                ctx.set_model(m)
+                ctx.set_scene(np.ascontiguousarray(p[b:b + c]), np_total=N)
+                out = run_protocol(ctx)
+                out["range"] = (b, c)
+                ranks[r] = out
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+            red.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    assert not errors, errors
+    assert all(o is not None for o in ranks)
+    return amd, m, p, single, ranks
+
+
+def test_c5_ranks_bitwise_identical(c5):
+    _, _, _, _, ranks = c5
+    r0 = ranks[0]
+    assert [o["range"][1] for o in ranks] == [N // W] * W
+    for o in ranks[1:]:
+        assert np.array_equal(o["err"], r0["err"])
+        assert o["res"].s == r0["res"].s
+        assert list(o["res"].R) == list(r0["res"].R) and list(o["res"].t) == list(r0["res"].t)
+
+
+def test_c5_shards_equal_single_context(c5):
+    _, m, _, single, ranks = c5
+    np.testing.assert_allclose(ranks[0]["err"], single["err"], rtol=1e-11, atol=0)
+    ext = float(np.abs(m).max())
+    for key in ("s2", "s3"):
+        cat = np.concatenate([o[key] for o in ranks])
+        np.testing.assert_allclose(cat, single[key], rtol=0, atol=1e-11 * ext)
+    # the last search's correspondences, element for element
+    assert np.array_equal(np.concatenate([o["idx"] for o in ranks]), single["idx"])
+    # per-iteration digests: local (sum, sum (j+1) idx[j]) -> global, mod 2^64
+    for k in range(3):
+        s_tot, w_tot = 0, 0
+        for o in ranks:
+            b = o["range"][0]
+            s_r, w_r = int(o["dig"][k][0]), int(o["dig"][k][1])
+            s_tot = (s_tot + s_r) & MASK
+            w_tot = (w_tot + w_r + b * s_r) & MASK
+        assert (s_tot, w_tot) == (int(single["dig"][k][0]), int(single["dig"][k][1])), f"iteration {k}"
+
+
+def test_c5_rank_samples_match_oracle(c5, oracle):
+    _, m, _, _, ranks = c5
+    rng = np.random.default_rng(11)
+    jobs = []
+    for o in ranks:
+        c = o["range"][1]
+        sel = np.sort(np.concatenate([1 + rng.choice(c - 2, 254, replace=False), [0, c - 1]]))
+        assert np.unique(sel).size == 256
+        jobs.append((o, sel))
+
+    def check(job):
+        o, sel = job
+        _, ref = oracle.closest_blocked(o["s2"][sel], m)
+        return np.array_equal(o["idx"][sel], ref)
+
+    with ThreadPoolExecutor(max_workers=8) as ex:  # the oracle's ctypes calls release the GIL
+        ok = list(ex.map(check, jobs))
+    assert all(ok), ok
+    assert ranks[0]["idx"].min() >= 0 and max(int(o["idx"].max()) for o in ranks) < N

@@ -128,12 +128,15 @@ def run(amd, nn_mode, variant, m, q, iters):
         return idx0, st0, res, errs, ctx.get_scene(), ctx.get_indices(), ctx.stats()
 
 
+@pytest.mark.parametrize("variant", ["mfma16", "bundle"])
 @pytest.mark.parametrize("name", list(SCENES))
-def test_f16_certificate_adversarial(amd, name):
+def test_f16_certificate_adversarial(amd, name, variant):
+    """The f16 certificate on its worst cases, behind the full N x M filter and behind the
+    bundle bound (whose exclusions must never drop the answer or a tie of it)."""
     rng = np.random.default_rng(list(SCENES).index(name) + 101)
     m, q = SCENES[name](rng)
     assert q.shape[0] >= NQ
-    d = run(amd, amd.NN_CERTIFIED, amd.VARIANT_MFMA16, m, q, 3)
+    d = run(amd, amd.NN_CERTIFIED, amd.VARIANT_MFMA16 if variant == "mfma16" else amd.VARIANT_BUNDLE, m, q, 3)
     f = run(amd, amd.NN_FP64, 0, m, q, 3)
     # unseeded search: identical indices
     np.testing.assert_array_equal(d[0], f[0])
@@ -150,6 +153,8 @@ def test_f16_certificate_adversarial(amd, name):
             assert st["cert_max_err_ratio"] < 1.0, st  # the bound held on every certified winner
     if name != "clusters":
         assert d[1]["cert_audited"] > 0 and d[6]["cert_audited"] > 0
+    if variant != "mfma16":
+        return
     AUDIT[name] = {"unseeded": {k: d[1][k] for k in ("cert_max_err_ratio", "cert_min_margin", "cert_audited",
                                                      "level1_queued", "grid_fallback")},
                    "icp_run": {k: d[6][k] for k in ("cert_max_err_ratio", "cert_min_margin", "cert_audited",

@@ -7,9 +7,9 @@ first search.  The engine finds each query's near-tie window on the device and e
 reference's CPU arithmetic with libm on the host for exactly those candidates.  Checked against
 the oracle built with real libm pow calls (oracle/Makefile: -fno-builtin-pow):
   * bunny's first search, all 40,097 queries: bit-exact (tests/golden/bun045_cpu_rule_idx0.npz);
-  * bunny, 10 ICP iterations (allow_unequal): err rtol 1e-9, s/R/t atol 1e-9
-    (tests/golden/cpu_rule.json, made by tests/golden/make_cpu_rule.py) -- under the squared
-    rule the same run agrees only to ~1e-3 (SURVEY §8c);
+  * bunny, the 50 ICP iterations of BASELINE config C2 (allow_unequal): err rtol 1e-9, s/R/t
+    atol 1e-9 (tests/golden/cpu_rule.json, made by tests/golden/make_cpu_rule.py) -- under the
+    squared rule the same run agrees only to ~1e-3 (SURVEY §8c);
   * cow (no near ties): the two rules give bit-identical runs;
   * a lattice model with half-integer queries (exact ties everywhere): bit-exact vs the oracle.
 """

@@ -21,8 +21,9 @@ GOLD = os.path.join(HERE, "golden")
 RNG = np.random.default_rng(99)
 # (nn_mode, filter variant): certified with the VALU filter, certified with the MFMA filter
 # (+ VALU second level + fp64), fp64 brute force
-MODES = ["valu", "mfma", "mfma16", "grid", "fp64"]
-_MODE_ARGS = {"valu": (0, 1), "mfma": (0, 2), "mfma16": (0, 3), "grid": (0, 4), "fp64": (1, 0)}
+# (+ "bundle": the f16 filter behind the per-(query, bundle) bound, for models >= 8192 points)
+MODES = ["valu", "mfma", "mfma16", "grid", "bundle", "fp64"]
+_MODE_ARGS = {"valu": (0, 1), "mfma": (0, 2), "mfma16": (0, 3), "grid": (0, 4), "bundle": (0, 5), "fp64": (1, 0)}
 
 
 @pytest.fixture(scope="module")
@@ -140,12 +141,13 @@ def test_nn_certified_equals_fp64_at_1m(amd, ctxs, oracle):
     np.testing.assert_array_equal(out["mfma"], out["fp64"])
     np.testing.assert_array_equal(out["mfma16"], out["fp64"])
     np.testing.assert_array_equal(out["grid"], out["fp64"])
+    np.testing.assert_array_equal(out["bundle"], out["fp64"])
     sel = RNG.choice(p.shape[0], size=96, replace=False)
     _, ref = oracle.closest(p[sel], m)
     np.testing.assert_array_equal(out["fp64"][sel], ref)
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [2, 3, 5])
 def test_mfma_level1_certifies_most_queries(amd, variant):
     # the MFMA filters recover their argmin by recomputing G (f32: VALU fma chain, f16:
     # re-running the MFMA); if those bits ever differed, the queries would all fall back to
@@ -202,7 +204,7 @@ def test_icp_synthetic_fixed_iterations(amd, golden_traces):
 def test_modes_bitwise_identical(amd):
     m, p = load(amd, "horse_ref"), load(amd, "horse_tr1")
     a = run_engine(amd, "valu", m, p, 6, -1.0)
-    for mode in ("mfma", "mfma16", "grid", "fp64"):
+    for mode in ("mfma", "mfma16", "grid", "bundle", "fp64"):
         b = run_engine(amd, mode, m, p, 6, -1.0)
         np.testing.assert_array_equal(a[1], b[1])
         np.testing.assert_array_equal(a[2], b[2])

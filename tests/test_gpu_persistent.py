@@ -363,7 +363,8 @@ def test_randomised_bitwise_fuzz(amd):
             np.testing.assert_array_equal(x, y, err_msg=f"case {c}: n={n} nm={nm} {kind}")
 
 
-def test_scale_fuzz_certified_equals_fp64(amd):
+@pytest.mark.parametrize("variant", ["auto", "bundle"])
+def test_scale_fuzz_certified_equals_fp64(amd, variant):
     """tools/scale_fuzz.py, a short run: the default cascade of the launch loop (f16 MFMA filter,
     certificate, grid resolver, fp64 fallback) against the fp64 brute force at 2^15..2^19 points,
     every model shape of persist_fuzz, rescaled and offset clouds; unseeded and seeded iterations
@@ -388,7 +389,7 @@ def test_scale_fuzz_certified_equals_fp64(amd):
         else:
             sc, off = 10.0 ** rng.uniform(-3, 3), rng.normal(size=3) * 100.0
             m, p = m * sc + off * sc, p * sc + off * sc
-        cert = sf.run(m, p, amd.NN_CERTIFIED, 3)
+        cert = sf.run(m, p, amd.NN_CERTIFIED, 3, amd.VARIANT_BUNDLE if variant == "bundle" else amd.VARIANT_AUTO)
         ref = sf.run(m, p, amd.NN_FP64, 3)
         assert cert[0] == ref[0] == 3, (c, n, nm, kind)
         for x, y in zip(cert[1:4], ref[1:4]):

@@ -108,6 +108,25 @@ for s in $STEPS; do
     testrccl) run pytest_rccl 300 python -m pytest tests/test_gpu_sharded.py -m gpu -q -rf -k rccl ;;
     cli)   run cli 300 bash -c "cd $OUT && ../../iterative-closest-point_amd/build/icp-gpu \
                \$(python3 -c 'import sys;sys.path.insert(0,\"../../tests\");import datasets;print(datasets.path(\"cow_ref\"),datasets.path(\"cow_tr1\"))') 20" ;;
+    test_c5) run pytest_c5 900 python -u -m pytest tests/test_gpu_c5_sharded.py tests/test_gpu_boundary.py -m gpu -v -rf \
+               --timeout 600 --timeout-method thread --durations=10 ;;
+    c3hbm) run c3_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c3_trace" -o c3 -- \
+               python3 tools/configs_probe.py --configs C3_horse --variants auto --reps 1 &&
+           run c3_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c3_pmc1" -o fetch -- \
+               python3 tools/configs_probe.py --configs C3_horse --variants auto --reps 1 &&
+           run c3_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c3_pmc2" -o write -- \
+               python3 tools/configs_probe.py --configs C3_horse --variants auto --reps 1 &&
+           ICP_PERSIST_STAMPS=1 run c3_stamps 120 python3 tools/configs_probe.py --configs C3_horse --variants auto --reps 1 ;;
+    gridhbm) run grid_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/grid_trace" -o grid -- \
+               python3 bench.py --variant grid --steps 10 --warmup 2 --no-cpu-baseline --no-cow --no-cases &&
+           run grid_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/grid_pmc1" -o fetch -- \
+               python3 bench.py --variant grid --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases &&
+           run grid_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/grid_pmc2" -o write -- \
+               python3 bench.py --variant grid --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases ;;
+    bprobe) run bprobe 600 python3 tools/bundle_probe.py --steps 10 --variants mfma16 bundle &&
+            run bprobe8 300 python3 tools/bundle_probe.py --steps 10 --shard 8 --variants mfma16 bundle ;;
+    test_bundle) run pytest_bundle 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c4c5.py -m gpu -x -v -rf \
+               --timeout 300 --timeout-method thread --durations=10 -k "bundle or c4" ;;
     *) echo "unknown step $s" ;;
     esac
 done

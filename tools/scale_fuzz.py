@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Randomised bit-identity check of the default NN cascade at scale (f16 MFMA filter + fp64
 certificate + grid resolver + fp64 fallback, the launch loop that C4 runs) against the fp64
-brute force (ICP_NN_FP64): random model / scene sizes from 2^15 to 2^19 points, the model shapes
+brute force (ICP_NN_FP64) (--variant: another level-1 filter): random model / scene sizes from 2^15 to 2^19 points, the model shapes
 of persist_fuzz.py, coordinate scales 10^-3 .. 10^3 with far offsets, small to far rigid motions.
 Each case runs a fixed number of ICP iterations (the first unseeded, the rest seeded) in both
 modes and must agree bit for bit: error trace, final cloud and every iteration's
@@ -24,9 +24,10 @@ import icp_amd  # noqa: E402
 from persist_fuzz import model, rigid  # noqa: E402
 
 
-def run(m, p, nn_mode, iters):
+def run(m, p, nn_mode, iters, variant=0):
     with icp_amd.Context(0, nn_mode) as ctx:
         ctx.set_run_mode(icp_amd.RUN_LAUNCHES)
+        ctx.set_nn_variant(variant)
         ctx.set_allow_unequal(m.shape[0] != p.shape[0])
         ctx.set_model(m)
         ctx.set_scene(p)
@@ -42,6 +43,8 @@ def main():
     ap.add_argument("--max-seconds", type=float, default=400.0)
     ap.add_argument("--log2", type=float, nargs=2, default=[15.0, 19.0], metavar=("LO", "HI"),
                     help="cloud sizes 2^U(LO, HI) (20 20: C4-size clouds)")
+    ap.add_argument("--variant", choices=["auto", "mfma16", "bundle"], default="auto",
+                    help="level-1 filter of the certified run (auto: the default)")
     a = ap.parse_args()
     rng = np.random.default_rng(a.seed)
     t0 = time.time()
@@ -63,7 +66,9 @@ def main():
             off = rng.normal(size=3) * sc * rng.choice([0.0, 10.0, 1e3])
             m, p = m * sc + off, p * sc + off
         iters = int(rng.integers(2, 6))
-        cert = run(m, p, icp_amd.NN_CERTIFIED, iters)
+        var = {"auto": icp_amd.VARIANT_AUTO, "mfma16": icp_amd.VARIANT_MFMA16,
+               "bundle": icp_amd.VARIANT_BUNDLE}[a.variant]
+        cert = run(m, p, icp_amd.NN_CERTIFIED, iters, var)
         ref = run(m, p, icp_amd.NN_FP64, iters)
         ok = (cert[0] == ref[0] and np.array_equal(cert[1], ref[1], equal_nan=True)
               and np.array_equal(cert[2], ref[2], equal_nan=True) and np.array_equal(cert[3], ref[3]))
