@@ -167,6 +167,63 @@ def _cow_paths():
     return datasets.path("cow_ref"), datasets.path("cow_tr1")
 
 
+BUNDLE_COUNT_STEPS = 3
+
+
+def bundle_roofline(n_local, n_model, t_kernel, work):
+    """The bundle filter (nn_bundle_kernel) against the f16 MFMA peak on the work it EXECUTES,
+    counted on the device (icp_set_bundle_counters): the stream's bound tests (one
+    v_mfma_f32_32x32x16_f16 = 2*32*32*16 flop per 32-bundle block per wave: 8 query groups x 32
+    bundles), one more per fired block (its re-issued stream test), the per-query bound tests on
+    the groups a fired block fired for (32 queries x 32 bundles each) and the pair tests (32
+    queries x 32 points each).  The N x M pairs the search decides are listed beside it as
+    effective_pairs_per_s; SURVEY §8d's 8 flop per pair over them is no roofline here (most pairs
+    are excluded by the bounds, not evaluated)."""
+    stream = work["stream_mfma"]
+    fired = work["block_triggers"]
+    fine = work["group_tests"]
+    pair = work["pair_tests"]
+    executed = 32768.0 * (stream + fired + fine + pair)
+    ach = executed / t_kernel / 1e12
+    return {"bound": "mfma", "compute_unit": "v_mfma_f32_32x32x16_f16: bound |x-c|^2-(D+r)^2 of each 32-query group "
+                                             "(then of each query) against each 32-point kd bundle (hi/lo split, "
+                                             "16 products), then the f16 pair test of the bundles it cannot exclude",
+            "achieved": ach, "peak": PEAK_F16_MFMA_TFLOPS, "frac": ach / PEAK_F16_MFMA_TFLOPS,
+            "flop_per_launch": executed,
+            "flop_definition": "executed f16 MFMA work (2*32*32*16 flop per instruction), per launch: "
+                               f"{stream:.0f} stream bound tests + {fired:.0f} re-issued on fired blocks + "
+                               f"{fine:.0f} per-query bound tests + {pair:.0f} pair tests (device counters over "
+                               f"{BUNDLE_COUNT_STEPS} seeded iterations)",
+            "wave_task_phases_us": work.get("us_per_wave_task"),
+            "work_per_launch": {"stream_mfma": stream, "fired_blocks": fired, "group_tests": fine,
+                                "pair_tests": pair, "pairs_evaluated": 1024.0 * pair,
+                                "pair_share_of_n_m": 1024.0 * pair / (n_local * n_model)},
+            "effective_pairs_per_s": n_local * n_model / t_kernel,
+            "pairs_per_s": n_local * n_model / t_kernel}
+
+
+def full_nxm_rate(device, m, p, steps=5, warmup=2):
+    """The full N x M f16 filter (ICP_NN_VARIANT_MFMA16, nn_mfma16r_kernel<8>) on the same C4
+    iterations, for comparison with the bundle filter: same results bit for bit."""
+    with icp_amd.Context(device) as ctx:
+        ctx.set_nn_variant(icp_amd.VARIANT_MFMA16)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        ctx.run(warmup, -1.0)
+        ctx.reset_stats()
+        t0 = time.perf_counter()
+        ctx.run(steps, -1.0)
+        dt = time.perf_counter() - t0
+        st = ctx.stats()
+    t = st["nn_ms"] / max(st["nn_launches"], 1) * 1e-3
+    pairs = float(p.shape[0]) * m.shape[0]
+    ach = FLOP_PER_PAIR * pairs / t / 1e12
+    return {"kernel": "nn_mfma16r_kernel<8>", "iterations_per_s": steps / dt, "avg_launch_ms": t * 1e3,
+            "achieved": ach, "peak": PEAK_F16_MFMA_TFLOPS, "frac": ach / PEAK_F16_MFMA_TFLOPS,
+            "flop_definition": "algorithmic: 8 flop per (query, model) pair over all N x M pairs",
+            "executed_tflops": MFMA16_FLOP_PER_PAIR * pairs / t / 1e12, "pairs_per_s": pairs / t}
+
+
 def reference_cases_gpu(min_time=0.3):
     """The reference's 8 GPU benchmark cases (src/bench.cc:391-445) through
     iterative-closest-point_amd/build/icp-bench, on the bundled cow pair."""
@@ -321,7 +378,7 @@ def main():
     # --nnodes / --nproc-per-node and stops)
     ap.add_argument("--points", "--n", dest="n", type=int, default=1 << 20)
     ap.add_argument("--nn", choices=["certified", "fp64"], default="certified")
-    ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16", "grid"], default="auto")
+    ap.add_argument("--variant", choices=["auto", "valu", "mfma", "mfma16", "grid", "bundle"], default="auto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
     ap.add_argument("--no-cases", action="store_true", help="skip the reference's 14 benchmark cases")
@@ -367,14 +424,15 @@ def main():
         ctx = icp_amd.Context(local, nn_mode)
 
     variant = {"auto": icp_amd.VARIANT_AUTO, "valu": icp_amd.VARIANT_VALU, "mfma": icp_amd.VARIANT_MFMA,
-               "mfma16": icp_amd.VARIANT_MFMA16, "grid": icp_amd.VARIANT_GRID}[args.variant]
+               "mfma16": icp_amd.VARIANT_MFMA16, "grid": icp_amd.VARIANT_GRID,
+               "bundle": icp_amd.VARIANT_BUNDLE}[args.variant]
     ctx.set_nn_variant(variant)
     m, p = icp_amd.synthetic_pair(args.n, seed=42)
     b, c = icp_amd.shard_range(args.n, rank, world)
-    big = c >= 8192 and args.n >= 8192  # level1_kind's f16 MFMA threshold
+    big = c >= 8192 and args.n >= 8192  # level1_kind's f16 MFMA threshold (AUTO: the bundle filter)
     level1 = None if args.nn != "certified" else (
-        "mfma16" if args.variant == "mfma16" or (args.variant == "auto" and big) else
-        ("mfma" if args.variant == "mfma" else None))
+        "bundle" if args.variant == "bundle" or (args.variant == "auto" and big) else
+        "mfma16" if args.variant == "mfma16" else ("mfma" if args.variant == "mfma" else None))
     ctx.set_model(m)
     ctx.set_scene(p[b:b + c], np_total=args.n)
 
@@ -394,6 +452,17 @@ def main():
 
     nn_avg_ms = st["nn_ms"] / max(st["nn_launches"], 1)
     ar_ms = st["allreduce_ms"] / st["allreduce_calls"] if st["allreduce_calls"] else None
+    work = None
+    if level1 == "bundle":
+        # untimed, after the timed region, on every rank (icp_run all-reduces): the bundle
+        # filter's executed work per search from its device counters, over a few more seeded
+        # iterations of the same registration
+        ctx.set_bundle_counters(True)
+        ctx.run(BUNDLE_COUNT_STEPS, -1.0)
+        bc = ctx.bundle_counters()
+        work = {k: v / BUNDLE_COUNT_STEPS for k, v in bc.items() if not isinstance(v, dict)}
+        work["us_per_wave_task"] = bc["us_per_wave_task"]
+        ctx.set_bundle_counters(False)
     host_reduce = world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1"
     per_rank = [rank_record(rank, ctx.comm_info(), nn_avg_ms, ar_ms, c, st["iterations"])]
     if dist is not None:
@@ -404,13 +473,13 @@ def main():
     pairs = c * args.n
     # algorithmic flop against the peak of the unit the kernel runs on
     flops = FLOP_PER_PAIR * pairs
-    peak = PEAK_F16_MFMA_TFLOPS if level1 == "mfma16" else PEAK_FP32_TFLOPS
+    peak = PEAK_F16_MFMA_TFLOPS if level1 in ("mfma16", "bundle") else PEAK_FP32_TFLOPS
     achieved = flops / (nn_avg_ms * 1e-3) / 1e12 if nn_avg_ms > 0 else 0.0
     # timed iterations are seeded (the first icp_run iteration after set_scene is warm-up)
     k16 = {"plain": "nn_mfma16_kernel<seeded>", "pipe": "nn_mfma16p_kernel<seeded>",
            "unroll": "nn_mfma16x_kernel<seeded>", "r4": "nn_mfma16r_kernel<4>"}.get(
         os.environ.get("ICP_MFMA16_KERNEL", ""), "nn_mfma16r_kernel<8>")
-    kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel"}.get(
+    kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel", "bundle": "nn_bundle_kernel"}.get(
         level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
     if args.variant == "grid":
         # timed iterations are seeded (warm-up leaves every query a correspondence): the seeded
@@ -427,6 +496,8 @@ def main():
               "pmc_hbm_frac": traffic / nn_s / 1e9 / 8000.0 if traffic and nn_s > 0 else None,
               "note": "the O(N*M) filter is compute-bound: its HBM fraction is small by construction (§8d)"}
     dtype = {"mfma16": "f16 hi/lo-split MFMA filter (fp32 accumulate); fp64 certificate, resolve and reductions",
+             "bundle": "f16 hi/lo-split MFMA bundle bound + pair filter (fp32 accumulate); fp64 certificate, "
+                       "resolve and reductions",
              "mfma": "f32 MFMA filter; fp64 certificate, resolve and reductions"}.get(
         level1, "f64" if args.nn == "fp64" else "f32 VALU filter; fp64 certificate, resolve and reductions")
 
@@ -470,6 +541,8 @@ def main():
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
         }
+        if level1 == "bundle" and nn_s > 0:
+            out["roofline"].update(bundle_roofline(c, args.n, nn_s, work))
         if level1 == "mfma16" and nn_s > 0:
             ex = MFMA16_FLOP_PER_PAIR * pairs / nn_s / 1e12
             out["roofline"]["mfma_pipe"] = {
@@ -508,6 +581,8 @@ def main():
             out["csv_io"] = csv_io(m)
             if args.variant != "grid" and args.nn == "certified":
                 out["grid_nn"] = grid_nn_rate(local, m, p, args.steps)
+            if level1 == "bundle":
+                out["full_nxm_filter"] = full_nxm_rate(local, m, p)
         if not args.no_cpu_baseline:  # rank 0 at every N: the same host-side baseline
             out["cpu_baseline"] = cpu_baseline(m, p)
             if not args.no_cases:

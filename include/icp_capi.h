@@ -249,12 +249,14 @@ int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap);
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out);
 int icp_reset_stats(icp_ctx *ctx);
 /* Instrumentation of the bundle filter (ICP_NN_VARIANT_BUNDLE): with enable = 1 its searches
- * count, from zero, (out[0]) the 32-bundle blocks whose joint bound test fired in a wave,
- * (out[1]) the 32-query groups with a bundle V <= 0 in them, (out[2]) the pair tests run
- * (one f16 MFMA of 32 queries x 32 points each) -- the executed work behind the roofline;
- * 0 = off (the default; no counting). */
+ * count, from zero, the executed f16 MFMAs behind the roofline -- (out[8]) the stream's bound
+ * tests, (out[0]) the 32-bundle blocks whose stream test fired in a wave (each re-issues its
+ * stream test), (out[1]) the per-query bound tests run on the groups they fired for, (out[2])
+ * the pair tests (32 queries x 32 points each) -- and, summed over the wave tasks (out[7] of
+ * them), the 100 MHz clock ticks each spent in its prologue (out[3]), bundle stream (out[4]),
+ * deferred fired blocks (out[5]) and epilogue (out[6]); 0 = off (the default; no counting). */
 int icp_set_bundle_counters(icp_ctx *ctx, int enable);
-int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[3]);
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[9]);
 /* Who this context talks to (evidence for multi-GPU runs): *comm_count / *comm_rank =
  * ncclCommCount / ncclCommUserRank of its RCCL communicator, or -1 / the context's rank when
  * it has none (plain or host all-reduce contexts); bus_id (nullable, len >= 16) = the PCI bus

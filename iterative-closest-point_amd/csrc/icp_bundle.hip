@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -49,6 +50,7 @@ constexpr int kBBlocksPerTile = kBTile / 32;          // 8 bundle blocks of 32 b
 constexpr int kBDmaPerWave = kBBlocksPerTile / 4;     // 2 wave-instructions per tile
 constexpr int kBVmcntDma = 0x0F70 | kBDmaPerWave;     // vmcnt(2): one tile's DMA may stay in flight
 constexpr int kBQG = 8;                               // 32-query groups per wave
+constexpr int kBPendCap = 64;                         // deferred 32-bundle blocks per wave (LDS)
 constexpr double kBQueryMax = 8192.0;                 // |a_k| range of the bundle operand
 constexpr double kBSeedMax = 11000.0;                 // d' range of the bundle operand
 
@@ -87,14 +89,68 @@ __device__ __forceinline__ half8_t bundle_query_frag(const double a[3], double d
     return b;
 }
 
+// The group bound: one column per 32-query group with the group's centre g^ (f16 hi/lo, the
+// midpoint of its in-range queries' box) and D_g = max over them of (d'_q + |q^ - g^|) (rounded
+// up), in bundle_query_frag's form.  |g^ - c^| > D_g + r' gives, for every query q of the group,
+// |q^ - c^| >= |g^ - c^| - |q^ - g^| > d'_q + r', so a bundle the group excludes is excluded for
+// each of its queries (same margins: V^ > 0 => V > 0).  A group with a kBqForced query is
+// forced; one without in-range queries never fires.  Reductions over the 32 lanes of each half
+// (lane and lane + 32 hold the same query).  Returns this lane's operand half for its group.
+__device__ __forceinline__ half8_t bundle_group_frag(const double a[3], double dq, int mode, int h)
+{
+    _Float16 hi, lo;
+    double q[3];
+    for (int k = 0; k < 3; ++k) {
+        split_f16(a[k], hi, lo);
+        q[k] = (double)hi + (double)lo;
+    }
+    const bool in = mode == kBqNormal;
+    double lo3[3], hi3[3];
+    for (int k = 0; k < 3; ++k) {
+        lo3[k] = in ? q[k] : INFINITY;
+        hi3[k] = in ? q[k] : -INFINITY;
+    }
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1)
+        for (int k = 0; k < 3; ++k) {
+            lo3[k] = fmin(lo3[k], __shfl_xor(lo3[k], o, 64));
+            hi3[k] = fmax(hi3[k], __shfl_xor(hi3[k], o, 64));
+        }
+    const unsigned long long forced = __ballot(mode == kBqForced), normal = __ballot(in);
+    const unsigned half_mask = h ? (unsigned)(forced >> 32) : (unsigned)forced;
+    const unsigned half_norm = h ? (unsigned)(normal >> 32) : (unsigned)normal;
+    double g[3];
+    for (int k = 0; k < 3; ++k) {
+        const double c = half_norm ? 0.5 * (lo3[k] + hi3[k]) : 0.0;
+        _Float16 gh, gl;
+        split_f16(c, gh, gl);
+        g[k] = (double)gh + (double)gl;
+    }
+    const double e0 = q[0] - g[0], e1 = q[1] - g[1], e2 = q[2] - g[2];
+    double D = in ? (dq + sqrt((e0 * e0 + e1 * e1) + e2 * e2) * (1.0 + 0x1.0p-48)) * (1.0 + 0x1.0p-48) : 0.0;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) D = fmax(D, __shfl_xor(D, o, 64));
+    int gmode = half_mask ? kBqForced : half_norm ? kBqNormal : kBqNever;
+    if (gmode == kBqNormal && !(fabs(g[0]) <= kBQueryMax && fabs(g[1]) <= kBQueryMax && fabs(g[2]) <= kBQueryMax &&
+                                D <= kBSeedMax))
+        gmode = kBqForced;
+    return bundle_query_frag(g, D, gmode, h);
+}
+
 // Seeded f16 filter behind the bundle bound.  Per wave 8 groups of 32 queries (256); the
 // queries of a workgroup are consecutive in `order` (a spatial order of the scene), so that
 // their bundles with V^ <= 0 coincide.  Per 32-bundle block: one bundle MFMA per group into
 // ONE joint v_min3 tree (carried, two MFMAs behind, as nn_mfma16r_kernel); when it is <= 0 the
 // trigger path re-issues the block's bundle MFMAs, collects per group the bundles with a
 // V^ <= 0 lane, and runs for each the pair MFMA (pair image in kd order, 1 KiB per bundle,
-// from L2) and the med3/min tracking of nn_mfma16r_kernel.  The groups' pair operands wait in
-// LDS for that path and for the index recovery (their VGPRs would cost the third wave).
+// from L2) and the med3/min tracking of nn_mfma16r_kernel, which here also records the kd
+// position of each lane's best (a rare path: no index-recovery pass at the end, whose 1 KiB
+// reloads per distinct winning block dominated short launches).  The groups' pair operands wait
+// in LDS for that path (their VGPRs would cost the third wave).
+// GB (the default): the stream tests the 8 groups of a wave first, one bundle MFMA per 32-bundle
+// block (columns 0..7 = the groups, the rest never fire), and the per-query bound runs only on
+// the groups a fired block fired for (ICP_BUNDLE_GROUP=0: the per-query bound in the stream).
+template <bool GB>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_bundle_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, int np,
     const int *__restrict__ order, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx,
@@ -106,18 +162,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     constexpr int QG = kBQG;
     unsigned n_blocks = 0, n_groups = 0, n_pairs = 0; // (counters: wave-uniform tallies)
+    // (counters: the 100 MHz clock at the phase boundaries of this wave)
+    const unsigned long long t_start = counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long t_pro = 0, t_stream = 0, t_defer = 0;
     __shared__ half8_t tiles[2][kBTile * 2];        // 2 x 8 KiB
     __shared__ half8_t s_bq[4][QG][64];             // 32 KiB: the pair operands
+    __shared__ int s_pend[4][kBPendCap];            // per wave: 32-bundle blocks to update later
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
-    const int split = blockIdx.y;
-    const int b0 = split * chunk;
-    const int b1 = min(b0 + chunk, nb_pad);
+    // split s of S takes the 32-bundle blocks s, s + S, s + 2S, ... (interleaved: a wave's fired
+    // blocks, which cluster in kd order around its queries, spread over all its splits instead of
+    // loading the one split that holds its region); past the last block: the null block nbb (32
+    // padding bundles, never fired by an in-range query)
+    const int split = blockIdx.y, S = gridDim.y;
+    const int nbb = nb_pad >> 5;
+    const int nk = (nbb - split + S - 1) / S;                      // this split's blocks
+    const int ntile = (nk + kBBlocksPerTile - 1) / kBBlocksPerTile;
+    auto gblock = [&](int k) { const int g = split + S * k; return g < nbb ? g : nbb; };
     const int sbase = blockIdx.x * (4 * QG * 32) + wave * (QG * 32) + col;
 
     half8_t bb[QG];
     float best[QG], second[QG];
-    int bblk[QG];
+    int bpos[QG]; // kd position of this lane's best (tracked in the update: no recovery pass)
+    half8_t gop; // GB: this wave's group operands (column q = group q, columns 8.. never)
+    {
+        const double z[3] = {0.0, 0.0, 0.0};
+        gop = bundle_query_frag(z, 0.0, kBqNever, h);
+    }
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
         const int s = sbase + q * 32;
@@ -144,27 +215,68 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         }
         s_bq[wave][q][lane] = query_frag(a, h, sd);
         bb[q] = bundle_query_frag(a, dq, mode, h);
+        if (GB) {
+            const half8_t gq = bundle_group_frag(a, dq, mode, h);
+            if (col == q) gop = gq;
+        }
         best[q] = 0.0f; // seeded: "nothing below s0'"
         second[q] = 0.0f;
-        bblk[q] = 0;
+        bpos[q] = -1;
     }
     const f32x16_t zero = {};
+    if (counters) {
+        __builtin_amdgcn_s_waitcnt(0);
+        t_pro = __builtin_amdgcn_s_memrealtime();
+    }
 
-    auto issue_tile = [&](int tb, int buf) {
+    auto issue_tile = [&](int t, int buf) {
 #pragma unroll
         for (int i = 0; i < kBDmaPerWave; ++i) {
             const int blk = wave + 4 * i;
-            __builtin_amdgcn_global_load_lds((const void *)(bimg + ((size_t)(tb >> 5) + blk) * 64 + lane),
+            __builtin_amdgcn_global_load_lds((const void *)(bimg + (size_t)gblock(kBBlocksPerTile * t + blk) * 64 + lane),
                                              (__attribute__((address_space(3))) void *)&tiles[buf][blk * 64],
                                              16, 0, 0);
         }
     };
     // the rare path: which bundles of this 32-bundle block may hold a point at least as close
     // as some query's seed, and the pair test against each of them
+    // pair test of group q against pair block blk (kd positions 32 blk ..): (best, second) and
+    // this lane's best position
+    auto pair_update = [&](int q, const f32x16_t &dd, int blk) {
+        const float mn = min16v(dd);
+        if (!__any(mn < second[q])) return;
+        if (__any(mn < best[q])) { // this lane's new best: the lowest row holding it
+            int row = 0; // (inline-constant selects; this lane's half added once)
+#pragma unroll
+            for (int r = 15; r >= 0; --r)
+                row = dd[r] == mn ? (r & 3) + 8 * (r >> 2) : row;
+            bpos[q] = mn < best[q] ? blk * 32 + 4 * h + row : bpos[q];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], dd[r]);
+            best[q] = fminf(best[q], dd[r]);
+        }
+    };
+    // the rare path: which bundles of this 32-bundle block may hold a point at least as close
+    // as some query's seed (per group), then the pair tests.  Each needed pair block is loaded
+    // once for all the groups that need it, four blocks' loads in flight together (the path is
+    // latency-bound: a wave's triggers concentrate in the split holding its region).
     auto update = [&](const half8_t &a8, int bblock) {
         ++n_blocks;
+        unsigned gm[QG], uni = 0u, gfire = 0xffu;
+        if (GB) { // the groups this block fired for
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, gop, zero, 0, 0, 0);
+            const unsigned long long f = __ballot(min16v(d) <= 0.0f);
+            gfire = (unsigned)(f | (f >> 32)) & 0xffu;
+        }
+        n_groups += __builtin_popcount(gfire); // per-query bound MFMAs run
 #pragma unroll
         for (int q = 0; q < QG; ++q) {
+            if (!((gfire >> q) & 1u)) {
+                gm[q] = 0u;
+                continue;
+            }
             const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bb[q], zero, 0, 0, 0);
             unsigned mask = 0u;
 #pragma unroll
@@ -173,31 +285,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
                 const int row = (r & 3) + 8 * (r >> 2);
                 mask |= ((unsigned)bl != 0u ? 1u << row : 0u) | ((unsigned)(bl >> 32) != 0u ? 1u << (row + 4) : 0u);
             }
-            if (!mask) continue;
-            ++n_groups;
+            gm[q] = mask;
+            uni |= mask;
             n_pairs += __builtin_popcount(mask);
-            const half8_t bqv = s_bq[wave][q][lane];
-            while (mask) {
-                const int b = __builtin_ctz(mask);
-                mask &= mask - 1u;
-                const int blk = bblock * 32 + b; // pair block = bundle (kd order)
-                const half8_t ap = pimg[(size_t)blk * 64 + lane];
-                const f32x16_t dd = __builtin_amdgcn_mfma_f32_32x32x16_f16(ap, bqv, zero, 0, 0, 0);
-                if (!__any(min16v(dd) < second[q])) continue;
-                const float prevb = best[q];
+        }
+        while (uni) {
+            int bs[4];
+            half8_t ap[4];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], dd[r]);
-                    best[q] = fminf(best[q], dd[r]);
+            for (int k = 0; k < 4; ++k) {
+                bs[k] = uni ? __builtin_ctz(uni) : -1;
+                uni &= uni - 1u;
+                if (bs[k] >= 0) ap[k] = pimg[((size_t)bblock * 32 + bs[k]) * 64 + lane];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (bs[k] < 0) break;
+#pragma unroll
+                for (int q = 0; q < QG; ++q) {
+                    if (!((gm[q] >> bs[k]) & 1u)) continue;
+                    const f32x16_t dd =
+                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ap[k], s_bq[wave][q][lane], zero, 0, 0, 0);
+                    pair_update(q, dd, bblock * 32 + bs[k]);
                 }
-                bblk[q] = best[q] < prevb ? blk : bblk[q];
             }
         }
     };
     // one 32-bundle block: d0, d1 = its q0, q1 results (issued one step earlier); issues the
     // next block's q0, q1 MFMAs into dn0, dn1 unless LAST (nn_mfma16r_kernel's pipeline)
+    // (a block whose test fires is only marked in `pend`; the tile's marked blocks run the
+    // update after its last block, from the same LDS tile: one copy of the update code per tile
+    // loop instead of one per unrolled block)
+    unsigned pend = 0u;
+    int npend = 0; // (wave-uniform)
     auto step = [&](const half8_t &a8, const half8_t &an, f32x16_t &d0, f32x16_t &d1, f32x16_t &dn0,
-                    f32x16_t &dn1, int bblock, auto last_tag) {
+                    f32x16_t &dn1, int bit, auto last_tag) {
         constexpr bool LAST = decltype(last_tag)::value;
         float u, v;
         f32x16_t dm2 = d0, dm1 = d1;
@@ -225,71 +347,102 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
         if (!LAST) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);
-        if (__builtin_expect(__any(need), 0)) update(a8, bblock);
+        pend |= __any(need) ? 1u << bit : 0u;
     };
     using More = std::integral_constant<bool, false>;
     using Last = std::integral_constant<bool, true>;
 
-    issue_tile(b0, 0);
-    int it = 0;
-    for (int t0 = b0; t0 < b1; t0 += kBTile, ++it) {
+    issue_tile(0, 0);
+    for (int it = 0; it < ntile; ++it) {
         const int cur = it & 1;
-        if (t0 + kBTile < b1) {
-            issue_tile(t0 + kBTile, cur ^ 1);
+        if (it + 1 < ntile) {
+            issue_tile(it + 1, cur ^ 1);
             __builtin_amdgcn_s_waitcnt(kBVmcntDma);
         } else {
             __builtin_amdgcn_s_waitcnt(kVmcnt0);
         }
         __builtin_amdgcn_s_barrier();
         const half8_t *tile = tiles[cur];
-        const int blk0 = t0 >> 5;
-        half8_t a0 = tile[lane], a1 = tile[64 + lane];
-        f32x16_t dA0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[0], zero, 0, 0, 0);
-        f32x16_t dA1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[1], zero, 0, 0, 0), dB0, dB1;
+        const int k0 = kBBlocksPerTile * it; // (this tile's blocks: gblock(k0 + b))
+        if (GB) {
+            // one group MFMA per block, two in flight ahead of the min tree that reads them
+            f32x16_t d0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tile[lane], gop, zero, 0, 0, 0);
+            f32x16_t d1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tile[64 + lane], gop, zero, 0, 0, 0);
 #pragma unroll
-        for (int b = 0; b < kBBlocksPerTile - 2; b += 2) {
-            step(a0, a1, dA0, dA1, dB0, dB1, blk0 + b, More{});
-            a0 = tile[(b + 2) * 64 + lane];
-            step(a1, a0, dB0, dB1, dA0, dA1, blk0 + b + 1, More{});
-            a1 = tile[(b + 3) * 64 + lane];
+            for (int b = 0; b < kBBlocksPerTile; ++b) {
+                f32x16_t d2;
+                if (b + 2 < kBBlocksPerTile)
+                    d2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tile[(b + 2) * 64 + lane], gop, zero, 0, 0, 0);
+                pend |= __any(min16v(d0) <= 0.0f) ? 1u << b : 0u;
+                d0 = d1;
+                if (b + 2 < kBBlocksPerTile) d1 = d2;
+            }
+        } else {
+            half8_t a0 = tile[lane], a1 = tile[64 + lane];
+            f32x16_t dA0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[0], zero, 0, 0, 0);
+            f32x16_t dA1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bb[1], zero, 0, 0, 0), dB0, dB1;
+#pragma unroll
+            for (int b = 0; b < kBBlocksPerTile - 2; b += 2) {
+                step(a0, a1, dA0, dA1, dB0, dB1, b, More{});
+                a0 = tile[(b + 2) * 64 + lane];
+                step(a1, a0, dB0, dB1, dA0, dA1, b + 1, More{});
+                a1 = tile[(b + 3) * 64 + lane];
+            }
+            step(a0, a1, dA0, dA1, dB0, dB1, kBBlocksPerTile - 2, More{});
+            step(a1, a0, dB0, dB1, dA0, dA1, kBBlocksPerTile - 1, Last{});
         }
-        step(a0, a1, dA0, dA1, dB0, dB1, blk0 + kBBlocksPerTile - 2, More{});
-        step(a1, a0, dB0, dB1, dA0, dA1, blk0 + kBBlocksPerTile - 1, Last{});
+        // a fired block is deferred to after the stream: the update's cost is then this wave's
+        // alone, where inside the loop every wave of the workgroup would wait for it at the
+        // next tile barrier (measured: with the update inline, a W = 8 shard's launch took 4x its
+        // streaming time).  A full list runs the update at once.
+        while (__builtin_expect(pend != 0u, 0)) {
+            const int b = __builtin_ctz(pend);
+            pend &= pend - 1u;
+            if (npend < kBPendCap) {
+                if (lane == 0) s_pend[wave][npend] = gblock(k0 + b);
+                ++npend;
+            } else {
+                update(tile[b * 64 + lane], gblock(k0 + b));
+            }
+        }
         __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
         __builtin_amdgcn_s_barrier();
     }
 
+    if (counters) t_stream = __builtin_amdgcn_s_memrealtime();
+    // the deferred blocks: their bundle operands from the (L2-resident) image, the next one's
+    // load in flight while this one is updated
+    if (npend) {
+        int bid = __builtin_amdgcn_readfirstlane(s_pend[wave][0]);
+        half8_t a8 = bimg[(size_t)bid * 64 + lane];
+        for (int i = 0; i < npend; ++i) {
+            const int nid = __builtin_amdgcn_readfirstlane(s_pend[wave][i + 1 < npend ? i + 1 : i]);
+            const half8_t an = bimg[(size_t)nid * 64 + lane];
+            update(a8, bid);
+            a8 = an;
+            bid = nid;
+        }
+    }
+    if (counters) {
+        __builtin_amdgcn_s_waitcnt(0);
+        t_defer = __builtin_amdgcn_s_memrealtime();
+    }
     if (counters && lane == 0) { // icp_set_bundle_counters: the executed work of this wave
         atomicAdd(counters, (unsigned long long)n_blocks);
         atomicAdd(counters + 1, (unsigned long long)n_groups);
         atomicAdd(counters + 2, (unsigned long long)n_pairs);
+        atomicAdd(counters + 3, t_pro - t_start);     // prologue (query loads, operands)
+        atomicAdd(counters + 4, t_stream - t_pro);    // bundle stream (incl. tile barriers)
+        atomicAdd(counters + 5, t_defer - t_stream);  // deferred fired blocks
+        atomicAdd(counters + 7, 1ull);                // wave tasks
+        atomicAdd(counters + 8, (unsigned long long)(ntile * kBBlocksPerTile * (GB ? 1 : QG))); // stream MFMAs
     }
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
         const float b = best[q];
         const float s2 = second[q];
-        const int blk = bblk[q];
-        const half8_t bqv = s_bq[wave][q][lane];
-        // index recovery (nn_mfma16r_kernel): re-run the pair MFMA on each distinct winning
-        // block; the lowest row with d == best (ties never certify: second would equal best)
-        int found = -1;
-        bool done = !(b < 0.0f);
-        for (int guard = 0; guard < 64; ++guard) {
-            const unsigned long long pend = __ballot(!done);
-            if (pend == 0ull) break;
-            const int lead = __ffsll((long long)pend) - 1;
-            const int rb = __shfl(blk, lead, 64);
-            const half8_t a8 = pimg[(size_t)rb * 64 + lane];
-            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bqv, zero, 0, 0, 0);
-            if (!done && blk == rb) {
-#pragma unroll
-                for (int r = 15; r >= 0; --r) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    found = (d[r] == b) ? rb * 32 + row : found;
-                }
-                done = true;
-            }
-        }
+        // (a tie of two rows leaves second == best: never certified, any of them is a hint)
+        const int found = b < 0.0f ? bpos[q] : -1;
         float bb2 = b, ss = s2;
         int id = found;
         {
@@ -312,6 +465,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
             part_second[o] = ss;
             part_idx[o] = id >= 0 ? kd_orig[id] : -1; // kd position -> original index (padding: nm)
         }
+    }
+    if (counters) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) atomicAdd(counters + 6, t_end - t_defer); // epilogue (split results)
     }
 }
 
@@ -358,7 +516,7 @@ __global__ __launch_bounds__(kBlock) void build_bundle_image_kernel(
     const int *__restrict__ kd, int nb_pad, double cx, double cy, double cz, double scale,
     half8_t *__restrict__ img, float *__restrict__ radius)
 {
-    for (int b = blockIdx.x * kBlock + threadIdx.x; b < nb_pad; b += gridDim.x * kBlock) {
+    for (int b = blockIdx.x * kBlock + threadIdx.x; b < nb_pad + 32; b += gridDim.x * kBlock) {
         half8_t lo8 = {}, hi8 = {};
         const int k0 = b * kBundle, k1 = min(k0 + kBundle, nm);
         float rad = -1.0f;
@@ -482,16 +640,30 @@ void launch_build_bundle_images(const double *mx, const double *my, const double
                                 int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
                                 float *radius, hipStream_t st)
 {
-    const int nm_b = nb_pad * kBundle;
+    const int nm_b = (nb_pad + 32) * kBundle; // (+ the null block)
     build_pair_image_kd_kernel<<<bgrid(nm_b), kBlock, 0, st>>>(mx, my, mz, nm, kd, nm_b, c[0], c[1], c[2], scale,
                                                                   (half8_t *)pimg, kd_orig);
-    build_bundle_image_kernel<<<bgrid(nb_pad), kBlock, 0, st>>>(mx, my, mz, nm, kd, nb_pad, c[0], c[1], c[2],
+    build_bundle_image_kernel<<<bgrid(nb_pad + 32), kBlock, 0, st>>>(mx, my, mz, nm, kd, nb_pad, c[0], c[1], c[2],
                                                                    scale, (half8_t *)bimg, radius);
+}
+
+static bool bundle_group()
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_BUNDLE_GROUP");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
 }
 
 NNPlan plan_nn_bundle(size_t np, int nb_pad)
 {
-    NNPlan pl = make_nn_plan(np, (size_t)nb_pad, kBTile, kBQG, 4 * kBQG * 32, (const void *)nn_bundle_kernel);
+    // one round of resident workgroups (interleaved splits balance the fired blocks; more
+    // rounds only repeat the per-query prologue: W = 8 shard 0.37 -> 0.25 ms, C4 unchanged,
+    // profiles/r03f/ bsweep*)
+    NNPlan pl = make_nn_plan(np, (size_t)nb_pad, kBTile, kBQG, 4 * kBQG * 32,
+                             bundle_group() ? (const void *)nn_bundle_kernel<true> : (const void *)nn_bundle_kernel<false>,
+                             1);
     pl.kernel = 100;
     return pl;
 }
@@ -503,9 +675,13 @@ void launch_nn_bundle(const double *px, const double *py, const double *pz, int 
                       unsigned long long *counters)
 {
     dim3 grid(pl.qblocks, pl.splits);
-    nn_bundle_kernel<<<grid, kBlock, 0, st>>>(px, py, pz, np, order, prev, m4, c[0], c[1], c[2], scale, seed16,
-                                              (const half8_t *)bimg, nb_pad, (const half8_t *)pimg, kd_orig, nm,
-                                              pl.chunk, part_best, part_second, part_idx, stop, counters);
+#define LAUNCHB(GB)                                                                                              \
+    nn_bundle_kernel<GB><<<grid, kBlock, 0, st>>>(px, py, pz, np, order, prev, m4, c[0], c[1], c[2], scale, seed16, \
+                                                  (const half8_t *)bimg, nb_pad, (const half8_t *)pimg, kd_orig, nm,  \
+                                                  pl.chunk, part_best, part_second, part_idx, stop, counters)
+    if (bundle_group()) LAUNCHB(true);
+    else LAUNCHB(false);
+#undef LAUNCHB
 }
 
 } // namespace icp

@@ -515,8 +515,14 @@ int level1_kind(const icp_ctx *ctx, size_t n)
     if (ctx->nn_variant == ICP_NN_VARIANT_VALU || ctx->nn_variant == ICP_NN_VARIANT_GRID) return 0;
     // measured crossover (tools/configs_probe.py, 50-iteration registrations of synthetic n x n
     // pairs): VALU wins at 4,096 (2.4 vs 8.9 ms), the f16 MFMA filter from 8,192 (3.3 vs 3.7
-    // ms) and by 2.2-2.6x at bunny / horse size, 8x at 65,536
-    return (n >= 8192 && ctx->nm >= 8192) ? 2 : 0;
+    // ms) and by 2.2-2.6x at bunny / horse size, 8x at 65,536.  Behind the bundle bound
+    // (icp_bundle.hip) it is 35x faster again at C4 (0.78 against 27.6 ms per search, the same
+    // indices bit for bit) and 14x at a W = 8 shard; the two break even near 40,000 x 40,000
+    // (16,384 x 16,384: 73 against 25 us), so the bundle filter takes searches from 2^31 pairs
+    // (tools/bundle_probe.py, profiles/r03f/)
+    if (n >= 8192 && ctx->nm >= 8192)
+        return ctx->nb_pad > 0 && (double)n * (double)ctx->nm >= 2147483648.0 ? 3 : 2;
+    return 0;
 }
 
 GridView grid_view(const icp_ctx *ctx)
@@ -989,22 +995,22 @@ int icp_set_bundle_counters(icp_ctx *ctx, int enable)
         ctx->b_counters = nullptr;
         return ICP_OK;
     }
-    if (!ctx->b_counters) HIPCHK(hipMalloc((void **)&ctx->b_counters, 4 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, 4 * sizeof(unsigned long long), ctx->st));
+    if (!ctx->b_counters) HIPCHK(hipMalloc((void **)&ctx->b_counters, 9 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, 9 * sizeof(unsigned long long), ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
 }
 
-int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[3])
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[9])
 {
     if (!ctx || !out) return ICP_E_ARG;
-    out[0] = out[1] = out[2] = 0;
+    for (int k = 0; k < 9; ++k) out[k] = 0;
     if (!ctx->b_counters) return ICP_OK;
     HIPCHK(hipSetDevice(ctx->device));
-    unsigned long long v[4] = {0, 0, 0, 0};
+    unsigned long long v[9] = {};
     HIPCHK(hipMemcpyAsync(v, ctx->b_counters, sizeof(v), hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
-    for (int k = 0; k < 3; ++k) out[k] = v[k];
+    for (int k = 0; k < 9; ++k) out[k] = v[k];
     return ICP_OK;
 }
 
@@ -1203,10 +1209,11 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         const std::vector<int> kd = bundle_kd_order(m_xyz, nm);
         const int nb_pad = bundle_pad(nm);
         TRY(grow(ctx, &ctx->b_kd, &ctx->b_kd_cap, nm));
-        TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, (size_t)nb_pad * 32));
-        TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, (size_t)nb_pad * 1024));
-        TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, (size_t)nb_pad * 32));
-        TRY(grow(ctx, &ctx->b_radius, &ctx->b_radius_cap, (size_t)nb_pad));
+        const size_t nbx = (size_t)nb_pad + 32; // + the null block (icp_bundle.hip)
+        TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, nbx * 32));
+        TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, nbx * 1024));
+        TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, nbx * 32));
+        TRY(grow(ctx, &ctx->b_radius, &ctx->b_radius_cap, nbx));
         HIPCHK(hipMemcpyAsync(ctx->b_kd, kd.data(), sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
         launch_build_bundle_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
                                    ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_radius, ctx->st);

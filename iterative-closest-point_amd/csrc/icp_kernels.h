@@ -121,12 +121,14 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                unsigned *audit = nullptr);
 // A split plan for `kernel` (make_plan): np queries in workgroups of queries_per_lane_block,
 // the model axis (nm rows, tiles of `tile`) split to fill >= 4 rounds of resident workgroups.
-NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel);
+NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel,
+                    int rounds = 0);
 // Bundle-bound f16 filter (icp_bundle.hip).  The model in kd order (bundle_kd_order): bundles
 // of 32 consecutive points, bundle_pad(nm) of them (whole 256-bundle LDS tiles); images built
 // once per model: bimg (1 KiB per 32 bundles), pimg (the f16 pair image in kd order, 1 KiB
 // per bundle), kd_orig (original index per kd position, nm for padding), radius (nullable,
-// per bundle, scaled units; -1 for padding).
+// per bundle, scaled units; -1 for padding), each for nb_pad + 32 bundles: the last 32 form the
+// null block, which the interleaved splits read past their last block.
 int bundle_pad(size_t nm);
 std::vector<int> bundle_kd_order(const double *m_xyz, size_t nm);
 void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,

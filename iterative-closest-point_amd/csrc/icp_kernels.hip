@@ -1903,9 +1903,9 @@ static NNPlan make_plan(size_t np, size_t nm, int tile, int q, int queries_per_l
     return pl;
 }
 
-NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel)
+NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel, int rounds)
 {
-    return make_plan(np, nm, tile, q, queries_per_lane_block, kernel);
+    return make_plan(np, nm, tile, q, queries_per_lane_block, kernel, rounds);
 }
 
 NNPlan plan_nn32(size_t np, size_t nm_pad)

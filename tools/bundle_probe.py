@@ -67,9 +67,11 @@ def main():
         if cnt:
             it = a.steps + a.warmup
             nb = (m.shape[0] + 31) // 32
-            rec["per_iteration"] = {k: v_ / it for k, v_ in cnt.items()}
-            rec["bundle_mfma_per_it"] = (p.shape[0] / 32) * nb / 32  # 32 queries x 32 bundles each
-            rec["pair_mfma_share"] = rec["per_iteration"]["pair_tests"] / (rec["bundle_mfma_per_it"] or 1)
+            rec["per_iteration"] = {k: v_ / it for k, v_ in cnt.items() if not isinstance(v_, dict)}
+            rec["us_per_wave_task"] = cnt["us_per_wave_task"]
+            pi = rec["per_iteration"]
+            rec["executed_mfma_per_it"] = pi["stream_mfma"] + pi["block_triggers"] + pi["group_tests"] + pi["pair_tests"]
+            rec["executed_tflops"] = 32768.0 * rec["executed_mfma_per_it"] / (rec["nn_kernel_ms"] * 1e-3) / 1e12
         print(json.dumps(rec), flush=True)
     names = list(runs)
     for v in names[1:]:

@@ -127,6 +127,18 @@ for s in $STEPS; do
             run bprobe8 300 python3 tools/bundle_probe.py --steps 10 --shard 8 --variants mfma16 bundle ;;
     test_bundle) run pytest_bundle 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c4c5.py -m gpu -x -v -rf \
                --timeout 300 --timeout-method thread --durations=10 -k "bundle or c4" ;;
+    bsweep) for r in 4 2 1; do
+               ICP_NN_MIN_ROUNDS=$r ICP_DEBUG_PLAN=1 run bsweep_r$r 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               ICP_NN_MIN_ROUNDS=$r ICP_DEBUG_PLAN=1 run bsweep8_r$r 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+             done
+             run bsweep2 300 python3 tools/bundle_probe.py --steps 20 --shard 2 --variants bundle &&
+             run bsweep4 300 python3 tools/bundle_probe.py --steps 20 --shard 4 --variants bundle ;;
+    bmid) for n in 16384 40000 65536 262144; do run bmid_$n 300 python3 tools/bundle_probe.py --n $n --steps 20 --variants mfma16 bundle || exit 1; done ;;
+    bgab) for g in 1 0 1 0; do
+              ICP_BUNDLE_GROUP=$g run bgab_$g 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+              ICP_BUNDLE_GROUP=$g run bgab8_$g 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+              cat $OUT/bgab_$g.log $OUT/bgab8_$g.log >> $OUT/bgab_all_$g.log
+          done ;;
     *) echo "unknown step $s" ;;
     esac
 done

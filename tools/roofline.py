@@ -102,12 +102,98 @@ def roofline(tag=None, n=1 << 20, world=1):
     return out
 
 
+# ---- the other captures: C3's one-launch registration, the grid variant's resolve ----------
+# profiles/<tag>_c3_kernel_stats.csv + <tag>_c3_pmc_traffic.json (+ <tag>_c3_stamps.log): rocprofv3
+# kernel trace and FETCH_SIZE / WRITE_SIZE passes of `tools/configs_probe.py --configs C3_horse
+# --variants auto --reps 1` (BASELINE config C3: horse_ref vs horse_tr1, 50 iterations, one launch
+# of icp_persistent_mid_kernel per registration), and its ICP_PERSIST_STAMPS=1 phase timers.
+# profiles/<tag>_grid_kernel_stats.csv + <tag>_grid_pmc_traffic.json: the same of `bench.py
+# --variant grid` at C4 (nn_grid_resolve_kernel: the seeded exact grid search of every query).
+C3_KERNEL = "icp_persistent_mid_kernel"
+C3_ITERATIONS = 50
+GRID_KERNEL = "nn_grid_resolve_kernel"
+# workgroup 0's phase timers of the one-launch kernels (icp_iter.hip persist_stamp tags): time
+# accumulated into the tag that ENDS each interval
+STAMP_PHASES = {0: "iteration turnaround", 1: "nn search", 2: "local sums + publish", 3: "grid barrier wait",
+                4: "fold of the published rows", 5: "horn solve + commit", 6: "transform + residual",
+                7: "last residual exchange"}
+
+
+def newest_config_tag(cfg):
+    tags = []
+    for f in glob.glob(os.path.join(PROFILES, f"*_{cfg}_pmc_traffic.json")):
+        tag = os.path.basename(f)[: -len(f"_{cfg}_pmc_traffic.json")]
+        if os.path.exists(os.path.join(PROFILES, f"{tag}_{cfg}_kernel_stats.csv")):
+            tags.append(tag)
+    return max(tags, key=_tag_key) if tags else None
+
+
+def stamp_phases(path):
+    """Mean per-registration time of each phase (us) over the [persist] lines of a stamps log."""
+    import re
+    runs = []
+    for line in open(path):
+        if not line.startswith("[persist] grid"):
+            continue
+        body = line.split("(calls):", 1)[1].split("|", 1)[0]
+        ph = {}
+        for tag, us, calls in re.findall(r"(\d+):([\d.]+)\((\d+)\)", body):
+            if int(calls) > 0 and int(tag) in STAMP_PHASES:
+                ph[STAMP_PHASES[int(tag)]] = float(us)
+        runs.append(ph)
+    if not runs:
+        return None
+    keys = runs[0].keys()
+    return {k: sum(r.get(k, 0.0) for r in runs) / len(runs) for k in keys}
+
+
+def config_roofline(cfg, tag=None, n=1 << 20):
+    """cfg "c3": bytes per registration of the one-launch kernel, its rate and HBM fraction, bytes
+    per iteration, the phase split; cfg "grid": the seeded grid resolve at C4 (n queries, n model
+    points) against its algorithmic bytes 28 n + 32 n."""
+    tag = tag or newest_config_tag(cfg)
+    if tag is None:
+        return None
+    times = kernel_times(os.path.join(PROFILES, f"{tag}_{cfg}_kernel_stats.csv"))
+    pmc = json.load(open(os.path.join(PROFILES, f"{tag}_{cfg}_pmc_traffic.json")))["kernels"]
+    k = C3_KERNEL if cfg == "c3" else GRID_KERNEL
+    t, p = times[k], pmc[k]
+    sec = t["avg_ms"] * 1e-3
+    b = p["traffic_bytes_per_launch"]
+    out = {"tag": tag, "kernel": k, "source": f"profiles/{tag}_{cfg}_kernel_stats.csv + profiles/{tag}_{cfg}_pmc_traffic.json",
+           "launches": t["calls"], "avg_ms": t["avg_ms"], "pmc_bytes_per_launch": b, "pmc_gbps": b / sec / 1e9,
+           "pmc_hbm_frac": b / sec / 1e9 / HBM_PEAK_GBS, "fetch_bytes": p.get("fetch_bytes_per_launch"),
+           "write_bytes": p.get("write_bytes_per_launch")}
+    if cfg == "c3":
+        out["iterations_per_launch"] = C3_ITERATIONS
+        out["pmc_bytes_per_iteration"] = b / C3_ITERATIONS
+        sp = os.path.join(PROFILES, f"{tag}_c3_stamps.log")
+        if os.path.exists(sp):
+            out["phases_us_per_registration"] = stamp_phases(sp)
+            out["phases_source"] = f"profiles/{tag}_c3_stamps.log (ICP_PERSIST_STAMPS=1, workgroup 0)"
+    else:
+        alg = 28.0 * n + 32.0 * n
+        out["algorithmic_bytes"] = alg
+        out["algorithmic_gbps"] = alg / sec / 1e9
+        out["hbm_frac"] = out["algorithmic_gbps"] / HBM_PEAK_GBS
+        out["over_fetch"] = b / alg
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag")
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--config", choices=["c4", "C3", "c3", "grid"], default="c4",
+                    help="c4: the bench's kernels; C3: the one-launch C3 registration; grid: the grid variant")
     a = ap.parse_args()
+    if a.config.lower() != "c4":
+        r = config_roofline(a.config.lower(), a.tag, a.n)
+        if r is None:
+            sys.exit(f"no profiles/<tag>_{a.config.lower()}_pmc_traffic.json + _kernel_stats.csv pair found")
+        print(json.dumps(r, indent=1))
+        return
     r = roofline(a.tag, a.n, a.world)
     if r is None:
         sys.exit("no profiles/<tag>_pmc_traffic.json + <tag>_bench_kernel_stats.csv pair found")
