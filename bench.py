@@ -170,20 +170,27 @@ def _cow_paths():
 BUNDLE_COUNT_STEPS = 3
 
 
-def bundle_roofline(n_local, n_model, t_kernel, work):
-    """The bundle filter (nn_bundle_kernel) against the f16 MFMA peak on the work it EXECUTES,
-    counted on the device (icp_set_bundle_counters): the stream's bound tests (one
-    v_mfma_f32_32x32x16_f16 = 2*32*32*16 flop per 32-bundle block per wave: 8 query groups x 32
-    bundles), one more per fired block (its re-issued stream test), the per-query bound tests on
-    the groups a fired block fired for (32 queries x 32 bundles each) and the pair tests (32
-    queries x 32 points each).  The N x M pairs the search decides are listed beside it as
+def bundle_v1():
+    """ICP_BUNDLE_KERNEL=1 selects the v1 bundle filter (nn_bundle_kernel); v2 (nn_bundle2_kernel,
+    with bundle_prep_kernel + bundle_group_kernel before it) is the default."""
+    return os.environ.get("ICP_BUNDLE_KERNEL") == "1"
+
+
+def bundle_roofline(n_local, n_model, t_kernel, work, v1=False):
+    """The bundle filter against the f16 MFMA peak on the work it EXECUTES, counted on the device
+    (icp_set_bundle_counters): the stream's group-bound tests (one v_mfma_f32_32x32x16_f16 =
+    2*32*32*16 flop per 32-bundle block per workgroup: the workgroup's 32 query groups x 32
+    bundles), the per-query bound tests on the groups a fired block fired for (32 queries x 32
+    bundles each) and the pair tests (32 queries x 32 points each); v1 also re-issued each fired
+    block's stream test.  The N x M pairs the search decides are listed beside it as
     effective_pairs_per_s; SURVEY §8d's 8 flop per pair over them is no roofline here (most pairs
     are excluded by the bounds, not evaluated)."""
     stream = work["stream_mfma"]
     fired = work["block_triggers"]
+    reissued = fired if v1 else 0.0
     fine = work["group_tests"]
     pair = work["pair_tests"]
-    executed = 32768.0 * (stream + fired + fine + pair)
+    executed = 32768.0 * (stream + reissued + fine + pair)
     ach = executed / t_kernel / 1e12
     return {"bound": "mfma", "compute_unit": "v_mfma_f32_32x32x16_f16: bound |x-c|^2-(D+r)^2 of each 32-query group "
                                              "(then of each query) against each 32-point kd bundle (hi/lo split, "
@@ -191,12 +198,12 @@ def bundle_roofline(n_local, n_model, t_kernel, work):
             "achieved": ach, "peak": PEAK_F16_MFMA_TFLOPS, "frac": ach / PEAK_F16_MFMA_TFLOPS,
             "flop_per_launch": executed,
             "flop_definition": "executed f16 MFMA work (2*32*32*16 flop per instruction), per launch: "
-                               f"{stream:.0f} stream bound tests + {fired:.0f} re-issued on fired blocks + "
+                               f"{stream:.0f} stream bound tests + {reissued:.0f} re-issued on fired blocks + "
                                f"{fine:.0f} per-query bound tests + {pair:.0f} pair tests (device counters over "
                                f"{BUNDLE_COUNT_STEPS} seeded iterations)",
             "wave_task_phases_us": work.get("us_per_wave_task"),
-            "work_per_launch": {"stream_mfma": stream, "fired_blocks": fired, "group_tests": fine,
-                                "pair_tests": pair, "pairs_evaluated": 1024.0 * pair,
+            "work_per_launch": {"stream_mfma": stream, "fired_blocks": fired, "reissued_stream_mfma": reissued,
+                                "group_tests": fine, "pair_tests": pair, "pairs_evaluated": 1024.0 * pair,
                                 "pair_share_of_n_m": 1024.0 * pair / (n_local * n_model)},
             "effective_pairs_per_s": n_local * n_model / t_kernel,
             "pairs_per_s": n_local * n_model / t_kernel}
@@ -286,7 +293,8 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
         st = ctx.stats()
     return {"iterations_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps,
             "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1), "brute_force_fallbacks": st["grid_fallback"],
-            "final_err": float(errs[-1]), "kernel": "nn_grid_resolve_kernel (seeded, every query)"}
+            "final_err": float(errs[-1]), "kernel": "nn_grid_resolve_kernel (seeded, every query)",
+            "roofline": committed_config_roofline("grid")}
 
 
 def baseline_configs(device, reps=3):
@@ -330,7 +338,24 @@ def baseline_configs(device, reps=3):
                                      "same_trajectory": bool(np.array_equal(lerrs, errs))},
                      "grid_variant": {"iterations_per_s": gres.iterations / gdt, "ms_per_registration": gdt * 1e3,
                                       "same_trajectory": bool(np.array_equal(gerrs, errs))}}
+    rf = committed_config_roofline("c3")
+    if rf is not None:
+        # the one-launch C3 registration's HBM bytes and rate from its committed rocprofv3 capture
+        # (tools/roofline.py --config C3): a measured profile of this same configuration, not of
+        # this run
+        out["C3_horse_ref_tr1"]["hbm"] = rf
     return out
+
+
+def committed_config_roofline(cfg):
+    """tools/roofline.config_roofline over the newest committed profiles/<tag>_<cfg>_* pair
+    (None when there is none; an error string when it does not parse)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import roofline as RF
+        return RF.config_roofline(cfg)
+    except Exception as e:  # a malformed profile must not break the bench line
+        return {"error": str(e)}
 
 
 def csv_io(m):
@@ -479,7 +504,8 @@ def main():
     k16 = {"plain": "nn_mfma16_kernel<seeded>", "pipe": "nn_mfma16p_kernel<seeded>",
            "unroll": "nn_mfma16x_kernel<seeded>", "r4": "nn_mfma16r_kernel<4>"}.get(
         os.environ.get("ICP_MFMA16_KERNEL", ""), "nn_mfma16r_kernel<8>")
-    kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel", "bundle": "nn_bundle_kernel"}.get(
+    kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel",
+              "bundle": "nn_bundle_kernel" if bundle_v1() else "nn_bundle2_kernel"}.get(
         level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
     if args.variant == "grid":
         # timed iterations are seeded (warm-up leaves every query a correspondence): the seeded
@@ -542,7 +568,7 @@ def main():
             "final_err": float(errs[-1]) if errs.size else None,
         }
         if level1 == "bundle" and nn_s > 0:
-            out["roofline"].update(bundle_roofline(c, args.n, nn_s, work))
+            out["roofline"].update(bundle_roofline(c, args.n, nn_s, work, v1=bundle_v1()))
         if level1 == "mfma16" and nn_s > 0:
             ex = MFMA16_FLOP_PER_PAIR * pairs / nn_s / 1e12
             out["roofline"]["mfma_pipe"] = {

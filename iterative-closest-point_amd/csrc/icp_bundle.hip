@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <type_traits>
@@ -96,7 +97,12 @@ __device__ __forceinline__ half8_t bundle_query_frag(const double a[3], double d
 // each of its queries (same margins: V^ > 0 => V > 0).  A group with a kBqForced query is
 // forced; one without in-range queries never fires.  Reductions over the 32 lanes of each half
 // (lane and lane + 32 hold the same query).  Returns this lane's operand half for its group.
-__device__ __forceinline__ half8_t bundle_group_frag(const double a[3], double dq, int mode, int h)
+struct GroupBound {
+    double g[3], D;
+    int mode;
+};
+// the group of the 32-lane half `gh` (its lanes' queries a, d', mode)
+__device__ __forceinline__ GroupBound bundle_group(const double a[3], double dq, int mode, int gh)
 {
     _Float16 hi, lo;
     double q[3];
@@ -117,8 +123,8 @@ __device__ __forceinline__ half8_t bundle_group_frag(const double a[3], double d
             hi3[k] = fmax(hi3[k], __shfl_xor(hi3[k], o, 64));
         }
     const unsigned long long forced = __ballot(mode == kBqForced), normal = __ballot(in);
-    const unsigned half_mask = h ? (unsigned)(forced >> 32) : (unsigned)forced;
-    const unsigned half_norm = h ? (unsigned)(normal >> 32) : (unsigned)normal;
+    const unsigned half_mask = gh ? (unsigned)(forced >> 32) : (unsigned)forced;
+    const unsigned half_norm = gh ? (unsigned)(normal >> 32) : (unsigned)normal;
     double g[3];
     for (int k = 0; k < 3; ++k) {
         const double c = half_norm ? 0.5 * (lo3[k] + hi3[k]) : 0.0;
@@ -134,7 +140,16 @@ __device__ __forceinline__ half8_t bundle_group_frag(const double a[3], double d
     if (gmode == kBqNormal && !(fabs(g[0]) <= kBQueryMax && fabs(g[1]) <= kBQueryMax && fabs(g[2]) <= kBQueryMax &&
                                 D <= kBSeedMax))
         gmode = kBqForced;
-    return bundle_query_frag(g, D, gmode, h);
+    GroupBound r;
+    for (int k = 0; k < 3; ++k) r.g[k] = g[k];
+    r.D = D;
+    r.mode = gmode;
+    return r;
+}
+__device__ __forceinline__ half8_t bundle_group_frag(const double a[3], double dq, int mode, int h)
+{
+    const GroupBound gb = bundle_group(a, dq, mode, h);
+    return bundle_query_frag(gb.g, gb.D, gb.mode, h);
 }
 
 // Seeded f16 filter behind the bundle bound.  Per wave 8 groups of 32 queries (256); the
@@ -571,6 +586,320 @@ __global__ __launch_bounds__(kBlock) void build_bundle_image_kernel(
     }
 }
 
+// ---- the bundle filter, v2 (the default) --------------------------------------------------
+// Per search, bundle_prep_kernel turns every query into its operands ONCE, in the filter's
+// processing order (slot s = query order[s]): the bound and pair operand halves (64 B a slot)
+// and, per 32-slot group, the group bound's operand (32 B).  The filter then reads them
+// coalesced; its v1 prologue gathered each query's coordinates, seed and seed point at random,
+// once per split (88 of 256 us per wave at C4, profiles/r03g/).
+struct BundleQuery {
+    half8_t bound[2]; // bundle_query_frag, lane halves 0 / 1
+    half8_t pair[2];  // query_frag (the seeded pair filter's operand)
+};
+
+// Query j's record goes to its slot pos[j] (reads in query order, coalesced but for the seed
+// point m4[prev[j]]; one scattered 64 B + 32 B write); threads past np fill the padding slots
+// [np, nslots) with never-firing records.  qraw[s] = (p_x, p_y, p_z, j | seed16 << 32): what the
+// certificate needs, in slot order.
+__global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, int np,
+    const int *__restrict__ pos, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx,
+    double cy, double cz, double scale, const unsigned *__restrict__ seed16, int nslots, BundleQuery *__restrict__ qop,
+    double4 *__restrict__ qraw, const int *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= nslots) return;
+    double a[3] = {0.0, 0.0, 0.0}, dq = 0.0;
+    unsigned sd = 0u;
+    int mode = kBqNever, s = t;
+    double4 raw = make_double4(0.0, 0.0, 0.0, __longlong_as_double(-1ll));
+    if (t < np) {
+        const int j = t;
+        s = pos ? pos[j] : j;
+        const double p0 = px[j], p1 = py[j], p2 = pz[j];
+        a[0] = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+        a[1] = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+        a[2] = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+        sd = seed16[j];
+        const double4 m = m4[prev[j]]; // the seed distance in the reference's arithmetic (compute.cu:112-117)
+        const double dx = p0 - m.x, dy = p1 - m.y, dz = p2 - m.z;
+        const double D = (dx * dx + dy * dy) + dz * dz;
+        const double eq = 0x1.0p-20 * ((fabs(a[0]) + fabs(a[1])) + fabs(a[2])) + 0x1.0p-22;
+        dq = (sqrt(D) * scale * (1.0 + 0x1.0p-40) + 1e-300 + eq) * (1.0 + 0x1.0p-20) + 0x1.0p-20;
+        mode = fabs(a[0]) <= kBQueryMax && fabs(a[1]) <= kBQueryMax && fabs(a[2]) <= kBQueryMax && dq <= kBSeedMax
+                   ? kBqNormal
+                   : kBqForced;
+        raw = make_double4(p0, p1, p2,
+                           __longlong_as_double((long long)(((unsigned long long)sd << 32) | (unsigned)j)));
+    }
+    BundleQuery r;
+    r.bound[0] = bundle_query_frag(a, dq, mode, 0);
+    r.bound[1] = bundle_query_frag(a, dq, mode, 1);
+    r.pair[0] = query_frag(a, 0, sd);
+    r.pair[1] = query_frag(a, 1, sd);
+    qop[s] = r;
+    qraw[s] = raw;
+}
+
+// The group bounds, one thread per slot (a 32-lane half = one group), from the slot records:
+// gop[2 g + h] = the stream operand half h of group g.  (Computed in the filter's prologue
+// instead, the fp64 shuffle chains cost ~28 us per wave task: profiles/r03k/.)
+__global__ __launch_bounds__(kBlock) void bundle_group_kernel(const BundleQuery *__restrict__ qop, int nslots,
+                                                              half8_t *__restrict__ gop, const int *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    const int s = blockIdx.x * kBlock + threadIdx.x; // (nslots: whole workgroups of slots)
+    const int lane = threadIdx.x & 63;
+    const half8_t b0 = qop[s].bound[0], b1 = qop[s].bound[1];
+    const double q[3] = {(double)b0[0] + (double)b0[1], (double)b0[3] + (double)b0[4], (double)b0[6] + (double)b0[7]};
+    const double d = (double)b1[5] + (double)b1[6];
+    const float w = (float)b1[1];
+    const int mode = w == -65504.0f ? kBqForced : w == 65504.0f ? kBqNever : kBqNormal;
+    const GroupBound gb = bundle_group(q, d * (1.0 + 0x1.0p-20) + 0x1.0p-20, mode, lane >> 5);
+    if ((lane & 31) < 2 && s < nslots) gop[(s >> 5) * 2 + (lane & 31)] = bundle_query_frag(gb.g, gb.D, gb.mode, lane & 31);
+}
+
+constexpr int kB2ListCap = 128; // LDS entries of a wave's fired-block list (then global)
+
+// The filter proper.  A workgroup = 4 waves x QG groups of 32 slots; wave w owns groups
+// w QG .. (w+1) QG - 1 (their bound / pair operands and (best, second, position) in its
+// registers).  The stream tests each of the split's 32-bundle blocks ONCE per workgroup, in the
+// wave (k mod 4) that streams it: one MFMA of the block's 32 bundles against the workgroup's
+// 4 QG group bounds (columns; QG = 4 leaves 16 never-firing), operands straight from L2 four
+// blocks ahead -- no LDS tile, no barrier.  A block that fires for some group is appended to the
+// owning waves' lists (LDS, spilling to `glist`); after one barrier each wave runs its list:
+// per-query bounds of the fired groups, then the pair tests (v1's update).  Partials are
+// written in slot order (nn_finalize_mfma16_kernel reads them through `order`).
+template <int QG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_bundle2_kernel(
+    const BundleQuery *__restrict__ qop, const half8_t *__restrict__ gop, int np, const half8_t *__restrict__ bimg,
+    int nb_pad, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int *__restrict__ glist,
+    float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx,
+    const int *__restrict__ stop, unsigned long long *__restrict__ counters)
+{
+    if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
+    constexpr int NG = 4 * QG; // groups per workgroup (<= 32: the stream MFMA's columns)
+    static_assert(NG <= 32, "one stream MFMA column per group");
+    __shared__ int s_cnt[4];
+    __shared__ int s_list[4][kB2ListCap];
+    __shared__ half8_t s_bq[4][QG][64]; // the pair operands (read by the fired-block updates only)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = lane >> 5, col = lane & 31;
+    const int split = blockIdx.y, S = gridDim.y;
+    const int nbb = nb_pad >> 5;
+    const int nk = (nbb - split + S - 1) / S, nkmax = (nbb + S - 1) / S;
+    auto gblock = [&](int k) { const int g = split + S * k; return g < nbb ? g : nbb; };
+    int *const gl = glist + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 * nkmax;
+    unsigned n_blocks = 0, n_groups = 0, n_pairs = 0;
+    const unsigned long long t_start = counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long t_pro = 0, t_stream = 0, t_defer = 0;
+    if (tid < 4) s_cnt[tid] = 0;
+
+    const int grp0 = blockIdx.x * NG; // this workgroup's first group
+    half8_t bb[QG];
+    float best[QG], second[QG];
+    int bpos[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const size_t slot = (size_t)(grp0 + wave * QG + q) * 32 + col;
+        bb[q] = qop[slot].bound[h];
+        s_bq[wave][q][lane] = qop[slot].pair[h];
+        best[q] = 0.0f; // seeded: "nothing below s0'"
+        second[q] = 0.0f;
+        bpos[q] = -1;
+    }
+    const f32x16_t zero = {};
+    __syncthreads(); // (s_cnt, s_bq)
+    half8_t gopB; // stream operand: column = group grp0 + col (columns past NG never fire)
+    if (col < NG) {
+        gopB = gop[(size_t)(grp0 + col) * 2 + h];
+    } else {
+        const double z[3] = {0.0, 0.0, 0.0};
+        gopB = bundle_query_frag(z, 0.0, kBqNever, h);
+    }
+    if (counters) {
+        __builtin_amdgcn_s_waitcnt(0);
+        t_pro = __builtin_amdgcn_s_memrealtime();
+    }
+
+    // ---- stream: blocks k = wave, wave + 4, ... of this split, four loads ahead
+    auto fire = [&](int k, const f32x16_t &d) {
+        const unsigned long long f = __ballot(min16v(d) <= 0.0f);
+        const unsigned gm = (unsigned)(f | (f >> 32));
+        if (__builtin_expect(gm != 0u, 0)) { // (uniform)
+            const int g = gblock(k);
+#pragma unroll
+            for (int w2 = 0; w2 < 4; ++w2) {
+                const unsigned m8 = (gm >> (QG * w2)) & ((1u << QG) - 1u);
+                if (!m8) continue;
+                int e = 0;
+                if (lane == 0) e = atomicAdd(&s_cnt[w2], 1);
+                e = __shfl(e, 0, 64);
+                const int v = g | (int)(m8 << 24);
+                if (lane == 0) {
+                    if (e < kB2ListCap) s_list[w2][e] = v;
+                    else gl[w2 * nkmax + (e - kB2ListCap)] = v;
+                }
+            }
+        }
+    };
+    {
+        constexpr int U = 4;
+        half8_t cur[U], nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = bimg[(size_t)gblock(wave + 4 * u) * 64 + lane];
+        for (int k0 = wave; k0 < nk; k0 += 4 * U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = bimg[(size_t)gblock(k0 + 4 * (U + u)) * 64 + lane];
+            f32x16_t d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[u], gopB, zero, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k0 + 4 * u < nk) fire(k0 + 4 * u, d[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+    }
+    __syncthreads(); // every wave's appends are in
+    if (counters) t_stream = __builtin_amdgcn_s_memrealtime();
+
+    // ---- this wave's fired blocks: per-query bounds of the fired groups, then the pair tests
+    auto pair_update = [&](int q, const f32x16_t &dd, int blk) {
+        const float mn = min16v(dd);
+        if (!__any(mn < second[q])) return;
+        if (__any(mn < best[q])) {
+            int row = 0;
+#pragma unroll
+            for (int r = 15; r >= 0; --r)
+                row = dd[r] == mn ? (r & 3) + 8 * (r >> 2) : row;
+            bpos[q] = mn < best[q] ? blk * 32 + 4 * h + row : bpos[q];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], dd[r]);
+            best[q] = fminf(best[q], dd[r]);
+        }
+    };
+    auto update = [&](const half8_t &a8, int bblock, unsigned gfire) {
+        ++n_blocks;
+        n_groups += __builtin_popcount(gfire);
+        unsigned gm[QG], uni = 0u;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            gm[q] = 0u;
+            if (!((gfire >> q) & 1u)) continue;
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bb[q], zero, 0, 0, 0);
+            unsigned mask = 0u;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const unsigned long long bl = __ballot(d[r] <= 0.0f);
+                const int row = (r & 3) + 8 * (r >> 2);
+                mask |= ((unsigned)bl != 0u ? 1u << row : 0u) | ((unsigned)(bl >> 32) != 0u ? 1u << (row + 4) : 0u);
+            }
+            gm[q] = mask;
+            uni |= mask;
+            n_pairs += __builtin_popcount(mask);
+        }
+        while (uni) {
+            int bs[4];
+            half8_t ap[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                bs[k] = uni ? __builtin_ctz(uni) : -1;
+                uni &= uni - 1u;
+                if (bs[k] >= 0) ap[k] = pimg[((size_t)bblock * 32 + bs[k]) * 64 + lane];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (bs[k] < 0) break;
+#pragma unroll
+                for (int q = 0; q < QG; ++q) {
+                    if (!((gm[q] >> bs[k]) & 1u)) continue;
+                    const f32x16_t dd =
+                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ap[k], s_bq[wave][q][lane], zero, 0, 0, 0);
+                    pair_update(q, dd, bblock * 32 + bs[k]);
+                }
+            }
+        }
+    };
+    {
+        const int n = s_cnt[wave];
+        auto entry = [&](int e) {
+            return __builtin_amdgcn_readfirstlane(e < kB2ListCap ? s_list[wave][e] : gl[wave * nkmax + (e - kB2ListCap)]);
+        };
+        if (n) { // the next entry's bound operands load while this one is tested
+            int v = entry(0);
+            half8_t a8 = bimg[(size_t)(v & 0xffffff) * 64 + lane];
+            for (int e = 0; e < n; ++e) {
+                const int vn = entry(e + 1 < n ? e + 1 : e);
+                const half8_t an = bimg[(size_t)(vn & 0xffffff) * 64 + lane];
+                update(a8, v & 0xffffff, (unsigned)v >> 24);
+                a8 = an;
+                v = vn;
+            }
+        }
+    }
+    if (counters) {
+        __builtin_amdgcn_s_waitcnt(0);
+        t_defer = __builtin_amdgcn_s_memrealtime();
+    }
+    // (counters: this wave task's own row of 9, accumulated over launches without atomics --
+    // a same-address atomic per wave serialised and tripled the launch)
+    unsigned long long *crow =
+        counters ? counters + 9 * ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) : nullptr;
+    if (crow && lane == 0) {
+        crow[0] += n_blocks;
+        crow[1] += n_groups;
+        crow[2] += n_pairs;
+        crow[3] += t_pro - t_start;
+        crow[4] += t_stream - t_pro;
+        crow[5] += t_defer - t_stream;
+        crow[7] += 1ull;
+        crow[8] += (unsigned long long)((nk - wave + 3) / 4); // stream MFMAs of this wave
+    }
+    // the two lane halves' (best, second, position) per query, then all QG original indices
+    // gathered at once (one dependent load per wave, not one per group)
+    float eb[QG], es[QG];
+    int eo[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        float bb2 = best[q], ss = second[q];
+        int id = bb2 < 0.0f ? bpos[q] : -1; // (a tie of two rows: second == best, never certified)
+        const float ob = __shfl_xor(bb2, 32, 64), os = __shfl_xor(ss, 32, 64);
+        const int oi = __shfl_xor(id, 32, 64);
+        if (ob < bb2) {
+            ss = fminf(bb2, os);
+            bb2 = ob;
+            id = oi;
+        } else {
+            ss = fminf(ss, ob);
+            if (ob == bb2 && oi >= 0 && (id < 0 || oi < id)) id = oi;
+        }
+        eb[q] = bb2;
+        es[q] = ss;
+        eo[q] = id;
+    }
+#pragma unroll
+    for (int q = 0; q < QG; ++q) eo[q] = eo[q] >= 0 ? kd_orig[eo[q]] : -1;
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const int slot = (grp0 + wave * QG + q) * 32 + col;
+        if (h == 0 && slot < np) { // slot order (coalesced)
+            const size_t o = (size_t)split * np + slot;
+            part_best[o] = eb[q];
+            part_second[o] = es[q];
+            part_idx[o] = eo[q];
+        }
+    }
+    if (crow) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) crow[6] += t_end - t_defer;
+    }
+}
+
 } // namespace
 
 int bundle_pad(size_t nm) // bundles, padded to whole LDS tiles
@@ -666,6 +995,94 @@ NNPlan plan_nn_bundle(size_t np, int nb_pad)
                              1);
     pl.kernel = 100;
     return pl;
+}
+
+// ---- v2 launchers ---------------------------------------------------------------------------
+static int bundle2_qg() // 32-slot groups per wave: ICP_BUNDLE_QG = 4 | 8 (A/B)
+{
+    static const int qg = [] {
+        const char *e = getenv("ICP_BUNDLE_QG");
+        return e && atoi(e) == 4 ? 4 : 8;
+    }();
+    return qg;
+}
+
+static bool bundle_v1() // ICP_BUNDLE_KERNEL=1: the v1 filter (A/B)
+{
+    static const bool v1 = [] {
+        const char *e = getenv("ICP_BUNDLE_KERNEL");
+        return e && atoi(e) == 1;
+    }();
+    return v1;
+}
+
+bool bundle_v2() { return !bundle_v1(); }
+
+// Splits: about 8,192 workgroups, at least 42 blocks of the model per split.  The per-query
+// work (operands, partials) is paid once per split, but fewer, longer workgroups leave the
+// fired-block deferred phases unbalanced: at C4 (1,024 query workgroups) 1 / 3 / 8 / 16 splits
+// ran the filter in 0.875 / 0.440 / 0.361 / 0.421 ms, at the W = 8 shard (128) 6 / 24 / 32 / 48
+// in 0.174 / 0.122 / 0.149 / 0.153 ms (profiles/r03l/, r03n/).  ICP_BUNDLE_SPLITS overrides (A/B).
+constexpr int kB2TargetWG = 8192;
+constexpr int kB2MinBlocksPerSplit = 42;
+
+NNPlan plan_nn_bundle2(size_t np, int nb_pad)
+{
+    const int qg = bundle2_qg();
+    NNPlan pl;
+    pl.q_per_lane = qg;
+    pl.qblocks = (int)std::max<size_t>(1, (np + 4 * qg * 32 - 1) / (4 * qg * 32));
+    const int nbb = nb_pad >> 5;
+    static const int forced = [] {
+        const char *e = getenv("ICP_BUNDLE_SPLITS");
+        return e ? atoi(e) : 0;
+    }();
+    pl.splits = forced > 0 ? forced
+                           : std::min((kB2TargetWG + pl.qblocks - 1) / pl.qblocks, nbb / kB2MinBlocksPerSplit);
+    pl.splits = std::max(1, std::min(pl.splits, nbb));
+    pl.chunk = 0;
+    pl.kernel = 200;
+    if (getenv("ICP_DEBUG_PLAN"))
+        fprintf(stderr, "[plan bundle2] np=%zu nbb=%d qg=%d qblocks=%d splits=%d\n", np, nbb, qg, pl.qblocks, pl.splits);
+    return pl;
+}
+
+size_t bundle2_slots(const NNPlan &pl) { return (size_t)pl.qblocks * 4 * pl.q_per_lane * 32; }
+
+size_t bundle2_list_ints(const NNPlan &pl, int nb_pad)
+{
+    const int nbb = nb_pad >> 5;
+    return (size_t)pl.qblocks * pl.splits * 4 * ((nbb + pl.splits - 1) / pl.splits);
+}
+
+void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
+                        const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
+                        size_t nslots, void *qop, double4 *qraw, hipStream_t st, const int *stop)
+{
+    bundle_prep_kernel<<<(int)((nslots + kBlock - 1) / kBlock), kBlock, 0, st>>>(
+        px, py, pz, np, pos, prev, m4, c[0], c[1], c[2], scale, seed16, (int)nslots, (BundleQuery *)qop, qraw, stop);
+}
+
+size_t bundle2_counter_rows(const NNPlan &pl) { return (size_t)pl.qblocks * pl.splits * 4; }
+
+void launch_bundle_groups(const void *qop, size_t nslots, void *gop, hipStream_t st, const int *stop)
+{
+    bundle_group_kernel<<<(int)(nslots / kBlock), kBlock, 0, st>>>((const BundleQuery *)qop, (int)nslots,
+                                                                   (half8_t *)gop, stop);
+}
+
+void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const void *pimg,
+                       const int *kd_orig, int *glist, const NNPlan &pl, float *part_best, float *part_second,
+                       int *part_idx, hipStream_t st, const int *stop, unsigned long long *counters)
+{
+    dim3 grid(pl.qblocks, pl.splits);
+#define LAUNCHB2(QG)                                                                                          \
+    nn_bundle2_kernel<QG><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,             \
+                                             (const half8_t *)bimg, nb_pad, (const half8_t *)pimg, kd_orig, glist, \
+                                             part_best, part_second, part_idx, stop, counters)
+    if (pl.q_per_lane == 4) LAUNCHB2(4);
+    else LAUNCHB2(8);
+#undef LAUNCHB2
 }
 
 void launch_nn_bundle(const double *px, const double *py, const double *pz, int np, const int *order,

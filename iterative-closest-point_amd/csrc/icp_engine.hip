@@ -274,11 +274,17 @@ struct icp_ctx {
     int nb_pad = 0;                           // bundles (whole LDS tiles)
     size_t b_img_cap = 0, b_pimg_cap = 0, b_kd_orig_cap = 0, b_radius_cap = 0, b_kd_cap = 0;
     int *q_order = nullptr;                   // the bundle filter's query order (launch_query_order)
+    int *q_pos = nullptr;                     // its inverse (query j's slot)
+    size_t q_pos_cap = 0;
     char *q_order_tmp = nullptr;
     size_t q_order_cap = 0, q_order_tmp_cap = 0;
     const double *q_order_src = nullptr;      // the cloud q_order was computed for (its x array)
     size_t q_order_n = 0;
     unsigned long long *b_counters = nullptr; // icp_set_bundle_counters: the filter's executed work
+    char *b_qop = nullptr, *b_gop = nullptr;  // v2: per-slot query operands, per-group bounds
+    double4 *b_qraw = nullptr;                // v2: per-slot query coordinates, index, seed
+    int *b_glist = nullptr;                   // v2: fired-block list overflow
+    size_t b_qop_cap = 0, b_gop_cap = 0, b_qraw_cap = 0, b_glist_cap = 0, b_counters_rows = 0;
 
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     icp_stats stats{};
@@ -568,10 +574,11 @@ int query_order(icp_ctx *ctx, const DevCloud &q, size_t n, const int **order)
     if (off) return ICP_OK;
     if (ctx->q_order_src != q.x || ctx->q_order_n != n) {
         TRY(grow(ctx, &ctx->q_order, &ctx->q_order_cap, n));
+        TRY(grow(ctx, &ctx->q_pos, &ctx->q_pos_cap, n));
         const size_t bytes = query_order_scratch_bytes((int)n);
         TRY(grow(ctx, &ctx->q_order_tmp, &ctx->q_order_tmp_cap, bytes));
         if (launch_query_order(q.x, q.y, q.z, (int)n, ctx->m_lo, ctx->m_hi, ctx->q_order_tmp, bytes, ctx->q_order,
-                               ctx->st) != 0)
+                               ctx->st, ctx->q_pos) != 0)
             return fail(ctx, ICP_E_HIP, "query_order: radix sort failed");
         LAUNCHCHK("query_order");
         ctx->q_order_src = q.x;
@@ -644,7 +651,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             seeds_ready = false; // the seeds come from these candidates, below
         }
         const bool sd = (seeded || gseed) && l1 >= 2;
-        const NNPlan pl = l1 == 3   ? plan_nn_bundle(n, ctx->nb_pad)
+        const bool v2 = l1 == 3 && bundle_v2();
+        const NNPlan pl = l1 == 3   ? (v2 ? plan_nn_bundle2(n, ctx->nb_pad) : plan_nn_bundle(n, ctx->nb_pad))
                           : l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd)
                                     : plan_nn_mfma(n, ctx->nm_pad);
         if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
@@ -664,8 +672,29 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         const int *order = nullptr;
         if (l1 == 3) TRY(query_order(ctx, q, n, &order));
+        if (v2) { // every query's operands, once, in the filter's slot order
+            const size_t nslots = bundle2_slots(pl);
+            TRY(grow(ctx, &ctx->b_qop, &ctx->b_qop_cap, nslots * 64));
+            TRY(grow(ctx, &ctx->b_qraw, &ctx->b_qraw_cap, nslots));
+            TRY(grow(ctx, &ctx->b_gop, &ctx->b_gop_cap, nslots));
+            TRY(grow(ctx, &ctx->b_glist, &ctx->b_glist_cap, bundle2_list_ints(pl, ctx->nb_pad)));
+            if (ctx->b_counters && ctx->b_counters_rows < bundle2_counter_rows(pl)) { // (per-wave rows)
+                HIPCHK(hipFree(ctx->b_counters));
+                ctx->b_counters = nullptr;
+                ctx->b_counters_rows = bundle2_counter_rows(pl);
+                HIPCHK(hipMalloc((void **)&ctx->b_counters, sizeof(unsigned long long) * 9 * ctx->b_counters_rows));
+                HIPCHK(hipMemsetAsync(ctx->b_counters, 0, sizeof(unsigned long long) * 9 * ctx->b_counters_rows,
+                                      ctx->st));
+            }
+            launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4, ctx->c,
+                               ctx->scale16, seeds, nslots, ctx->b_qop, ctx->b_qraw, ctx->st, stop);
+            launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->st, stop);
+        }
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
-        if (l1 == 3)
+        if (v2)
+            launch_nn_bundle2(ctx->b_qop, ctx->b_gop, (int)n, ctx->b_img, ctx->nb_pad, ctx->b_pimg, ctx->b_kd_orig, ctx->b_glist, pl,
+                              pb, ps, pi, ctx->st, stop, ctx->b_counters);
+        else if (l1 == 3)
             launch_nn_bundle(q.x, q.y, q.z, (int)n, order, ctx->idx, ctx->m4, ctx->c, ctx->scale16, seeds, ctx->b_img,
                              ctx->nb_pad, ctx->b_pimg, ctx->b_kd_orig, (int)ctx->nm, pl, pb, ps, pi, ctx->st, stop,
                              ctx->b_counters);
@@ -678,7 +707,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (l1 >= 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
-                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit);
+                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit, v2 ? ctx->b_qraw : nullptr);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
@@ -993,24 +1022,34 @@ int icp_set_bundle_counters(icp_ctx *ctx, int enable)
     if (!enable) {
         if (ctx->b_counters) HIPCHK(hipFree(ctx->b_counters));
         ctx->b_counters = nullptr;
+        ctx->b_counters_rows = 0;
         return ICP_OK;
     }
-    if (!ctx->b_counters) HIPCHK(hipMalloc((void **)&ctx->b_counters, 9 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, 9 * sizeof(unsigned long long), ctx->st));
+    // (rows: one for v1's shared counters, per wave task for v2; sized at the next search)
+    if (!ctx->b_counters) {
+        ctx->b_counters_rows = 1;
+        HIPCHK(hipMalloc((void **)&ctx->b_counters, 9 * sizeof(unsigned long long)));
+    }
+    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, 9 * sizeof(unsigned long long) * ctx->b_counters_rows, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
 }
 
-int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[9])
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[10])
 {
     if (!ctx || !out) return ICP_E_ARG;
-    for (int k = 0; k < 9; ++k) out[k] = 0;
+    for (int k = 0; k < 10; ++k) out[k] = 0;
     if (!ctx->b_counters) return ICP_OK;
     HIPCHK(hipSetDevice(ctx->device));
-    unsigned long long v[9] = {};
-    HIPCHK(hipMemcpyAsync(v, ctx->b_counters, sizeof(v), hipMemcpyDeviceToHost, ctx->st));
+    std::vector<unsigned long long> v(9 * ctx->b_counters_rows);
+    HIPCHK(hipMemcpyAsync(v.data(), ctx->b_counters, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost,
+                          ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
-    for (int k = 0; k < 9; ++k) out[k] = v[k];
+    for (size_t r = 0; r < ctx->b_counters_rows; ++r) {
+        for (int k = 0; k < 9; ++k) out[k] += v[9 * r + k];
+        const uint64_t t = v[9 * r + 3] + v[9 * r + 4] + v[9 * r + 5] + v[9 * r + 6];
+        out[9] = std::max<uint64_t>(out[9], t); // the slowest wave task's clock ticks
+    }
     return ICP_OK;
 }
 
@@ -1049,7 +1088,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
                     (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->b_img, (void *)ctx->b_pimg, (void *)ctx->b_kd_orig,
-                    (void *)ctx->b_radius, (void *)ctx->b_kd, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters, (void *)ctx->cr_entries,
+                    (void *)ctx->b_radius, (void *)ctx->b_kd, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters,
+                    (void *)ctx->b_qop, (void *)ctx->b_gop, (void *)ctx->b_qraw, (void *)ctx->b_glist, (void *)ctx->q_pos, (void *)ctx->cr_entries,
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt})
         if (p) (void)hipFree(p);

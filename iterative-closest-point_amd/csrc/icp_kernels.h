@@ -118,7 +118,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop = nullptr, const double4 *m4 = nullptr,
-                               unsigned *audit = nullptr);
+                               unsigned *audit = nullptr, const double4 *qraw = nullptr);
 // A split plan for `kernel` (make_plan): np queries in workgroups of queries_per_lane_block,
 // the model axis (nm rows, tiles of `tile`) split to fill >= 4 rounds of resident workgroups.
 NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel,
@@ -145,11 +145,32 @@ void launch_nn_bundle(const double *px, const double *py, const double *pz, int 
                       unsigned long long *counters = nullptr);
 // counters (nullable) += per launch: (32-bundle blocks whose joint test fired, per wave; groups
 // with a bundle V^ <= 0 in such a block; pair tests run = (group, bundle) pairs)
+// v2 (the default; bundle_v2(), ICP_BUNDLE_KERNEL=1 runs v1): bundle_prep_kernel writes every
+// query's operands once per search to its slot pos[j] (qop: 64 B per slot, qraw: its
+// coordinates, index and seed; bundle2_slots(plan) slots), then nn_bundle2_kernel streams the
+// blocks barrier-free; glist: bundle2_list_ints(plan, nb_pad) ints of fired-block list overflow;
+// counters (nullable): 9 x bundle2_counter_rows(plan) per-wave rows.  Partials in slot order:
+// finalize with launch_nn_finalize_mfma16(..., qraw).
+bool bundle_v2();
+NNPlan plan_nn_bundle2(size_t np, int nb_pad);
+size_t bundle2_slots(const NNPlan &pl);
+size_t bundle2_list_ints(const NNPlan &pl, int nb_pad);
+size_t bundle2_counter_rows(const NNPlan &pl);
+void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
+                        const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
+                        size_t nslots, void *qop, double4 *qraw, hipStream_t st, const int *stop = nullptr);
+// gop (nslots bytes): the 32-slot groups' bounds from the records (after the prep)
+void launch_bundle_groups(const void *qop, size_t nslots, void *gop, hipStream_t st, const int *stop = nullptr);
+void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const void *pimg,
+                       const int *kd_orig, int *glist, const NNPlan &pl, float *part_best, float *part_second,
+                       int *part_idx, hipStream_t st, const int *stop = nullptr, unsigned long long *counters = nullptr);
 // order[k] = the query processed k-th: the queries sorted by the Morton code of their cell in a
-// 1024^3 grid over the box [lo, hi] (icp_order.hip); scratch: query_order_scratch_bytes(n)
+// 1024^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
+// = k); scratch: query_order_scratch_bytes(n)
 size_t query_order_scratch_bytes(int n);
 int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
-                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st);
+                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st,
+                       int *pos = nullptr);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,

@@ -1214,24 +1214,44 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const double *__restrict__ py, const double *__restrict__ pz, int np, int nm, double cx,
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint,
-    const int *__restrict__ stop, const double4 *__restrict__ m4, unsigned *__restrict__ audit)
+    const int *__restrict__ stop, const double4 *__restrict__ m4, unsigned *__restrict__ audit,
+    const double4 *__restrict__ qraw)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
-    const int j = blockIdx.x * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
-    const bool valid = j < np; // no early exit: block_append is workgroup-wide
-    const int jj = valid ? j : 0;
+    // qraw (the bundle filter): the partials are in the filter's slot order, and slot s's query
+    // (coordinates, index j, seed) is qraw[s] -- read in order, no gather
+    const int s = blockIdx.x * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
+    const bool valid = s < np; // no early exit: block_append is workgroup-wide
+    double q0, q1, q2;
+    unsigned sdq = 0u;
+    int j = s;
+    if (qraw) {
+        const double4 r = qraw[valid ? s : 0];
+        const unsigned long long w = (unsigned long long)__double_as_longlong(r.w);
+        q0 = r.x;
+        q1 = r.y;
+        q2 = r.z;
+        j = (int)(unsigned)(w & 0xffffffffull);
+        sdq = (unsigned)(w >> 32);
+    } else {
+        const int jj = valid ? j : 0;
+        q0 = px[jj];
+        q1 = py[jj];
+        q2 = pz[jj];
+        if (SEEDED) sdq = seed16[jj];
+    }
     float b = 0.0f, s2 = 0.0f;
     int id = -1;
-    if (valid) merge_splits_group<G>(part_best, part_second, part_idx, splits, np, j, sub, b, s2, id);
+    if (valid) merge_splits_group<G>(part_best, part_second, part_idx, splits, np, s, sub, b, s2, id);
     if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
-    const double ax = (px[jj] - cx) * scale, ay = (py[jj] - cy) * scale, az = (pz[jj] - cz) * scale;
+    const double ax = (q0 - cx) * scale, ay = (q1 - cy) * scale, az = (q2 - cz) * scale;
     bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
               fabs(az) <= kF16QueryClamp;
     if (ok) {
         const double u = 0x1.0p-24;
         const double a2 = ax * ax + ay * ay + az * az;
         const double A = sqrt(a2);
-        const double sh = SEEDED ? seed_shift(seed16[jj]) : 0.0;
+        const double sh = SEEDED ? seed_shift(sdq) : 0.0;
         auto delta = [&](double R) {
             return SEEDED ? 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * fabs(sh) + 4.0 * u * (A + R) + 1e-3
                           : 26.0 * u * R * R + 60.0 * u * A * R + 4.0 * u * (A + R) + 1e-3;
@@ -2094,7 +2114,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
-                               hipStream_t st, const int *stop, const double4 *m4, unsigned *audit)
+                               hipStream_t st, const int *stop, const double4 *m4, unsigned *audit,
+                               const double4 *qraw)
 {
     // (its fp64 certificate is heavy and every lane of a group repeats it: lanes only pay off
     // for very many splits; ICP_FIN16_LANES = 1 | 4 | 8 overrides, for experiments)
@@ -2107,7 +2128,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
 #define FIN16(SD, G)                                                                                         \
     nn_finalize_mfma16_kernel<SD, G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
                                                               pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
-                                                              idx, amb_count, amb_list, amb_hint, stop, m4, audit)
+                                                              idx, amb_count, amb_list, amb_hint, stop, m4, audit, \
+                                                              qraw)
     if (seed16) {
         if (g == 8) FIN16(true, 8); else if (g == 4) FIN16(true, 4); else FIN16(true, 1);
     } else {

@@ -87,7 +87,7 @@ size_t query_order_scratch_bytes(int n)
 }
 
 int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
-                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st)
+                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st, int *pos)
 {
     OrderBox bx;
     for (int k = 0; k < 3; ++k) {
@@ -99,10 +99,10 @@ int launch_query_order(const double *px, const double *py, const double *pz, int
     void *temp = v0 + n;
     size_t temp_bytes = bytes - 3 * (size_t)n * sizeof(int);
     query_keys_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(px, py, pz, n, bx, k0, v0);
-    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, order, n, 0, kQueryOrderBits, st) ==
-                   hipSuccess
-               ? 0
-               : -1;
+    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, order, n, 0, kQueryOrderBits, st) != hipSuccess)
+        return -1;
+    if (pos) order_pos_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(order, n, pos);
+    return 0;
 }
 
 size_t mid_order_scratch_bytes(int n)

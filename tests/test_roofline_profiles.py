@@ -58,12 +58,15 @@ def test_frac_matches_the_kernels_work_over_f16_peak():
     r = d["roofline"]
     pairs = d["config"]["n_model"] * d["config"]["n_scene"]
     t = r["avg_launch_ms"] * 1e-3
-    if r["kernel"] == "nn_bundle_kernel":
-        # the bundle filter: executed f16 MFMA work (stream bound tests, re-issued fired blocks,
-        # per-query bound tests, pair tests: 2*32*32*16 flop each, device-counted) over the launch;
-        # the N x M pairs it decides, separately
+    if r["kernel"] in ("nn_bundle_kernel", "nn_bundle2_kernel"):
+        # the bundle filter: executed f16 MFMA work (stream bound tests, v1's re-issued fired
+        # blocks, per-query bound tests, pair tests: 2*32*32*16 flop each, device-counted) over
+        # the launch; the N x M pairs it decides, separately
         w = r["work_per_launch"]
-        executed = 32768.0 * (w["stream_mfma"] + w["fired_blocks"] + w["group_tests"] + w["pair_tests"])
+        reissued = w.get("reissued_stream_mfma", w["fired_blocks"])  # (v1 lines predate the field)
+        if r["kernel"] == "nn_bundle2_kernel":
+            assert reissued == 0.0
+        executed = 32768.0 * (w["stream_mfma"] + reissued + w["group_tests"] + w["pair_tests"])
         assert r["flop_per_launch"] == pytest.approx(executed, rel=1e-12)
         assert r["achieved"] == pytest.approx(executed / t / 1e12, rel=1e-9)
         assert r["peak"] == 2500.0 and r["frac"] == pytest.approx(r["achieved"] / 2500.0, rel=1e-9)

@@ -50,6 +50,10 @@ for s in $STEPS; do
                run sq2_$v 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INST_CYCLES_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE \
                    --output-format csv -d "$OUT/sq2_$v" -o sq -- python3 tools/nn_probe.py --variant $v --reps 1
            done ;;
+    sqb)   run sqb1 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE \
+               --output-format csv -d "$OUT/sqb1" -o sq -- python3 tools/bundle_probe.py --steps 5 --variants bundle &&
+           run sqb2 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INST_CYCLES_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE \
+               --output-format csv -d "$OUT/sqb2" -o sq -- python3 tools/bundle_probe.py --steps 5 --variants bundle ;;
     probe) for v in mfma16 mfma valu; do run probe_$v 300 python3 tools/nn_probe.py --variant $v; done ;;
     abpipe) for ld in plain pipe unroll r4 r8; do ICP_MFMA16_KERNEL=$ld run abp_${ld} 300 python3 tools/nn_probe.py --variant mfma16 --icp 12; done ;;
     test16k) for ld in ${K16:-unroll r4}; do
@@ -139,6 +143,37 @@ for s in $STEPS; do
               ICP_BUNDLE_GROUP=$g run bgab8_$g 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
               cat $OUT/bgab_$g.log $OUT/bgab8_$g.log >> $OUT/bgab_all_$g.log
           done ;;
+    bv2) for cfg in "ICP_BUNDLE_KERNEL=2 ICP_BUNDLE_QG=8" "ICP_BUNDLE_KERNEL=2 ICP_BUNDLE_QG=4" "ICP_BUNDLE_KERNEL=1" "ICP_BUNDLE_KERNEL=2 ICP_BUNDLE_QG=8"; do
+             tag=$(echo $cfg | tr -d ' =_' | tr 'A-Z' 'a-z')
+             env $cfg timeout -k 10 300 python3 tools/bundle_probe.py --steps 20 --variants bundle >> $OUT/bv2_$tag.log 2>&1 || exit 1
+             env $cfg timeout -k 10 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle >> $OUT/bv2_$tag.log 2>&1 || exit 1
+             env $cfg timeout -k 10 300 python3 tools/bundle_probe.py --n 8388608 --shard 8 --steps 5 --warmup 1 --variants bundle >> $OUT/bv2_$tag.log 2>&1 || exit 1
+             echo "== bv2 $cfg done" | tee -a $OUT/steps.log
+           done ;;
+    bprof) run bprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bprof" -o c4 -- \
+               python3 tools/bundle_probe.py --steps 20 --variants bundle &&
+           run bprof8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bprof8" -o s8 -- \
+               python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle ;;
+    bsplit) for sp in 1 2 3 4 6 8; do
+               ICP_BUNDLE_SPLITS=$sp run bsplit_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             done
+             for sp in 6 12 18 24; do
+               ICP_BUNDLE_SPLITS=$sp run bsplit8_$sp 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+             done
+             for sp in 2 3 4; do
+               ICP_BUNDLE_QG=4 ICP_BUNDLE_SPLITS=$sp run bsplitq4_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             done ;;
+    bsplit2) run bdef 300 python3 tools/bundle_probe.py --steps 20 --variants bundle mfma16 || exit 1
+             run bdef8 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+             for sp in 6 12 16; do
+               ICP_BUNDLE_SPLITS=$sp run bsplit_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             done
+             for sp in 24 48; do
+               ICP_BUNDLE_SPLITS=$sp run bsplit8_$sp 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+             done
+             for sp in 8 16; do
+               ICP_BUNDLE_QG=4 ICP_BUNDLE_SPLITS=$sp run bsplitq4_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             done ;;
     *) echo "unknown step $s" ;;
     esac
 done
