@@ -526,15 +526,17 @@ __global__ __launch_bounds__(kBlock) void build_pair_image_kd_kernel(
 // 32-bundle block holds slots 8h..8h+7: -2cx hi, hi, lo, -2cy hi, hi, lo, -2cz hi, hi |
 // -2cz lo, 4096, 4096, W hi, W lo, -2r hi, hi, lo with W = (|c^|^2 - r'^2 - mu_c) / 4096.
 // Padding bundles (no real point): W = +65504 (V^ > 0 for every in-range query).
+// bctr[b] = (c^, r') in scaled units for the block bounds: r' = -1 for a padding bundle, +inf
+// for one the image always searches.
 __global__ __launch_bounds__(kBlock) void build_bundle_image_kernel(
     const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz, int nm,
     const int *__restrict__ kd, int nb_pad, double cx, double cy, double cz, double scale,
-    half8_t *__restrict__ img, float *__restrict__ radius)
+    half8_t *__restrict__ img, double4 *__restrict__ bctr)
 {
     for (int b = blockIdx.x * kBlock + threadIdx.x; b < nb_pad + 32; b += gridDim.x * kBlock) {
         half8_t lo8 = {}, hi8 = {};
         const int k0 = b * kBundle, k1 = min(k0 + kBundle, nm);
-        float rad = -1.0f;
+        double4 rec = make_double4(0.0, 0.0, 0.0, -1.0);
         if (k0 < nm) {
             double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
             for (int k = k0; k < k1; ++k) {
@@ -571,19 +573,54 @@ __global__ __launch_bounds__(kBlock) void build_bundle_image_kernel(
             lo8[4] = m2 * ch[1]; lo8[5] = m2 * cl[1]; lo8[6] = m2 * ch[2]; lo8[7] = m2 * ch[2];
             hi8[0] = m2 * cl[2]; hi8[1] = (_Float16)4096.0f; hi8[2] = (_Float16)4096.0f; hi8[3] = wh;
             hi8[4] = wl; hi8[5] = m2 * rh; hi8[6] = m2 * rh; hi8[7] = m2 * rl;
+            rec = make_double4(c[0], c[1], c[2], r);
             if (!(r <= 15000.0)) { // (cannot happen for a model in [-2^12, 2^12)^3) search it always
                 hi8[3] = (_Float16)-65504.0f;
                 hi8[4] = (_Float16)0.0f;
+                rec.w = INFINITY;
             }
-            rad = (float)r;
         } else {
             hi8[3] = (_Float16)65504.0f;
         }
         const int g = b >> 5, i = b & 31;
         img[(size_t)g * 64 + i] = lo8;
         img[(size_t)g * 64 + 32 + i] = hi8;
-        if (radius) radius[b] = rad;
+        bctr[b] = rec;
     }
+}
+
+// Block bounds: per 32-bundle block B, a centre C (the midpoint of its bundles' c^ box) and
+// R >= max over its bundles of (|c^_b - C| + r'_b), rounded up; R = -1 for a block of padding
+// bundles only, +inf when a bundle of it is always searched.  One thread per block.
+__global__ __launch_bounds__(kBlock) void build_block_bounds_kernel(const double4 *__restrict__ bctr, int nbb,
+                                                                    double4 *__restrict__ blk)
+{
+    const int B = blockIdx.x * kBlock + threadIdx.x;
+    if (B > nbb) return; // (nbb: the null block)
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    bool any = false, always = false;
+    for (int i = 0; i < 32; ++i) {
+        const double4 r = bctr[(size_t)B * 32 + i];
+        if (r.w < 0.0) continue;
+        any = true;
+        always |= !(r.w <= 15000.0);
+        lo[0] = fmin(lo[0], r.x); hi[0] = fmax(hi[0], r.x);
+        lo[1] = fmin(lo[1], r.y); hi[1] = fmax(hi[1], r.y);
+        lo[2] = fmin(lo[2], r.z); hi[2] = fmax(hi[2], r.z);
+    }
+    double4 out = make_double4(0.0, 0.0, 0.0, -1.0);
+    if (any) {
+        const double C[3] = {0.5 * (lo[0] + hi[0]), 0.5 * (lo[1] + hi[1]), 0.5 * (lo[2] + hi[2])};
+        double R = 0.0;
+        for (int i = 0; i < 32; ++i) {
+            const double4 r = bctr[(size_t)B * 32 + i];
+            if (r.w < 0.0) continue;
+            const double e0 = r.x - C[0], e1 = r.y - C[1], e2 = r.z - C[2];
+            R = fmax(R, sqrt((e0 * e0 + e1 * e1) + e2 * e2) * (1.0 + 0x1.0p-48) + r.w);
+        }
+        out = make_double4(C[0], C[1], C[2], always ? INFINITY : R * (1.0 + 0x1.0p-40));
+    }
+    blk[B] = out;
 }
 
 // ---- the bundle filter, v2 (the default) --------------------------------------------------
@@ -645,8 +682,11 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
 // The group bounds, one thread per slot (a 32-lane half = one group), from the slot records:
 // gop[2 g + h] = the stream operand half h of group g.  (Computed in the filter's prologue
 // instead, the fp64 shuffle chains cost ~28 us per wave task: profiles/r03k/.)
+// gctr[g] = (g^, D_g) for the workgroup candidate lists: D_g = +inf for a forced group, -1 for
+// one without queries.
 __global__ __launch_bounds__(kBlock) void bundle_group_kernel(const BundleQuery *__restrict__ qop, int nslots,
-                                                              half8_t *__restrict__ gop, const int *__restrict__ stop)
+                                                              half8_t *__restrict__ gop, double4 *__restrict__ gctr,
+                                                              const int *__restrict__ stop)
 {
     if (stop && *stop) return;
     const int s = blockIdx.x * kBlock + threadIdx.x; // (nslots: whole workgroups of slots)
@@ -658,9 +698,141 @@ __global__ __launch_bounds__(kBlock) void bundle_group_kernel(const BundleQuery 
     const int mode = w == -65504.0f ? kBqForced : w == 65504.0f ? kBqNever : kBqNormal;
     const GroupBound gb = bundle_group(q, d * (1.0 + 0x1.0p-20) + 0x1.0p-20, mode, lane >> 5);
     if ((lane & 31) < 2 && s < nslots) gop[(s >> 5) * 2 + (lane & 31)] = bundle_query_frag(gb.g, gb.D, gb.mode, lane & 31);
+    if ((lane & 31) == 0 && s < nslots)
+        gctr[s >> 5] = make_double4(gb.g[0], gb.g[1], gb.g[2],
+                                    gb.mode == kBqNormal ? gb.D : gb.mode == kBqForced ? INFINITY : -1.0);
+}
+
+// The candidate blocks of each filter workgroup (4 QG groups of 32 slots): the workgroup's
+// centre W (the midpoint of its groups' g^ box) and D_W >= max over its groups of
+// (D_g + |g^ - W|), rounded up; block B (centre C, radius R: build_block_bounds_kernel) is a
+// candidate unless |W - C| > D_W + R (fp64, both sides rounded against the test).  A block it
+// excludes has, for every group g of the workgroup and every bundle b of B,
+//     |g^ - c^_b| >= |W - C| - |g^ - W| - |c^_b - C| > D_g + r'_b,
+// so for every query q of g, |q^ - c^_b| >= |g^ - c^_b| - |q^ - g^| > d'_q + r'_b: no point of b is
+// as close as q's seed (the per-query bound of the file header, exactly, without the f16
+// margins).  A workgroup with a forced group takes every block.  Output: the candidate blocks in
+// increasing order, cand[w * nbb + e], e < cand_n[w].  all != 0: every block with a real point
+// (A/B: ICP_BUNDLE_CAND=0).
+__global__ __launch_bounds__(kBlock) void bundle_candidates_kernel(const double4 *__restrict__ gctr, int ng,
+                                                                   const double4 *__restrict__ blk, int nbb, int all,
+                                                                   int *__restrict__ cand, int *__restrict__ cand_n,
+                                                                   const int *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    __shared__ double s_wd[4];
+    __shared__ int s_mode, s_cnt[4];
+    const int w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 64) {
+        const double4 g = lane < ng ? gctr[(size_t)w * ng + lane] : make_double4(0.0, 0.0, 0.0, -1.0);
+        const bool forced = g.w == INFINITY, normal = g.w >= 0.0 && !forced;
+        double lo[3] = {normal ? g.x : INFINITY, normal ? g.y : INFINITY, normal ? g.z : INFINITY};
+        double hi[3] = {normal ? g.x : -INFINITY, normal ? g.y : -INFINITY, normal ? g.z : -INFINITY};
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = fmin(lo[k], __shfl_xor(lo[k], o, 64));
+                hi[k] = fmax(hi[k], __shfl_xor(hi[k], o, 64));
+            }
+        const bool any_normal = __any(normal), any_forced = __any(forced);
+        double W[3];
+        for (int k = 0; k < 3; ++k) W[k] = any_normal ? 0.5 * (lo[k] + hi[k]) : 0.0;
+        const double e0 = g.x - W[0], e1 = g.y - W[1], e2 = g.z - W[2];
+        double D = normal ? sqrt((e0 * e0 + e1 * e1) + e2 * e2) * (1.0 + 0x1.0p-48) + g.w : 0.0;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) D = fmax(D, __shfl_xor(D, o, 64));
+        if (lane == 0) {
+            s_wd[0] = W[0];
+            s_wd[1] = W[1];
+            s_wd[2] = W[2];
+            s_wd[3] = D * (1.0 + 0x1.0p-40);
+            s_mode = (all || any_forced) ? kBqForced : any_normal ? kBqNormal : kBqNever;
+        }
+    }
+    __syncthreads();
+    const int mode = s_mode;
+    const double W0 = s_wd[0], W1 = s_wd[1], W2 = s_wd[2], DW = s_wd[3];
+    int base = 0;
+    for (int b0 = 0; b0 < nbb; b0 += kBlock) {
+        const int b = b0 + tid;
+        bool c = false;
+        if (b < nbb && mode != kBqNever) {
+            const double4 B = blk[b];
+            if (B.w >= 0.0) {
+                if (mode == kBqForced) {
+                    c = true;
+                } else {
+                    const double e0 = W0 - B.x, e1 = W1 - B.y, e2 = W2 - B.z;
+                    const double dist = sqrt((e0 * e0 + e1 * e1) + e2 * e2) * (1.0 - 0x1.0p-48);
+                    c = !(dist > (DW + B.w) * (1.0 + 0x1.0p-48));
+                }
+            }
+        }
+        const unsigned long long bl = __ballot(c);
+        if (lane == 0) s_cnt[wave] = __popcll(bl);
+        __syncthreads();
+        int before = base;
+        for (int k = 0; k < wave; ++k) before += s_cnt[k];
+        const int total = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        if (c) cand[(size_t)w * nbb + before + __popcll(bl & ((1ull << lane) - 1ull))] = b;
+        base += total;
+        __syncthreads(); // (s_cnt reused)
+    }
+    if (tid == 0) cand_n[w] = base;
 }
 
 constexpr int kB2ListCap = 128; // LDS entries of a wave's fired-block list (then global)
+
+// The filter's task list: query workgroup w runs as S_w = clamp(ceil(ncand_w / ch), 1, smax)
+// tasks (w, s), s < S_w, each taking every S_w-th of w's candidate blocks; tasks are ordered by
+// their candidate count, largest first (a counting sort in LDS; the order within one count is
+// the LDS atomics' and does not matter: a task's outputs go to fixed places), so that the
+// persistent filter starts the long tasks first.  tctl = (number of tasks, the filter's task
+// counter, reset here); wsplit[w] = S_w for the finalize.  One workgroup of 1024 threads.
+constexpr int kTaskBins = 1024;
+__global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restrict__ cand_n, int qblocks, int smax,
+                                                            int ch, int *__restrict__ wsplit,
+                                                            int2 *__restrict__ tasks, int *__restrict__ tctl,
+                                                            const int *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    __shared__ int s_hist[kTaskBins];
+    __shared__ int s_total;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kTaskBins; i += 1024) s_hist[i] = 0;
+    if (tid == 0) s_total = 0;
+    __syncthreads();
+    auto split_of = [&](int w) { return min(smax, max(1, (cand_n[w] + ch - 1) / ch)); };
+    auto bin_of = [&](int w, int S) { // descending candidates per task -> ascending bin
+        const int per = (cand_n[w] + S - 1) / S;
+        return kTaskBins - 1 - min(per, kTaskBins - 1);
+    };
+    for (int w = tid; w < qblocks; w += 1024) {
+        const int S = split_of(w);
+        wsplit[w] = S;
+        atomicAdd(&s_hist[bin_of(w, S)], S);
+    }
+    __syncthreads();
+    if (tid == 0) { // exclusive scan of the bins (1024 adds)
+        int acc = 0;
+        for (int i = 0; i < kTaskBins; ++i) {
+            const int v = s_hist[i];
+            s_hist[i] = acc;
+            acc += v;
+        }
+        s_total = acc;
+    }
+    __syncthreads();
+    for (int w = tid; w < qblocks; w += 1024) {
+        const int S = split_of(w);
+        const int pos = atomicAdd(&s_hist[bin_of(w, S)], S);
+        for (int sp = 0; sp < S; ++sp) tasks[pos + sp] = make_int2(w, sp | (S << 16));
+    }
+    if (tid == 0) {
+        tctl[0] = s_total;
+        tctl[1] = 0;
+    }
+}
 
 // The filter proper.  A workgroup = 4 waves x QG groups of 32 slots; wave w owns groups
 // w QG .. (w+1) QG - 1 (their bound / pair operands and (best, second, position) in its
@@ -674,7 +846,8 @@ constexpr int kB2ListCap = 128; // LDS entries of a wave's fired-block list (the
 template <int QG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_bundle2_kernel(
     const BundleQuery *__restrict__ qop, const half8_t *__restrict__ gop, int np, const half8_t *__restrict__ bimg,
-    int nb_pad, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int *__restrict__ glist,
+    int nb_pad, const int *__restrict__ cand, const int *__restrict__ cand_n, const int2 *__restrict__ tasks,
+    int *__restrict__ tctl, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int *__restrict__ glist,
     float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx,
     const int *__restrict__ stop, unsigned long long *__restrict__ counters)
 {
@@ -684,19 +857,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     __shared__ int s_cnt[4];
     __shared__ int s_list[4][kB2ListCap];
     __shared__ half8_t s_bq[4][QG][64]; // the pair operands (read by the fired-block updates only)
+    __shared__ int s_task;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = lane >> 5, col = lane & 31;
-    const int split = blockIdx.y, S = gridDim.y;
     const int nbb = nb_pad >> 5;
-    const int nk = (nbb - split + S - 1) / S, nkmax = (nbb + S - 1) / S;
-    auto gblock = [&](int k) { const int g = split + S * k; return g < nbb ? g : nbb; };
-    int *const gl = glist + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 * nkmax;
+    const int ntasks = tctl[0];
+    // this workgroup's fired-block list overflow (reused task after task: <= nbb per wave)
+    int *const gl = glist + (size_t)blockIdx.x * 4 * nbb;
+    const int nkmax = nbb;
+    for (;;) { // tasks (query workgroup w, split s of S_w), heaviest first (bundle_tasks_kernel)
+    if (tid == 0) s_task = atomicAdd(&tctl[1], 1);
+    __syncthreads();
+    const int t = s_task;
+    if (t >= ntasks) break; // (uniform)
+    const int2 tk = tasks[t];
+    const int qw = tk.x, split = tk.y & 0xffff, S = tk.y >> 16;
+    // this wave's share of the workgroup's candidate blocks (bundle_candidates_kernel): entries
+    // e = wave S + split + 4 S k, i.e. split e mod S, interleaved over the 4 waves
+    const int ncand = cand_n[qw], first = wave * S + split, step = 4 * S;
+    const int nk = ncand > first ? (ncand - first + step - 1) / step : 0;
+    const int *const crow_l = cand + (size_t)qw * nbb;
+    auto gblock = [&](int k) {
+        const int e = first + step * k;
+        return e < ncand ? __builtin_amdgcn_readfirstlane(crow_l[e]) : nbb; // (past the end: the null block)
+    };
     unsigned n_blocks = 0, n_groups = 0, n_pairs = 0;
     const unsigned long long t_start = counters ? __builtin_amdgcn_s_memrealtime() : 0ull;
     unsigned long long t_pro = 0, t_stream = 0, t_defer = 0;
     if (tid < 4) s_cnt[tid] = 0;
 
-    const int grp0 = blockIdx.x * NG; // this workgroup's first group
+    const int grp0 = qw * NG; // the query workgroup's first group
     half8_t bb[QG];
     float best[QG], second[QG];
     int bpos[QG];
@@ -724,11 +914,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     }
 
     // ---- stream: blocks k = wave, wave + 4, ... of this split, four loads ahead
-    auto fire = [&](int k, const f32x16_t &d) {
+    auto fire = [&](int g, const f32x16_t &d) {
         const unsigned long long f = __ballot(min16v(d) <= 0.0f);
         const unsigned gm = (unsigned)(f | (f >> 32));
         if (__builtin_expect(gm != 0u, 0)) { // (uniform)
-            const int g = gblock(k);
 #pragma unroll
             for (int w2 = 0; w2 < 4; ++w2) {
                 const unsigned m8 = (gm >> (QG * w2)) & ((1u << QG) - 1u);
@@ -747,19 +936,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     {
         constexpr int U = 4;
         half8_t cur[U], nxt[U];
+        int cid[U], nid[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = bimg[(size_t)gblock(wave + 4 * u) * 64 + lane];
-        for (int k0 = wave; k0 < nk; k0 += 4 * U) {
+        for (int u = 0; u < U; ++u) {
+            cid[u] = gblock(u);
+            cur[u] = bimg[(size_t)cid[u] * 64 + lane];
+        }
+        for (int k0 = 0; k0 < nk; k0 += U) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = bimg[(size_t)gblock(k0 + 4 * (U + u)) * 64 + lane];
+            for (int u = 0; u < U; ++u) {
+                nid[u] = gblock(k0 + U + u);
+                nxt[u] = bimg[(size_t)nid[u] * 64 + lane];
+            }
             f32x16_t d[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[u], gopB, zero, 0, 0, 0);
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (k0 + 4 * u < nk) fire(k0 + 4 * u, d[u]);
+                if (k0 + u < nk) fire(cid[u], d[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+            for (int u = 0; u < U; ++u) {
+                cur[u] = nxt[u];
+                cid[u] = nid[u];
+            }
         }
     }
     __syncthreads(); // every wave's appends are in
@@ -848,7 +1047,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     // (counters: this wave task's own row of 9, accumulated over launches without atomics --
     // a same-address atomic per wave serialised and tripled the launch)
     unsigned long long *crow =
-        counters ? counters + 9 * ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) : nullptr;
+        counters ? counters + 9 * ((size_t)t * 4 + wave) : nullptr;
     if (crow && lane == 0) {
         crow[0] += n_blocks;
         crow[1] += n_groups;
@@ -857,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         crow[4] += t_stream - t_pro;
         crow[5] += t_defer - t_stream;
         crow[7] += 1ull;
-        crow[8] += (unsigned long long)((nk - wave + 3) / 4); // stream MFMAs of this wave
+        crow[8] += (unsigned long long)nk; // stream MFMAs of this wave
     }
     // the two lane halves' (best, second, position) per query, then all QG original indices
     // gathered at once (one dependent load per wave, not one per group)
@@ -897,6 +1096,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         __builtin_amdgcn_s_waitcnt(0);
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) crow[6] += t_end - t_defer;
+    }
+    __syncthreads(); // (s_task, s_cnt, s_list, s_bq are the next task's)
     }
 }
 
@@ -967,13 +1168,15 @@ std::vector<int> bundle_kd_order(const double *m, size_t nm)
 
 void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
                                 int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
-                                float *radius, hipStream_t st)
+                                double4 *bctr, double4 *blk, hipStream_t st)
 {
     const int nm_b = (nb_pad + 32) * kBundle; // (+ the null block)
     build_pair_image_kd_kernel<<<bgrid(nm_b), kBlock, 0, st>>>(mx, my, mz, nm, kd, nm_b, c[0], c[1], c[2], scale,
                                                                   (half8_t *)pimg, kd_orig);
     build_bundle_image_kernel<<<bgrid(nb_pad + 32), kBlock, 0, st>>>(mx, my, mz, nm, kd, nb_pad, c[0], c[1], c[2],
-                                                                   scale, (half8_t *)bimg, radius);
+                                                                   scale, (half8_t *)bimg, bctr);
+    const int nbb = nb_pad >> 5;
+    build_block_bounds_kernel<<<(nbb + 1 + kBlock - 1) / kBlock, kBlock, 0, st>>>(bctr, nbb, blk);
 }
 
 static bool bundle_group()
@@ -1018,13 +1221,17 @@ static bool bundle_v1() // ICP_BUNDLE_KERNEL=1: the v1 filter (A/B)
 
 bool bundle_v2() { return !bundle_v1(); }
 
-// Splits: about 8,192 workgroups, at least 42 blocks of the model per split.  The per-query
-// work (operands, partials) is paid once per split, but fewer, longer workgroups leave the
-// fired-block deferred phases unbalanced: at C4 (1,024 query workgroups) 1 / 3 / 8 / 16 splits
-// ran the filter in 0.875 / 0.440 / 0.361 / 0.421 ms, at the W = 8 shard (128) 6 / 24 / 32 / 48
-// in 0.174 / 0.122 / 0.149 / 0.153 ms (profiles/r03l/, r03n/).  ICP_BUNDLE_SPLITS overrides (A/B).
-constexpr int kB2TargetWG = 8192;
-constexpr int kB2MinBlocksPerSplit = 42;
+// Tasks: a query workgroup with ncand candidate blocks runs as clamp(ceil(ncand / ch), 1, smax)
+// tasks (bundle_tasks_kernel), on a persistent grid of the resident workgroups.  ICP_BUNDLE_CH /
+// ICP_BUNDLE_SMAX override (A/B).
+constexpr int kB2Ch = 8;
+constexpr int kB2Smax = 16;
+
+static int env_int(const char *name, int dflt)
+{
+    const char *e = getenv(name);
+    return e && atoi(e) > 0 ? atoi(e) : dflt;
+}
 
 NNPlan plan_nn_bundle2(size_t np, int nb_pad)
 {
@@ -1033,27 +1240,34 @@ NNPlan plan_nn_bundle2(size_t np, int nb_pad)
     pl.q_per_lane = qg;
     pl.qblocks = (int)std::max<size_t>(1, (np + 4 * qg * 32 - 1) / (4 * qg * 32));
     const int nbb = nb_pad >> 5;
-    static const int forced = [] {
-        const char *e = getenv("ICP_BUNDLE_SPLITS");
-        return e ? atoi(e) : 0;
-    }();
-    pl.splits = forced > 0 ? forced
-                           : std::min((kB2TargetWG + pl.qblocks - 1) / pl.qblocks, nbb / kB2MinBlocksPerSplit);
-    pl.splits = std::max(1, std::min(pl.splits, nbb));
-    pl.chunk = 0;
+    static const int smax = env_int("ICP_BUNDLE_SMAX", kB2Smax), ch = env_int("ICP_BUNDLE_CH", kB2Ch);
+    pl.splits = std::max(1, std::min(smax, nbb)); // partial sets (the finalize reads wsplit[w] of them)
+    pl.chunk = ch;
     pl.kernel = 200;
+    static int cap[2] = {0, 0};
+    int &c = cap[qg == 4 ? 0 : 1];
+    if (!c) {
+        const void *k = qg == 4 ? (const void *)nn_bundle2_kernel<4> : (const void *)nn_bundle2_kernel<8>;
+        int dev = 0, cus = 256, per_cu = 2;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0) != hipSuccess || per_cu < 1)
+                per_cu = 2;
+        }
+        c = std::max(1, cus * per_cu);
+    }
+    pl.grid = c; // (persistent: the resident workgroups)
     if (getenv("ICP_DEBUG_PLAN"))
-        fprintf(stderr, "[plan bundle2] np=%zu nbb=%d qg=%d qblocks=%d splits=%d\n", np, nbb, qg, pl.qblocks, pl.splits);
+        fprintf(stderr, "[plan bundle2] np=%zu nbb=%d qg=%d qblocks=%d smax=%d ch=%d grid=%d\n", np, nbb, qg,
+                pl.qblocks, pl.splits, ch, c);
     return pl;
 }
 
 size_t bundle2_slots(const NNPlan &pl) { return (size_t)pl.qblocks * 4 * pl.q_per_lane * 32; }
 
-size_t bundle2_list_ints(const NNPlan &pl, int nb_pad)
-{
-    const int nbb = nb_pad >> 5;
-    return (size_t)pl.qblocks * pl.splits * 4 * ((nbb + pl.splits - 1) / pl.splits);
-}
+size_t bundle2_list_ints(const NNPlan &pl, int nb_pad) { return (size_t)pl.grid * 4 * (nb_pad >> 5); }
+
+size_t bundle2_task_count(const NNPlan &pl) { return (size_t)pl.qblocks * pl.splits; }
 
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
                         const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
@@ -1063,23 +1277,42 @@ void launch_bundle_prep(const double *px, const double *py, const double *pz, in
         px, py, pz, np, pos, prev, m4, c[0], c[1], c[2], scale, seed16, (int)nslots, (BundleQuery *)qop, qraw, stop);
 }
 
-size_t bundle2_counter_rows(const NNPlan &pl) { return (size_t)pl.qblocks * pl.splits * 4; }
+size_t bundle2_counter_rows(const NNPlan &pl) { return bundle2_task_count(pl) * 4; }
 
-void launch_bundle_groups(const void *qop, size_t nslots, void *gop, hipStream_t st, const int *stop)
+void launch_bundle_groups(const void *qop, size_t nslots, void *gop, double4 *gctr, hipStream_t st, const int *stop)
 {
     bundle_group_kernel<<<(int)(nslots / kBlock), kBlock, 0, st>>>((const BundleQuery *)qop, (int)nslots,
-                                                                   (half8_t *)gop, stop);
+                                                                   (half8_t *)gop, gctr, stop);
 }
 
-void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const void *pimg,
-                       const int *kd_orig, int *glist, const NNPlan &pl, float *part_best, float *part_second,
-                       int *part_idx, hipStream_t st, const int *stop, unsigned long long *counters)
+static bool bundle_cand_all() // ICP_BUNDLE_CAND=0: every block a candidate (A/B)
 {
-    dim3 grid(pl.qblocks, pl.splits);
+    static const bool all = [] {
+        const char *e = getenv("ICP_BUNDLE_CAND");
+        return e && atoi(e) == 0;
+    }();
+    return all;
+}
+
+void launch_bundle_candidates(const NNPlan &pl, const double4 *gctr, const double4 *blk, int nb_pad, int *cand,
+                              int *cand_n, int *wsplit, int2 *tasks, int *tctl, hipStream_t st, const int *stop)
+{
+    bundle_candidates_kernel<<<pl.qblocks, kBlock, 0, st>>>(gctr, 4 * pl.q_per_lane, blk, nb_pad >> 5,
+                                                            bundle_cand_all() ? 1 : 0, cand, cand_n, stop);
+    bundle_tasks_kernel<<<1, 1024, 0, st>>>(cand_n, pl.qblocks, pl.splits, pl.chunk, wsplit, tasks, tctl, stop);
+}
+
+void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const int *cand,
+                       const int *cand_n, const int2 *tasks, int *tctl, const void *pimg, const int *kd_orig,
+                       int *glist, const NNPlan &pl, float *part_best, float *part_second, int *part_idx,
+                       hipStream_t st, const int *stop, unsigned long long *counters)
+{
+    const int grid = pl.grid; // persistent: the resident workgroups pull tasks
 #define LAUNCHB2(QG)                                                                                          \
     nn_bundle2_kernel<QG><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,             \
-                                             (const half8_t *)bimg, nb_pad, (const half8_t *)pimg, kd_orig, glist, \
-                                             part_best, part_second, part_idx, stop, counters)
+                                             (const half8_t *)bimg, nb_pad, cand, cand_n, tasks, tctl,             \
+                                             (const half8_t *)pimg, kd_orig, glist, part_best, part_second,        \
+                                             part_idx, stop, counters)
     if (pl.q_per_lane == 4) LAUNCHB2(4);
     else LAUNCHB2(8);
 #undef LAUNCHB2

@@ -269,10 +269,10 @@ struct icp_ctx {
     // per model of >= kBundleMinModel points; the query order of the scene it searches
     char *b_img = nullptr, *b_pimg = nullptr; // 1 KiB per 32 bundles; 1 KiB per bundle
     int *b_kd_orig = nullptr;                 // original index per kd position (nm: padding)
-    float *b_radius = nullptr;                // per bundle (scaled units)
+    double4 *b_bctr = nullptr, *b_blk = nullptr; // per bundle / per 32-bundle block: centre, radius
     int *b_kd = nullptr;                      // the kd order (upload staging)
     int nb_pad = 0;                           // bundles (whole LDS tiles)
-    size_t b_img_cap = 0, b_pimg_cap = 0, b_kd_orig_cap = 0, b_radius_cap = 0, b_kd_cap = 0;
+    size_t b_img_cap = 0, b_pimg_cap = 0, b_kd_orig_cap = 0, b_bctr_cap = 0, b_blk_cap = 0, b_kd_cap = 0;
     int *q_order = nullptr;                   // the bundle filter's query order (launch_query_order)
     int *q_pos = nullptr;                     // its inverse (query j's slot)
     size_t q_pos_cap = 0;
@@ -284,6 +284,11 @@ struct icp_ctx {
     char *b_qop = nullptr, *b_gop = nullptr;  // v2: per-slot query operands, per-group bounds
     double4 *b_qraw = nullptr;                // v2: per-slot query coordinates, index, seed
     int *b_glist = nullptr;                   // v2: fired-block list overflow
+    double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
+    int *b_cand = nullptr, *b_cand_n = nullptr; // v2: per filter workgroup, its candidate blocks
+    int *b_wsplit = nullptr, *b_tctl = nullptr; // v2: per filter workgroup its tasks; (count, counter)
+    int2 *b_tasks = nullptr;                  // v2: the task list
+    size_t b_gctr_cap = 0, b_cand_cap = 0, b_cand_n_cap = 0, b_wsplit_cap = 0, b_tctl_cap = 0, b_tasks_cap = 0;
     size_t b_qop_cap = 0, b_gop_cap = 0, b_qraw_cap = 0, b_glist_cap = 0, b_counters_rows = 0;
 
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -678,6 +683,12 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             TRY(grow(ctx, &ctx->b_qraw, &ctx->b_qraw_cap, nslots));
             TRY(grow(ctx, &ctx->b_gop, &ctx->b_gop_cap, nslots));
             TRY(grow(ctx, &ctx->b_glist, &ctx->b_glist_cap, bundle2_list_ints(pl, ctx->nb_pad)));
+            TRY(grow(ctx, &ctx->b_gctr, &ctx->b_gctr_cap, nslots / 32));
+            TRY(grow(ctx, &ctx->b_cand, &ctx->b_cand_cap, (size_t)pl.qblocks * (ctx->nb_pad >> 5)));
+            TRY(grow(ctx, &ctx->b_cand_n, &ctx->b_cand_n_cap, (size_t)pl.qblocks));
+            TRY(grow(ctx, &ctx->b_wsplit, &ctx->b_wsplit_cap, (size_t)pl.qblocks));
+            TRY(grow(ctx, &ctx->b_tasks, &ctx->b_tasks_cap, bundle2_task_count(pl)));
+            TRY(grow(ctx, &ctx->b_tctl, &ctx->b_tctl_cap, 2));
             if (ctx->b_counters && ctx->b_counters_rows < bundle2_counter_rows(pl)) { // (per-wave rows)
                 HIPCHK(hipFree(ctx->b_counters));
                 ctx->b_counters = nullptr;
@@ -688,12 +699,15 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             }
             launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4, ctx->c,
                                ctx->scale16, seeds, nslots, ctx->b_qop, ctx->b_qraw, ctx->st, stop);
-            launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->st, stop);
+            launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->b_gctr, ctx->st, stop);
+            launch_bundle_candidates(pl, ctx->b_gctr, ctx->b_blk, ctx->nb_pad, ctx->b_cand, ctx->b_cand_n,
+                                     ctx->b_wsplit, ctx->b_tasks, ctx->b_tctl, ctx->st, stop);
         }
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         if (v2)
-            launch_nn_bundle2(ctx->b_qop, ctx->b_gop, (int)n, ctx->b_img, ctx->nb_pad, ctx->b_pimg, ctx->b_kd_orig, ctx->b_glist, pl,
-                              pb, ps, pi, ctx->st, stop, ctx->b_counters);
+            launch_nn_bundle2(ctx->b_qop, ctx->b_gop, (int)n, ctx->b_img, ctx->nb_pad, ctx->b_cand, ctx->b_cand_n,
+                              ctx->b_tasks, ctx->b_tctl, ctx->b_pimg, ctx->b_kd_orig, ctx->b_glist, pl, pb, ps, pi,
+                              ctx->st, stop, ctx->b_counters);
         else if (l1 == 3)
             launch_nn_bundle(q.x, q.y, q.z, (int)n, order, ctx->idx, ctx->m4, ctx->c, ctx->scale16, seeds, ctx->b_img,
                              ctx->nb_pad, ctx->b_pimg, ctx->b_kd_orig, (int)ctx->nm, pl, pb, ps, pi, ctx->st, stop,
@@ -707,7 +721,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (l1 >= 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
-                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit, v2 ? ctx->b_qraw : nullptr);
+                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit, v2 ? ctx->b_qraw : nullptr,
+                                      v2 ? ctx->b_wsplit : nullptr, v2 ? 4 * pl.q_per_lane * 32 : 0);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
@@ -1088,7 +1103,9 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
                     (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->b_img, (void *)ctx->b_pimg, (void *)ctx->b_kd_orig,
-                    (void *)ctx->b_radius, (void *)ctx->b_kd, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters,
+                    (void *)ctx->b_bctr, (void *)ctx->b_blk, (void *)ctx->b_gctr, (void *)ctx->b_cand,
+                    (void *)ctx->b_cand_n, (void *)ctx->b_wsplit, (void *)ctx->b_tasks, (void *)ctx->b_tctl,
+                    (void *)ctx->b_kd, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters,
                     (void *)ctx->b_qop, (void *)ctx->b_gop, (void *)ctx->b_qraw, (void *)ctx->b_glist, (void *)ctx->q_pos, (void *)ctx->cr_entries,
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt})
@@ -1253,10 +1270,12 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, nbx * 32));
         TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, nbx * 1024));
         TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, nbx * 32));
-        TRY(grow(ctx, &ctx->b_radius, &ctx->b_radius_cap, nbx));
+        TRY(grow(ctx, &ctx->b_bctr, &ctx->b_bctr_cap, nbx));
+        TRY(grow(ctx, &ctx->b_blk, &ctx->b_blk_cap, nbx / 32));
         HIPCHK(hipMemcpyAsync(ctx->b_kd, kd.data(), sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
         launch_build_bundle_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
-                                   ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_radius, ctx->st);
+                                   ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_bctr, ctx->b_blk,
+                                   ctx->st);
         LAUNCHCHK("build_bundle_images");
         HIPCHK(hipStreamSynchronize(ctx->st)); // (kd is freed on return)
         ctx->nb_pad = nb_pad;

@@ -80,6 +80,7 @@ struct NNPlan {
     int chunk;      // model points per split (multiple of the tile)
     int tile = 0;   // LDS tile of the VALU filter when not the default (kTileSmall)
     int kernel = -1; // f16 filter kernel picked for this size (plan_nn_mfma16)
+    int grid = 0;    // persistent kernels (the bundle filter): workgroups launched
 };
 NNPlan plan_nn32(size_t np, size_t nm_pad);
 NNPlan plan_nn64(size_t np, size_t nm_pad);
@@ -118,7 +119,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop = nullptr, const double4 *m4 = nullptr,
-                               unsigned *audit = nullptr, const double4 *qraw = nullptr);
+                               unsigned *audit = nullptr, const double4 *qraw = nullptr,
+                               const int *wsplit = nullptr, int wslots = 0);
 // A split plan for `kernel` (make_plan): np queries in workgroups of queries_per_lane_block,
 // the model axis (nm rows, tiles of `tile`) split to fill >= 4 rounds of resident workgroups.
 NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel,
@@ -126,14 +128,15 @@ NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_
 // Bundle-bound f16 filter (icp_bundle.hip).  The model in kd order (bundle_kd_order): bundles
 // of 32 consecutive points, bundle_pad(nm) of them (whole 256-bundle LDS tiles); images built
 // once per model: bimg (1 KiB per 32 bundles), pimg (the f16 pair image in kd order, 1 KiB
-// per bundle), kd_orig (original index per kd position, nm for padding), radius (nullable,
-// per bundle, scaled units; -1 for padding), each for nb_pad + 32 bundles: the last 32 form the
-// null block, which the interleaved splits read past their last block.
+// per bundle), kd_orig (original index per kd position, nm for padding), bctr (per bundle: its
+// centre and radius in scaled units, radius -1 for padding), each for nb_pad + 32 bundles: the
+// last 32 form the null block, which the splits read past their last block; blk (per 32-bundle
+// block and the null block, nb_pad / 32 + 1: centre and radius over its bundles).
 int bundle_pad(size_t nm);
 std::vector<int> bundle_kd_order(const double *m_xyz, size_t nm);
 void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
                                 int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
-                                float *radius, hipStream_t st);
+                                double4 *bctr, double4 *blk, hipStream_t st);
 NNPlan plan_nn_bundle(size_t np, int nb_pad);
 // Seeded search (prev: each query's seed index, seed16 its f16 shift): partial (best, second,
 // original index) per (split, query) in the format of launch_nn_mfma16 (same finalize).
@@ -159,11 +162,21 @@ size_t bundle2_counter_rows(const NNPlan &pl);
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
                         const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
                         size_t nslots, void *qop, double4 *qraw, hipStream_t st, const int *stop = nullptr);
-// gop (nslots bytes): the 32-slot groups' bounds from the records (after the prep)
-void launch_bundle_groups(const void *qop, size_t nslots, void *gop, hipStream_t st, const int *stop = nullptr);
-void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const void *pimg,
-                       const int *kd_orig, int *glist, const NNPlan &pl, float *part_best, float *part_second,
-                       int *part_idx, hipStream_t st, const int *stop = nullptr, unsigned long long *counters = nullptr);
+// gop (nslots bytes): the 32-slot groups' bounds from the records (after the prep); gctr
+// (nslots / 32 double4): the same as (centre, D) for the candidate lists
+void launch_bundle_groups(const void *qop, size_t nslots, void *gop, double4 *gctr, hipStream_t st,
+                          const int *stop = nullptr);
+// cand (qblocks x nb_pad / 32 ints), cand_n (qblocks): each filter workgroup's candidate blocks;
+// then the task list: wsplit (qblocks: the partial sets of each query workgroup), tasks
+// (bundle2_task_count(plan) int2), tctl (2 ints: count, the filter's task counter)
+void launch_bundle_candidates(const NNPlan &pl, const double4 *gctr, const double4 *blk, int nb_pad, int *cand,
+                              int *cand_n, int *wsplit, int2 *tasks, int *tctl, hipStream_t st,
+                              const int *stop = nullptr);
+size_t bundle2_task_count(const NNPlan &pl);
+void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const int *cand,
+                       const int *cand_n, const int2 *tasks, int *tctl, const void *pimg, const int *kd_orig,
+                       int *glist, const NNPlan &pl, float *part_best, float *part_second, int *part_idx,
+                       hipStream_t st, const int *stop = nullptr, unsigned long long *counters = nullptr);
 // order[k] = the query processed k-th: the queries sorted by the Morton code of their cell in a
 // 1024^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
 // = k); scratch: query_order_scratch_bytes(n)

@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint,
     const int *__restrict__ stop, const double4 *__restrict__ m4, unsigned *__restrict__ audit,
-    const double4 *__restrict__ qraw)
+    const double4 *__restrict__ qraw, const int *__restrict__ wsplit, int wslots)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
     // qraw (the bundle filter): the partials are in the filter's slot order, and slot s's query
@@ -1242,7 +1242,10 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     }
     float b = 0.0f, s2 = 0.0f;
     int id = -1;
-    if (valid) merge_splits_group<G>(part_best, part_second, part_idx, splits, np, s, sub, b, s2, id);
+    // (wsplit: the bundle filter's per-workgroup task counts -- slot s's partial sets)
+    if (valid)
+        merge_splits_group<G>(part_best, part_second, part_idx, wsplit ? wsplit[s / wslots] : splits, np, s, sub, b,
+                              s2, id);
     if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
     const double ax = (q0 - cx) * scale, ay = (q1 - cy) * scale, az = (q2 - cz) * scale;
     bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
@@ -2115,7 +2118,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop, const double4 *m4, unsigned *audit,
-                               const double4 *qraw)
+                               const double4 *qraw, const int *wsplit, int wslots)
 {
     // (its fp64 certificate is heavy and every lane of a group repeats it: lanes only pay off
     // for very many splits; ICP_FIN16_LANES = 1 | 4 | 8 overrides, for experiments)
@@ -2129,7 +2132,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
     nn_finalize_mfma16_kernel<SD, G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
                                                               pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
                                                               idx, amb_count, amb_list, amb_hint, stop, m4, audit, \
-                                                              qraw)
+                                                              qraw, wsplit, wslots)
     if (seed16) {
         if (g == 8) FIN16(true, 8); else if (g == 4) FIN16(true, 4); else FIN16(true, 1);
     } else {

@@ -163,6 +163,34 @@ for s in $STEPS; do
              for sp in 2 3 4; do
                ICP_BUNDLE_QG=4 ICP_BUNDLE_SPLITS=$sp run bsplitq4_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
              done ;;
+    btask2) for cfg in "32 16" "64 16" "128 16" "32 32" "64 32" "16 32"; do
+             set -- $cfg
+             ICP_BUNDLE_CH=$1 ICP_BUNDLE_SMAX=$2 run bt_$1_$2 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             ICP_BUNDLE_CH=$1 ICP_BUNDLE_SMAX=$2 run bt8_$1_$2 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+           done ;;
+    btask) run bdef 300 python3 tools/bundle_probe.py --steps 20 --variants bundle mfma16 || exit 1
+           run bdef8 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+           for ch in 4 16 32; do
+             ICP_BUNDLE_CH=$ch run bch_$ch 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             ICP_BUNDLE_CH=$ch run bch8_$ch 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+           done
+           for sm in 8 32; do
+             ICP_BUNDLE_SMAX=$sm run bsm_$sm 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             ICP_BUNDLE_SMAX=$sm run bsm8_$sm 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+           done
+           ICP_BUNDLE_QG=4 run bq4 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1 ;;
+    bsplit3) run bdef 300 python3 tools/bundle_probe.py --steps 20 --variants bundle mfma16 || exit 1
+             run bdef8 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+             ICP_BUNDLE_CAND=0 run bnocand 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             for sp in 1 2 4 8; do
+               ICP_BUNDLE_SPLITS=$sp run bsplit_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             done
+             for sp in 4 8 24; do
+               ICP_BUNDLE_SPLITS=$sp run bsplit8_$sp 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+             done
+             for sp in 1 2 4; do
+               ICP_BUNDLE_QG=4 ICP_BUNDLE_SPLITS=$sp run bsplitq4_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+             done ;;
     bsplit2) run bdef 300 python3 tools/bundle_probe.py --steps 20 --variants bundle mfma16 || exit 1
              run bdef8 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
              for sp in 6 12 16; do
