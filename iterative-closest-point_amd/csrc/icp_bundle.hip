@@ -101,15 +101,10 @@ struct GroupBound {
     double g[3], D;
     int mode;
 };
-// the group of the 32-lane half `gh` (its lanes' queries a, d', mode)
-__device__ __forceinline__ GroupBound bundle_group(const double a[3], double dq, int mode, int gh)
+// the group of the 32-lane half `gh` (its lanes' queries q^ = hi + lo as the MFMA sees them,
+// d', mode)
+__device__ __forceinline__ GroupBound bundle_group_hat(const double q[3], double dq, int mode, int gh)
 {
-    _Float16 hi, lo;
-    double q[3];
-    for (int k = 0; k < 3; ++k) {
-        split_f16(a[k], hi, lo);
-        q[k] = (double)hi + (double)lo;
-    }
     const bool in = mode == kBqNormal;
     double lo3[3], hi3[3];
     for (int k = 0; k < 3; ++k) {
@@ -145,6 +140,17 @@ __device__ __forceinline__ GroupBound bundle_group(const double a[3], double dq,
     r.D = D;
     r.mode = gmode;
     return r;
+}
+// the same from the (clamped, scaled) queries a
+__device__ __forceinline__ GroupBound bundle_group(const double a[3], double dq, int mode, int gh)
+{
+    _Float16 hi, lo;
+    double q[3];
+    for (int k = 0; k < 3; ++k) {
+        split_f16(a[k], hi, lo);
+        q[k] = (double)hi + (double)lo;
+    }
+    return bundle_group_hat(q, dq, mode, gh);
 }
 __device__ __forceinline__ half8_t bundle_group_frag(const double a[3], double dq, int mode, int h)
 {
@@ -640,9 +646,10 @@ struct BundleQuery {
 // certificate needs, in slot order.
 __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, int np,
-    const int *__restrict__ pos, const int *__restrict__ prev, const double4 *__restrict__ m4, double cx,
-    double cy, double cz, double scale, const unsigned *__restrict__ seed16, int nslots, BundleQuery *__restrict__ qop,
-    double4 *__restrict__ qraw, const int *__restrict__ stop)
+    const int *__restrict__ pos, const int *__restrict__ prev, const double4 *__restrict__ m4,
+    const double *__restrict__ seedd, double cx, double cy, double cz, double scale,
+    const unsigned *__restrict__ seed16, int nslots, BundleQuery *__restrict__ qop, double4 *__restrict__ qraw,
+    const int *__restrict__ stop)
 {
     if (stop && *stop) return;
     const int t = blockIdx.x * kBlock + threadIdx.x;
@@ -659,9 +666,16 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
         a[1] = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
         a[2] = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
         sd = seed16[j];
-        const double4 m = m4[prev[j]]; // the seed distance in the reference's arithmetic (compute.cu:112-117)
-        const double dx = p0 - m.x, dy = p1 - m.y, dz = p2 - m.z;
-        const double D = (dx * dx + dy * dy) + dz * dz;
+        // the seed distance in the reference's arithmetic (compute.cu:112-117): from the transform
+        // that moved the point (the same expression over the same values), else gathered
+        double D;
+        if (seedd) {
+            D = seedd[j];
+        } else {
+            const double4 m = m4[prev[j]];
+            const double dx = p0 - m.x, dy = p1 - m.y, dz = p2 - m.z;
+            D = (dx * dx + dy * dy) + dz * dz;
+        }
         const double eq = 0x1.0p-20 * ((fabs(a[0]) + fabs(a[1])) + fabs(a[2])) + 0x1.0p-22;
         dq = (sqrt(D) * scale * (1.0 + 0x1.0p-40) + 1e-300 + eq) * (1.0 + 0x1.0p-20) + 0x1.0p-20;
         mode = fabs(a[0]) <= kBQueryMax && fabs(a[1]) <= kBQueryMax && fabs(a[2]) <= kBQueryMax && dq <= kBSeedMax
@@ -696,7 +710,7 @@ __global__ __launch_bounds__(kBlock) void bundle_group_kernel(const BundleQuery 
     const double d = (double)b1[5] + (double)b1[6];
     const float w = (float)b1[1];
     const int mode = w == -65504.0f ? kBqForced : w == 65504.0f ? kBqNever : kBqNormal;
-    const GroupBound gb = bundle_group(q, d * (1.0 + 0x1.0p-20) + 0x1.0p-20, mode, lane >> 5);
+    const GroupBound gb = bundle_group_hat(q, d * (1.0 + 0x1.0p-20) + 0x1.0p-20, mode, lane >> 5);
     if ((lane & 31) < 2 && s < nslots) gop[(s >> 5) * 2 + (lane & 31)] = bundle_query_frag(gb.g, gb.D, gb.mode, lane & 31);
     if ((lane & 31) == 0 && s < nslots)
         gctr[s >> 5] = make_double4(gb.g[0], gb.g[1], gb.g[2],
@@ -790,6 +804,10 @@ constexpr int kB2ListCap = 128; // LDS entries of a wave's fired-block list (the
 // persistent filter starts the long tasks first.  tctl = (number of tasks, the filter's task
 // counter, reset here); wsplit[w] = S_w for the finalize.  One workgroup of 1024 threads.
 constexpr int kTaskBins = 1024;
+// Candidates per task (ch <= 0: automatic): C4's 57,380 candidates ran the filter in 0.219 /
+// 0.208 / 0.199 / 0.203 ms at 16 / 32 / 64 / 128 per task, the W = 8 shard's 22,984 in 0.112 /
+// 0.111 / 0.177 / 0.212 ms (profiles/r03t/): ch = the total / 1,024 (C4 56, the shard 23)
+constexpr int kB2TargetTasks = 1024, kB2ChMin = 8, kB2ChMax = 64;
 __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restrict__ cand_n, int qblocks, int smax,
                                                             int ch, int *__restrict__ wsplit,
                                                             int2 *__restrict__ tasks, int *__restrict__ tctl,
@@ -797,11 +815,23 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
 {
     if (stop && *stop) return;
     __shared__ int s_hist[kTaskBins];
-    __shared__ int s_total;
+    __shared__ int s_total, s_ch;
     const int tid = threadIdx.x;
     for (int i = tid; i < kTaskBins; i += 1024) s_hist[i] = 0;
     if (tid == 0) s_total = 0;
     __syncthreads();
+    if (ch <= 0) { // candidates per task: about kB2TargetTasks tasks in all, within [kB2ChMin, kB2ChMax]
+        int c = 0;
+        for (int w = tid; w < qblocks; w += 1024) c += cand_n[w];
+        atomicAdd(&s_total, c);
+        __syncthreads();
+        if (tid == 0) {
+            s_ch = min(kB2ChMax, max(kB2ChMin, (s_total + kB2TargetTasks - 1) / kB2TargetTasks));
+            s_total = 0;
+        }
+        __syncthreads();
+        ch = s_ch;
+    }
     auto split_of = [&](int w) { return min(smax, max(1, (cand_n[w] + ch - 1) / ch)); };
     auto bin_of = [&](int w, int S) { // descending candidates per task -> ascending bin
         const int per = (cand_n[w] + S - 1) / S;
@@ -813,16 +843,25 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
         atomicAdd(&s_hist[bin_of(w, S)], S);
     }
     __syncthreads();
-    if (tid == 0) { // exclusive scan of the bins (1024 adds)
-        int acc = 0;
-        for (int i = 0; i < kTaskBins; ++i) {
-            const int v = s_hist[i];
-            s_hist[i] = acc;
-            acc += v;
+    { // exclusive scan of the bins: one bin per thread, wave scans, then the 16 wave totals
+        static_assert(kTaskBins == 1024, "one bin per thread");
+        __shared__ int s_wsum[16];
+        const int lane = tid & 63, wv = tid >> 6;
+        const int v = s_hist[tid];
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
-        s_total = acc;
+        if (lane == 63) s_wsum[wv] = x;
+        __syncthreads();
+        int before = 0;
+        for (int k = 0; k < wv; ++k) before += s_wsum[k];
+        s_hist[tid] = before + x - v;
+        if (tid == 1023) s_total = before + x;
+        __syncthreads();
     }
-    __syncthreads();
     for (int w = tid; w < qblocks; w += 1024) {
         const int S = split_of(w);
         const int pos = atomicAdd(&s_hist[bin_of(w, S)], S);
@@ -834,16 +873,18 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
     }
 }
 
-// The filter proper.  A workgroup = 4 waves x QG groups of 32 slots; wave w owns groups
-// w QG .. (w+1) QG - 1 (their bound / pair operands and (best, second, position) in its
-// registers).  The stream tests each of the split's 32-bundle blocks ONCE per workgroup, in the
-// wave (k mod 4) that streams it: one MFMA of the block's 32 bundles against the workgroup's
-// 4 QG group bounds (columns; QG = 4 leaves 16 never-firing), operands straight from L2 four
-// blocks ahead -- no LDS tile, no barrier.  A block that fires for some group is appended to the
-// owning waves' lists (LDS, spilling to `glist`); after one barrier each wave runs its list:
-// per-query bounds of the fired groups, then the pair tests (v1's update).  Partials are
-// written in slot order (nn_finalize_mfma16_kernel reads them through `order`).
-template <int QG>
+// The filter proper, a persistent grid of the resident workgroups taking tasks off the list
+// (bundle_tasks_kernel) until it is empty.  Task (w, s of S_w) = query workgroup w's 4 waves x
+// QG groups of 32 slots (wave v owns groups v QG .. (v+1) QG - 1: their bound / pair operands
+// and (best, second, position) in its registers) against every S_w-th of w's candidate blocks.
+// The stream tests each of those 32-bundle blocks ONCE, in the wave that streams it: one MFMA
+// of the block's 32 bundles against the workgroup's 4 QG group bounds (columns; QG = 4 leaves
+// 16 never-firing), operands straight from L2 four blocks ahead -- no LDS tile, no barrier.  A
+// block that fires for some group is appended to the owning waves' lists (LDS, spilling to
+// `glist`); after one barrier each wave runs its list: per-query bounds of the fired groups,
+// then the pair tests (v1's update).  Partials go to partial set s in slot order
+// (nn_finalize_mfma16_kernel reads S_w sets of them, wsplit).
+template <int QG, int PB>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_bundle2_kernel(
     const BundleQuery *__restrict__ qop, const half8_t *__restrict__ gop, int np, const half8_t *__restrict__ bimg,
     int nb_pad, const int *__restrict__ cand, const int *__restrict__ cand_n, const int2 *__restrict__ tasks,
@@ -1001,17 +1042,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
             uni |= mask;
             n_pairs += __builtin_popcount(mask);
         }
-        while (uni) {
-            int bs[4];
-            half8_t ap[4];
+        while (uni) { // PB pair blocks in flight
+            int bs[PB];
+            half8_t ap[PB];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < PB; ++k) {
                 bs[k] = uni ? __builtin_ctz(uni) : -1;
                 uni &= uni - 1u;
                 if (bs[k] >= 0) ap[k] = pimg[((size_t)bblock * 32 + bs[k]) * 64 + lane];
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < PB; ++k) {
                 if (bs[k] < 0) break;
 #pragma unroll
                 for (int q = 0; q < QG; ++q) {
@@ -1224,8 +1265,8 @@ bool bundle_v2() { return !bundle_v1(); }
 // Tasks: a query workgroup with ncand candidate blocks runs as clamp(ceil(ncand / ch), 1, smax)
 // tasks (bundle_tasks_kernel), on a persistent grid of the resident workgroups.  ICP_BUNDLE_CH /
 // ICP_BUNDLE_SMAX override (A/B).
-constexpr int kB2Ch = 8;
-constexpr int kB2Smax = 16;
+constexpr int kB2Ch = 0; // (automatic: bundle_tasks_kernel)
+constexpr int kB2Smax = 32;
 
 static int env_int(const char *name, int dflt)
 {
@@ -1240,14 +1281,14 @@ NNPlan plan_nn_bundle2(size_t np, int nb_pad)
     pl.q_per_lane = qg;
     pl.qblocks = (int)std::max<size_t>(1, (np + 4 * qg * 32 - 1) / (4 * qg * 32));
     const int nbb = nb_pad >> 5;
-    static const int smax = env_int("ICP_BUNDLE_SMAX", kB2Smax), ch = env_int("ICP_BUNDLE_CH", kB2Ch);
+    static const int smax = env_int("ICP_BUNDLE_SMAX", kB2Smax), ch = env_int("ICP_BUNDLE_CH", kB2Ch); // (0: auto)
     pl.splits = std::max(1, std::min(smax, nbb)); // partial sets (the finalize reads wsplit[w] of them)
     pl.chunk = ch;
     pl.kernel = 200;
     static int cap[2] = {0, 0};
     int &c = cap[qg == 4 ? 0 : 1];
     if (!c) {
-        const void *k = qg == 4 ? (const void *)nn_bundle2_kernel<4> : (const void *)nn_bundle2_kernel<8>;
+        const void *k = qg == 4 ? (const void *)nn_bundle2_kernel<4, 4> : (const void *)nn_bundle2_kernel<8, 4>;
         int dev = 0, cus = 256, per_cu = 2;
         if (hipGetDevice(&dev) == hipSuccess) {
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1270,11 +1311,13 @@ size_t bundle2_list_ints(const NNPlan &pl, int nb_pad) { return (size_t)pl.grid 
 size_t bundle2_task_count(const NNPlan &pl) { return (size_t)pl.qblocks * pl.splits; }
 
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
-                        const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
-                        size_t nslots, void *qop, double4 *qraw, hipStream_t st, const int *stop)
+                        const int *prev, const double4 *m4, const double *seedd, const double c[3], double scale,
+                        const unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
+                        const int *stop)
 {
     bundle_prep_kernel<<<(int)((nslots + kBlock - 1) / kBlock), kBlock, 0, st>>>(
-        px, py, pz, np, pos, prev, m4, c[0], c[1], c[2], scale, seed16, (int)nslots, (BundleQuery *)qop, qraw, stop);
+        px, py, pz, np, pos, prev, m4, seedd, c[0], c[1], c[2], scale, seed16, (int)nslots, (BundleQuery *)qop, qraw,
+        stop);
 }
 
 size_t bundle2_counter_rows(const NNPlan &pl) { return bundle2_task_count(pl) * 4; }
@@ -1308,13 +1351,15 @@ void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bim
                        hipStream_t st, const int *stop, unsigned long long *counters)
 {
     const int grid = pl.grid; // persistent: the resident workgroups pull tasks
-#define LAUNCHB2(QG)                                                                                          \
-    nn_bundle2_kernel<QG><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,             \
+#define LAUNCHB2(QG, PB)                                                                                      \
+    nn_bundle2_kernel<QG, PB><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,             \
                                              (const half8_t *)bimg, nb_pad, cand, cand_n, tasks, tctl,             \
                                              (const half8_t *)pimg, kd_orig, glist, part_best, part_second,        \
                                              part_idx, stop, counters)
-    if (pl.q_per_lane == 4) LAUNCHB2(4);
-    else LAUNCHB2(8);
+    static const int pb = env_int("ICP_BUNDLE_PB", 4); // pair blocks in flight: 4 | 8 (A/B)
+    if (pl.q_per_lane == 4) LAUNCHB2(4, 4);
+    else if (pb == 8) LAUNCHB2(8, 8);
+    else LAUNCHB2(8, 4);
 #undef LAUNCHB2
 }
 

@@ -83,6 +83,9 @@ __device__ __forceinline__ double residual2(double y0, double y1, double y2, dou
 
 // f16 MFMA filter: queries whose scaled |coordinate| exceeds this are clamped and never certified
 constexpr double kF16QueryClamp = 32000.0;
+// every scaled model point b_s has |b_s| below this: the f16 image's scale puts each centred
+// coordinate's magnitude below 2^12 (icp_set_model), and 2^12 sqrt 3 = 7094.6
+constexpr double kF16ModelNormMax = 7095.0;
 
 // Seeds of the seeded f16 filter from the previous correspondences prev[j] (exact fp64):
 // s0 = G(m_prev) + 4 delta_s + 1 (the certificate window above that candidate's value, see

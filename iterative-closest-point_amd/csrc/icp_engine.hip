@@ -285,6 +285,10 @@ struct icp_ctx {
     double4 *b_qraw = nullptr;                // v2: per-slot query coordinates, index, seed
     int *b_glist = nullptr;                   // v2: fired-block list overflow
     double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
+    double *b_seedd = nullptr;                // v2: per point, D64 to its seed (icp_run's transform)
+    char *tail_backup = nullptr;              // icp_run with the fused tail: the starting scene / idx
+    size_t tail_backup_cap = 0;
+    size_t b_seedd_cap = 0;
     int *b_cand = nullptr, *b_cand_n = nullptr; // v2: per filter workgroup, its candidate blocks
     int *b_wsplit = nullptr, *b_tctl = nullptr; // v2: per filter workgroup its tasks; (count, counter)
     int2 *b_tasks = nullptr;                  // v2: the task list
@@ -697,8 +701,11 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                 HIPCHK(hipMemsetAsync(ctx->b_counters, 0, sizeof(unsigned long long) * 9 * ctx->b_counters_rows,
                                       ctx->st));
             }
-            launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4, ctx->c,
-                               ctx->scale16, seeds, nslots, ctx->b_qop, ctx->b_qraw, ctx->st, stop);
+            // (seeds_ready: icp_run's previous transform wrote the seeds, and with them each
+            // point's seed distance, SeedArgs::seedd)
+            launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4,
+                               seeds_ready ? ctx->b_seedd : nullptr, ctx->c, ctx->scale16, seeds, nslots, ctx->b_qop,
+                               ctx->b_qraw, ctx->st, stop);
             launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->b_gctr, ctx->st, stop);
             launch_bundle_candidates(pl, ctx->b_gctr, ctx->b_blk, ctx->nb_pad, ctx->b_cand, ctx->b_cand_n,
                                      ctx->b_wsplit, ctx->b_tasks, ctx->b_tctl, ctx->st, stop);
@@ -1105,7 +1112,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->b_img, (void *)ctx->b_pimg, (void *)ctx->b_kd_orig,
                     (void *)ctx->b_bctr, (void *)ctx->b_blk, (void *)ctx->b_gctr, (void *)ctx->b_cand,
                     (void *)ctx->b_cand_n, (void *)ctx->b_wsplit, (void *)ctx->b_tasks, (void *)ctx->b_tctl,
-                    (void *)ctx->b_kd, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters,
+                    (void *)ctx->b_kd, (void *)ctx->b_seedd, (void *)ctx->tail_backup, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters,
                     (void *)ctx->b_qop, (void *)ctx->b_gop, (void *)ctx->b_qraw, (void *)ctx->b_glist, (void *)ctx->q_pos, (void *)ctx->cr_entries,
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt})
@@ -1632,7 +1639,21 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
 // After the iteration whose err < threshold the device flag freezes the state (the one
 // iteration already enqueued behind it changes nothing), which is exactly where the
 // reference's loop breaks (gpu.cc:79-80).
+static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res, bool no_tail);
+constexpr int kTailAborted = -1000; // run_loop: a fused tail's grid barrier timed out (state restored)
+
 int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res)
+{
+    const int r = run_loop(ctx, max_iter, threshold, err_trace, res, false);
+    if (r != kTailAborted) return r;
+    // A grid barrier of the fused mid-size tail timed out (its workgroups were not all resident:
+    // another process's persistent kernel on the same GPU).  The scene and correspondences the
+    // run started from were restored; the same registration again with the separate launches
+    // (bit-identical, icp_iter.hip) -- the stats count both attempts.
+    return run_loop(ctx, max_iter, threshold, err_trace, res, true);
+}
+
+static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res, bool no_tail)
 {
     TRY(check_ready(ctx, true));
     // alignement_check (gpu.cc:54-62)
@@ -1672,6 +1693,10 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         sa.seed16 = ctx->seed16;
         for (int a = 0; a < 3; ++a) sa.c[a] = ctx->c[a];
         sa.scale = ctx->scale16;
+        if (level1_kind(ctx, n) == 3 && bundle_v2()) { // the bundle filter's seed distances too
+            TRY(grow(ctx, &ctx->b_seedd, &ctx->b_seedd_cap, n));
+            sa.seedd = ctx->b_seedd;
+        }
     }
     int slot_ticket[kRing] = {};
     TRY(grow(ctx, &ctx->err_trace_dev, &ctx->err_trace_cap, (size_t)(max_iter > 0 ? max_iter : 1)));
@@ -1696,15 +1721,25 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         return e && std::strcmp(e, "launches") == 0 ? ICP_RUN_LAUNCHES : -1;
     }();
     const int tail_blocks = red_blocks(n);
-    const bool fused_tail = (forced_mode < 0 ? ctx->run_mode : forced_mode) != ICP_RUN_LAUNCHES && !lag_run(ctx) &&
-                            n > (size_t)kRedSingle && tail_blocks <= kTailMaxBlocks &&
+    const bool fused_tail = !no_tail && (forced_mode < 0 ? ctx->run_mode : forced_mode) != ICP_RUN_LAUNCHES &&
+                            !lag_run(ctx) && n > (size_t)kRedSingle && tail_blocks <= kTailMaxBlocks &&
                             tail_blocks <= ctx->n_cu * 3 / 4;
     unsigned tail_epoch = 0;
+    const bool seeds_at_start = ctx->seeds_valid;
     if (fused_tail) {
         TRY(grow(ctx, &ctx->tail_part, &ctx->tail_part_cap, (size_t)19 * kTailMaxBlocks));
         TRY(grow(ctx, &ctx->tail_sync, &ctx->tail_sync_cap, kPersistSyncWords));
         HIPCHK(hipMemsetAsync(ctx->tail_sync, 0, kPersistSyncWords * sizeof(unsigned), ctx->st));
         ctx->h_flags[11] = 0; // its barriers' abort word (mapped host)
+        // the state the run starts from (n <= kTailMaxBlocks * kBlock points: a few MB), for
+        // the separate-launch rerun should a tail barrier time out
+        TRY(grow(ctx, &ctx->tail_backup, &ctx->tail_backup_cap, n * (3 * sizeof(double) + sizeof(float4) + sizeof(int))));
+        char *bk = ctx->tail_backup;
+        HIPCHK(hipMemcpyAsync(bk, P.x, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->st));
+        HIPCHK(hipMemcpyAsync(bk + n * 8, P.y, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->st));
+        HIPCHK(hipMemcpyAsync(bk + n * 16, P.z, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->st));
+        if (P.f) HIPCHK(hipMemcpyAsync(bk + n * 24, P.f, n * sizeof(float4), hipMemcpyDeviceToDevice, ctx->st));
+        if (seeds_at_start) HIPCHK(hipMemcpyAsync(bk + n * 40, ctx->idx, n * sizeof(int), hipMemcpyDeviceToDevice, ctx->st));
     }
     if (ctx->digest_cap) HIPCHK(hipMemsetAsync(ctx->digest, 0, sizeof(unsigned long long) * 3 * ctx->digest_cap, ctx->st));
     bool ar_timed[kRing] = {};
@@ -1804,6 +1839,10 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
                 ta.h_trace = ctx->d_trace;
                 static const bool split_err = getenv("ICP_TAIL_SPLIT_ERR") != nullptr; // (A/B)
                 ta.sums_out = split_err ? ctx->sums : nullptr;
+                { // tests: ICP_TAIL_TEST_ABORT=1 fails the tail's first barrier (the rerun path)
+                    const char *e = getenv("ICP_TAIL_TEST_ABORT");
+                    ta.test_abort = e && e[0] == '1';
+                }
                 launch_iteration_tail_grid(ta, tail_blocks, ctx->st);
                 LAUNCHCHK("iteration_tail_grid");
                 if (split_err) TRY(enqueue_err_step(enqueued));
@@ -1840,7 +1879,11 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
             continue;
         }
         const int slot = waited % kRing;
-        TRY(wait_flag(ctx, ctx->h_flags + 4 * slot + 2, slot_ticket[slot]));
+        const int wr = wait_flag(ctx, ctx->h_flags + 4 * slot + 2, slot_ticket[slot]);
+        if (wr != ICP_OK) {
+            if (fused_tail && __atomic_load_n(ctx->h_flags + 11, __ATOMIC_ACQUIRE) != 0) break; // (rerun below)
+            return wr;
+        }
         ++waited;
         const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
@@ -1867,8 +1910,17 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
         stop = done != 0;
     }
     HIPCHK(hipStreamSynchronize(ctx->st)); // (the iterations queued behind the last one drain)
-    if (fused_tail && __atomic_load_n(ctx->h_flags + 11, __ATOMIC_ACQUIRE) != 0)
-        return fail(ctx, ICP_E_HIP, "icp_run: a grid barrier of the fused iteration tail timed out");
+    if (fused_tail && __atomic_load_n(ctx->h_flags + 11, __ATOMIC_ACQUIRE) != 0) {
+        const char *bk = ctx->tail_backup;
+        HIPCHK(hipMemcpyAsync(P.x, bk, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->st));
+        HIPCHK(hipMemcpyAsync(P.y, bk + n * 8, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->st));
+        HIPCHK(hipMemcpyAsync(P.z, bk + n * 16, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->st));
+        if (P.f) HIPCHK(hipMemcpyAsync(P.f, bk + n * 24, n * sizeof(float4), hipMemcpyDeviceToDevice, ctx->st));
+        if (seeds_at_start) HIPCHK(hipMemcpyAsync(ctx->idx, bk + n * 40, n * sizeof(int), hipMemcpyDeviceToDevice, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+        ctx->seeds_valid = seeds_at_start;
+        return kTailAborted;
+    }
     return finish_run(ctx, threshold, err_trace, res, wall0);
 }
 

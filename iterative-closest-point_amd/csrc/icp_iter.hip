@@ -975,7 +975,7 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
         __syncthreads();
         if (tid < 17) pub_store(a.part17 + (size_t)b * 18 + tid, loc[tid]); // (18: 16-byte rows)
     }
-    if (!persist_barrier(a.sync, a.epoch_base + 1, a.h_abort, &s_ok)) return;
+    if (!persist_barrier(a.sync, a.epoch_base + 1, a.h_abort, &s_ok, false, a.test_abort != 0)) return;
     tail_fold<17, 18>(a.part17, nb, sums); // reduce_kernel<17>
     // horn_step_kernel (workgroup 0 folds and clears the NN queue counters)
     if (tid == 0) horn_step_body(sums, a.N, a.c0, a.c1, a.c2, 1, b == 0 ? a.cnt : cnt0, &st);
@@ -996,6 +996,10 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
                 if (a.sa.seed16)
                     a.sa.seed16[i] = mfma16_seed_value(q0, q1, q2, a.yx[i], a.yy[i], a.yz[i], a.sa.c[0], a.sa.c[1],
                                                        a.sa.c[2], a.sa.scale);
+                if (a.sa.seedd) { // (transform_err_kernel's seed distance: the bundle filter's prep reads it)
+                    const double dx = q0 - a.yx[i], dy = q1 - a.yy[i], dz = q2 - a.yz[i];
+                    a.sa.seedd[i] = (dx * dx + dy * dy) + dz * dz;
+                }
             }
         }
         block_sum_store<1>(e, loc);

@@ -159,9 +159,12 @@ NNPlan plan_nn_bundle2(size_t np, int nb_pad);
 size_t bundle2_slots(const NNPlan &pl);
 size_t bundle2_list_ints(const NNPlan &pl, int nb_pad);
 size_t bundle2_counter_rows(const NNPlan &pl);
+// seedd (nullable): each query's seed distance D64(p, m[prev]) from the transform (SeedArgs),
+// else gathered here
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
-                        const int *prev, const double4 *m4, const double c[3], double scale, const unsigned *seed16,
-                        size_t nslots, void *qop, double4 *qraw, hipStream_t st, const int *stop = nullptr);
+                        const int *prev, const double4 *m4, const double *seedd, const double c[3], double scale,
+                        const unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
+                        const int *stop = nullptr);
 // gop (nslots bytes): the 32-slot groups' bounds from the records (after the prep); gctr
 // (nslots / 32 double4): the same as (centre, D) for the candidate lists
 void launch_bundle_groups(const void *qop, size_t nslots, void *gop, double4 *gctr, hipStream_t st,
@@ -306,6 +309,7 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
 // when seed16 != nullptr; c / scale = the f16 image's centre and scale
 struct SeedArgs {
     unsigned *seed16 = nullptr;
+    double *seedd = nullptr; // (nullable) D64(p', y) of each point: the bundle filter's seed distance
     double c[3] = {0.0, 0.0, 0.0};
     double scale = 1.0;
 };
@@ -435,6 +439,7 @@ struct TailArgs {
     IterState *h_state;
     double *h_trace;
     double *sums_out; // non-null: write the reduced sums there and leave the error step to a launch
+    int test_abort;   // tests (ICP_TAIL_TEST_ABORT=1): the first barrier fails, as if not co-resident
 };
 constexpr int kTailMaxBlocks = 192; // red_blocks(n) <= this (n <= 49,152): co-resident with room
 void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t st);

@@ -1261,7 +1261,14 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         };
         // shift back to G (fp64 sums of an fp32 and an exact value: relative 2^-53)
         const double bg = (double)b + sh, sg = (double)s2 + sh;
-        const double db = delta(sqrt((double)mms[id]) * (1.0 + 0x1.0p-20));
+        // delta_b = delta(R_b) at an upper bound of the winner's norm R_b = |b~|, without loading
+        // it: G_b <= bg + delta(R_max) (every model point has |b~| < R_max = 2^12 sqrt 3: the
+        // image's scale puts the max |coordinate| below 2^12), so R_b <= A + sqrt(G_b + |a|^2),
+        // Rc's bound one step earlier.  (The gathered |b~| was a dependent random load per
+        // query; the bound is looser by ~2 sqrt(delta(R_max)) in R: ~1 in delta_b at C4.)
+        const double Rb = A * (1.0 + 2.0 * u) +
+                          sqrt(fmax(bg + delta(kF16ModelNormMax) + a2 * (1.0 + 4.0 * u), 0.0) * (1.0 + 0x1.0p-40));
+        const double db = delta(Rb);
         const double Db = fmax(bg + db + a2 * (1.0 + 4.0 * u), 0.0);
         const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
         double T = bg + db + delta(Rc) + 0x1.0p-48 * Db;
@@ -1770,6 +1777,10 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
             if (sa.seed16)
                 sa.seed16[i] = mfma16_seed_value(q0, q1, q2, yx[i], yy[i], yz[i], sa.c[0], sa.c[1], sa.c[2],
                                                  sa.scale);
+            if (sa.seedd) { // (bundle_prep_kernel's seed distance, in its arithmetic: no gather there)
+                const double dx = q0 - yx[i], dy = q1 - yy[i], dz = q2 - yz[i];
+                sa.seedd[i] = (dx * dx + dy * dy) + dz * dz;
+            }
         }
     }
     block_sum_store<1>(a, partials + blockIdx.x);

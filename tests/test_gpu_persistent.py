@@ -332,6 +332,41 @@ def test_first_barrier_abort_falls_back_to_the_launch_loop(amd, pair, monkeypatc
         np.testing.assert_array_equal(ctx.get_scene(), loop[7])
 
 
+def test_fused_tail_barrier_abort_reruns_with_launches(amd, monkeypatch):
+    """the launch loop's fused mid-size tail (moments ... error step in one
+    launch, 4,096 < n <= 49,152) has grid barriers too.  If one times out (its workgroups not all
+    co-resident), icp_run restores the scene and correspondences it started from and runs the
+    registration again with the separate launches.  ICP_PERSIST_TEST_ABORT=1 keeps the one-launch
+    kernel out (the run falls back to the loop, whose tails are then fused) and
+    ICP_TAIL_TEST_ABORT=1 fails the first tail's first barrier: the result must be the launch
+    loop's, bit for bit, and a second run on the same context (seeded by its correspondences)
+    must match the loop's second run too."""
+    m = amd.load_matrix(datasets.path("horse_ref"))
+    p = amd.load_matrix(datasets.path("horse_tr1"))
+    with amd.Context(0) as ctx:
+        ctx.set_run_mode(amd.RUN_LAUNCHES)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        ref1 = ctx.run(12, -1.0)
+        s1, i1 = ctx.get_scene(), ctx.get_indices()
+        ref2 = ctx.run(5, -1.0)
+        s2, i2 = ctx.get_scene(), ctx.get_indices()
+    monkeypatch.setenv("ICP_PERSIST_TEST_ABORT", "1")
+    monkeypatch.setenv("ICP_TAIL_TEST_ABORT", "1")
+    with amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        res, errs = ctx.run(12, -1.0)
+        assert res.iterations == ref1[0].iterations
+        np.testing.assert_array_equal(errs, ref1[1])
+        np.testing.assert_array_equal(ctx.get_scene(), s1)
+        np.testing.assert_array_equal(ctx.get_indices(), i1)
+        res, errs = ctx.run(5, -1.0)
+        np.testing.assert_array_equal(errs, ref2[1])
+        np.testing.assert_array_equal(ctx.get_scene(), s2)
+        np.testing.assert_array_equal(ctx.get_indices(), i2)
+
+
 def test_randomised_bitwise_fuzz(amd):
     """tools/persist_fuzz.py, a short run: random sizes over both one-launch kernels' ranges,
     uniform / surface / clustered / lattice (exact ties) / duplicated models, small to far

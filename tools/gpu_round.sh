@@ -129,8 +129,8 @@ for s in $STEPS; do
                python3 bench.py --variant grid --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases ;;
     bprobe) run bprobe 600 python3 tools/bundle_probe.py --steps 10 --variants mfma16 bundle &&
             run bprobe8 300 python3 tools/bundle_probe.py --steps 10 --shard 8 --variants mfma16 bundle ;;
-    test_bundle) run pytest_bundle 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_c4c5.py -m gpu -x -v -rf \
-               --timeout 300 --timeout-method thread --durations=10 -k "bundle or c4" ;;
+    test_bundle) run pytest_bundle 900 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py tests/test_gpu_c4c5.py -m gpu -x -v -rf \
+               --timeout 300 --timeout-method thread --durations=10 -k "bundle or c4 or split" ;;
     bsweep) for r in 4 2 1; do
                ICP_NN_MIN_ROUNDS=$r ICP_DEBUG_PLAN=1 run bsweep_r$r 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
                ICP_NN_MIN_ROUNDS=$r ICP_DEBUG_PLAN=1 run bsweep8_r$r 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
@@ -163,6 +163,13 @@ for s in $STEPS; do
              for sp in 2 3 4; do
                ICP_BUNDLE_QG=4 ICP_BUNDLE_SPLITS=$sp run bsplitq4_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
              done ;;
+    splitdiag) run splitdiag 60 ./tools/split_probe ;;
+    test_tail) run pytest_tail 300 python -u -m pytest tests/test_gpu_persistent.py -m gpu -x -v -rf --timeout 120 \
+               --timeout-method thread -k "abort" ;;
+    btask3) run bdef 300 python3 tools/bundle_probe.py --steps 20 --variants bundle mfma16 || exit 1
+            run bdef8 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+            run bdef4 300 python3 tools/bundle_probe.py --steps 20 --shard 4 --variants bundle || exit 1
+            run bdef2 300 python3 tools/bundle_probe.py --steps 20 --shard 2 --variants bundle || exit 1 ;;
     btask2) for cfg in "32 16" "64 16" "128 16" "32 32" "64 32" "16 32"; do
              set -- $cfg
              ICP_BUNDLE_CH=$1 ICP_BUNDLE_SMAX=$2 run bt_$1_$2 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
