@@ -255,9 +255,11 @@ int icp_reset_stats(icp_ctx *ctx);
  * the pair tests (32 queries x 32 points each) -- and, summed over the wave tasks (out[7] of
  * them), the 100 MHz clock ticks each spent in its prologue (out[3]), bundle stream (out[4]),
  * deferred fired blocks (out[5]) and epilogue (out[6]), and (out[9]) the largest total of one
- * wave task over all the launches counted; 0 = off (the default; no counting). */
+ * wave task over all the launches counted; within the deferred phase (v2, which waits for each
+ * step's memory while counting) the per-query bound tests (out[10]), the waits for the pair
+ * blocks (out[11]) and the pair tests (out[12]); 0 = off (the default; no counting). */
 int icp_set_bundle_counters(icp_ctx *ctx, int enable);
-int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[10]);
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[16]);
 /* Who this context talks to (evidence for multi-GPU runs): *comm_count / *comm_rank =
  * ncclCommCount / ncclCommUserRank of its RCCL communicator, or -1 / the context's rank when
  * it has none (plain or host all-reduce contexts); bus_id (nullable, len >= 16) = the PCI bus

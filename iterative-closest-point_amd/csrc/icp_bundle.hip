@@ -30,6 +30,7 @@
 #include "icp_kernels.h"
 #include "icp_device.h"
 #include "icp_mfma16.h"
+#include "icp_bundle_rec.h"
 
 #include <algorithm>
 #include <cmath>
@@ -52,44 +53,6 @@ constexpr int kBDmaPerWave = kBBlocksPerTile / 4;     // 2 wave-instructions per
 constexpr int kBVmcntDma = 0x0F70 | kBDmaPerWave;     // vmcnt(2): one tile's DMA may stay in flight
 constexpr int kBQG = 8;                               // 32-query groups per wave
 constexpr int kBPendCap = 64;                         // deferred 32-bundle blocks per wave (LDS)
-constexpr double kBQueryMax = 8192.0;                 // |a_k| range of the bundle operand
-constexpr double kBSeedMax = 11000.0;                 // d' range of the bundle operand
-
-// Query side of the bundle MFMA (see the file header): lane half h of query a (scaled,
-// clamped), seed distance d' (already inflated).  Slots: h = 0: qx hi, lo, hi, qy hi, lo, hi,
-// qz hi, lo; h = 1: qz hi, W hi, W lo, 4096, 4096, d hi, d lo, d hi, with
-// W = (|q^|^2 - d'^2 - mu_q) / 4096.  kBqForced: V^ <= 0 for every bundle (a query outside the
-// operand range); kBqNever: V^ > 0 for every bundle (a slot past the last query).
-enum { kBqNormal = 0, kBqForced = 1, kBqNever = 2 };
-__device__ __forceinline__ half8_t bundle_query_frag(const double a[3], double dq, int mode, int h)
-{
-    _Float16 xh, xl, yh, yl, zh, zl;
-    split_f16(a[0], xh, xl);
-    split_f16(a[1], yh, yl);
-    split_f16(a[2], zh, zl);
-    half8_t b;
-    if (h == 0) {
-        b[0] = xh; b[1] = xl; b[2] = xh; b[3] = yh;
-        b[4] = yl; b[5] = yh; b[6] = zh; b[7] = zl;
-        return b;
-    }
-    const double q0 = (double)xh + (double)xl, q1 = (double)yh + (double)yl, q2 = (double)zh + (double)zl;
-    const double qq = (q0 * q0 + q1 * q1) + q2 * q2;
-    const double mu = 0x1.0p-16 * (qq + dq * dq) + 0x1.0p-4;
-    _Float16 wh, wl, dh, dl;
-    split_f16((qq - dq * dq - mu) / 4096.0, wh, wl);
-    split_f16(dq, dh, dl);
-    if (mode != kBqNormal) { // forced: V^ < -6.7e7 for every bundle; never (no query): V^ > 6.7e7
-        wh = mode == kBqForced ? (_Float16)-65504.0f : (_Float16)65504.0f;
-        wl = (_Float16)0.0f;
-        dh = (_Float16)0.0f;
-        dl = (_Float16)0.0f;
-    }
-    b[0] = zh; b[1] = wh; b[2] = wl; b[3] = (_Float16)4096.0f;
-    b[4] = (_Float16)4096.0f; b[5] = dh; b[6] = dl; b[7] = dh;
-    return b;
-}
-
 // The group bound: one column per 32-query group with the group's centre g^ (f16 hi/lo, the
 // midpoint of its in-range queries' box) and D_g = max over them of (d'_q + |q^ - g^|) (rounded
 // up), in bundle_query_frag's form.  |g^ - c^| > D_g + r' gives, for every query q of the group,
@@ -635,10 +598,6 @@ __global__ __launch_bounds__(kBlock) void build_block_bounds_kernel(const double
 // and, per 32-slot group, the group bound's operand (32 B).  The filter then reads them
 // coalesced; its v1 prologue gathered each query's coordinates, seed and seed point at random,
 // once per split (88 of 256 us per wave at C4, profiles/r03g/).
-struct BundleQuery {
-    half8_t bound[2]; // bundle_query_frag, lane halves 0 / 1
-    half8_t pair[2];  // query_frag (the seeded pair filter's operand)
-};
 
 // Query j's record goes to its slot pos[j] (reads in query order, coalesced but for the seed
 // point m4[prev[j]]; one scattered 64 B + 32 B write); threads past np fill the padding slots
@@ -654,18 +613,13 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
     if (stop && *stop) return;
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= nslots) return;
-    double a[3] = {0.0, 0.0, 0.0}, dq = 0.0;
-    unsigned sd = 0u;
-    int mode = kBqNever, s = t;
-    double4 raw = make_double4(0.0, 0.0, 0.0, __longlong_as_double(-1ll));
+    BundleQuery r;
+    double4 raw;
+    int s = t;
     if (t < np) {
         const int j = t;
         s = pos ? pos[j] : j;
         const double p0 = px[j], p1 = py[j], p2 = pz[j];
-        a[0] = fmin(fmax((p0 - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
-        a[1] = fmin(fmax((p1 - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
-        a[2] = fmin(fmax((p2 - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
-        sd = seed16[j];
         // the seed distance in the reference's arithmetic (compute.cu:112-117): from the transform
         // that moved the point (the same expression over the same values), else gathered
         double D;
@@ -676,19 +630,10 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
             const double dx = p0 - m.x, dy = p1 - m.y, dz = p2 - m.z;
             D = (dx * dx + dy * dy) + dz * dz;
         }
-        const double eq = 0x1.0p-20 * ((fabs(a[0]) + fabs(a[1])) + fabs(a[2])) + 0x1.0p-22;
-        dq = (sqrt(D) * scale * (1.0 + 0x1.0p-40) + 1e-300 + eq) * (1.0 + 0x1.0p-20) + 0x1.0p-20;
-        mode = fabs(a[0]) <= kBQueryMax && fabs(a[1]) <= kBQueryMax && fabs(a[2]) <= kBQueryMax && dq <= kBSeedMax
-                   ? kBqNormal
-                   : kBqForced;
-        raw = make_double4(p0, p1, p2,
-                           __longlong_as_double((long long)(((unsigned long long)sd << 32) | (unsigned)j)));
+        bundle_record(p0, p1, p2, j, D, seed16[j], cx, cy, cz, scale, r, raw);
+    } else {
+        bundle_never_record(r, raw);
     }
-    BundleQuery r;
-    r.bound[0] = bundle_query_frag(a, dq, mode, 0);
-    r.bound[1] = bundle_query_frag(a, dq, mode, 1);
-    r.pair[0] = query_frag(a, 0, sd);
-    r.pair[1] = query_frag(a, 1, sd);
     qop[s] = r;
     qraw[s] = raw;
 }
@@ -890,7 +835,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     int nb_pad, const int *__restrict__ cand, const int *__restrict__ cand_n, const int2 *__restrict__ tasks,
     int *__restrict__ tctl, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int *__restrict__ glist,
     float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx,
-    const int *__restrict__ stop, unsigned long long *__restrict__ counters)
+    const int *__restrict__ stop, unsigned long long *__restrict__ counters, int ilv)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     constexpr int NG = 4 * QG; // groups per workgroup (<= 32: the stream MFMA's columns)
@@ -933,7 +878,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     int bpos[QG];
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
-        const size_t slot = (size_t)(grp0 + wave * QG + q) * 32 + col;
+        const size_t slot = (size_t)(grp0 + (ilv ? q * 4 + wave : wave * QG + q)) * 32 + col;
         bb[q] = qop[slot].bound[h];
         s_bq[wave][q][lane] = qop[slot].pair[h];
         best[q] = 0.0f; // seeded: "nothing below s0'"
@@ -961,7 +906,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         if (__builtin_expect(gm != 0u, 0)) { // (uniform)
 #pragma unroll
             for (int w2 = 0; w2 < 4; ++w2) {
-                const unsigned m8 = (gm >> (QG * w2)) & ((1u << QG) - 1u);
+                unsigned m8 = 0u; // the fired groups wave w2 owns, as its QG-bit mask
+                if (ilv) {
+#pragma unroll
+                    for (int k = 0; k < QG; ++k) m8 |= ((gm >> (4 * k + w2)) & 1u) << k;
+                } else {
+                    m8 = (gm >> (QG * w2)) & ((1u << QG) - 1u);
+                }
                 if (!m8) continue;
                 int e = 0;
                 if (lane == 0) e = atomicAdd(&s_cnt[w2], 1);
@@ -1022,26 +973,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
             best[q] = fminf(best[q], dd[r]);
         }
     };
+    unsigned long long t_bound = 0, t_wait = 0, t_pair = 0, t_mark = 0; // (counters: deferred sub-phases)
+    auto stamp = [&](unsigned long long &acc) {
+        if (counters) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            acc += t - t_mark;
+            t_mark = t;
+        }
+    };
     auto update = [&](const half8_t &a8, int bblock, unsigned gfire) {
         ++n_blocks;
+        if (counters) t_mark = __builtin_amdgcn_s_memrealtime();
         n_groups += __builtin_popcount(gfire);
         unsigned gm[QG], uni = 0u;
 #pragma unroll
         for (int q = 0; q < QG; ++q) {
             gm[q] = 0u;
             if (!((gfire >> q) & 1u)) continue;
-            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a8, bb[q], zero, 0, 0, 0);
-            unsigned mask = 0u;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const unsigned long long bl = __ballot(d[r] <= 0.0f);
-                const int row = (r & 3) + 8 * (r >> 2);
-                mask |= ((unsigned)bl != 0u ? 1u << row : 0u) | ((unsigned)(bl >> 32) != 0u ? 1u << (row + 4) : 0u);
-            }
+            // the group's 32 queries as the rows, the block's 32 bundles as the columns (the same
+            // products): lane l holds bundle l mod 32 against 16 of the queries, so ONE ballot of
+            // the lanes' minima gives the bundles any query needs (16 ballots the other way round)
+            const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(bb[q], a8, zero, 0, 0, 0);
+            const unsigned long long bl = __ballot(min16v(d) <= 0.0f);
+            const unsigned mask = (unsigned)bl | (unsigned)(bl >> 32);
             gm[q] = mask;
             uni |= mask;
             n_pairs += __builtin_popcount(mask);
         }
+        stamp(t_bound);
         while (uni) { // PB pair blocks in flight
             int bs[PB];
             half8_t ap[PB];
@@ -1051,6 +1011,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
                 uni &= uni - 1u;
                 if (bs[k] >= 0) ap[k] = pimg[((size_t)bblock * 32 + bs[k]) * 64 + lane];
             }
+            stamp(t_wait);
 #pragma unroll
             for (int k = 0; k < PB; ++k) {
                 if (bs[k] < 0) break;
@@ -1062,6 +1023,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
                     pair_update(q, dd, bblock * 32 + bs[k]);
                 }
             }
+            stamp(t_pair);
         }
     };
     {
@@ -1088,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     // (counters: this wave task's own row of 9, accumulated over launches without atomics --
     // a same-address atomic per wave serialised and tripled the launch)
     unsigned long long *crow =
-        counters ? counters + 9 * ((size_t)t * 4 + wave) : nullptr;
+        counters ? counters + kBundleCounterFields * ((size_t)t * 4 + wave) : nullptr;
     if (crow && lane == 0) {
         crow[0] += n_blocks;
         crow[1] += n_groups;
@@ -1098,6 +1060,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         crow[5] += t_defer - t_stream;
         crow[7] += 1ull;
         crow[8] += (unsigned long long)nk; // stream MFMAs of this wave
+        crow[9] += t_bound;
+        crow[10] += t_wait;
+        crow[11] += t_pair;
     }
     // the two lane halves' (best, second, position) per query, then all QG original indices
     // gathered at once (one dependent load per wave, not one per group)
@@ -1125,7 +1090,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     for (int q = 0; q < QG; ++q) eo[q] = eo[q] >= 0 ? kd_orig[eo[q]] : -1;
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
-        const int slot = (grp0 + wave * QG + q) * 32 + col;
+        const int slot = (grp0 + (ilv ? q * 4 + wave : wave * QG + q)) * 32 + col;
         if (h == 0 && slot < np) { // slot order (coalesced)
             const size_t o = (size_t)split * np + slot;
             part_best[o] = eb[q];
@@ -1355,8 +1320,10 @@ void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bim
     nn_bundle2_kernel<QG, PB><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,             \
                                              (const half8_t *)bimg, nb_pad, cand, cand_n, tasks, tctl,             \
                                              (const half8_t *)pimg, kd_orig, glist, part_best, part_second,        \
-                                             part_idx, stop, counters)
+                                             part_idx, stop, counters, ilv)
     static const int pb = env_int("ICP_BUNDLE_PB", 4); // pair blocks in flight: 4 | 8 (A/B)
+    // wave v owns groups v, v + 4, ... of its workgroup (ICP_BUNDLE_ILV=1) or v QG .. (v+1) QG - 1
+    static const int ilv = env_int("ICP_BUNDLE_ILV", 2) == 1 ? 1 : 0;
     if (pl.q_per_lane == 4) LAUNCHB2(4, 4);
     else if (pb == 8) LAUNCHB2(8, 8);
     else LAUNCHB2(8, 4);

@@ -284,11 +284,11 @@ struct icp_ctx {
     char *b_qop = nullptr, *b_gop = nullptr;  // v2: per-slot query operands, per-group bounds
     double4 *b_qraw = nullptr;                // v2: per-slot query coordinates, index, seed
     int *b_glist = nullptr;                   // v2: fired-block list overflow
-    double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
     double *b_seedd = nullptr;                // v2: per point, D64 to its seed (icp_run's transform)
+    size_t b_seedd_cap = 0;
     char *tail_backup = nullptr;              // icp_run with the fused tail: the starting scene / idx
     size_t tail_backup_cap = 0;
-    size_t b_seedd_cap = 0;
+    double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
     int *b_cand = nullptr, *b_cand_n = nullptr; // v2: per filter workgroup, its candidate blocks
     int *b_wsplit = nullptr, *b_tctl = nullptr; // v2: per filter workgroup its tasks; (count, counter)
     int2 *b_tasks = nullptr;                  // v2: the task list
@@ -687,18 +687,20 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             TRY(grow(ctx, &ctx->b_qraw, &ctx->b_qraw_cap, nslots));
             TRY(grow(ctx, &ctx->b_gop, &ctx->b_gop_cap, nslots));
             TRY(grow(ctx, &ctx->b_glist, &ctx->b_glist_cap, bundle2_list_ints(pl, ctx->nb_pad)));
-            TRY(grow(ctx, &ctx->b_gctr, &ctx->b_gctr_cap, nslots / 32));
             TRY(grow(ctx, &ctx->b_cand, &ctx->b_cand_cap, (size_t)pl.qblocks * (ctx->nb_pad >> 5)));
             TRY(grow(ctx, &ctx->b_cand_n, &ctx->b_cand_n_cap, (size_t)pl.qblocks));
             TRY(grow(ctx, &ctx->b_wsplit, &ctx->b_wsplit_cap, (size_t)pl.qblocks));
             TRY(grow(ctx, &ctx->b_tasks, &ctx->b_tasks_cap, bundle2_task_count(pl)));
             TRY(grow(ctx, &ctx->b_tctl, &ctx->b_tctl_cap, 2));
+            TRY(grow(ctx, &ctx->b_gctr, &ctx->b_gctr_cap, nslots / 32));
             if (ctx->b_counters && ctx->b_counters_rows < bundle2_counter_rows(pl)) { // (per-wave rows)
                 HIPCHK(hipFree(ctx->b_counters));
                 ctx->b_counters = nullptr;
                 ctx->b_counters_rows = bundle2_counter_rows(pl);
-                HIPCHK(hipMalloc((void **)&ctx->b_counters, sizeof(unsigned long long) * 9 * ctx->b_counters_rows));
-                HIPCHK(hipMemsetAsync(ctx->b_counters, 0, sizeof(unsigned long long) * 9 * ctx->b_counters_rows,
+                HIPCHK(hipMalloc((void **)&ctx->b_counters,
+                                 sizeof(unsigned long long) * kBundleCounterFields * ctx->b_counters_rows));
+                HIPCHK(hipMemsetAsync(ctx->b_counters, 0,
+                                      sizeof(unsigned long long) * kBundleCounterFields * ctx->b_counters_rows,
                                       ctx->st));
             }
             // (seeds_ready: icp_run's previous transform wrote the seeds, and with them each
@@ -1050,26 +1052,29 @@ int icp_set_bundle_counters(icp_ctx *ctx, int enable)
     // (rows: one for v1's shared counters, per wave task for v2; sized at the next search)
     if (!ctx->b_counters) {
         ctx->b_counters_rows = 1;
-        HIPCHK(hipMalloc((void **)&ctx->b_counters, 9 * sizeof(unsigned long long)));
+        HIPCHK(hipMalloc((void **)&ctx->b_counters, kBundleCounterFields * sizeof(unsigned long long)));
     }
-    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, 9 * sizeof(unsigned long long) * ctx->b_counters_rows, ctx->st));
+    HIPCHK(hipMemsetAsync(ctx->b_counters, 0, kBundleCounterFields * sizeof(unsigned long long) * ctx->b_counters_rows,
+                          ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
 }
 
-int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[10])
+int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[16])
 {
     if (!ctx || !out) return ICP_E_ARG;
-    for (int k = 0; k < 10; ++k) out[k] = 0;
+    for (int k = 0; k < 16; ++k) out[k] = 0;
     if (!ctx->b_counters) return ICP_OK;
     HIPCHK(hipSetDevice(ctx->device));
-    std::vector<unsigned long long> v(9 * ctx->b_counters_rows);
+    constexpr int F = kBundleCounterFields;
+    std::vector<unsigned long long> v(F * ctx->b_counters_rows);
     HIPCHK(hipMemcpyAsync(v.data(), ctx->b_counters, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost,
                           ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     for (size_t r = 0; r < ctx->b_counters_rows; ++r) {
-        for (int k = 0; k < 9; ++k) out[k] += v[9 * r + k];
-        const uint64_t t = v[9 * r + 3] + v[9 * r + 4] + v[9 * r + 5] + v[9 * r + 6];
+        for (int k = 0; k < 9; ++k) out[k] += v[F * r + k];
+        for (int k = 9; k < F; ++k) out[k + 1] += v[F * r + k]; // (out[9]: the slowest task)
+        const uint64_t t = v[F * r + 3] + v[F * r + 4] + v[F * r + 5] + v[F * r + 6];
         out[9] = std::max<uint64_t>(out[9], t); // the slowest wave task's clock ticks
     }
     return ICP_OK;
@@ -1760,12 +1765,13 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         return e ? std::max(1, atoi(e)) : 0;
     }();
     const int timing_stride = forced_stride ? forced_stride : ((double)n * (double)ctx->nm >= kTimedPairs ? 1 : 8);
-    auto enqueue_err_step = [&](int it) -> int {
+    // (partials: the residual's unreduced rows, folded in the same launch)
+    auto enqueue_err_step = [&](int it, const double *partials = nullptr) -> int {
         const int sl = it % kRing;
         // (done, iter) straight into mapped host memory, then the slot's ticket
         slot_ticket[sl] = ++ctx->flag_ticket;
         launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->d_flags + 4 * sl,
-                        slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace, ctx->st);
+                        slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace, ctx->st, partials, red_blocks(n));
         LAUNCHCHK("err_step");
         return ICP_OK;
     };
@@ -1867,10 +1873,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
             launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f,
                                      red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
-            red_finish(ctx, n, 1, ctx->sums + kSumErr);
+            const bool fold_err = !lag && red_blocks(n) > 1; // (folded by the error step's launch)
+            if (!fold_err) red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
-            if (!lag) TRY(enqueue_err_step(enqueued));
+            if (!lag) TRY(enqueue_err_step(enqueued, fold_err ? ctx->partials : nullptr));
             ++enqueued;
             if (lag && enqueued == max_iter) { // the last residual has no next iteration to ride on
                 TRY(allreduce(ctx, ctx->sums + kSumErr, 1));

@@ -948,6 +948,24 @@ template <int K, int S = K> __device__ __forceinline__ void tail_fold(const doub
     __syncthreads();
 }
 
+// reduce_kernel<1> + err_step_kernel in one workgroup (tail_fold: reduce_kernel's order, bit
+// for bit): one launch fewer per iteration of a one-rank run (reduce 4.6 + err step 4.6 us ->
+// 4.3 us at C4, profiles/r03y/; the same for reduce_kernel<17> + the Horn step measured slower,
+// 17.6 against 7.0 + 5.7 us, and is not used).
+__global__ __launch_bounds__(kBlock) void reduce_err_kernel(const double *__restrict__ partials, int nblocks,
+                                                            double *__restrict__ sums, double N, double threshold,
+                                                            int max_iter, double *__restrict__ err_trace,
+                                                            IterState *__restrict__ s, int *hflag, int ticket,
+                                                            IterState *h_state, double *h_trace)
+{
+    __shared__ double loc[1];
+    tail_fold<1>(partials, nblocks, loc);
+    if (threadIdx.x == 0) {
+        sums[kSumErr] = loc[0];
+        err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
 {
     __shared__ IterState st;
@@ -1756,12 +1774,16 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], int
     horn_step_kernel<<<1, 1, 0, st>>>(sums, n_total, c[0], c[1], c[2], shifted, amb_count, st_dev);
 }
 
-void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
+void launch_err_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                      IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
-                     hipStream_t st)
+                     hipStream_t st, const double *partials, int nblocks)
 {
-    err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, st_dev, hflag_dev, ticket,
-                                     h_state_dev, h_trace_dev);
+    if (partials)
+        reduce_err_kernel<<<1, kBlock, 0, st>>>(partials, nblocks, sums, n_total, threshold, max_iter, err_trace,
+                                                st_dev, hflag_dev, ticket, h_state_dev, h_trace_dev);
+    else
+        err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, st_dev, hflag_dev, ticket,
+                                         h_state_dev, h_trace_dev);
 }
 
 void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, double *py, double *pz, int n,

@@ -154,6 +154,8 @@ void launch_nn_bundle(const double *px, const double *py, const double *pz, int 
 // blocks barrier-free; glist: bundle2_list_ints(plan, nb_pad) ints of fired-block list overflow;
 // counters (nullable): 9 x bundle2_counter_rows(plan) per-wave rows.  Partials in slot order:
 // finalize with launch_nn_finalize_mfma16(..., qraw).
+// u64 fields per counter row (icp_set_bundle_counters): 9 of v1's shared row, 12 per v2 wave task
+constexpr int kBundleCounterFields = 12;
 bool bundle_v2();
 NNPlan plan_nn_bundle2(size_t np, int nb_pad);
 size_t bundle2_slots(const NNPlan &pl);
@@ -309,7 +311,10 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
 // when seed16 != nullptr; c / scale = the f16 image's centre and scale
 struct SeedArgs {
     unsigned *seed16 = nullptr;
-    double *seedd = nullptr; // (nullable) D64(p', y) of each point: the bundle filter's seed distance
+    // (nullable) D64(p', y) of each moved point: the next search's seed distance, which
+    // bundle_prep_kernel would otherwise gather (writing the whole records here instead made
+    // transform_err_kernel 20 -> 74 us at C4 against the prep's 47: profiles/r03x/)
+    double *seedd = nullptr;
     double c[3] = {0.0, 0.0, 0.0};
     double scale = 1.0;
 };
@@ -347,9 +352,10 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], int
 // (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold
 // or iter == max_iter; a recorded iteration is mirrored to mapped host memory (h_state, h_trace[iter]);
 // finally hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope, mapped host memory)
-void launch_err_step(const double *sums, double n_total, double threshold, int max_iter, double *err_trace,
+// partials (nullable): reduce_kernel<1>'s input (nblocks rows), folded into sums[kSumErr] first
+void launch_err_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                      IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
-                     hipStream_t st);
+                     hipStream_t st, const double *partials = nullptr, int nblocks = 0);
 // iterations >= 2 of a <= kRedSingle-point single-rank run, after the NN search: moments,
 // Horn step, transform + residual and error step in one workgroup (same arithmetic)
 void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, double *py, double *pz, int n,

@@ -2165,7 +2165,9 @@ void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *
                        const float4 *m32, const double *mx, const double *my, const double *mz,
                        int nm, int max_items, int *idx, hipStream_t st, const int *stop)
 {
-    int grid = max_items < 2048 ? max_items : 2048;
+    // (one workgroup per CU, grid-striding over the device-side count: the launch is on every
+    // search's path and usually finds nothing to do -- 2,048 idle workgroups cost ~4.6 us)
+    int grid = max_items < 256 ? max_items : 256;
     if (grid < 1) grid = 1;
     nn_resolve_kernel<<<grid, kBlock, 0, st>>>(amb_count, amb_list, amb_T, p32, px, py, pz, m32, mx,
                                                 my, mz, nm, idx, stop);

@@ -416,13 +416,16 @@ class Context:
 
     def bundle_counters(self) -> dict:
         """The bundle filter's executed work since set_bundle_counters(True)."""
-        out = (C.c_uint64 * 10)()
+        out = (C.c_uint64 * 16)()
         self._check(lib().icp_get_bundle_counters(self._h, out))
         tasks = max(int(out[7]), 1)
         return {"stream_mfma": int(out[8]), "block_triggers": int(out[0]), "group_tests": int(out[1]),
                 "pair_tests": int(out[2]), "wave_tasks": int(out[7]),
                 "us_per_wave_task": {"prologue": out[3] * 0.01 / tasks, "stream": out[4] * 0.01 / tasks,
                                      "deferred": out[5] * 0.01 / tasks, "epilogue": out[6] * 0.01 / tasks},
+                "deferred_us_per_wave_task": {"bound_tests": out[10] * 0.01 / tasks,
+                                              "pair_block_waits": out[11] * 0.01 / tasks,
+                                              "pair_tests": out[12] * 0.01 / tasks},
                 "slowest_task_us_total": out[9] * 0.01}
 
     def comm_info(self) -> dict:

@@ -69,9 +69,12 @@ def main():
             nb = (m.shape[0] + 31) // 32
             rec["per_iteration"] = {k: v_ / it for k, v_ in cnt.items() if not isinstance(v_, dict)}
             rec["us_per_wave_task"] = cnt["us_per_wave_task"]
+            rec["deferred_us_per_wave_task"] = cnt.get("deferred_us_per_wave_task")
             rec["slowest_task_us"] = cnt["slowest_task_us_total"] / it
             pi = rec["per_iteration"]
-            rec["executed_mfma_per_it"] = pi["stream_mfma"] + pi["block_triggers"] + pi["group_tests"] + pi["pair_tests"]
+            # (v1 re-issued each fired block's stream test; v2 does not)
+            reissued = pi["block_triggers"] if os.environ.get("ICP_BUNDLE_KERNEL") == "1" else 0.0
+            rec["executed_mfma_per_it"] = pi["stream_mfma"] + reissued + pi["group_tests"] + pi["pair_tests"]
             rec["executed_tflops"] = 32768.0 * rec["executed_mfma_per_it"] / (rec["nn_kernel_ms"] * 1e-3) / 1e12
         print(json.dumps(rec), flush=True)
     names = list(runs)

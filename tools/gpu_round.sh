@@ -166,6 +166,21 @@ for s in $STEPS; do
     splitdiag) run splitdiag 60 ./tools/split_probe ;;
     test_tail) run pytest_tail 300 python -u -m pytest tests/test_gpu_persistent.py -m gpu -x -v -rf --timeout 120 \
                --timeout-method thread -k "abort" ;;
+    test_cert) run pytest_cert 600 python -u -m pytest tests/test_gpu_cert_stress.py tests/test_gpu_persistent.py -m gpu -x -v -rf \
+               --timeout 300 --timeout-method thread -k "cert or scale_fuzz" ;;
+    bpb) for pb in 4 8 4 8; do
+           ICP_BUNDLE_PB=$pb run bpb_$pb 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+           ICP_BUNDLE_PB=$pb run bpb8_$pb 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+           cat $OUT/bpb_$pb.log $OUT/bpb8_$pb.log >> $OUT/bpb_all_$pb.log
+         done ;;
+    bilv) for il in 1 0 1 0; do
+            ICP_BUNDLE_ILV=$il run bilv_$il 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+            ICP_BUNDLE_ILV=$il run bilv8_$il 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+            cat $OUT/bilv_$il.log $OUT/bilv8_$il.log >> $OUT/bilv_all_$il.log
+          done
+          for sm in 64 128; do
+            ICP_BUNDLE_SMAX=$sm run bsm8_$sm 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+          done ;;
     btask3) run bdef 300 python3 tools/bundle_probe.py --steps 20 --variants bundle mfma16 || exit 1
             run bdef8 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
             run bdef4 300 python3 tools/bundle_probe.py --steps 20 --shard 4 --variants bundle || exit 1
