@@ -52,58 +52,8 @@ constexpr int kBBlocksPerTile = kBTile / 32;          // 8 bundle blocks of 32 b
 constexpr int kBDmaPerWave = kBBlocksPerTile / 4;     // 2 wave-instructions per tile
 constexpr int kBVmcntDma = 0x0F70 | kBDmaPerWave;     // vmcnt(2): one tile's DMA may stay in flight
 constexpr int kBQG = 8;                               // 32-query groups per wave
+constexpr int kTaskQueues = 8, kTaskQueueStride = 32; // nn_bundle2_kernel's task queues (tctl)
 constexpr int kBPendCap = 64;                         // deferred 32-bundle blocks per wave (LDS)
-// The group bound: one column per 32-query group with the group's centre g^ (f16 hi/lo, the
-// midpoint of its in-range queries' box) and D_g = max over them of (d'_q + |q^ - g^|) (rounded
-// up), in bundle_query_frag's form.  |g^ - c^| > D_g + r' gives, for every query q of the group,
-// |q^ - c^| >= |g^ - c^| - |q^ - g^| > d'_q + r', so a bundle the group excludes is excluded for
-// each of its queries (same margins: V^ > 0 => V > 0).  A group with a kBqForced query is
-// forced; one without in-range queries never fires.  Reductions over the 32 lanes of each half
-// (lane and lane + 32 hold the same query).  Returns this lane's operand half for its group.
-struct GroupBound {
-    double g[3], D;
-    int mode;
-};
-// the group of the 32-lane half `gh` (its lanes' queries q^ = hi + lo as the MFMA sees them,
-// d', mode)
-__device__ __forceinline__ GroupBound bundle_group_hat(const double q[3], double dq, int mode, int gh)
-{
-    const bool in = mode == kBqNormal;
-    double lo3[3], hi3[3];
-    for (int k = 0; k < 3; ++k) {
-        lo3[k] = in ? q[k] : INFINITY;
-        hi3[k] = in ? q[k] : -INFINITY;
-    }
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1)
-        for (int k = 0; k < 3; ++k) {
-            lo3[k] = fmin(lo3[k], __shfl_xor(lo3[k], o, 64));
-            hi3[k] = fmax(hi3[k], __shfl_xor(hi3[k], o, 64));
-        }
-    const unsigned long long forced = __ballot(mode == kBqForced), normal = __ballot(in);
-    const unsigned half_mask = gh ? (unsigned)(forced >> 32) : (unsigned)forced;
-    const unsigned half_norm = gh ? (unsigned)(normal >> 32) : (unsigned)normal;
-    double g[3];
-    for (int k = 0; k < 3; ++k) {
-        const double c = half_norm ? 0.5 * (lo3[k] + hi3[k]) : 0.0;
-        _Float16 gh, gl;
-        split_f16(c, gh, gl);
-        g[k] = (double)gh + (double)gl;
-    }
-    const double e0 = q[0] - g[0], e1 = q[1] - g[1], e2 = q[2] - g[2];
-    double D = in ? (dq + sqrt((e0 * e0 + e1 * e1) + e2 * e2) * (1.0 + 0x1.0p-48)) * (1.0 + 0x1.0p-48) : 0.0;
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) D = fmax(D, __shfl_xor(D, o, 64));
-    int gmode = half_mask ? kBqForced : half_norm ? kBqNormal : kBqNever;
-    if (gmode == kBqNormal && !(fabs(g[0]) <= kBQueryMax && fabs(g[1]) <= kBQueryMax && fabs(g[2]) <= kBQueryMax &&
-                                D <= kBSeedMax))
-        gmode = kBqForced;
-    GroupBound r;
-    for (int k = 0; k < 3; ++k) r.g[k] = g[k];
-    r.D = D;
-    r.mode = gmode;
-    return r;
-}
 // the same from the (clamped, scaled) queries a
 __device__ __forceinline__ GroupBound bundle_group(const double a[3], double dq, int mode, int gh)
 {
@@ -608,11 +558,11 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
     const int *__restrict__ pos, const int *__restrict__ prev, const double4 *__restrict__ m4,
     const double *__restrict__ seedd, double cx, double cy, double cz, double scale,
     const unsigned *__restrict__ seed16, int nslots, BundleQuery *__restrict__ qop, double4 *__restrict__ qraw,
-    const int *__restrict__ stop)
+    const int *__restrict__ stop, half8_t *__restrict__ gop, double4 *__restrict__ gctr)
 {
     if (stop && *stop) return;
     const int t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= nslots) return;
+    if (t >= nslots) return; // (nslots: whole workgroups, so whole waves stay for the group step)
     BundleQuery r;
     double4 raw;
     int s = t;
@@ -635,7 +585,10 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
         bundle_never_record(r, raw);
     }
     qop[s] = r;
-    qraw[s] = raw;
+    if (qraw) qraw[s] = raw; // (null: the slots are the queries in order, the certificate reads p)
+    // gop (pos == null: slot = thread): the group bounds from the records in registers, as
+    // bundle_group_kernel would from memory
+    if (gop) bundle_group_store(r, s, nslots, gop, gctr);
 }
 
 // The group bounds, one thread per slot (a 32-lane half = one group), from the slot records:
@@ -649,17 +602,7 @@ __global__ __launch_bounds__(kBlock) void bundle_group_kernel(const BundleQuery 
 {
     if (stop && *stop) return;
     const int s = blockIdx.x * kBlock + threadIdx.x; // (nslots: whole workgroups of slots)
-    const int lane = threadIdx.x & 63;
-    const half8_t b0 = qop[s].bound[0], b1 = qop[s].bound[1];
-    const double q[3] = {(double)b0[0] + (double)b0[1], (double)b0[3] + (double)b0[4], (double)b0[6] + (double)b0[7]};
-    const double d = (double)b1[5] + (double)b1[6];
-    const float w = (float)b1[1];
-    const int mode = w == -65504.0f ? kBqForced : w == 65504.0f ? kBqNever : kBqNormal;
-    const GroupBound gb = bundle_group_hat(q, d * (1.0 + 0x1.0p-20) + 0x1.0p-20, mode, lane >> 5);
-    if ((lane & 31) < 2 && s < nslots) gop[(s >> 5) * 2 + (lane & 31)] = bundle_query_frag(gb.g, gb.D, gb.mode, lane & 31);
-    if ((lane & 31) == 0 && s < nslots)
-        gctr[s >> 5] = make_double4(gb.g[0], gb.g[1], gb.g[2],
-                                    gb.mode == kBqNormal ? gb.D : gb.mode == kBqForced ? INFINITY : -1.0);
+    bundle_group_store(qop[s], s, nslots, gop, gctr);
 }
 
 // The candidate blocks of each filter workgroup (4 QG groups of 32 slots): the workgroup's
@@ -746,8 +689,8 @@ constexpr int kB2ListCap = 128; // LDS entries of a wave's fired-block list (the
 // tasks (w, s), s < S_w, each taking every S_w-th of w's candidate blocks; tasks are ordered by
 // their candidate count, largest first (a counting sort in LDS; the order within one count is
 // the LDS atomics' and does not matter: a task's outputs go to fixed places), so that the
-// persistent filter starts the long tasks first.  tctl = (number of tasks, the filter's task
-// counter, reset here); wsplit[w] = S_w for the finalize.  One workgroup of 1024 threads.
+// persistent filter starts the long tasks first.  tctl = (number of tasks, then the filter's
+// kTaskQueues task counters, reset here); wsplit[w] = S_w for the finalize.  One workgroup of 1024 threads.
 constexpr int kTaskBins = 1024;
 // Candidates per task (ch <= 0: automatic): C4's 57,380 candidates ran the filter in 0.219 /
 // 0.208 / 0.199 / 0.203 ms at 16 / 32 / 64 / 128 per task, the W = 8 shard's 22,984 in 0.112 /
@@ -812,10 +755,8 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
         const int pos = atomicAdd(&s_hist[bin_of(w, S)], S);
         for (int sp = 0; sp < S; ++sp) tasks[pos + sp] = make_int2(w, sp | (S << 16));
     }
-    if (tid == 0) {
-        tctl[0] = s_total;
-        tctl[1] = 0;
-    }
+    if (tid == 0) tctl[0] = s_total;
+    if (tid < kTaskQueues) tctl[kTaskQueueStride * (tid + 1)] = 0; // (the queues' counters)
 }
 
 // The filter proper, a persistent grid of the resident workgroups taking tasks off the list
@@ -852,7 +793,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
     int *const gl = glist + (size_t)blockIdx.x * 4 * nbb;
     const int nkmax = nbb;
     for (;;) { // tasks (query workgroup w, split s of S_w), heaviest first (bundle_tasks_kernel)
-    if (tid == 0) s_task = atomicAdd(&tctl[1], 1);
+    // task t = q + kTaskQueues k from queue q = blockIdx.x mod kTaskQueues (the XCD the dispatcher
+    // placed this workgroup on): one counter per queue, each on its own 128 B line, so the
+    // same-address device atomics (~12 ns each, serialised) spread over eight addresses; every
+    // queue is a heaviest-first subsequence of the list
+    if (tid == 0) { // (a grid of fewer workgroups than queues uses as many queues as it has)
+        const int nq = (int)min(gridDim.x, (unsigned)kTaskQueues), q = (int)(blockIdx.x % (unsigned)nq);
+        s_task = q + nq * atomicAdd(&tctl[kTaskQueueStride * (q + 1)], 1);
+    }
     __syncthreads();
     const int t = s_task;
     if (t >= ntasks) break; // (uniform)
@@ -1260,6 +1208,8 @@ NNPlan plan_nn_bundle2(size_t np, int nb_pad)
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kBlock, 0) != hipSuccess || per_cu < 1)
                 per_cu = 2;
         }
+        static const int forced_per_cu = env_int("ICP_BUNDLE_PER_CU", 0); // (A/B: workgroups per CU)
+        if (forced_per_cu > 0) per_cu = forced_per_cu;
         c = std::max(1, cus * per_cu);
     }
     pl.grid = c; // (persistent: the resident workgroups)
@@ -1278,11 +1228,12 @@ size_t bundle2_task_count(const NNPlan &pl) { return (size_t)pl.qblocks * pl.spl
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
                         const int *prev, const double4 *m4, const double *seedd, const double c[3], double scale,
                         const unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
-                        const int *stop)
+                        const int *stop, void *gop, double4 *gctr)
 {
+    if (pos) gop = nullptr, gctr = nullptr; // (a scattered slot order: bundle_group_kernel after)
     bundle_prep_kernel<<<(int)((nslots + kBlock - 1) / kBlock), kBlock, 0, st>>>(
         px, py, pz, np, pos, prev, m4, seedd, c[0], c[1], c[2], scale, seed16, (int)nslots, (BundleQuery *)qop, qraw,
-        stop);
+        stop, (half8_t *)gop, gctr);
 }
 
 size_t bundle2_counter_rows(const NNPlan &pl) { return bundle2_task_count(pl) * 4; }

@@ -87,5 +87,74 @@ __device__ __forceinline__ void bundle_never_record(BundleQuery &r, double4 &raw
     r.pair[1] = query_frag(a, 1, 0u);
 }
 
+// The group bound: one column per 32-query group with the group's centre g^ (f16 hi/lo, the
+// midpoint of its in-range queries' box) and D_g = max over them of (d'_q + |q^ - g^|) (rounded
+// up), in bundle_query_frag's form.  |g^ - c^| > D_g + r' gives, for every query q of the group,
+// |q^ - c^| >= |g^ - c^| - |q^ - g^| > d'_q + r', so a bundle the group excludes is excluded for
+// each of its queries (same margins: V^ > 0 => V > 0).  A group with a kBqForced query is
+// forced; one without in-range queries never fires.  Reductions over the 32 lanes of each half
+// (lane and lane + 32 hold the same query).  Returns this lane's operand half for its group.
+struct GroupBound {
+    double g[3], D;
+    int mode;
+};
+// the group of the 32-lane half `gh` (its lanes' queries q^ = hi + lo as the MFMA sees them,
+// d', mode)
+__device__ __forceinline__ GroupBound bundle_group_hat(const double q[3], double dq, int mode, int gh)
+{
+    const bool in = mode == kBqNormal;
+    double lo3[3], hi3[3];
+    for (int k = 0; k < 3; ++k) {
+        lo3[k] = in ? q[k] : INFINITY;
+        hi3[k] = in ? q[k] : -INFINITY;
+    }
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1)
+        for (int k = 0; k < 3; ++k) {
+            lo3[k] = fmin(lo3[k], __shfl_xor(lo3[k], o, 64));
+            hi3[k] = fmax(hi3[k], __shfl_xor(hi3[k], o, 64));
+        }
+    const unsigned long long forced = __ballot(mode == kBqForced), normal = __ballot(in);
+    const unsigned half_mask = gh ? (unsigned)(forced >> 32) : (unsigned)forced;
+    const unsigned half_norm = gh ? (unsigned)(normal >> 32) : (unsigned)normal;
+    double g[3];
+    for (int k = 0; k < 3; ++k) {
+        const double c = half_norm ? 0.5 * (lo3[k] + hi3[k]) : 0.0;
+        _Float16 gh, gl;
+        split_f16(c, gh, gl);
+        g[k] = (double)gh + (double)gl;
+    }
+    const double e0 = q[0] - g[0], e1 = q[1] - g[1], e2 = q[2] - g[2];
+    double D = in ? (dq + sqrt((e0 * e0 + e1 * e1) + e2 * e2) * (1.0 + 0x1.0p-48)) * (1.0 + 0x1.0p-48) : 0.0;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) D = fmax(D, __shfl_xor(D, o, 64));
+    int gmode = half_mask ? kBqForced : half_norm ? kBqNormal : kBqNever;
+    if (gmode == kBqNormal && !(fabs(g[0]) <= kBQueryMax && fabs(g[1]) <= kBQueryMax && fabs(g[2]) <= kBQueryMax &&
+                                D <= kBSeedMax))
+        gmode = kBqForced;
+    GroupBound r;
+    for (int k = 0; k < 3; ++k) r.g[k] = g[k];
+    r.D = D;
+    r.mode = gmode;
+    return r;
+}
+// group g = s / 32's bound from the record of this lane's slot s (lane = threadIdx.x & 63: the
+// wave's two 32-lane halves are two groups); every lane of the wave takes part
+__device__ __forceinline__ void bundle_group_store(const BundleQuery &rec, int s, int nslots, half8_t *__restrict__ gop,
+                                                   double4 *__restrict__ gctr)
+{
+    const int lane = threadIdx.x & 63;
+    const half8_t b0 = rec.bound[0], b1 = rec.bound[1];
+    const double q[3] = {(double)b0[0] + (double)b0[1], (double)b0[3] + (double)b0[4], (double)b0[6] + (double)b0[7]};
+    const double d = (double)b1[5] + (double)b1[6];
+    const float w = (float)b1[1];
+    const int mode = w == -65504.0f ? kBqForced : w == 65504.0f ? kBqNever : kBqNormal;
+    const GroupBound gb = bundle_group_hat(q, d * (1.0 + 0x1.0p-20) + 0x1.0p-20, mode, lane >> 5);
+    if ((lane & 31) < 2 && s < nslots) gop[(s >> 5) * 2 + (lane & 31)] = bundle_query_frag(gb.g, gb.D, gb.mode, lane & 31);
+    if ((lane & 31) == 0 && s < nslots)
+        gctr[s >> 5] = make_double4(gb.g[0], gb.g[1], gb.g[2],
+                                    gb.mode == kBqNormal ? gb.D : gb.mode == kBqForced ? INFINITY : -1.0);
+}
+
 } // namespace
 } // namespace icp

@@ -294,6 +294,15 @@ struct icp_ctx {
     int2 *b_tasks = nullptr;                  // v2: the task list
     size_t b_gctr_cap = 0, b_cand_cap = 0, b_cand_n_cap = 0, b_wsplit_cap = 0, b_tctl_cap = 0, b_tasks_cap = 0;
     size_t b_qop_cap = 0, b_gop_cap = 0, b_qraw_cap = 0, b_glist_cap = 0, b_counters_rows = 0;
+    // The resident scene in slot order (scene_in_slot_order): point s of the scene (and idx[s]
+    // while seeds_valid) is the caller's point s_order[s].  icp_get_scene / icp_get_indices and
+    // the index digests map back; every other per-point pass is order-agnostic.
+    bool scene_slot = false;
+    int *s_order = nullptr;
+    size_t s_order_cap = 0;
+    DevCloud s_tmp;                           // the permutation's second buffer
+    int *s_tmp_idx = nullptr;
+    size_t s_tmp_idx_cap = 0;
 
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     icp_stats stats{};
@@ -597,6 +606,51 @@ int query_order(icp_ctx *ctx, const DevCloud &q, size_t n, const int **order)
     return ICP_OK;
 }
 
+// icp_run keeps a resident scene of this size in slot order: the bundle filter's Morton order
+// over the model's box (launch_query_order), so that its per-query records and the
+// certificate's reads and index writes stream in order instead of scattering, and neighbouring
+// queries share cells in the grid levels.  The condition depends on the sizes only, not on the
+// NN variant, so that every variant runs the same per-point order and the same reductions
+// (their trajectories stay bitwise equal); below it (n <= 49,152) the one-launch paths keep
+// their own orders.  ICP_SCENE_ORDER=0: file order (A/B).
+static bool want_slot_order(const icp_ctx *ctx, size_t n)
+{
+    static const bool off = [] {
+        const char *e = getenv("ICP_SCENE_ORDER");
+        return e && atoi(e) == 0;
+    }();
+    return !off && n > (size_t)kTailMaxBlocks * kBlock && ctx->nm >= (size_t)kBundleMinModel &&
+           (double)n * (double)ctx->nm >= 2147483648.0;
+}
+
+// The resident scene (and its correspondences while seeds_valid) into slot order, once per
+// uploaded scene: gathered into the second buffer, which then becomes the scene.
+static int scene_to_slot_order(icp_ctx *ctx)
+{
+    if (ctx->scene_slot || !ctx->scene.n) return ICP_OK;
+    DevCloud &P = ctx->scene;
+    const size_t n = P.n;
+    TRY(grow(ctx, &ctx->s_order, &ctx->s_order_cap, n));
+    const size_t bytes = query_order_scratch_bytes((int)n);
+    TRY(grow(ctx, &ctx->q_order_tmp, &ctx->q_order_tmp_cap, bytes));
+    if (launch_query_order(P.x, P.y, P.z, (int)n, ctx->m_lo, ctx->m_hi, ctx->q_order_tmp, bytes, ctx->s_order,
+                           ctx->st) != 0)
+        return fail(ctx, ICP_E_HIP, "scene order: radix sort failed");
+    TRY(grow_cloud(ctx, ctx->s_tmp, n, true));
+    const bool with_idx = ctx->seeds_valid;
+    if (with_idx) TRY(grow(ctx, &ctx->s_tmp_idx, &ctx->s_tmp_idx_cap, n));
+    launch_permute_cloud(ctx->s_order, (int)n, 0, P.x, P.y, P.z, P.f, with_idx ? ctx->idx : nullptr, ctx->s_tmp.x,
+                         ctx->s_tmp.y, ctx->s_tmp.z, ctx->s_tmp.f, with_idx ? ctx->s_tmp_idx : nullptr, ctx->st);
+    LAUNCHCHK("scene_to_slot_order");
+    std::swap(ctx->scene, ctx->s_tmp);
+    if (with_idx) {
+        std::swap(ctx->idx, ctx->s_tmp_idx);
+        std::swap(ctx->idx_cap, ctx->s_tmp_idx_cap);
+    }
+    ctx->scene_slot = true;
+    return ICP_OK;
+}
+
 constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger model: nn_resolve, 256 per query)
 
 // Launches the complete NN search of the n queries in q against the resident model ->
@@ -606,7 +660,8 @@ constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger mod
 // O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
 // zero_counts = false: amb_count is already zero (icp_run: horn_step clears it)
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
-                    bool zero_counts = true, bool seeds_ready = false, const int *stop = nullptr)
+                    bool zero_counts = true, bool seeds_ready = false, const int *stop = nullptr,
+                    bool slot_order = false, bool records_ready = false)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     if (!n) return ICP_OK;
@@ -680,7 +735,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         const int *order = nullptr;
-        if (l1 == 3) TRY(query_order(ctx, q, n, &order));
+        // (slot_order: q is the resident scene, already stored in the filter's order)
+        if (l1 == 3 && !slot_order) TRY(query_order(ctx, q, n, &order));
         if (v2) { // every query's operands, once, in the filter's slot order
             const size_t nslots = bundle2_slots(pl);
             TRY(grow(ctx, &ctx->b_qop, &ctx->b_qop_cap, nslots * 64));
@@ -691,7 +747,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             TRY(grow(ctx, &ctx->b_cand_n, &ctx->b_cand_n_cap, (size_t)pl.qblocks));
             TRY(grow(ctx, &ctx->b_wsplit, &ctx->b_wsplit_cap, (size_t)pl.qblocks));
             TRY(grow(ctx, &ctx->b_tasks, &ctx->b_tasks_cap, bundle2_task_count(pl)));
-            TRY(grow(ctx, &ctx->b_tctl, &ctx->b_tctl_cap, 2));
+            TRY(grow(ctx, &ctx->b_tctl, &ctx->b_tctl_cap, kBundleTctlInts));
             TRY(grow(ctx, &ctx->b_gctr, &ctx->b_gctr_cap, nslots / 32));
             if (ctx->b_counters && ctx->b_counters_rows < bundle2_counter_rows(pl)) { // (per-wave rows)
                 HIPCHK(hipFree(ctx->b_counters));
@@ -704,11 +760,13 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                                       ctx->st));
             }
             // (seeds_ready: icp_run's previous transform wrote the seeds, and with them each
-            // point's seed distance, SeedArgs::seedd)
-            launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4,
+            // point's seed distance, SeedArgs::seedd; records_ready: the records and group bounds
+            // themselves, SeedArgs::qop)
+            if (!records_ready) launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4,
                                seeds_ready ? ctx->b_seedd : nullptr, ctx->c, ctx->scale16, seeds, nslots, ctx->b_qop,
-                               ctx->b_qraw, ctx->st, stop);
-            launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->b_gctr, ctx->st, stop);
+                               order ? ctx->b_qraw : nullptr, ctx->st, stop, order ? nullptr : ctx->b_gop,
+                               order ? nullptr : ctx->b_gctr);
+            if (order && !records_ready) launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->b_gctr, ctx->st, stop);
             launch_bundle_candidates(pl, ctx->b_gctr, ctx->b_blk, ctx->nb_pad, ctx->b_cand, ctx->b_cand_n,
                                      ctx->b_wsplit, ctx->b_tasks, ctx->b_tctl, ctx->st, stop);
         }
@@ -730,7 +788,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (l1 >= 2)
             launch_nn_finalize_mfma16(pb, ps, pi, pl.splits, q.x, q.y, q.z, (int)n, (int)ctx->nm, ctx->c,
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
-                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit, v2 ? ctx->b_qraw : nullptr,
+                                      ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit,
+                                      v2 && order ? ctx->b_qraw : nullptr, // (slot s = query s: p read in order)
                                       v2 ? ctx->b_wsplit : nullptr, v2 ? 4 * pl.q_per_lane * 32 : 0);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
@@ -1104,6 +1163,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     free_cloud(ctx->Y);
     free_cloud(ctx->qa);
     free_cloud(ctx->qb);
+    free_cloud(ctx->s_tmp);
     for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
@@ -1120,7 +1180,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->b_kd, (void *)ctx->b_seedd, (void *)ctx->tail_backup, (void *)ctx->q_order, (void *)ctx->q_order_tmp, (void *)ctx->b_counters,
                     (void *)ctx->b_qop, (void *)ctx->b_gop, (void *)ctx->b_qraw, (void *)ctx->b_glist, (void *)ctx->q_pos, (void *)ctx->cr_entries,
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
-                    (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt})
+                    (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
+                    (void *)ctx->s_order, (void *)ctx->s_tmp_idx})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -1343,6 +1404,7 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     ctx->has_scene = true;
     ctx->seeds_valid = false;
     ctx->q_order_src = nullptr; // new contents: a new query order
+    ctx->scene_slot = false;    // (in the caller's order)
     return ICP_OK;
 }
 
@@ -1351,6 +1413,14 @@ int icp_get_scene(icp_ctx *ctx, double *p_xyz_out)
     if (!ctx || (!p_xyz_out && ctx->scene.n)) return ICP_E_ARG;
     if (!ctx->has_scene) return fail(ctx, ICP_E_NO_MODEL, "scene not set");
     HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->scene_slot && ctx->scene.n) { // back to the caller's order, in the second buffer
+        const DevCloud &P = ctx->scene;
+        TRY(grow_cloud(ctx, ctx->s_tmp, P.n, true));
+        launch_permute_cloud(ctx->s_order, (int)P.n, 1, P.x, P.y, P.z, nullptr, nullptr, ctx->s_tmp.x, ctx->s_tmp.y,
+                             ctx->s_tmp.z, nullptr, nullptr, ctx->st);
+        LAUNCHCHK("scene_to_file_order");
+        return download_cloud(ctx, ctx->s_tmp, P.n, p_xyz_out);
+    }
     return download_cloud(ctx, ctx->scene, ctx->scene.n, p_xyz_out);
 }
 
@@ -1703,6 +1773,10 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             sa.seedd = ctx->b_seedd;
         }
     }
+    static const bool transform_records = [] { // ICP_TRANSFORM_RECORDS=0: the prep kernel writes them (A/B)
+        const char *e = getenv("ICP_TRANSFORM_RECORDS");
+        return !(e && atoi(e) == 0);
+    }();
     int slot_ticket[kRing] = {};
     TRY(grow(ctx, &ctx->err_trace_dev, &ctx->err_trace_cap, (size_t)(max_iter > 0 ? max_iter : 1)));
     while (ctx->iter_ev.size() < 5 * (size_t)kRing) { // (nn begin, nn end, -, all-reduce begin, end) per slot
@@ -1719,6 +1793,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             if (r != kPersistFallback) return r;
         }
     }
+    if (want_slot_order(ctx, n)) TRY(scene_to_slot_order(ctx));
+    const int *digest_order = ctx->scene_slot ? ctx->s_order : nullptr;
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     // mid-size single-rank runs: iterations >= 2 end in ONE fused launch (moments ... error step)
     static const int forced_mode = [] {
@@ -1783,12 +1859,26 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             // (the search of an iteration queued behind the converged one returns at once)
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
-                                &sd->done)); // (run_init zeroed the counters)
+                                &sd->done, ctx->scene_slot, sa.qop && enqueued > 0)); // (run_init zeroed the counters)
+            if (enqueued == 0 && sa.seedd && ctx->scene_slot && transform_records) {
+                // a scene in slot order: from here on each transform writes the next search's
+                // slot records and group bounds in order (the first search sized the buffers;
+                // its prep wrote the padding slots, which no transform touches)
+                const size_t nslots = bundle2_slots(plan_nn_bundle2(n, ctx->nb_pad));
+                if (ctx->b_qop && ctx->b_qop_cap >= nslots * 64 && ctx->b_gop_cap >= nslots &&
+                    ctx->b_gctr_cap >= nslots / 32) {
+                    sa.qop = ctx->b_qop;
+                    sa.gop = ctx->b_gop;
+                    sa.gctr = ctx->b_gctr;
+                    sa.nslots = (int)nslots;
+                }
+            }
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
             TRY(cpu_rule_fixup(ctx, P, n, &sd->done)); // (ICP_NN_RULE_CPU_SQRT only: host near ties)
             ar_timed[slot] = false;
             if ((size_t)enqueued < ctx->digest_cap) {
-                launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st);
+                launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st,
+                                  digest_order);
                 LAUNCHCHK("idx_digest");
             }
             if (!lag && enqueued > 0 && n > 0 && n <= (size_t)kRedSingle) {
@@ -2256,8 +2346,16 @@ int icp_get_indices(icp_ctx *ctx, int32_t *idx_out)
     if (!ctx->has_scene || !ctx->seeds_valid)
         return fail(ctx, ICP_E_NO_MODEL, "no NN search over the resident scene since icp_set_scene");
     HIPCHK(hipSetDevice(ctx->device));
+    const int *src = ctx->idx;
+    if (ctx->scene_slot && ctx->scene.n) { // back to the caller's order
+        TRY(grow(ctx, &ctx->s_tmp_idx, &ctx->s_tmp_idx_cap, ctx->scene.n));
+        launch_permute_cloud(ctx->s_order, (int)ctx->scene.n, 1, nullptr, nullptr, nullptr, nullptr, ctx->idx, nullptr,
+                             nullptr, nullptr, nullptr, ctx->s_tmp_idx, ctx->st);
+        LAUNCHCHK("indices_to_file_order");
+        src = ctx->s_tmp_idx;
+    }
     if (ctx->scene.n)
-        HIPCHK(hipMemcpyAsync(idx_out, ctx->idx, sizeof(int32_t) * ctx->scene.n, hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipMemcpyAsync(idx_out, src, sizeof(int32_t) * ctx->scene.n, hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
 }

@@ -51,6 +51,38 @@ __device__ __forceinline__ int block_append(int *counter, bool pred, int *counte
     __syncthreads();
     return pred ? s_base + s_cnt[wave] + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
 }
+
+// block_append for `cnt` entries per thread (a kernel that handles several queries a thread,
+// so that a workgroup takes one atomic for all of them): returns this thread's first slot.
+// Slots follow thread order; every thread of the workgroup must call it.
+__device__ __forceinline__ int block_append_n(int *counter, int cnt, int *counter2 = nullptr, int cnt2 = 0)
+{
+    __shared__ int s_w[kBlock / 64], s_w2[kBlock / 64], s_b;
+    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+    int x = cnt, x2 = cnt2; // inclusive wave scan of cnt, wave sum of cnt2
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+        x2 += __shfl_xor(x2, o, 64);
+    }
+    if (lane == 63) s_w[wave] = x;
+    if (lane == 0) s_w2[wave] = x2;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0, tot2 = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const int c = s_w[w];
+            s_w[w] = tot;
+            tot += c;
+            tot2 += s_w2[w];
+        }
+        s_b = tot ? atomicAdd(counter, tot) : 0;
+        if (counter2 && tot2) atomicAdd(counter2, tot2);
+    }
+    __syncthreads();
+    return s_b + s_w[wave] + x - cnt;
+}
 #endif
 
 // Parameters of the fp32 certificate (see icp_kernels.hip, "certified NN").
@@ -158,6 +190,7 @@ void launch_nn_bundle(const double *px, const double *py, const double *pz, int 
 constexpr int kBundleCounterFields = 12;
 bool bundle_v2();
 NNPlan plan_nn_bundle2(size_t np, int nb_pad);
+constexpr int kBundleTctlInts = 32 * 9;
 size_t bundle2_slots(const NNPlan &pl);
 size_t bundle2_list_ints(const NNPlan &pl, int nb_pad);
 size_t bundle2_counter_rows(const NNPlan &pl);
@@ -166,14 +199,17 @@ size_t bundle2_counter_rows(const NNPlan &pl);
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
                         const int *prev, const double4 *m4, const double *seedd, const double c[3], double scale,
                         const unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
-                        const int *stop = nullptr);
+                        const int *stop = nullptr, void *gop = nullptr, double4 *gctr = nullptr);
+// (gop / gctr with pos == null: the prep also writes the group bounds, launch_bundle_groups's
+// output, from the records in registers)
 // gop (nslots bytes): the 32-slot groups' bounds from the records (after the prep); gctr
 // (nslots / 32 double4): the same as (centre, D) for the candidate lists
 void launch_bundle_groups(const void *qop, size_t nslots, void *gop, double4 *gctr, hipStream_t st,
                           const int *stop = nullptr);
 // cand (qblocks x nb_pad / 32 ints), cand_n (qblocks): each filter workgroup's candidate blocks;
 // then the task list: wsplit (qblocks: the partial sets of each query workgroup), tasks
-// (bundle2_task_count(plan) int2), tctl (2 ints: count, the filter's task counter)
+// (bundle2_task_count(plan) int2), tctl (kBundleTctlInts ints: the count, then the filter's
+// eight task-queue counters, 128 B apart)
 void launch_bundle_candidates(const NNPlan &pl, const double4 *gctr, const double4 *blk, int nb_pad, int *cand,
                               int *cand_n, int *wsplit, int2 *tasks, int *tctl, hipStream_t st,
                               const int *stop = nullptr);
@@ -189,6 +225,12 @@ size_t query_order_scratch_bytes(int n);
 int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
                        const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st,
                        int *pos = nullptr);
+// the resident scene into (inverse = 0: dst[s] = src[order[s]]) or out of (inverse = 1:
+// dst[order[s]] = src[s]) a query order; a stream (xyz, fp32 copy, indices) moves when both its
+// pointers are non-null
+void launch_permute_cloud(const int *order, int n, int inverse, const double *sx, const double *sy,
+                          const double *sz, const float4 *sf, const int *sidx, double *dx, double *dy, double *dz,
+                          float4 *df, int *didx, hipStream_t st);
 // exact fp64 resolution of the queued queries (candidates d32 <= T only).
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
@@ -294,7 +336,9 @@ void launch_subtract(double *x, double *y, double *z, int n, double mx, double m
 // out = in - m (AoS; substract_col with a caller-given m, compute.cu:381-398)
 void launch_subtract_aos(const double *in, int n, const double m[3], double *out, hipStream_t st);
 // out3 += (sum idx, sum (j+1) idx[j], #{idx[j] == j}) mod 2^64 (test digest); a no-op if *done
-void launch_idx_digest(const int *idx, int n, const int *done, unsigned long long *out3, hipStream_t st);
+// order (nullable): idx[i] belongs to query order[i] (a scene stored in slot order)
+void launch_idx_digest(const int *idx, int n, const int *done, unsigned long long *out3, hipStream_t st,
+                       const int *order = nullptr);
 // partial [sum ||y||^2, sum ||p||^2] (y_p_norm)
 void launch_norms(const double *yx, const double *yy, const double *yz, const double *px,
                   const double *py, const double *pz, int n, double *partials, hipStream_t st);
@@ -317,6 +361,12 @@ struct SeedArgs {
     double *seedd = nullptr;
     double c[3] = {0.0, 0.0, 0.0};
     double scale = 1.0;
+    // (nullable) a scene stored in the bundle filter's slot order (slot = point): the next
+    // search's slot records, group operands and group centres, bundle_prep_kernel's output for
+    // the nslots slots, written in order here instead (the prep and its reads are skipped)
+    void *qop = nullptr, *gop = nullptr;
+    double4 *gctr = nullptr;
+    int nslots = 0;
 };
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,

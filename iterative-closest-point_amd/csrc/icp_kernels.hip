@@ -29,6 +29,7 @@
 #include "icp_kernels.h"
 #include "icp_device.h"
 #include "icp_mfma16.h"
+#include "icp_bundle_rec.h"
 
 #include <cmath>
 #include <cstdio>
@@ -1207,7 +1208,7 @@ __global__ __launch_bounds__(kBlock) void mfma16_seed_kernel(
 // products (the shift) enter the accumulation: (16 + 3 + 4) u sum|p| with sum|p| including
 // |s0'|, so delta_s(R) = 28u R^2 + 64u A R + 24u |s0'| + 4u (A + R) + 1e-3.  Any s0' keeps
 // the test sound; a poor one only queues the query.
-template <bool SEEDED, int G>
+template <bool SEEDED, int G, int R>
 __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const float *__restrict__ part_best, const float *__restrict__ part_second,
     const int *__restrict__ part_idx, int splits, const double *__restrict__ px,
@@ -1218,84 +1219,154 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     const double4 *__restrict__ qraw, const int *__restrict__ wsplit, int wslots)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
-    // qraw (the bundle filter): the partials are in the filter's slot order, and slot s's query
-    // (coordinates, index j, seed) is qraw[s] -- read in order, no gather
-    const int s = blockIdx.x * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
-    const bool valid = s < np; // no early exit: block_append is workgroup-wide
-    double q0, q1, q2;
-    unsigned sdq = 0u;
-    int j = s;
-    if (qraw) {
-        const double4 r = qraw[valid ? s : 0];
-        const unsigned long long w = (unsigned long long)__double_as_longlong(r.w);
-        q0 = r.x;
-        q1 = r.y;
-        q2 = r.z;
-        j = (int)(unsigned)(w & 0xffffffffull);
-        sdq = (unsigned)(w >> 32);
-    } else {
-        const int jj = valid ? j : 0;
-        q0 = px[jj];
-        q1 = py[jj];
-        q2 = pz[jj];
-        if (SEEDED) sdq = seed16[jj];
-    }
-    float b = 0.0f, s2 = 0.0f;
-    int id = -1;
-    // (wsplit: the bundle filter's per-workgroup task counts -- slot s's partial sets)
-    if (valid)
-        merge_splits_group<G>(part_best, part_second, part_idx, wsplit ? wsplit[s / wslots] : splits, np, s, sub, b,
-                              s2, id);
-    if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
-    const double ax = (q0 - cx) * scale, ay = (q1 - cy) * scale, az = (q2 - cz) * scale;
-    bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
-              fabs(az) <= kF16QueryClamp;
-    if (ok) {
-        const double u = 0x1.0p-24;
-        const double a2 = ax * ax + ay * ay + az * az;
-        const double A = sqrt(a2);
-        const double sh = SEEDED ? seed_shift(sdq) : 0.0;
-        auto delta = [&](double R) {
-            return SEEDED ? 28.0 * u * R * R + 64.0 * u * A * R + 24.0 * u * fabs(sh) + 4.0 * u * (A + R) + 1e-3
-                          : 26.0 * u * R * R + 60.0 * u * A * R + 4.0 * u * (A + R) + 1e-3;
-        };
-        // shift back to G (fp64 sums of an fp32 and an exact value: relative 2^-53)
-        const double bg = (double)b + sh, sg = (double)s2 + sh;
-        // delta_b = delta(R_b) at an upper bound of the winner's norm R_b = |b~|, without loading
-        // it: G_b <= bg + delta(R_max) (every model point has |b~| < R_max = 2^12 sqrt 3: the
-        // image's scale puts the max |coordinate| below 2^12), so R_b <= A + sqrt(G_b + |a|^2),
-        // Rc's bound one step earlier.  (The gathered |b~| was a dependent random load per
-        // query; the bound is looser by ~2 sqrt(delta(R_max)) in R: ~1 in delta_b at C4.)
-        const double Rb = A * (1.0 + 2.0 * u) +
-                          sqrt(fmax(bg + delta(kF16ModelNormMax) + a2 * (1.0 + 4.0 * u), 0.0) * (1.0 + 0x1.0p-40));
-        const double db = delta(Rb);
-        const double Db = fmax(bg + db + a2 * (1.0 + 4.0 * u), 0.0);
-        const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
-        double T = bg + db + delta(Rc) + 0x1.0p-48 * Db;
-        T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
-        ok = sg > T;
-        if (audit && ok && sub == 0) {
-            // certificate audit (icp_set_cert_audit): the winner's filter error against its bound,
-            // |G^ - G64| / delta_b (G64 = fp64 G of the winner, in the same scaled units), and the
-            // certified margin (second - T) / (T - b) in units of the threshold's own width
-            const double4 mb = m4[id];
-            const double b0 = (mb.x - cx) * scale, b1 = (mb.y - cy) * scale, b2 = (mb.z - cz) * scale;
-            const double g64 = (b0 * b0 + b1 * b1 + b2 * b2) - 2.0 * ((ax * b0 + ay * b1) + az * b2);
-            const float ratio = (float)(fabs(bg - g64) / db);
-            const float margin = (float)fmax((sg - T) / (T - bg), 0.0);
-            atomicMax(audit, __float_as_uint(ratio));
-            atomicMin(audit + 1, __float_as_uint(margin));
-            atomicAdd(audit + 2, 1u);
+    // R queries per lane group (rounds r: slots (blockIdx.x R + r) kBlock / G + threadIdx.x / G,
+    // coalesced per round), then ONE queue append for the workgroup's R kBlock / G queries: the
+    // append is a same-address device atomic, which serialises across the chip (~12 ns each: one
+    // per 256 queries cost ~50 us at 1M queries)
+    int qj[R], qid[R];
+    int nq = 0, nnoc = 0;
+    // G == 1: the R rounds' split merges interleaved (split-major), so that each split's loads of
+    // all R slots are in flight together (merge_splits' fold per slot, in the same order)
+    float mb[R], ms[R];
+    int mi[R];
+    if (G == 1) {
+        int S[R], smax = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int s = (blockIdx.x * R + r) * kBlock + threadIdx.x;
+            S[r] = s < np ? (wsplit ? wsplit[s / wslots] : splits) : 0;
+            smax = max(smax, S[r]);
+            mb[r] = INFINITY;
+            ms[r] = INFINITY;
+            mi[r] = -1;
+        }
+        for (int sp = 0; sp < smax; ++sp) {
+            float pb[R], ps[R];
+            int pi[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const size_t o = (size_t)sp * np + (size_t)((blockIdx.x * R + r) * kBlock + threadIdx.x);
+                if (sp < S[r]) {
+                    pb[r] = part_best[o];
+                    ps[r] = part_second[o];
+                    pi[r] = part_idx[o];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (sp >= S[r]) continue;
+                if (sp == 0) {
+                    mb[r] = pb[r];
+                    ms[r] = ps[r];
+                    mi[r] = pi[r];
+                } else if (pb[r] < mb[r]) {
+                    ms[r] = fminf(mb[r], ps[r]);
+                    mb[r] = pb[r];
+                    mi[r] = pi[r];
+                } else {
+                    ms[r] = fminf(ms[r], pb[r]);
+                }
+            }
         }
     }
-    ok = ok || !valid || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
-    if (ok && valid && sub == 0) idx[j] = id;
-    // queue + the statistic of queries without a level-1 candidate, one atomic each per workgroup
-    const int slot = block_append(amb_count, !ok, amb_count + 1, !ok && id < 0);
-    if (!ok) {
-        amb_list[slot] = j;
-        amb_hint[slot] = id; // the grid resolver's candidate
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        // qraw (the bundle filter): the partials are in the filter's slot order, and slot s's
+        // query (coordinates, index j, seed) is qraw[s] -- read in order, no gather
+        const int s = (blockIdx.x * R + r) * (kBlock / G) + threadIdx.x / G, sub = threadIdx.x % G;
+        const bool valid = s < np;
+        double q0 = 0.0, q1 = 0.0, q2 = 0.0;
+        unsigned sdq = 0u;
+        int j = s;
+        if (valid) {
+            if (qraw) {
+                const double4 rw = qraw[s];
+                const unsigned long long w = (unsigned long long)__double_as_longlong(rw.w);
+                q0 = rw.x;
+                q1 = rw.y;
+                q2 = rw.z;
+                j = (int)(unsigned)(w & 0xffffffffull);
+                sdq = (unsigned)(w >> 32);
+            } else {
+                q0 = px[j];
+                q1 = py[j];
+                q2 = pz[j];
+                if (SEEDED) sdq = seed16[j];
+            }
+        }
+        float b = 0.0f, s2 = 0.0f;
+        int id = -1;
+        // (wsplit: the bundle filter's per-workgroup task counts -- slot s's partial sets)
+        if (G == 1) {
+            b = mb[r];
+            s2 = ms[r];
+            id = mi[r];
+        } else if (valid) {
+            merge_splits_group<G>(part_best, part_second, part_idx, wsplit ? wsplit[s / wslots] : splits, np, s, sub,
+                                  b, s2, id);
+        }
+        if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
+        const double ax = (q0 - cx) * scale, ay = (q1 - cy) * scale, az = (q2 - cz) * scale;
+        bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
+                  fabs(az) <= kF16QueryClamp;
+        if (ok) {
+            const double u = 0x1.0p-24;
+            const double a2 = ax * ax + ay * ay + az * az;
+            const double A = sqrt(a2);
+            const double sh = SEEDED ? seed_shift(sdq) : 0.0;
+            auto delta = [&](double Rr) {
+                return SEEDED ? 28.0 * u * Rr * Rr + 64.0 * u * A * Rr + 24.0 * u * fabs(sh) + 4.0 * u * (A + Rr) + 1e-3
+                              : 26.0 * u * Rr * Rr + 60.0 * u * A * Rr + 4.0 * u * (A + Rr) + 1e-3;
+            };
+            // shift back to G (fp64 sums of an fp32 and an exact value: relative 2^-53)
+            const double bg = (double)b + sh, sg = (double)s2 + sh;
+            // delta_b = delta(R_b) at an upper bound of the winner's norm R_b = |b~|, without
+            // loading it: G_b <= bg + delta(R_max) (every model point has |b~| < R_max = 2^12 sqrt 3:
+            // the image's scale puts the max |coordinate| below 2^12), so R_b <= A + sqrt(G_b +
+            // |a|^2), Rc's bound one step earlier.  (The gathered |b~| was a dependent random load
+            // per query; the bound is looser by ~2 sqrt(delta(R_max)) in R: ~1 in delta_b at C4.)
+            const double Rb = A * (1.0 + 2.0 * u) +
+                              sqrt(fmax(bg + delta(kF16ModelNormMax) + a2 * (1.0 + 4.0 * u), 0.0) * (1.0 + 0x1.0p-40));
+            const double db = delta(Rb);
+            const double Db = fmax(bg + db + a2 * (1.0 + 4.0 * u), 0.0);
+            const double Rc = A * (1.0 + 2.0 * u) + sqrt(Db * (1.0 + 0x1.0p-40));
+            double T = bg + db + delta(Rc) + 0x1.0p-48 * Db;
+            T += (fabs(T) + fabs(sh)) * 1e-12 + 1e-300;
+            ok = sg > T;
+            if (audit && ok && sub == 0) {
+                // certificate audit (icp_set_cert_audit): the winner's filter error against its
+                // bound, |G^ - G64| / delta_b (G64 = fp64 G of the winner, in the same scaled
+                // units), and the certified margin (second - T) / (T - b) in units of the
+                // threshold's own width
+                const double4 mb = m4[id];
+                const double b0 = (mb.x - cx) * scale, b1 = (mb.y - cy) * scale, b2 = (mb.z - cz) * scale;
+                const double g64 = (b0 * b0 + b1 * b1 + b2 * b2) - 2.0 * ((ax * b0 + ay * b1) + az * b2);
+                const float ratio = (float)(fabs(bg - g64) / db);
+                const float margin = (float)fmax((sg - T) / (T - bg), 0.0);
+                atomicMax(audit, __float_as_uint(ratio));
+                atomicMin(audit + 1, __float_as_uint(margin));
+                atomicAdd(audit + 2, 1u);
+            }
+        }
+        ok = ok || !valid || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
+        if (ok && valid && sub == 0) idx[j] = id;
+        qj[r] = -1;
+        if (!ok) {
+            qj[r] = j;
+            qid[r] = id; // the grid resolver's candidate
+            ++nq;
+            nnoc += id < 0; // the statistic of queries without a level-1 candidate
+        }
     }
+    // the workgroup's queue entries, one atomic each for the queue and the statistic
+    int slot = block_append_n(amb_count, nq, amb_count + 1, nnoc);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (qj[r] >= 0) {
+            amb_list[slot] = qj[r];
+            amb_hint[slot] = qid[r];
+            ++slot;
+        }
 }
 
 // model image for the f16 filter (see nn_mfma16_kernel); padding points get G ~ 2.7e8
@@ -1667,15 +1738,17 @@ __global__ __launch_bounds__(kBlock) void subtract_aos_kernel(const double *__re
 // one search's correspondences, mod 2^64 -- integer sums, so independent of the summation order.
 __global__ __launch_bounds__(kBlock) void idx_digest_kernel(const int *__restrict__ idx, int n,
                                                            const int *__restrict__ done,
-                                                           unsigned long long *__restrict__ out)
+                                                           unsigned long long *__restrict__ out,
+                                                           const int *__restrict__ order)
 {
     if (done && *done) return;
     unsigned long long a = 0, w = 0, id = 0;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         const unsigned long long v = (unsigned long long)(long long)idx[i];
+        const int j = order ? order[i] : i; // (the query idx[i] belongs to)
         a += v;
-        w += v * (unsigned long long)(i + 1);
-        id += idx[i] == i;
+        w += v * (unsigned long long)(j + 1);
+        id += idx[i] == j;
     }
     for (int o = 32; o >= 1; o >>= 1) {
         a += __shfl_xor(a, o, 64);
@@ -1761,6 +1834,39 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     if (sdone) return;
     const Xform xf = sxf;
     double a[1] = {0.0};
+    if (sa.qop && write_p) {
+        // slot records (a scene in slot order): whole waves run to n rounded up to 64 (the
+        // stride is a multiple of 64), so that each 32-slot group's lanes are all present for
+        // its bound; the lanes past n build the padding's never-firing records
+        const int n64 = (n + 63) & ~63;
+        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n64; i += gridDim.x * kBlock) {
+            BundleQuery r;
+            if (i < n) {
+                double q0, q1, q2;
+                transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
+                const double y0 = yx[i], y1 = yy[i], y2 = yz[i];
+                a[0] += residual2(y0, y1, y2, q0, q1, q2);
+                px[i] = q0;
+                py[i] = q1;
+                pz[i] = q2;
+                if (p32)
+                    p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
+                const unsigned sd = mfma16_seed_value(q0, q1, q2, y0, y1, y2, sa.c[0], sa.c[1], sa.c[2], sa.scale);
+                sa.seed16[i] = sd;
+                const double dx = q0 - y0, dy = q1 - y1, dz = q2 - y2;
+                double4 raw;
+                bundle_record(q0, q1, q2, i, (dx * dx + dy * dy) + dz * dz, sd, sa.c[0], sa.c[1], sa.c[2], sa.scale,
+                              r, raw);
+            } else {
+                double4 raw;
+                bundle_never_record(r, raw);
+            }
+            ((BundleQuery *)sa.qop)[i] = r;
+            bundle_group_store(r, i, sa.nslots, (half8_t *)sa.gop, sa.gctr);
+        }
+        block_sum_store<1>(a, partials + blockIdx.x);
+        return;
+    }
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
         double q0, q1, q2;
         transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
@@ -2124,6 +2230,10 @@ void launch_nn_mfma16(const double *px, const double *py, const double *pz, int 
 #undef LAUNCH16
 }
 
+// queries per lane group of nn_finalize_mfma16_kernel: 1M queries -> 512 workgroups, one queue
+// atomic each (1 query a lane: 4,096 atomics, ~56 us of the ~57 us launch, profiles/r03ac/)
+constexpr int kFin16Rounds = 8, kFin16RoundsMin = 1 << 18;
+
 void launch_nn_finalize_mfma16(const float *part_best, const float *part_second, const int *part_idx,
                                int splits, const double *px, const double *py, const double *pz,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
@@ -2137,19 +2247,27 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
         const char *e = getenv("ICP_FIN16_LANES");
         return e ? atoi(e) : 0;
     }();
-    const int g = forced == 1 || forced == 4 || forced == 8 ? forced : 1, per_block = kBlock / g;
+    const int g = forced == 1 || forced == 4 || forced == 8 ? forced : 1;
+    // (small searches keep one query a lane: their few workgroups would serialise the rounds)
+    const int rounds = np >= kFin16RoundsMin ? kFin16Rounds : 1, per_block = kBlock / g * rounds;
     const int grid = (np + per_block - 1) / per_block;
-#define FIN16(SD, G)                                                                                         \
-    nn_finalize_mfma16_kernel<SD, G><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
+#define FIN16R(SD, G, R)                                                                                     \
+    nn_finalize_mfma16_kernel<SD, G, R><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
                                                               pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
                                                               idx, amb_count, amb_list, amb_hint, stop, m4, audit, \
                                                               qraw, wsplit, wslots)
+#define FIN16(SD, G)                                                                                         \
+    do {                                                                                                     \
+        if (rounds == kFin16Rounds) FIN16R(SD, G, kFin16Rounds);                                             \
+        else FIN16R(SD, G, 1);                                                                               \
+    } while (0)
     if (seed16) {
         if (g == 8) FIN16(true, 8); else if (g == 4) FIN16(true, 4); else FIN16(true, 1);
     } else {
         if (g == 8) FIN16(false, 8); else if (g == 4) FIN16(false, 4); else FIN16(false, 1);
     }
 #undef FIN16
+#undef FIN16R
 }
 
 void launch_nn_finalize_mfma(const float *part_best, const float *part_second, const int *part_idx,
@@ -2278,10 +2396,11 @@ void launch_subtract_aos(const double *in, int n, const double m[3], double *out
     subtract_aos_kernel<<<grid_for(n), kBlock, 0, st>>>(in, n, m[0], m[1], m[2], out);
 }
 
-void launch_idx_digest(const int *idx, int n, const int *done, unsigned long long *out3, hipStream_t st)
+void launch_idx_digest(const int *idx, int n, const int *done, unsigned long long *out3, hipStream_t st,
+                       const int *order)
 {
     if (n <= 0) return;
-    idx_digest_kernel<<<grid_for(n, 1024), kBlock, 0, st>>>(idx, n, done, out3);
+    idx_digest_kernel<<<grid_for(n, 1024), kBlock, 0, st>>>(idx, n, done, out3, order);
 }
 
 void launch_subtract(double *x, double *y, double *z, int n, double mx, double my, double mz,

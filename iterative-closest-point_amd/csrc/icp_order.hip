@@ -76,7 +76,36 @@ __global__ __launch_bounds__(kBlock) void query_keys_kernel(const double *__rest
 
 constexpr int kQueryOrderBits = 30;
 
+// dst[s] = src[order[s]] (into the slot order) or dst[order[s]] = src[s] (back to file order);
+// each of the xyz / fp32 / index streams is moved when both its pointers are non-null
+__global__ __launch_bounds__(kBlock) void permute_cloud_kernel(
+    const int *__restrict__ order, int n, int inverse, const double *__restrict__ sx, const double *__restrict__ sy,
+    const double *__restrict__ sz, const float4 *__restrict__ sf, const int *__restrict__ sidx, double *__restrict__ dx,
+    double *__restrict__ dy, double *__restrict__ dz, float4 *__restrict__ df, int *__restrict__ didx)
+{
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n) return;
+    const int j = order[s];
+    const int from = inverse ? s : j, to = inverse ? j : s;
+    if (sx && dx) {
+        dx[to] = sx[from];
+        dy[to] = sy[from];
+        dz[to] = sz[from];
+    }
+    if (sf && df) df[to] = sf[from];
+    if (sidx && didx) didx[to] = sidx[from];
+}
+
 } // namespace
+
+void launch_permute_cloud(const int *order, int n, int inverse, const double *sx, const double *sy,
+                          const double *sz, const float4 *sf, const int *sidx, double *dx, double *dy, double *dz,
+                          float4 *df, int *didx, hipStream_t st)
+{
+    if (n <= 0) return;
+    permute_cloud_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(order, n, inverse, sx, sy, sz, sf, sidx, dx,
+                                                                        dy, dz, df, didx);
+}
 
 size_t query_order_scratch_bytes(int n)
 {

@@ -224,6 +224,30 @@ for s in $STEPS; do
              for sp in 8 16; do
                ICP_BUNDLE_QG=4 ICP_BUNDLE_SPLITS=$sp run bsplitq4_$sp 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
              done ;;
+    sceneab) for o in 1 0 1 0; do
+               ICP_SCENE_ORDER=$o run sceneab_$o 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               cat $OUT/sceneab_$o.log >> $OUT/sceneab_all_$o.log
+               ICP_SCENE_ORDER=$o run sceneab8_$o 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+               cat $OUT/sceneab8_$o.log >> $OUT/sceneab_all_$o.log
+               ICP_SCENE_ORDER=$o run sceneabg_$o 300 python3 bench.py --variant grid --steps 20 --no-cpu-baseline --no-cow --no-cases || exit 1
+               cat $OUT/sceneabg_$o.log >> $OUT/sceneab_all_$o.log
+             done ;;
+    recab) for o in 1 0 1 0; do
+               ICP_TRANSFORM_RECORDS=$o run recab_$o 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               cat $OUT/recab_$o.log >> $OUT/recab_all_$o.log
+               ICP_TRANSFORM_RECORDS=$o run recab8_$o 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+               cat $OUT/recab8_$o.log >> $OUT/recab_all_$o.log
+             done ;;
+    pmcsq) run pmcsq1 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+               --output-format csv -d "$OUT/pmcsq1" -o sq -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases &&
+           run pmcsq2 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAVES SQ_INST_LEVEL_VMEM SQ_ACCUM_PREV_HIRES GRBM_GUI_ACTIVE \
+               --output-format csv -d "$OUT/pmcsq2" -o sq -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-cow --no-cases ;;
+    percu) for pc in 2 3 4 2 3 4; do
+               ICP_BUNDLE_PER_CU=$pc ICP_DEBUG_PLAN=1 run percu_$pc 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               cat $OUT/percu_$pc.log >> $OUT/percu_all_$pc.log
+               ICP_BUNDLE_PER_CU=$pc run percu8_$pc 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+               cat $OUT/percu8_$pc.log >> $OUT/percu_all_$pc.log
+             done ;;
     *) echo "unknown step $s" ;;
     esac
 done
