@@ -683,6 +683,13 @@ __global__ __launch_bounds__(kBlock) void bundle_candidates_kernel(const double4
     if (tid == 0) cand_n[w] = base;
 }
 
+#ifndef ICP_B2_WAVES
+#define ICP_B2_WAVES 4 // waves per SIMD the QG = 4 filter is compiled for (112 VGPRs, no spill)
+#endif
+#ifndef ICP_B2_STREAM_U
+#define ICP_B2_STREAM_U 4
+#endif
+constexpr int kB2WavesQG4 = ICP_B2_WAVES;
 constexpr int kB2ListCap = 128; // LDS entries of a wave's fired-block list (then global)
 
 // The filter's task list: query workgroup w runs as S_w = clamp(ceil(ncand_w / ch), 1, smax)
@@ -771,7 +778,7 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
 // then the pair tests (v1's update).  Partials go to partial set s in slot order
 // (nn_finalize_mfma16_kernel reads S_w sets of them, wsplit).
 template <int QG, int PB>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) void nn_bundle2_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 ? kB2WavesQG4 : 3, 8))) void nn_bundle2_kernel(
     const BundleQuery *__restrict__ qop, const half8_t *__restrict__ gop, int np, const half8_t *__restrict__ bimg,
     int nb_pad, const int *__restrict__ cand, const int *__restrict__ cand_n, const int2 *__restrict__ tasks,
     int *__restrict__ tctl, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int *__restrict__ glist,
@@ -874,7 +881,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
         }
     };
     {
-        constexpr int U = 4;
+        constexpr int U = ICP_B2_STREAM_U; // blocks in flight per wave
         half8_t cur[U], nxt[U];
         int cid[U], nid[U];
 #pragma unroll
@@ -888,12 +895,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 8))) 
                 nid[u] = gblock(k0 + U + u);
                 nxt[u] = bimg[(size_t)nid[u] * 64 + lane];
             }
-            f32x16_t d[U];
+            // one MFMA result live at a time (16 VGPRs, not 4 x 16): 157 -> 1xx VGPRs, so that a
+            // fourth wave per SIMD fits (the deferred phase is latency-bound)
 #pragma unroll
-            for (int u = 0; u < U; ++u) d[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[u], gopB, zero, 0, 0, 0);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (k0 + u < nk) fire(cid[u], d[u]);
+            for (int u = 0; u < U; ++u) {
+                const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(cur[u], gopB, zero, 0, 0, 0);
+                if (k0 + u < nk) fire(cid[u], d);
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 cur[u] = nxt[u];
@@ -1155,11 +1163,14 @@ NNPlan plan_nn_bundle(size_t np, int nb_pad)
 }
 
 // ---- v2 launchers ---------------------------------------------------------------------------
-static int bundle2_qg() // 32-slot groups per wave: ICP_BUNDLE_QG = 4 | 8 (A/B)
+// 32-slot groups per wave: 4 (ICP_BUNDLE_QG = 8 for A/B).  QG = 4 fits four waves per SIMD
+// (112 VGPRs, 18 KiB LDS) where QG = 8 fits three (157 VGPRs): C4 0.115 against 0.141 ms, the
+// W = 8 shard 0.060 against 0.086 ms per search (profiles/r03ag/)
+static int bundle2_qg()
 {
     static const int qg = [] {
         const char *e = getenv("ICP_BUNDLE_QG");
-        return e && atoi(e) == 4 ? 4 : 8;
+        return e && atoi(e) == 8 ? 8 : 4;
     }();
     return qg;
 }

@@ -248,6 +248,21 @@ for s in $STEPS; do
                ICP_BUNDLE_PER_CU=$pc run percu8_$pc 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
                cat $OUT/percu8_$pc.log >> $OUT/percu_all_$pc.log
              done ;;
+    libab) # LIBS="name ..." (iterative-closest-point_amd/build_ab/<name>/libicp_hip.so; "tree" = the working tree's)
+           for k in 1 2; do
+             for L in ${LIBS:-tree}; do
+               lib=""; [ "$L" != tree ] && lib=iterative-closest-point_amd/build_ab/$L/libicp_hip.so
+               ICP_AMD_LIB=$lib run libab_${L}_$k 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               cat $OUT/libab_${L}_$k.log >> $OUT/libab_all_$L.log
+               ICP_AMD_LIB=$lib run libab8_${L}_$k 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+               cat $OUT/libab8_${L}_$k.log >> $OUT/libab_all_$L.log
+             done
+           done ;;
+    qg4) for k in 1 2; do
+           ICP_BUNDLE_QG=4 run qg4_$k 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+           ICP_BUNDLE_QG=4 run qg48_$k 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+           cat $OUT/qg4_$k.log $OUT/qg48_$k.log >> $OUT/qg4_all.log
+         done ;;
     *) echo "unknown step $s" ;;
     esac
 done
