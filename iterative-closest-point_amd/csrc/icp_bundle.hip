@@ -447,6 +447,109 @@ __global__ __launch_bounds__(kBlock) void build_pair_image_kd_kernel(
 // Padding bundles (no real point): W = +65504 (V^ > 0 for every in-range query).
 // bctr[b] = (c^, r') in scaled units for the block bounds: r' = -1 for a padding bundle, +inf
 // for one the image always searches.
+// The local pair test's frames (icp_bundle_rec.h): per 32-bundle block B (1,024 kd-ordered
+// points) c_B = the midpoint of its scaled points' box rounded to fp32 and R_B >= max |m - c_B|
+// (fp64, rounded up to fp32); a block without real points gets (0, 0, 0, 0).  One workgroup a
+// block.
+__global__ __launch_bounds__(kBlock) void build_block_frames_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz, int nm,
+    const int *__restrict__ kd, double cx, double cy, double cz, double scale, float4 *__restrict__ frame)
+{
+    __shared__ double s_v[6][kBlock / 64];
+    const int B = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    auto point = [&](int P, double m[3]) {
+        const int o = kd[P];
+        m[0] = (mx[o] - cx) * scale;
+        m[1] = (my[o] - cy) * scale;
+        m[2] = (mz[o] - cz) * scale;
+    };
+    double v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 1024 / kBlock; ++k) {
+        const int P = B * 1024 + k * kBlock + tid;
+        if (P >= nm) continue;
+        double m[3];
+        point(P, m);
+        for (int a = 0; a < 3; ++a) {
+            v[a] = fmin(v[a], m[a]);
+            v[3 + a] = fmax(v[3 + a], m[a]);
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1)
+        for (int a = 0; a < 3; ++a) {
+            v[a] = fmin(v[a], __shfl_xor(v[a], o, 64));
+            v[3 + a] = fmax(v[3 + a], __shfl_xor(v[3 + a], o, 64));
+        }
+    if (lane == 0)
+        for (int a = 0; a < 6; ++a) s_v[a][wave] = v[a];
+    __syncthreads();
+    float c[3];
+    bool any = false;
+    for (int a = 0; a < 3; ++a) {
+        double lo = s_v[a][0], hi = s_v[3 + a][0];
+        for (int w = 1; w < kBlock / 64; ++w) {
+            lo = fmin(lo, s_v[a][w]);
+            hi = fmax(hi, s_v[3 + a][w]);
+        }
+        any = lo <= hi;
+        c[a] = any ? (float)(0.5 * (lo + hi)) : 0.0f;
+    }
+    __syncthreads();
+    double r = 0.0;
+    for (int k = 0; k < 1024 / kBlock; ++k) {
+        const int P = B * 1024 + k * kBlock + tid;
+        if (P >= nm) continue;
+        double m[3];
+        point(P, m);
+        const double e0 = m[0] - (double)c[0], e1 = m[1] - (double)c[1], e2 = m[2] - (double)c[2];
+        r = fmax(r, sqrt((e0 * e0 + e1 * e1) + e2 * e2));
+    }
+    for (int o = 32; o >= 1; o >>= 1) r = fmax(r, __shfl_xor(r, o, 64));
+    if (lane == 0) s_v[0][wave] = r;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) r = fmax(r, s_v[0][w]);
+        r *= 1.0 + 0x1.0p-40;
+        float rf = (float)r;
+        if ((double)rf < r) rf = __uint_as_float(__float_as_uint(rf) + 1u);
+        frame[B] = any ? make_float4(c[0], c[1], c[2], rf) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}
+
+// The local pair image: build_pair_image_kd_kernel's layout with the points in their block's
+// frame, m - c_B (icp_bundle_rec.h)
+__global__ __launch_bounds__(kBlock) void build_pair_image_local_kernel(
+    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz, int nm,
+    const int *__restrict__ kd, int nm_b, double cx, double cy, double cz, double scale,
+    const float4 *__restrict__ frame, half8_t *__restrict__ img)
+{
+    for (int P = blockIdx.x * kBlock + threadIdx.x; P < nm_b; P += gridDim.x * kBlock) {
+        half8_t lo8 = {}, hi8 = {};
+        if (P < nm) {
+            const int o = kd[P];
+            const float4 f = frame[P >> 10];
+            const double b0 = (mx[o] - cx) * scale - (double)f.x, b1 = (my[o] - cy) * scale - (double)f.y,
+                         b2 = (mz[o] - cz) * scale - (double)f.z;
+            const double mm = b0 * b0 + b1 * b1 + b2 * b2;
+            _Float16 xh, xl, yh, yl, zh, zl, mh, ml;
+            split_f16(b0, xh, xl);
+            split_f16(b1, yh, yl);
+            split_f16(b2, zh, zl);
+            split_f16(mm / 4096.0, mh, ml);
+            lo8[0] = xh; lo8[1] = xl; lo8[2] = xh; lo8[3] = yh;
+            lo8[4] = yl; lo8[5] = yh; lo8[6] = zh; lo8[7] = zl;
+            hi8[0] = zh; hi8[1] = mh; hi8[2] = ml; hi8[3] = xl;
+            hi8[4] = yl; hi8[5] = zl; hi8[6] = (_Float16)16384.0f; hi8[7] = (_Float16)16384.0f;
+        } else {
+            hi8[1] = (_Float16)65504.0f;
+            hi8[6] = (_Float16)16384.0f;
+            hi8[7] = (_Float16)16384.0f;
+        }
+        const int blk = P >> 5, i = P & 31;
+        img[(size_t)blk * 64 + i] = lo8;
+        img[(size_t)blk * 64 + 32 + i] = hi8;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void build_bundle_image_kernel(
     const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz, int nm,
     const int *__restrict__ kd, int nb_pad, double cx, double cy, double cz, double scale,
@@ -557,8 +660,8 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, int np,
     const int *__restrict__ pos, const int *__restrict__ prev, const double4 *__restrict__ m4,
     const double *__restrict__ seedd, double cx, double cy, double cz, double scale,
-    const unsigned *__restrict__ seed16, int nslots, BundleQuery *__restrict__ qop, double4 *__restrict__ qraw,
-    const int *__restrict__ stop, half8_t *__restrict__ gop, double4 *__restrict__ gctr)
+    unsigned *__restrict__ seed16, int nslots, BundleQuery *__restrict__ qop, double4 *__restrict__ qraw,
+    const int *__restrict__ stop, half8_t *__restrict__ gop, double4 *__restrict__ gctr, double local_r)
 {
     if (stop && *stop) return;
     const int t = blockIdx.x * kBlock + threadIdx.x;
@@ -580,7 +683,13 @@ __global__ __launch_bounds__(kBlock) void bundle_prep_kernel(
             const double dx = p0 - m.x, dy = p1 - m.y, dz = p2 - m.z;
             D = (dx * dx + dy * dy) + dz * dz;
         }
-        bundle_record(p0, p1, p2, j, D, seed16[j], cx, cy, cz, scale, r, raw);
+        if (local_r >= 0.0) { // (the local pair test: this query's shift s0 is the certificate's seed)
+            float s0;
+            bundle_record(p0, p1, p2, j, D, 0u, cx, cy, cz, scale, r, raw, local_r, &s0);
+            seed16[j] = __float_as_uint(s0);
+        } else {
+            bundle_record(p0, p1, p2, j, D, seed16[j], cx, cy, cz, scale, r, raw);
+        }
     } else {
         bundle_never_record(r, raw);
     }
@@ -777,14 +886,16 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
 // `glist`); after one barrier each wave runs its list: per-query bounds of the fired groups,
 // then the pair tests (v1's update).  Partials go to partial set s in slot order
 // (nn_finalize_mfma16_kernel reads S_w sets of them, wsplit).
-template <int QG, int PB>
+template <int QG, int PB, bool LOCAL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 ? kB2WavesQG4 : 3, 8))) void nn_bundle2_kernel(
     const BundleQuery *__restrict__ qop, const half8_t *__restrict__ gop, int np, const half8_t *__restrict__ bimg,
     int nb_pad, const int *__restrict__ cand, const int *__restrict__ cand_n, const int2 *__restrict__ tasks,
     int *__restrict__ tctl, const half8_t *__restrict__ pimg, const int *__restrict__ kd_orig, int *__restrict__ glist,
     float *__restrict__ part_best, float *__restrict__ part_second, int *__restrict__ part_idx,
-    const int *__restrict__ stop, unsigned long long *__restrict__ counters, int ilv)
+    const int *__restrict__ stop, unsigned long long *__restrict__ counters, int ilv, const float4 *__restrict__ bframe)
 {
+    // LOCAL: the pair image is in block frames (pimg = the local image, bframe its frames) and
+    // s_bq holds each query's (fl32 a, s0): the pair operand is built per (group, fired block)
     if (stop && *stop) return; // a frozen (converged) ICP iteration: nothing to search
     constexpr int NG = 4 * QG; // groups per workgroup (<= 32: the stream MFMA's columns)
     static_assert(NG <= 32, "one stream MFMA column per group");
@@ -835,7 +946,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
     for (int q = 0; q < QG; ++q) {
         const size_t slot = (size_t)(grp0 + (ilv ? q * 4 + wave : wave * QG + q)) * 32 + col;
         bb[q] = qop[slot].bound[h];
-        s_bq[wave][q][lane] = qop[slot].pair[h];
+        s_bq[wave][q][lane] = qop[slot].pair[LOCAL ? 0 : h];
         best[q] = 0.0f; // seeded: "nothing below s0'"
         second[q] = 0.0f;
         bpos[q] = -1;
@@ -958,6 +1069,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
             n_pairs += __builtin_popcount(mask);
         }
         stamp(t_bound);
+        half8_t lop[QG]; // (LOCAL: each fired group's pair operand in this block's frame)
+        if constexpr (LOCAL) {
+            if (uni) {
+                const float4 cB = bframe[bblock];
+#pragma unroll
+                for (int q = 0; q < QG; ++q)
+                    if (gm[q]) lop[q] = local_query_frag(__builtin_bit_cast(float4, s_bq[wave][q][lane]), cB, h);
+            }
+        }
         while (uni) { // PB pair blocks in flight
             int bs[PB];
             half8_t ap[PB];
@@ -974,8 +1094,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
 #pragma unroll
                 for (int q = 0; q < QG; ++q) {
                     if (!((gm[q] >> bs[k]) & 1u)) continue;
-                    const f32x16_t dd =
-                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ap[k], s_bq[wave][q][lane], zero, 0, 0, 0);
+                    const f32x16_t dd = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                        ap[k], LOCAL ? lop[q] : s_bq[wave][q][lane], zero, 0, 0, 0);
                     pair_update(q, dd, bblock * 32 + bs[k]);
                 }
             }
@@ -1141,6 +1261,16 @@ void launch_build_bundle_images(const double *mx, const double *my, const double
     build_block_bounds_kernel<<<(nbb + 1 + kBlock - 1) / kBlock, kBlock, 0, st>>>(bctr, nbb, blk);
 }
 
+void launch_build_local_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
+                               int nb_pad, const double c[3], double scale, void *pimg_l, float4 *frame,
+                               hipStream_t st)
+{
+    const int nm_b = (nb_pad + 32) * kBundle; // (+ the null block)
+    build_block_frames_kernel<<<nm_b / 1024, kBlock, 0, st>>>(mx, my, mz, nm, kd, c[0], c[1], c[2], scale, frame);
+    build_pair_image_local_kernel<<<bgrid(nm_b), kBlock, 0, st>>>(mx, my, mz, nm, kd, nm_b, c[0], c[1], c[2],
+                                                                     scale, frame, (half8_t *)pimg_l);
+}
+
 static bool bundle_group()
 {
     static const bool on = [] {
@@ -1186,6 +1316,7 @@ static bool bundle_v1() // ICP_BUNDLE_KERNEL=1: the v1 filter (A/B)
 
 bool bundle_v2() { return !bundle_v1(); }
 
+
 // Tasks: a query workgroup with ncand candidate blocks runs as clamp(ceil(ncand / ch), 1, smax)
 // tasks (bundle_tasks_kernel), on a persistent grid of the resident workgroups.  ICP_BUNDLE_CH /
 // ICP_BUNDLE_SMAX override (A/B).
@@ -1196,6 +1327,14 @@ static int env_int(const char *name, int dflt)
 {
     const char *e = getenv(name);
     return e && atoi(e) > 0 ? atoi(e) : dflt;
+}
+bool bundle_local() // the local pair test (icp_bundle_rec.h); ICP_BUNDLE_LOCAL=0: the global one (A/B)
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_BUNDLE_LOCAL");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
 }
 
 NNPlan plan_nn_bundle2(size_t np, int nb_pad)
@@ -1212,7 +1351,7 @@ NNPlan plan_nn_bundle2(size_t np, int nb_pad)
     static int cap[2] = {0, 0};
     int &c = cap[qg == 4 ? 0 : 1];
     if (!c) {
-        const void *k = qg == 4 ? (const void *)nn_bundle2_kernel<4, 4> : (const void *)nn_bundle2_kernel<8, 4>;
+        const void *k = qg == 4 ? (const void *)nn_bundle2_kernel<4, 4, true> : (const void *)nn_bundle2_kernel<8, 4, false>;
         int dev = 0, cus = 256, per_cu = 2;
         if (hipGetDevice(&dev) == hipSuccess) {
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1238,13 +1377,13 @@ size_t bundle2_task_count(const NNPlan &pl) { return (size_t)pl.qblocks * pl.spl
 
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
                         const int *prev, const double4 *m4, const double *seedd, const double c[3], double scale,
-                        const unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
-                        const int *stop, void *gop, double4 *gctr)
+                        unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
+                        const int *stop, void *gop, double4 *gctr, double local_r)
 {
-    if (pos) gop = nullptr, gctr = nullptr; // (a scattered slot order: bundle_group_kernel after)
+    if (pos) gop = nullptr, gctr = nullptr, local_r = -1.0; // (scattered: bundle_group_kernel after; global pair test)
     bundle_prep_kernel<<<(int)((nslots + kBlock - 1) / kBlock), kBlock, 0, st>>>(
         px, py, pz, np, pos, prev, m4, seedd, c[0], c[1], c[2], scale, seed16, (int)nslots, (BundleQuery *)qop, qraw,
-        stop, (half8_t *)gop, gctr);
+        stop, (half8_t *)gop, gctr, local_r);
 }
 
 size_t bundle2_counter_rows(const NNPlan &pl) { return bundle2_task_count(pl) * 4; }
@@ -1275,14 +1414,19 @@ void launch_bundle_candidates(const NNPlan &pl, const double4 *gctr, const doubl
 void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const int *cand,
                        const int *cand_n, const int2 *tasks, int *tctl, const void *pimg, const int *kd_orig,
                        int *glist, const NNPlan &pl, float *part_best, float *part_second, int *part_idx,
-                       hipStream_t st, const int *stop, unsigned long long *counters)
+                       hipStream_t st, const int *stop, unsigned long long *counters, const float4 *bframe)
 {
     const int grid = pl.grid; // persistent: the resident workgroups pull tasks
-#define LAUNCHB2(QG, PB)                                                                                      \
-    nn_bundle2_kernel<QG, PB><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,             \
+#define LAUNCHB2L(QG, PB, L)                                                                                  \
+    nn_bundle2_kernel<QG, PB, L><<<grid, kBlock, 0, st>>>((const BundleQuery *)qop, (const half8_t *)gop, np,          \
                                              (const half8_t *)bimg, nb_pad, cand, cand_n, tasks, tctl,             \
                                              (const half8_t *)pimg, kd_orig, glist, part_best, part_second,        \
-                                             part_idx, stop, counters, ilv)
+                                             part_idx, stop, counters, ilv, bframe)
+#define LAUNCHB2(QG, PB)                                                                                      \
+    do {                                                                                                      \
+        if (bframe) LAUNCHB2L(QG, PB, true);                                                                  \
+        else LAUNCHB2L(QG, PB, false);                                                                        \
+    } while (0)
     static const int pb = env_int("ICP_BUNDLE_PB", 4); // pair blocks in flight: 4 | 8 (A/B)
     // wave v owns groups v, v + 4, ... of its workgroup (ICP_BUNDLE_ILV=1) or v QG .. (v+1) QG - 1
     static const int ilv = env_int("ICP_BUNDLE_ILV", 2) == 1 ? 1 : 0;
@@ -1290,6 +1434,7 @@ void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bim
     else if (pb == 8) LAUNCHB2(8, 8);
     else LAUNCHB2(8, 4);
 #undef LAUNCHB2
+#undef LAUNCHB2L
 }
 
 void launch_nn_bundle(const double *px, const double *py, const double *pz, int np, const int *order,

@@ -297,6 +297,12 @@ struct icp_ctx {
     // The resident scene in slot order (scene_in_slot_order): point s of the scene (and idx[s]
     // while seeds_valid) is the caller's point s_order[s].  icp_get_scene / icp_get_indices and
     // the index digests map back; every other per-point pass is order-agnostic.
+    // the local pair test (icp_bundle_rec.h): the pair image in block frames, the frames (c_B,
+    // R_B) and max R_B (-1: not built)
+    char *b_pimg_l = nullptr;
+    float4 *b_frame = nullptr;
+    size_t b_pimg_l_cap = 0, b_frame_cap = 0;
+    double b_rlmax = -1.0;
     bool scene_slot = false;
     int *s_order = nullptr;
     size_t s_order_cap = 0;
@@ -719,10 +725,14 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         const NNPlan pl = l1 == 3   ? (v2 ? plan_nn_bundle2(n, ctx->nb_pad) : plan_nn_bundle(n, ctx->nb_pad))
                           : l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd)
                                     : plan_nn_mfma(n, ctx->nm_pad);
+        // the local pair test (icp_bundle_rec.h): with the queries in slot order (no scattered
+        // records) and the model's block frames built; ICP_BUNDLE_LOCAL=0 keeps the global one
+        const bool local = v2 && slot_order && ctx->b_rlmax >= 0.0 && bundle_local();
         if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
-            launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->m4, ctx->c, ctx->scale16, ctx->seed16,
-                               ctx->st);
+            if (!local) // (local: the prep writes each query's shift there)
+                launch_mfma16_seed(q.x, q.y, q.z, (int)n, ctx->idx, ctx->m4, ctx->c, ctx->scale16, ctx->seed16,
+                                   ctx->st);
         }
         const unsigned *seeds = sd ? ctx->seed16 : nullptr;
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap,
@@ -763,9 +773,9 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             // point's seed distance, SeedArgs::seedd; records_ready: the records and group bounds
             // themselves, SeedArgs::qop)
             if (!records_ready) launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4,
-                               seeds_ready ? ctx->b_seedd : nullptr, ctx->c, ctx->scale16, seeds, nslots, ctx->b_qop,
+                               seeds_ready ? ctx->b_seedd : nullptr, ctx->c, ctx->scale16, sd ? ctx->seed16 : nullptr, nslots, ctx->b_qop,
                                order ? ctx->b_qraw : nullptr, ctx->st, stop, order ? nullptr : ctx->b_gop,
-                               order ? nullptr : ctx->b_gctr);
+                               order ? nullptr : ctx->b_gctr, local ? ctx->b_rlmax : -1.0);
             if (order && !records_ready) launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->b_gctr, ctx->st, stop);
             launch_bundle_candidates(pl, ctx->b_gctr, ctx->b_blk, ctx->nb_pad, ctx->b_cand, ctx->b_cand_n,
                                      ctx->b_wsplit, ctx->b_tasks, ctx->b_tctl, ctx->st, stop);
@@ -773,8 +783,9 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         if (v2)
             launch_nn_bundle2(ctx->b_qop, ctx->b_gop, (int)n, ctx->b_img, ctx->nb_pad, ctx->b_cand, ctx->b_cand_n,
-                              ctx->b_tasks, ctx->b_tctl, ctx->b_pimg, ctx->b_kd_orig, ctx->b_glist, pl, pb, ps, pi,
-                              ctx->st, stop, ctx->b_counters);
+                              ctx->b_tasks, ctx->b_tctl, local ? ctx->b_pimg_l : ctx->b_pimg, ctx->b_kd_orig,
+                              ctx->b_glist, pl, pb, ps, pi, ctx->st, stop, ctx->b_counters,
+                              local ? ctx->b_frame : nullptr);
         else if (l1 == 3)
             launch_nn_bundle(q.x, q.y, q.z, (int)n, order, ctx->idx, ctx->m4, ctx->c, ctx->scale16, seeds, ctx->b_img,
                              ctx->nb_pad, ctx->b_pimg, ctx->b_kd_orig, (int)ctx->nm, pl, pb, ps, pi, ctx->st, stop,
@@ -790,7 +801,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                                       ctx->scale16, seeds, ctx->mms16, ctx->idx, ctx->amb_count + 2, ctx->amb1,
                                       ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit,
                                       v2 && order ? ctx->b_qraw : nullptr, // (slot s = query s: p read in order)
-                                      v2 ? ctx->b_wsplit : nullptr, v2 ? 4 * pl.q_per_lane * 32 : 0);
+                                      v2 ? ctx->b_wsplit : nullptr, v2 ? 4 * pl.q_per_lane * 32 : 0,
+                                      local ? ctx->b_rlmax : -1.0);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
@@ -1181,7 +1193,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->b_qop, (void *)ctx->b_gop, (void *)ctx->b_qraw, (void *)ctx->b_glist, (void *)ctx->q_pos, (void *)ctx->cr_entries,
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
-                    (void *)ctx->s_order, (void *)ctx->s_tmp_idx})
+                    (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -1335,6 +1347,7 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
             ctx->m_hi[k] = std::max(ctx->m_hi[k], m_xyz[3 * j + k]);
         }
     ctx->nb_pad = 0;
+    ctx->b_rlmax = -1.0;
     if (nm >= (size_t)kBundleMinModel) { // the bundle filter's kd images (icp_bundle.hip)
         const std::vector<int> kd = bundle_kd_order(m_xyz, nm);
         const int nb_pad = bundle_pad(nm);
@@ -1350,7 +1363,19 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
                                    ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_bctr, ctx->b_blk,
                                    ctx->st);
         LAUNCHCHK("build_bundle_images");
+        // the local pair test's image and block frames, and max R_B (the certificate's R)
+        const size_t nfr = nbx / 32;
+        TRY(grow(ctx, &ctx->b_pimg_l, &ctx->b_pimg_l_cap, nbx * 1024));
+        TRY(grow(ctx, &ctx->b_frame, &ctx->b_frame_cap, nfr));
+        launch_build_local_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
+                                  ctx->scale16, ctx->b_pimg_l, ctx->b_frame, ctx->st);
+        LAUNCHCHK("build_local_images");
+        std::vector<float4> fr(nfr);
+        HIPCHK(hipMemcpyAsync(fr.data(), ctx->b_frame, sizeof(float4) * nfr, hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st)); // (kd is freed on return)
+        double rl = 0.0;
+        for (const float4 &f : fr) rl = std::max(rl, (double)f.w);
+        ctx->b_rlmax = rl;
         ctx->nb_pad = nb_pad;
     }
     HIPCHK(hipStreamSynchronize(ctx->st));
@@ -1871,6 +1896,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     sa.gop = ctx->b_gop;
                     sa.gctr = ctx->b_gctr;
                     sa.nslots = (int)nslots;
+                    sa.local_r = ctx->b_rlmax >= 0.0 && bundle_local() ? ctx->b_rlmax : -1.0; // (as the search decides)
                 }
             }
             ctx->seeds_valid = true; // idx pairs every point of the resident scene

@@ -152,7 +152,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop = nullptr, const double4 *m4 = nullptr,
                                unsigned *audit = nullptr, const double4 *qraw = nullptr,
-                               const int *wsplit = nullptr, int wslots = 0);
+                               const int *wsplit = nullptr, int wslots = 0,
+                               double local_r = -1.0); // (>= 0: the local pair test's certificate, seed16 = s0 bits)
 // A split plan for `kernel` (make_plan): np queries in workgroups of queries_per_lane_block,
 // the model axis (nm rows, tiles of `tile`) split to fill >= 4 rounds of resident workgroups.
 NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel,
@@ -166,6 +167,11 @@ NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_
 // block and the null block, nb_pad / 32 + 1: centre and radius over its bundles).
 int bundle_pad(size_t nm);
 std::vector<int> bundle_kd_order(const double *m_xyz, size_t nm);
+// the local pair test's block frames (float4 (c_B, R_B) per 32-bundle block, nb_pad / 32 + 1)
+// and its pair image (1 KiB per bundle, the points relative to their block's frame)
+void launch_build_local_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
+                               int nb_pad, const double c[3], double scale, void *pimg_l, float4 *frame,
+                               hipStream_t st);
 void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
                                 int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
                                 double4 *bctr, double4 *blk, hipStream_t st);
@@ -189,6 +195,7 @@ void launch_nn_bundle(const double *px, const double *py, const double *pz, int 
 // u64 fields per counter row (icp_set_bundle_counters): 9 of v1's shared row, 12 per v2 wave task
 constexpr int kBundleCounterFields = 12;
 bool bundle_v2();
+bool bundle_local(); // the local-frame pair test with a scene in slot order (ICP_BUNDLE_LOCAL=0: off)
 NNPlan plan_nn_bundle2(size_t np, int nb_pad);
 constexpr int kBundleTctlInts = 32 * 9;
 size_t bundle2_slots(const NNPlan &pl);
@@ -198,8 +205,11 @@ size_t bundle2_counter_rows(const NNPlan &pl);
 // else gathered here
 void launch_bundle_prep(const double *px, const double *py, const double *pz, int np, const int *pos,
                         const int *prev, const double4 *m4, const double *seedd, const double c[3], double scale,
-                        const unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
-                        const int *stop = nullptr, void *gop = nullptr, double4 *gctr = nullptr);
+                        unsigned *seed16, size_t nslots, void *qop, double4 *qraw, hipStream_t st,
+                        const int *stop = nullptr, void *gop = nullptr, double4 *gctr = nullptr,
+                        double local_r = -1.0);
+// (local_r >= 0 with pos == null: the local pair test's records, R = local_r, and seed16[j]
+// receives query j's shift s0 as float bits -- the finalize's seed)
 // (gop / gctr with pos == null: the prep also writes the group bounds, launch_bundle_groups's
 // output, from the records in registers)
 // gop (nslots bytes): the 32-slot groups' bounds from the records (after the prep); gctr
@@ -217,7 +227,8 @@ size_t bundle2_task_count(const NNPlan &pl);
 void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const int *cand,
                        const int *cand_n, const int2 *tasks, int *tctl, const void *pimg, const int *kd_orig,
                        int *glist, const NNPlan &pl, float *part_best, float *part_second, int *part_idx,
-                       hipStream_t st, const int *stop = nullptr, unsigned long long *counters = nullptr);
+                       hipStream_t st, const int *stop = nullptr, unsigned long long *counters = nullptr,
+                       const float4 *bframe = nullptr); // (bframe: the local pair test, pimg = its image);
 // order[k] = the query processed k-th: the queries sorted by the Morton code of their cell in a
 // 1024^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
 // = k); scratch: query_order_scratch_bytes(n)
@@ -367,6 +378,9 @@ struct SeedArgs {
     void *qop = nullptr, *gop = nullptr;
     double4 *gctr = nullptr;
     int nslots = 0;
+    // >= 0: the records are the local pair test's (icp_bundle_rec.h; its R = max block radius),
+    // and seed16 receives each point's shift s0 (float bits) instead of the f16 seed
+    double local_r = -1.0;
 };
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,

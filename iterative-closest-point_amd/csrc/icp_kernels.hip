@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint,
     const int *__restrict__ stop, const double4 *__restrict__ m4, unsigned *__restrict__ audit,
-    const double4 *__restrict__ qraw, const int *__restrict__ wsplit, int wslots)
+    const double4 *__restrict__ qraw, const int *__restrict__ wsplit, int wslots, double local_r)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
     // R queries per lane group (rounds r: slots (blockIdx.x R + r) kBlock / G + threadIdx.x / G,
@@ -1309,7 +1309,28 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
         const double ax = (q0 - cx) * scale, ay = (q1 - cy) * scale, az = (q2 - cz) * scale;
         bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
                   fabs(az) <= kF16QueryClamp;
-        if (ok) {
+        if (ok && local_r >= 0.0) {
+            // the local pair test (icp_bundle_rec.h): values D - s0 with s0 = the query's shift
+            // (seed16: its float bits), every evaluated pair within delta_local of it.  With d0 =
+            // delta_local at D = max(b, 0) + 64 (<= 64, and delta grows slower than D, so the
+            // winner's true D <= b + d0 and every competitor as near is within d0 too): second > b
+            // + 2 d0 proves the winner unique.  Out-of-range (forced) queries are not certified.
+            const double s0 = (double)__uint_as_float(sdq);
+            const double a2 = ax * ax + ay * ay + az * az, an = sqrt(a2);
+            const double bg = (double)b + s0, sg = (double)s2 + s0, bp = fmax(bg, 0.0);
+            const double d0 = delta_local(bp + 64.0, an, local_r, s0);
+            const double T = bg + 2.0 * d0 + 0x1.0p-40 * (bp + 64.0) + (fabs(bg) + fabs(s0)) * 1e-12 + 1e-300;
+            ok = fabs(ax) <= kBQueryMax && fabs(ay) <= kBQueryMax && fabs(az) <= kBQueryMax && s0 == s0 &&
+                 s0 < 1.0e30 && d0 <= 64.0 && bp <= 1048576.0 && sg > T;
+            if (audit && ok && sub == 0) { // (the winner's error against d0, the margin against 2 d0)
+                const double4 mb = m4[id];
+                const double b0 = (mb.x - cx) * scale - ax, b1 = (mb.y - cy) * scale - ay, b2 = (mb.z - cz) * scale - az;
+                const double d64 = (b0 * b0 + b1 * b1) + b2 * b2;
+                atomicMax(audit, __float_as_uint((float)(fabs(bg - d64) / d0)));
+                atomicMin(audit + 1, __float_as_uint((float)fmax((sg - T) / (T - bg), 0.0)));
+                atomicAdd(audit + 2, 1u);
+            }
+        } else if (ok) {
             const double u = 0x1.0p-24;
             const double a2 = ax * ax + ay * ay + az * az;
             const double A = sqrt(a2);
@@ -1851,12 +1872,20 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
                 pz[i] = q2;
                 if (p32)
                     p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
-                const unsigned sd = mfma16_seed_value(q0, q1, q2, y0, y1, y2, sa.c[0], sa.c[1], sa.c[2], sa.scale);
-                sa.seed16[i] = sd;
                 const double dx = q0 - y0, dy = q1 - y1, dz = q2 - y2;
                 double4 raw;
-                bundle_record(q0, q1, q2, i, (dx * dx + dy * dy) + dz * dz, sd, sa.c[0], sa.c[1], sa.c[2], sa.scale,
-                              r, raw);
+                if (sa.local_r >= 0.0) { // (the local pair test: the shift is the finalize's seed)
+                    float s0;
+                    bundle_record(q0, q1, q2, i, (dx * dx + dy * dy) + dz * dz, 0u, sa.c[0], sa.c[1], sa.c[2],
+                                  sa.scale, r, raw, sa.local_r, &s0);
+                    sa.seed16[i] = __float_as_uint(s0);
+                } else {
+                    const unsigned sd =
+                        mfma16_seed_value(q0, q1, q2, y0, y1, y2, sa.c[0], sa.c[1], sa.c[2], sa.scale);
+                    sa.seed16[i] = sd;
+                    bundle_record(q0, q1, q2, i, (dx * dx + dy * dy) + dz * dz, sd, sa.c[0], sa.c[1], sa.c[2],
+                                  sa.scale, r, raw);
+                }
             } else {
                 double4 raw;
                 bundle_never_record(r, raw);
@@ -2239,7 +2268,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop, const double4 *m4, unsigned *audit,
-                               const double4 *qraw, const int *wsplit, int wslots)
+                               const double4 *qraw, const int *wsplit, int wslots, double local_r)
 {
     // (its fp64 certificate is heavy and every lane of a group repeats it: lanes only pay off
     // for very many splits; ICP_FIN16_LANES = 1 | 4 | 8 overrides, for experiments)
@@ -2255,7 +2284,7 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
     nn_finalize_mfma16_kernel<SD, G, R><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
                                                               pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
                                                               idx, amb_count, amb_list, amb_hint, stop, m4, audit, \
-                                                              qraw, wsplit, wslots)
+                                                              qraw, wsplit, wslots, local_r)
 #define FIN16(SD, G)                                                                                         \
     do {                                                                                                     \
         if (rounds == kFin16Rounds) FIN16R(SD, G, kFin16Rounds);                                             \

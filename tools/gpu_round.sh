@@ -263,6 +263,11 @@ for s in $STEPS; do
            ICP_BUNDLE_QG=4 run qg48_$k 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
            cat $OUT/qg4_$k.log $OUT/qg48_$k.log >> $OUT/qg4_all.log
          done ;;
+    localab) for o in 1 0 1 0; do
+               ICP_BUNDLE_LOCAL=$o run localab_$o 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               ICP_BUNDLE_LOCAL=$o run localab8_$o 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
+               cat $OUT/localab_$o.log $OUT/localab8_$o.log >> $OUT/localab_all_$o.log
+             done ;;
     *) echo "unknown step $s" ;;
     esac
 done
