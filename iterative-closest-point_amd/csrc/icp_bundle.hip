@@ -447,6 +447,21 @@ __global__ __launch_bounds__(kBlock) void build_pair_image_kd_kernel(
 // Padding bundles (no real point): W = +65504 (V^ > 0 for every in-range query).
 // bctr[b] = (c^, r') in scaled units for the block bounds: r' = -1 for a padding bundle, +inf
 // for one the image always searches.
+// The model in kd order, m4kd[P] = m4[kd_orig[P]], and the kd order's inverse kd_of[o] = P
+// (real points): a scene resident in slot order gathers its correspondences from the kd-ordered
+// copy (kpos, which the searches maintain next to idx), where the neighbouring queries' points
+// are neighbours -- the moments' gather from the model's own order fetched 2x its bytes
+__global__ __launch_bounds__(kBlock) void build_kd_tables_kernel(const double4 *__restrict__ m4,
+                                                                 const int *__restrict__ kd_orig, int nm,
+                                                                 double4 *__restrict__ m4kd, int *__restrict__ kd_of)
+{
+    for (int P = blockIdx.x * kBlock + threadIdx.x; P < nm; P += gridDim.x * kBlock) {
+        const int o = kd_orig[P];
+        m4kd[P] = m4[o];
+        kd_of[o] = P;
+    }
+}
+
 // The local pair test's frames (icp_bundle_rec.h): per 32-bundle block B (1,024 kd-ordered
 // points) c_B = the midpoint of its scaled points' box rounded to fp32 and R_B >= max |m - c_B|
 // (fp64, rounded up to fp32); a block without real points gets (0, 0, 0, 0).  One workgroup a
@@ -1162,8 +1177,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
         es[q] = ss;
         eo[q] = id;
     }
+    // (LOCAL: the partials carry kd positions -- the finalize maps them, and keeps them for the
+    // moments' kd-ordered gather)
+    if constexpr (!LOCAL) {
 #pragma unroll
-    for (int q = 0; q < QG; ++q) eo[q] = eo[q] >= 0 ? kd_orig[eo[q]] : -1;
+        for (int q = 0; q < QG; ++q) eo[q] = eo[q] >= 0 ? kd_orig[eo[q]] : -1;
+    }
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
         const int slot = (grp0 + (ilv ? q * 4 + wave : wave * QG + q)) * 32 + col;
@@ -1259,6 +1278,11 @@ void launch_build_bundle_images(const double *mx, const double *my, const double
                                                                    scale, (half8_t *)bimg, bctr);
     const int nbb = nb_pad >> 5;
     build_block_bounds_kernel<<<(nbb + 1 + kBlock - 1) / kBlock, kBlock, 0, st>>>(bctr, nbb, blk);
+}
+
+void launch_build_kd_tables(const double4 *m4, const int *kd_orig, int nm, double4 *m4kd, int *kd_of, hipStream_t st)
+{
+    if (nm > 0) build_kd_tables_kernel<<<bgrid(nm), kBlock, 0, st>>>(m4, kd_orig, nm, m4kd, kd_of);
 }
 
 void launch_build_local_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,

@@ -38,9 +38,11 @@ __device__ __forceinline__ void shifted_moment_point(int i, const int *__restric
                                                      const double *__restrict__ py, const double *__restrict__ pz,
                                                      double *__restrict__ yx, double *__restrict__ yy,
                                                      double *__restrict__ yz, double cp0, double cp1, double cp2,
-                                                     double cy0, double cy1, double cy2, double (&a)[17])
+                                                     double cy0, double cy1, double cy2, double (&a)[17],
+                                                     const int *__restrict__ kpos = nullptr,
+                                                     const double4 *__restrict__ m4kd = nullptr)
 {
-    const double4 m = m4[idx[i]];
+    const double4 m = kpos ? m4kd[kpos[i]] : m4[idx[i]]; // (kpos: the same point, kd-ordered copy)
     yx[i] = m.x;
     yy[i] = m.y;
     yz[i] = m.z;

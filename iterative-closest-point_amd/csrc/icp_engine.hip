@@ -303,7 +303,14 @@ struct icp_ctx {
     float4 *b_frame = nullptr;
     size_t b_pimg_l_cap = 0, b_frame_cap = 0;
     double b_rlmax = -1.0;
+    // the model in kd order and the kd order's inverse (launch_build_kd_tables), and per query
+    // its correspondence's kd position (kpos_valid: the last search over the resident scene kept it)
+    double4 *m4kd = nullptr;
+    int *kd_of = nullptr, *kpos = nullptr;
+    size_t m4kd_cap = 0, kd_of_cap = 0, kpos_cap = 0;
+    bool kpos_valid = false;
     bool scene_slot = false;
+    bool p32_stale = false; // the scene's fp32 copy was not kept by the last icp_run (its path never read it)
     int *s_order = nullptr;
     size_t s_order_cap = 0;
     DevCloud s_tmp;                           // the permutation's second buffer
@@ -508,7 +515,7 @@ int ensure_reduction_space(icp_ctx *ctx)
     // NN queue counters: present even for an empty shard (horn_step folds and resets them
     // every iteration, whether or not this rank searched anything)
     HIPCHK(hipMalloc((void **)&ctx->amb_count, sizeof(int) * 4));
-    HIPCHK(hipMemset(ctx->amb_count, 0, sizeof(int) * 4));
+    HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st)); // (ordered before the stream's kernels)
     return ICP_OK;
 }
 
@@ -670,7 +677,9 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                     bool slot_order = false, bool records_ready = false)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
+    ctx->kpos_valid = false;
     if (!n) return ICP_OK;
+    int *kpos_out = nullptr; // (the local bundle filter: each writer of idx also writes kpos)
     // small models: the grid resolver scans its rare leftovers exactly in place (no fp64
     // brute-force launch, which would almost always find an empty queue)
     const int inline_nm = ctx->nm <= (size_t)kInlineFallbackModel ? (int)ctx->nm : 0;
@@ -728,6 +737,12 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // the local pair test (icp_bundle_rec.h): with the queries in slot order (no scattered
         // records) and the model's block frames built; ICP_BUNDLE_LOCAL=0 keeps the global one
         const bool local = v2 && slot_order && ctx->b_rlmax >= 0.0 && bundle_local();
+        // (local: the partials carry kd positions; every writer of idx below then keeps kpos too,
+        // unless the CPU rule's host fix-up may rewrite idx after the search)
+        if (local && ctx->nn_rule == ICP_NN_RULE_SQUARED && ctx->m4kd) {
+            TRY(grow(ctx, &ctx->kpos, &ctx->kpos_cap, n));
+            kpos_out = ctx->kpos;
+        }
         if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
             if (!local) // (local: the prep writes each query's shift there)
@@ -802,7 +817,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                                       ctx->amb1_hint, ctx->st, stop, ctx->m4, ctx->cert_audit,
                                       v2 && order ? ctx->b_qraw : nullptr, // (slot s = query s: p read in order)
                                       v2 ? ctx->b_wsplit : nullptr, v2 ? 4 * pl.q_per_lane * 32 : 0,
-                                      local ? ctx->b_rlmax : -1.0);
+                                      local ? ctx->b_rlmax : -1.0, local ? ctx->b_kd_orig : nullptr, kpos_out);
         else
             launch_nn_finalize_mfma(pb, ps, pi, pl.splits, q.f, (int)n, ctx->mm, (int)ctx->nm, ctx->idx, ctx->amb_count + 2,
                                     ctx->amb1, ctx->amb1_hint, ctx->st);
@@ -810,12 +825,13 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // what it cannot take (none at C4): fp64 over every model point, one workgroup each
         launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                                grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
-                               ctx->fb_T, ctx->st, stop, inline_nm);
+                               ctx->fb_T, ctx->st, stop, inline_nm, kpos_out, ctx->kd_of);
         if (!inline_nm)
             launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32,
                               ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st,
-                              stop);
+                              stop, kpos_out, ctx->kd_of);
         LAUNCHCHK("nn_mfma");
+        ctx->kpos_valid = kpos_out != nullptr;
     } else {
         const NNPlan pl = plan_nn32(n, ctx->nm_pad);
         const size_t need = (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int));
@@ -1193,7 +1209,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->b_qop, (void *)ctx->b_gop, (void *)ctx->b_qraw, (void *)ctx->b_glist, (void *)ctx->q_pos, (void *)ctx->cr_entries,
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
-                    (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame})
+                    (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame,
+                    (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -1370,6 +1387,10 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         launch_build_local_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
                                   ctx->scale16, ctx->b_pimg_l, ctx->b_frame, ctx->st);
         LAUNCHCHK("build_local_images");
+        TRY(grow(ctx, &ctx->m4kd, &ctx->m4kd_cap, nm));
+        TRY(grow(ctx, &ctx->kd_of, &ctx->kd_of_cap, nm));
+        launch_build_kd_tables(ctx->m4, ctx->b_kd_orig, (int)nm, ctx->m4kd, ctx->kd_of, ctx->st);
+        LAUNCHCHK("build_kd_tables");
         std::vector<float4> fr(nfr);
         HIPCHK(hipMemcpyAsync(fr.data(), ctx->b_frame, sizeof(float4) * nfr, hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st)); // (kd is freed on return)
@@ -1393,6 +1414,7 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1],
                         ctx->c[2], ctx->scene.f, ctx->st);
         LAUNCHCHK("make_f32");
+        ctx->p32_stale = false;
         HIPCHK(hipStreamSynchronize(ctx->st));
     }
     return ICP_OK;
@@ -1430,6 +1452,7 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     ctx->seeds_valid = false;
     ctx->q_order_src = nullptr; // new contents: a new query order
     ctx->scene_slot = false;    // (in the caller's order)
+    ctx->p32_stale = false;
     return ICP_OK;
 }
 
@@ -1454,7 +1477,8 @@ int icp_get_scene(icp_ctx *ctx, double *p_xyz_out)
 static int moments_phase(icp_ctx *ctx, size_t n)
 {
     const DevCloud &P = ctx->scene, &Y = ctx->Y;
-    launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, red_target(ctx, n, ctx->sums + kSumP), ctx->st);
+    launch_gather_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, red_target(ctx, n, ctx->sums + kSumP),
+                          ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr, ctx->m4kd);
     red_finish(ctx, n, 6, ctx->sums + kSumP);
     LAUNCHCHK("moments");
     TRY(allreduce(ctx, ctx->sums + kSumP, 6));
@@ -1809,6 +1833,17 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         ctx->iter_ev.push_back(e);
     }
+    // the scene's fp32 copy is read only by the fp32 filters (level 1 VALU / f32 MFMA), their
+    // windowed resolve and the one-launch paths: other runs let the transform skip it (16 B a
+    // point) and leave it to be refreshed here when a later run needs it
+    const bool need_p32 = (ctx->nn_mode == ICP_NN_CERTIFIED && level1_kind(ctx, n) <= 1 &&
+                           ctx->nn_variant != ICP_NN_VARIANT_GRID) ||
+                          n <= (size_t)kTailMaxBlocks * kBlock;
+    if (need_p32 && ctx->p32_stale) {
+        if (n) launch_make_f32(P.x, P.y, P.z, n, ctx->c[0], ctx->c[1], ctx->c[2], P.f, ctx->st);
+        LAUNCHCHK("make_f32");
+        ctx->p32_stale = false;
+    }
     {
         size_t lds = 0;
         bool mid = false;
@@ -1920,6 +1955,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 ++enqueued;
                 continue;
             }
+            bool horn_fused = false; // (reduce_horn: the Horn step rode on the moments' fold)
             // 2-3. centroids, centred cross-covariance and norms (gpu.cc:98-104, :142): the first
             // iteration two-pass (the reference's order); later ones in one pass around the shifts
             // the previous Horn step left (its transformed centroid, its correspondence centroid)
@@ -1973,8 +2009,15 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 continue;
             } else {
                 launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
-                                       red_target(ctx, n, ctx->sums), ctx->st);
-                red_finish(ctx, n, 17, ctx->sums);
+                                       red_target(ctx, n, ctx->sums), ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr,
+                                       ctx->m4kd);
+                if (!lag && red_blocks(n) > 1) { // the fold and the Horn step in one launch
+                    launch_reduce_horn(ctx->partials, red_blocks(n), ctx->sums, N, ctx->c, 1, ctx->amb_count, sd,
+                                       ctx->st);
+                    horn_fused = true;
+                } else {
+                    red_finish(ctx, n, 17, ctx->sums);
+                }
                 LAUNCHCHK("shifted_moments");
                 if (lag) { // + the previous iteration's residual (sums[kSumErr], local until now)
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 3], ctx->st));
@@ -1985,10 +2028,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 }
             }
             // 4. Horn solve (gpu.cc:106-146) on the device
-            launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
+            if (!horn_fused) launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
-            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, P.f,
+            launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, need_p32 ? P.f : nullptr,
                                      red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
+            if (!need_p32) ctx->p32_stale = true;
             const bool fold_err = !lag && red_blocks(n) > 1; // (folded by the error step's launch)
             if (!fold_err) red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
@@ -2397,7 +2441,11 @@ int icp_set_index_digest(icp_ctx *ctx, size_t cap)
             ctx->digest = nullptr;
             HIPCHK(hipMalloc((void **)&ctx->digest, sizeof(unsigned long long) * 3 * cap));
         }
-        HIPCHK(hipMemset(ctx->digest, 0, sizeof(unsigned long long) * 3 * cap));
+        // (on the engine stream: a null-stream hipMemset is not ordered against the non-blocking
+        // engine stream and may land in the middle of the next run's digests -- seen once in
+        // the 8-context C5 test, a digest 9% short)
+        HIPCHK(hipMemsetAsync(ctx->digest, 0, sizeof(unsigned long long) * 3 * cap, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
     }
     ctx->digest_cap = cap;
     return ICP_OK;

@@ -250,8 +250,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count,
     int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out, const int *__restrict__ stop,
-    int inline_nm, int n_all)
+    int inline_nm, int n_all, int *__restrict__ kpos, const int *__restrict__ kd_of)
 {
+    // (kpos, nullable: the resolved queries' kd positions, kd_of[index], next to idx)
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     // list == nullptr: every query t = 0 .. n_all-1, its candidate the previous correspondence
     // already in idx[t] (the seeded grid variant)
@@ -276,7 +277,10 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
         if (ok) {
             scan_box_sel<G, FLAT>(q, c0, c1, gv, sub, best, bi);
             group_lex_min<G>(best, bi);
-            if (sub == 0) idx[j] = bi;
+            if (sub == 0) {
+                idx[j] = bi;
+                if (kpos) kpos[j] = kd_of[bi];
+            }
         } else if (inline_nm > 0) { // small model: the exact fp64 scan of every point, right here
             best = INFINITY;
             bi = -1;
@@ -285,7 +289,10 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
                 lex_min(best, bi, d64g(q[0], q[1], q[2], m.x, m.y, m.z), k);
             }
             group_lex_min<G>(best, bi);
-            if (sub == 0) idx[j] = bi < 0 ? 0 : bi; // (no comparison held: a NaN query -> index 0)
+            if (sub == 0) {
+                idx[j] = bi < 0 ? 0 : bi;
+                if (kpos) kpos[j] = kd_of[bi < 0 ? 0 : bi];
+            } // (no comparison held: a NaN query -> index 0)
         }
         // queue for nn_resolve -- or, scanned inline, only counted (the fallback statistic)
         const bool fb = !ok && sub == 0;
@@ -509,7 +516,8 @@ void launch_nn_grid_seed(int np, const double *px, const double *py, const doubl
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
-                            const double *T_in, double *T_out, hipStream_t st, const int *stop, int inline_nm)
+                            const double *T_in, double *T_out, hipStream_t st, const int *stop, int inline_nm,
+                            int *kpos, const int *kd_of)
 {
     // lanes per queued query, measured: a whole wave for searches of 8,192 to 2^18 queries (horse /
     // bunny surfaces: big boxes of dense surface cells; 64 lanes 4,289 vs 16 lanes 3,231 it/s
@@ -521,10 +529,17 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
     }();
     const int g = forced == 4 || forced == 16 || forced == 64 ? forced : (max_items >= 8192 && max_items < (1 << 18) ? 64 : 16);
     const int per_block = kBlock / g;
-    const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, 4096));
+    // (a grid-stride over the device-side count: the cap bounds the launch when the queue is a
+    // small share of max_items; ICP_GRID_RBLOCKS overrides it for A/B)
+    static const int cap = [] {
+        const char *e = getenv("ICP_GRID_RBLOCKS");
+        return e && atoi(e) > 0 ? atoi(e) : 4096;
+    }();
+    const int blocks = std::max(1, std::min((max_items + per_block - 1) / per_block, cap));
 #define RESOLVE(GG, F)                                                                                  \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx, \
-                                                             fb_count, fb_list, T_in, T_out, stop, inline_nm, 0)
+                                                             fb_count, fb_list, T_in, T_out, stop, inline_nm, 0, \
+                                                             kpos, kd_of)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE(4, true);
         else if (g == 64) RESOLVE(64, true);
@@ -552,7 +567,8 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
     const int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
 #define RESOLVE_ALL(GG, F)                                                                                       \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(nullptr, nullptr, nullptr, px, py, pz, m4, gv, budget, \
-                                                             idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n)
+                                                             idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n, \
+                                                             nullptr, nullptr)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE_ALL(4, true);
         else RESOLVE_ALL(16, true);

@@ -94,6 +94,46 @@ __global__ __launch_bounds__(64) void horn_step_kernel(const double *__restrict_
     horn_step_body(sums, N, c0, c1, c2, shifted, cnt, s);
 }
 
+// reduce_kernel<17> and horn_step_kernel in one launch (one rank: no all-reduce between them):
+// the same fold (per-thread rows b = t, t + kBlock, ..., the xor-shuffle tree per wave, the wave
+// sums in wave order), then thread 0 solves from the folded sums
+__global__ __launch_bounds__(kBlock) void reduce_horn_kernel(const double *__restrict__ partials, int nblocks,
+                                                             double *__restrict__ sums, double N, double c0, double c1,
+                                                             double c2, int shifted, int *__restrict__ cnt,
+                                                             IterState *__restrict__ s)
+{
+    constexpr int K = 17;
+    __shared__ double sh[kBlock / 64][K];
+    __shared__ double s_sum[K];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.0;
+    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += partials[(size_t)b * K + k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[wave][k] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        double r = sh[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
+        sums[threadIdx.x] = r;
+        s_sum[threadIdx.x] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) horn_step_body(s_sum, N, c0, c1, c2, shifted, cnt, s);
+}
+
 __global__ __launch_bounds__(64) void err_step_kernel(const double *__restrict__ sums, double N, double threshold, int max_iter,
                                 double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag, int ticket,
                                 IterState *h_state, double *h_trace)
@@ -1772,6 +1812,13 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], int
                       IterState *st_dev, hipStream_t st)
 {
     horn_step_kernel<<<1, 1, 0, st>>>(sums, n_total, c[0], c[1], c[2], shifted, amb_count, st_dev);
+}
+
+void launch_reduce_horn(const double *partials, int nblocks, double *sums, double n_total, const double c[3],
+                        int shifted, int *amb_count, IterState *st_dev, hipStream_t st)
+{
+    reduce_horn_kernel<<<1, kBlock, 0, st>>>(partials, nblocks, sums, n_total, c[0], c[1], c[2], shifted, amb_count,
+                                             st_dev);
 }
 
 void launch_err_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,

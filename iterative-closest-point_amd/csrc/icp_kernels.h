@@ -153,7 +153,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                hipStream_t st, const int *stop = nullptr, const double4 *m4 = nullptr,
                                unsigned *audit = nullptr, const double4 *qraw = nullptr,
                                const int *wsplit = nullptr, int wslots = 0,
-                               double local_r = -1.0); // (>= 0: the local pair test's certificate, seed16 = s0 bits)
+                               double local_r = -1.0, // (>= 0: the local pair test's certificate, seed16 = s0 bits)
+                               const int *kd_orig = nullptr, int *kpos = nullptr); // (partials in kd positions)
 // A split plan for `kernel` (make_plan): np queries in workgroups of queries_per_lane_block,
 // the model axis (nm rows, tiles of `tile`) split to fill >= 4 rounds of resident workgroups.
 NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_block, const void *kernel,
@@ -167,6 +168,8 @@ NNPlan make_nn_plan(size_t np, size_t nm, int tile, int q, int queries_per_lane_
 // block and the null block, nb_pad / 32 + 1: centre and radius over its bundles).
 int bundle_pad(size_t nm);
 std::vector<int> bundle_kd_order(const double *m_xyz, size_t nm);
+// m4kd[P] = m4[kd_orig[P]] and kd_of[kd_orig[P]] = P for the nm real points (bundle kd order)
+void launch_build_kd_tables(const double4 *m4, const int *kd_orig, int nm, double4 *m4kd, int *kd_of, hipStream_t st);
 // the local pair test's block frames (float4 (c_B, R_B) per 32-bundle block, nb_pad / 32 + 1)
 // and its pair image (1 KiB per bundle, the points relative to their block's frame)
 void launch_build_local_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
@@ -246,7 +249,8 @@ void launch_permute_cloud(const int *order, int n, int inverse, const double *sx
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
                        const float4 *m32, const double *mx, const double *my, const double *mz,
-                       int nm, int max_items, int *idx, hipStream_t st, const int *stop = nullptr);
+                       int nm, int max_items, int *idx, hipStream_t st, const int *stop = nullptr,
+                       int *kpos = nullptr, const int *kd_of = nullptr); // (kpos[j] = kd_of[idx[j]])
 // fp64 brute force: partial (best d64, argbest) per (split, query), then merge.
 void launch_nn_fp64(const double *px, const double *py, const double *pz, int np,
                     const double *mx, const double *my, const double *mz, int nm,
@@ -296,7 +300,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st, const int *stop = nullptr,
-                            int inline_nm = 0);
+                            int inline_nm = 0, int *kpos = nullptr, const int *kd_of = nullptr);
 
 // The reference CPU rule's near ties (icp_grid.hip): queries whose squared-rule winner idx[j]
 // has another point within the window are appended to out[*count] (count zeroed by the caller).
@@ -322,9 +326,11 @@ int red_blocks(size_t n);
 // m4: the model as (x, y, z, 0) double4 (one 32-byte read per gathered point)
 // partials: red_blocks(n) x K doubles, folded by launch_reduce; with red_blocks(n) == 1 the
 // single workgroup's K sums are final (the engine then passes the destination itself)
+// (kpos / m4kd, nullable: the correspondences' kd positions, gathered from the kd-ordered model)
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
-                           double *partials, hipStream_t st);
+                           double *partials, hipStream_t st, const int *kpos = nullptr,
+                           const double4 *m4kd = nullptr);
 // *out = (double)*cnt (a device count joining an all-reduced vector of sums)
 void launch_count_to_double(const int *cnt, double *out, hipStream_t st);
 // dst[pairs[2i]] = pairs[2i + 1] for i < n (the CPU rule's host fix-ups)
@@ -406,11 +412,15 @@ struct IterState {
 // sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)
 void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
-                            double *partials, hipStream_t st);
+                            double *partials, hipStream_t st, const int *kpos = nullptr,
+                            const double4 *m4kd = nullptr);
 // (1 thread) NN queue sizes amb_count[0..3] -> nn_counts (unless done), then zeroed for the next
 // search; then, unless done, the Horn solve (icp_horn.h) from the reduced sums -- two-pass
 // sums (Σp, Σy, centred S, d_caps, sp) or, if shifted, launch_shifted_moments' -- and the
 // shifts of the next iteration: sR mu_p + t (the centroid of the transformed scene) and mu_y
+// reduce_kernel<17> of `partials` into sums, then horn_step_kernel, in one launch (bit for bit the two)
+void launch_reduce_horn(const double *partials, int nblocks, double *sums, double n_total, const double c[3],
+                        int shifted, int *amb_count, IterState *st_dev, hipStream_t st);
 void launch_horn_step(const double *sums, double n_total, const double c[3], int shifted, int *amb_count,
                       IterState *st_dev, hipStream_t st);
 // (1 thread) err = (e + e) / N from sums[kSumErr] -> err_trace[iter++]; done if err < threshold

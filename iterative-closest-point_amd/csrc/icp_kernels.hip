@@ -1216,8 +1216,11 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
     double cy, double cz, double scale, const unsigned *__restrict__ seed16,
     const float *__restrict__ mms, int *__restrict__ idx, int *amb_count, int *amb_list, int *amb_hint,
     const int *__restrict__ stop, const double4 *__restrict__ m4, unsigned *__restrict__ audit,
-    const double4 *__restrict__ qraw, const int *__restrict__ wsplit, int wslots, double local_r)
+    const double4 *__restrict__ qraw, const int *__restrict__ wsplit, int wslots, double local_r,
+    const int *__restrict__ kd_orig, int *__restrict__ kpos)
 {
+    // kd_orig (the local bundle filter): the partials carry kd positions, mapped to original
+    // indices here; kpos (nullable) receives the certified queries' positions
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
     // R queries per lane group (rounds r: slots (blockIdx.x R + r) kBlock / G + threadIdx.x / G,
     // coalesced per round), then ONE queue append for the workgroup's R kBlock / G queries: the
@@ -1306,6 +1309,8 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
                                   b, s2, id);
         }
         if (id >= nm || (SEEDED && !(b < 0.0f))) id = -1; // no candidate (seeded: nothing below s0')
+        const int pos = id;
+        if (kd_orig && id >= 0) id = kd_orig[id];
         const double ax = (q0 - cx) * scale, ay = (q1 - cy) * scale, az = (q2 - cz) * scale;
         bool ok = id >= 0 && fabs(ax) <= kF16QueryClamp && fabs(ay) <= kF16QueryClamp &&
                   fabs(az) <= kF16QueryClamp;
@@ -1370,7 +1375,10 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
             }
         }
         ok = ok || !valid || sub != 0; // (the G lanes agree; lane 0 speaks for the query)
-        if (ok && valid && sub == 0) idx[j] = id;
+        if (ok && valid && sub == 0) {
+            idx[j] = id;
+            if (kpos) kpos[j] = pos;
+        }
         qj[r] = -1;
         if (!ok) {
             qj[r] = j;
@@ -1473,7 +1481,8 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
     const double *__restrict__ amb_T, const float4 *__restrict__ p32,
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const float4 *__restrict__ m32, const double *__restrict__ mx, const double *__restrict__ my,
-    const double *__restrict__ mz, int nm, int *__restrict__ idx, const int *__restrict__ stop)
+    const double *__restrict__ mz, int nm, int *__restrict__ idx, const int *__restrict__ stop,
+    int *__restrict__ kpos, const int *__restrict__ kd_of)
 {
     __shared__ double shd[kBlock];
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
@@ -1483,13 +1492,15 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
     for (int item = blockIdx.x; item < count; item += gridDim.x) {
         const int j = amb_list[item];
         const double T = amb_T[item];
-        const float4 p = p32[j];
+        // (T = +inf: every model point, without the fp32 pre-test -- and without p32, which a
+        // search that only queues such items does not keep current)
+        const bool all = !(T < INFINITY);
+        const float4 p = all ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : p32[j];
         const double qx = px[j], qy = py[j], qz = pz[j];
         double bd = INFINITY;
         int bi = 0x7fffffff;
         for (int k = threadIdx.x; k < nm; k += kBlock) {
-            const float d = d32(p.x, p.y, p.z, m32[k]);
-            if ((double)d <= T) {
+            if (all || (double)d32(p.x, p.y, p.z, m32[k]) <= T) {
                 const double e = d64(qx, qy, qz, mx[k], my[k], mz[k]);
                 if (e < bd) { // k increases per thread: strict keeps the first
                     bd = e;
@@ -1512,7 +1523,11 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
             __syncthreads();
         }
         // (no comparison held -- a NaN query: index 0, the reference GPU scan's answer)
-        if (threadIdx.x == 0) idx[j] = shi[0] == 0x7fffffff ? 0 : shi[0];
+        if (threadIdx.x == 0) {
+            const int w = shi[0] == 0x7fffffff ? 0 : shi[0];
+            idx[j] = w;
+            if (kpos) kpos[j] = kd_of[w];
+        }
         __syncthreads();
     }
 }
@@ -1676,11 +1691,12 @@ __global__ __launch_bounds__(kBlock) void nn_finalize64_kernel(const double *__r
 __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
-    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials)
+    double *__restrict__ yy, double *__restrict__ yz, double *__restrict__ partials,
+    const int *__restrict__ kpos, const double4 *__restrict__ m4kd)
 {
     double a[6] = {0, 0, 0, 0, 0, 0};
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-        const double4 m = m4[idx[i]];
+        const double4 m = kpos ? m4kd[kpos[i]] : m4[idx[i]]; // (the same point: kd-ordered copy)
         const double y0 = m.x, y1 = m.y, y2 = m.z;
         yx[i] = y0;
         yy[i] = y1;
@@ -1701,7 +1717,7 @@ __global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st,
-    double *__restrict__ partials)
+    double *__restrict__ partials, const int *__restrict__ kpos, const double4 *__restrict__ m4kd)
 {
     if (st->done) return; // a frozen (converged) ICP iteration: its sums are never used
     const double cp0 = st->shift_p[0], cp1 = st->shift_p[1], cp2 = st->shift_p[2];
@@ -1710,7 +1726,7 @@ __global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
 #pragma unroll
     for (int k = 0; k < 17; ++k) a[k] = 0.0;
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-        shifted_moment_point(i, idx, m4, px, py, pz, yx, yy, yz, cp0, cp1, cp2, cy0, cy1, cy2, a);
+        shifted_moment_point(i, idx, m4, px, py, pz, yx, yy, yz, cp0, cp1, cp2, cy0, cy1, cy2, a, kpos, m4kd);
     block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
 }
 
@@ -2268,7 +2284,8 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
                                int np, int nm, const double c[3], double scale, const unsigned *seed16,
                                const float *mms, int *idx, int *amb_count, int *amb_list, int *amb_hint,
                                hipStream_t st, const int *stop, const double4 *m4, unsigned *audit,
-                               const double4 *qraw, const int *wsplit, int wslots, double local_r)
+                               const double4 *qraw, const int *wsplit, int wslots, double local_r,
+                               const int *kd_orig, int *kpos)
 {
     // (its fp64 certificate is heavy and every lane of a group repeats it: lanes only pay off
     // for very many splits; ICP_FIN16_LANES = 1 | 4 | 8 overrides, for experiments)
@@ -2278,16 +2295,25 @@ void launch_nn_finalize_mfma16(const float *part_best, const float *part_second,
     }();
     const int g = forced == 1 || forced == 4 || forced == 8 ? forced : 1;
     // (small searches keep one query a lane: their few workgroups would serialise the rounds)
-    const int rounds = np >= kFin16RoundsMin ? kFin16Rounds : 1, per_block = kBlock / g * rounds;
+    static const int forced_rounds = [] { // ICP_FIN16_ROUNDS = 1 | 2 | 4 | 8 (A/B)
+        const char *e = getenv("ICP_FIN16_ROUNDS");
+        return e ? atoi(e) : 0;
+    }();
+    const int rounds = forced_rounds == 1 || forced_rounds == 2 || forced_rounds == 4 || forced_rounds == 8
+                           ? forced_rounds
+                           : (np >= kFin16RoundsMin ? kFin16Rounds : 1),
+              per_block = kBlock / g * rounds;
     const int grid = (np + per_block - 1) / per_block;
 #define FIN16R(SD, G, R)                                                                                     \
     nn_finalize_mfma16_kernel<SD, G, R><<<grid, kBlock, 0, st>>>(part_best, part_second, part_idx, splits, px, py, \
                                                               pz, np, nm, c[0], c[1], c[2], scale, seed16, mms,  \
                                                               idx, amb_count, amb_list, amb_hint, stop, m4, audit, \
-                                                              qraw, wsplit, wslots, local_r)
+                                                              qraw, wsplit, wslots, local_r, kd_orig, kpos)
 #define FIN16(SD, G)                                                                                         \
     do {                                                                                                     \
-        if (rounds == kFin16Rounds) FIN16R(SD, G, kFin16Rounds);                                             \
+        if (rounds == 8) FIN16R(SD, G, 8);                                                                   \
+        else if (rounds == 4) FIN16R(SD, G, 4);                                                              \
+        else if (rounds == 2) FIN16R(SD, G, 2);                                                              \
         else FIN16R(SD, G, 1);                                                                               \
     } while (0)
     if (seed16) {
@@ -2310,14 +2336,15 @@ void launch_nn_finalize_mfma(const float *part_best, const float *part_second, c
 void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *amb_T,
                        const float4 *p32, const double *px, const double *py, const double *pz,
                        const float4 *m32, const double *mx, const double *my, const double *mz,
-                       int nm, int max_items, int *idx, hipStream_t st, const int *stop)
+                       int nm, int max_items, int *idx, hipStream_t st, const int *stop, int *kpos,
+                       const int *kd_of)
 {
     // (one workgroup per CU, grid-striding over the device-side count: the launch is on every
     // search's path and usually finds nothing to do -- 2,048 idle workgroups cost ~4.6 us)
     int grid = max_items < 256 ? max_items : 256;
     if (grid < 1) grid = 1;
     nn_resolve_kernel<<<grid, kBlock, 0, st>>>(amb_count, amb_list, amb_T, p32, px, py, pz, m32, mx,
-                                                my, mz, nm, idx, stop);
+                                                my, mz, nm, idx, stop, kpos, kd_of);
 }
 
 void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm, int *idx_out, double *y_aos,
@@ -2352,16 +2379,18 @@ int red_blocks(size_t n) { return n <= (size_t)kRedSingle ? 1 : grid_for(n, kRed
 
 void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
-                            double *partials, hipStream_t st)
+                            double *partials, hipStream_t st, const int *kpos, const double4 *m4kd)
 {
-    shifted_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, partials);
+    shifted_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, partials,
+                                                             kpos, m4kd);
 }
 
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                            const double *pz, int n, double *yx, double *yy, double *yz,
-                           double *partials, hipStream_t st)
+                           double *partials, hipStream_t st, const int *kpos, const double4 *m4kd)
 {
-    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials);
+    gather_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, partials, kpos,
+                                                            m4kd);
 }
 
 __global__ __launch_bounds__(kBlock) void make_aos4_kernel(const double *__restrict__ x,

@@ -268,6 +268,12 @@ for s in $STEPS; do
                ICP_BUNDLE_LOCAL=$o run localab8_$o 300 python3 tools/bundle_probe.py --steps 20 --shard 8 --variants bundle || exit 1
                cat $OUT/localab_$o.log $OUT/localab8_$o.log >> $OUT/localab_all_$o.log
              done ;;
+    finab) for k in 1 2; do
+             for r in 8 4 2 1; do
+               ICP_FIN16_ROUNDS=$r run finab_${r}_$k 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+               cat $OUT/finab_${r}_$k.log >> $OUT/finab_all_$r.log
+             done
+           done ;;
     *) echo "unknown step $s" ;;
     esac
 done
