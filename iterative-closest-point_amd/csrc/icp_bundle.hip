@@ -1039,8 +1039,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
     if (counters) t_stream = __builtin_amdgcn_s_memrealtime();
 
     // ---- this wave's fired blocks: per-query bounds of the fired groups, then the pair tests
+    // (best, second) <- the two smallest of {best, second, dd[0..15]} (a multiset): a tournament
+    // of min3 / med3 on triples, then pairs merged three at a time, (a1, a2) (b1, b2) (c1, c2) ->
+    // (min3 a1 b1 c1, min(med3 a1 b1 c1, min3 a2 b2 c2)) -- 23 VALU at depth 4, where the
+    // med3 / min chain over the 16 values took 32 in one dependent chain; the same values
     auto pair_update = [&](int q, const f32x16_t &dd, int blk) {
-        const float mn = min16v(dd);
+        const float m0 = fmin3(dd[0], dd[1], dd[2]), s0 = __builtin_amdgcn_fmed3f(dd[0], dd[1], dd[2]);
+        const float m1 = fmin3(dd[3], dd[4], dd[5]), s1 = __builtin_amdgcn_fmed3f(dd[3], dd[4], dd[5]);
+        const float m2 = fmin3(dd[6], dd[7], dd[8]), s2 = __builtin_amdgcn_fmed3f(dd[6], dd[7], dd[8]);
+        const float m3 = fmin3(dd[9], dd[10], dd[11]), s3 = __builtin_amdgcn_fmed3f(dd[9], dd[10], dd[11]);
+        const float m4 = fmin3(dd[12], dd[13], dd[14]), s4 = __builtin_amdgcn_fmed3f(dd[12], dd[13], dd[14]);
+        const float ma = fmin3(m0, m1, m2), sa = fminf(__builtin_amdgcn_fmed3f(m0, m1, m2), fmin3(s0, s1, s2));
+        const float mb = fmin3(m3, m4, dd[15]), sb = fminf(__builtin_amdgcn_fmed3f(m3, m4, dd[15]), fminf(s3, s4));
+        const float mn = fminf(ma, mb);
         if (!__any(mn < second[q])) return;
         if (__any(mn < best[q])) {
             int row = 0;
@@ -1049,11 +1060,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
                 row = dd[r] == mn ? (r & 3) + 8 * (r >> 2) : row;
             bpos[q] = mn < best[q] ? blk * 32 + 4 * h + row : bpos[q];
         }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            second[q] = __builtin_amdgcn_fmed3f(best[q], second[q], dd[r]);
-            best[q] = fminf(best[q], dd[r]);
-        }
+        const float b0 = best[q], c0 = second[q];
+        second[q] = fminf(__builtin_amdgcn_fmed3f(b0, ma, mb), fmin3(c0, sa, sb));
+        best[q] = fmin3(b0, ma, mb);
     };
     unsigned long long t_bound = 0, t_wait = 0, t_pair = 0, t_mark = 0; // (counters: deferred sub-phases)
     auto stamp = [&](unsigned long long &acc) {

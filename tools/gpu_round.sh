@@ -274,6 +274,12 @@ for s in $STEPS; do
                cat $OUT/finab_${r}_$k.log >> $OUT/finab_all_$r.log
              done
            done ;;
+    rbab) for k in 1 2; do
+            for b in 4096 1024 256; do
+              ICP_GRID_RBLOCKS=$b run rbab_${b}_$k 300 python3 tools/bundle_probe.py --steps 20 --variants bundle || exit 1
+              cat $OUT/rbab_${b}_$k.log >> $OUT/rbab_all_$b.log
+            done
+          done ;;
     *) echo "unknown step $s" ;;
     esac
 done
