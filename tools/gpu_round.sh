@@ -280,6 +280,22 @@ for s in $STEPS; do
               cat $OUT/rbab_${b}_$k.log >> $OUT/rbab_all_$b.log
             done
           done ;;
+    midth) for k in 1 2; do
+             for t in 512 768 1024; do
+               ICP_MID_THREADS=$t run midth_${t}_$k 300 python3 tools/configs_probe.py --configs C2_bunny C3_horse --variants auto --reps 5 || exit 1
+               cat $OUT/midth_${t}_$k.log >> $OUT/midth_all_$t.log
+             done
+           done ;;
+    test_midth) for t in ${MIDTH:-768 1024}; do
+               ICP_MID_THREADS=$t run pytest_midth_$t 300 python -u -m pytest tests/test_gpu_persistent.py tests/test_gpu_cpu_rule.py -m gpu -x -q -rf \
+                   --timeout 120 --timeout-method thread || exit 1
+             done ;;
+    momab) for k in 1 2; do
+             for b in 1 4 2; do
+               ICP_MOM_BATCH=$b run momab_${b}_$k 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/momab_${b}_$k" -o c4 -- \
+                   python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cow --no-cases || exit 1
+             done
+           done ;;
     *) echo "unknown step $s" ;;
     esac
 done

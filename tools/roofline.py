@@ -19,7 +19,9 @@ against the 2.5 PF dense f16 MFMA peak of the unit it runs on, and the executed 
 Algorithmic bytes per scene point (fp64 SoA clouds):
   shifted_moments_kernel / gather_moments_kernel: idx 4 + m4[idx] 32 + p 24 + write Y 24 = 84
   centred_moments_kernel: p 24 + Y 24 = 48
-  transform_err_kernel (icp_run form): p 24 + Y 24 + write p 24 + p32 16 + seed16 4 = 92
+  transform_err_kernel (icp_run over a scene in the bundle filter's slot order, the C4 default):
+    p 24 + Y 24 + write p 24 + the next search's 64 B slot record + seed16 4 = 140 (no fp32 copy;
+    captures up to r03z ran the 92 B form: p 24 + Y 24 + write p 24 + p32 16 + seed16 4)
   NN filter: SURVEY §8d compulsory 12 N + 12 M + 4 N (fp32 xyz in, int32 index out)
 """
 from __future__ import annotations
@@ -39,7 +41,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense ~2.5 PF
 NN_KERNELS = ("nn_mfma16r_kernel<8>", "nn_mfma16r_kernel<4>", "nn_mfma16_kernel", "nn_mfma16_kernel<seeded>")
 BYTES_PER_POINT = {"shifted_moments_kernel": 84, "gather_moments_kernel": 84, "centred_moments_kernel": 48,
-                   "transform_err_kernel": 92}
+                   "transform_err_kernel": 140}
+
+
+def bytes_per_point(kernel, tag):
+    """BYTES_PER_POINT, with the form of transform_err_kernel the capture ran: the slot-record
+    form (140 B) from profiles/r03ac on, the fp32-copy form (92 B) before it."""
+    if kernel == "transform_err_kernel" and _tag_key(tag) < _tag_key("r03ac"):
+        return 92
+    return BYTES_PER_POINT[kernel]
 
 
 def _tag_key(tag):
@@ -83,7 +93,7 @@ def roofline(tag=None, n=1 << 20, world=1):
             row["pmc_gbps"] = p["traffic_bytes_per_launch"] / (t["avg_ms"] * 1e-3) / 1e9
             row["pmc_hbm_frac"] = row["pmc_gbps"] / HBM_PEAK_GBS
         if k in BYTES_PER_POINT:
-            b = BYTES_PER_POINT[k] * n_local
+            b = bytes_per_point(k, tag) * n_local
             row["algorithmic_bytes"] = b
             row["algorithmic_gbps"] = b / (t["avg_ms"] * 1e-3) / 1e9
             row["hbm_frac"] = row["algorithmic_gbps"] / HBM_PEAK_GBS
