@@ -31,6 +31,10 @@ __device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
     }
 }
 
+__device__ __forceinline__ void shifted_moment_terms(double px, double py, double pz, const double4 &m, double cp0,
+                                                     double cp1, double cp2, double cy0, double cy1, double cy2,
+                                                     double (&a)[17]);
+
 // y_i = m[idx_i] (stored), then point i's terms of the one-pass moments around (cp, cy):
 // sum (p - cp), sum (y - cy), sum (p - cp)(y - cy)^T, sum ||y - cy||^2, sum ||p - cp||^2
 __device__ __forceinline__ void shifted_moment_point(int i, const int *__restrict__ idx,
@@ -46,7 +50,16 @@ __device__ __forceinline__ void shifted_moment_point(int i, const int *__restric
     yx[i] = m.x;
     yy[i] = m.y;
     yz[i] = m.z;
-    const double p0 = px[i] - cp0, p1 = py[i] - cp1, p2 = pz[i] - cp2;
+    shifted_moment_terms(px[i], py[i], pz[i], m, cp0, cp1, cp2, cy0, cy1, cy2, a);
+}
+
+// point i's terms of the one-pass moments from its loaded p and y = m (shifted_moment_point's
+// arithmetic, shared with the batched form of shifted_moments_kernel)
+__device__ __forceinline__ void shifted_moment_terms(double px, double py, double pz, const double4 &m, double cp0,
+                                                     double cp1, double cp2, double cy0, double cy1, double cy2,
+                                                     double (&a)[17])
+{
+    const double p0 = px - cp0, p1 = py - cp1, p2 = pz - cp2;
     const double y0 = m.x - cy0, y1 = m.y - cy1, y2 = m.z - cy2;
     a[0] += p0;
     a[1] += p1;

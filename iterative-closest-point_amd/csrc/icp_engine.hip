@@ -1902,12 +1902,18 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }();
     const int timing_stride = forced_stride ? forced_stride : ((double)n * (double)ctx->nm >= kTimedPairs ? 1 : 8);
     // (partials: the residual's unreduced rows, folded in the same launch)
-    auto enqueue_err_step = [&](int it, const double *partials = nullptr) -> int {
+    // (horn: this iteration's Horn step in the same single-thread launch, right after it)
+    auto enqueue_err_step = [&](int it, const double *partials = nullptr, bool horn = false) -> int {
         const int sl = it % kRing;
         // (done, iter) straight into mapped host memory, then the slot's ticket
         slot_ticket[sl] = ++ctx->flag_ticket;
-        launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->d_flags + 4 * sl,
-                        slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace, ctx->st, partials, red_blocks(n));
+        if (horn)
+            launch_err_horn_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->d_flags + 4 * sl,
+                                 slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace, ctx->c, 1, ctx->amb_count,
+                                 ctx->st);
+        else
+            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, ctx->d_flags + 4 * sl,
+                            slot_ticket[sl], ctx->d_iter_mirror, ctx->d_trace, ctx->st, partials, red_blocks(n));
         LAUNCHCHK("err_step");
         return ICP_OK;
     };
@@ -2024,7 +2030,9 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     TRY(allreduce(ctx, ctx->sums, kNumSums));
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 4], ctx->st));
                     ar_timed[slot] = timed;
-                    TRY(enqueue_err_step(enqueued - 1));
+                    // (enqueued > 0 here: the Horn step is the shifted one)
+                    TRY(enqueue_err_step(enqueued - 1, nullptr, true));
+                    horn_fused = true;
                 }
             }
             // 4. Horn solve (gpu.cc:106-146) on the device

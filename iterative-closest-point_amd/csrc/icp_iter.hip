@@ -4,6 +4,7 @@
 // enqueues iterations without waiting on each one; a `done` flag freezes the state after
 // the iteration whose err < threshold, exactly where the reference's loop breaks.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "icp_device.h"
 #include "icp_horn.h"
@@ -139,6 +140,21 @@ __global__ __launch_bounds__(64) void err_step_kernel(const double *__restrict__
                                 IterState *h_state, double *h_trace)
 {
     err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
+}
+
+// The lagged error step of the previous iteration (its residual rode on this iteration's
+// all-reduce) and this iteration's Horn step, one thread, one launch: the multi-rank loop ran
+// them as two single-thread launches back to back (4.1 + 4.9 us at the W = 8 shard,
+// profiles/r03bd/).  Same bodies in the same order.
+__global__ __launch_bounds__(64) void err_horn_step_kernel(double *__restrict__ sums, double N, double threshold,
+                                                           int max_iter, double *__restrict__ err_trace,
+                                                           IterState *__restrict__ s, int *hflag, int ticket,
+                                                           IterState *h_state, double *h_trace, double c0, double c1,
+                                                           double c2, int shifted, int *__restrict__ cnt)
+{
+    if (threadIdx.x != 0) return;
+    err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
+    horn_step_body(sums, N, c0, c1, c2, shifted, cnt, s);
 }
 
 // One ICP iteration after the NN search, for a cloud of <= kRedSingle points on one rank, in
@@ -1115,7 +1131,17 @@ __global__ __launch_bounds__(kBlock) void iteration_tail_grid_kernel(TailArgs a)
 // query u.  Distances follow compute.cu:112-117.
 constexpr int kMidSb = 16;     // 64-point tiles per superblock
 static_assert(kTailMaxBlocks <= kBlock, "the stamps buffer holds kBlock workgroups' timers");
-constexpr int kMidThreads = 512;
+// threads per workgroup of the mid kernel: 512 (2 waves per SIMD at its 246 VGPRs), or
+// ICP_MID_THREADS=768 / 1024 (3 / 4 waves per SIMD: more batches in flight, registers squeezed)
+static int mid_threads()
+{
+    static const int t = [] {
+        const char *e = std::getenv("ICP_MID_THREADS");
+        const int v = e ? std::atoi(e) : 512;
+        return v == 768 || v == 1024 ? v : 512;
+    }();
+    return t;
+}
 
 // squared distance from q to the box (lo x, lo y, lo z, hi x, hi y, hi z) -- the small kernel's
 template <typename T> __device__ __forceinline__ double box_dist2(const T *bx, double qx, double qy, double qz)
@@ -1208,6 +1234,7 @@ __device__ __forceinline__ int pub_load_i(const int *p)
     return __hip_atomic_load((int *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <int kMidThreads>
 __global__ __launch_bounds__(kMidThreads) void icp_persistent_mid_kernel(PersistArgs a)
 {
     // tile boxes (ntile x 6 floats) | block boxes (nb16 x 6 floats), outward-rounded fp32
@@ -1722,13 +1749,18 @@ void launch_iteration_tail_grid(const TailArgs &args, int nblocks, hipStream_t s
 void launch_icp_persistent_mid(const PersistArgs &args, int grid, size_t lds_bytes, hipStream_t st)
 {
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void *)icp_persistent_mid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  kPersistMidLdsMax);
+        for (const void *k : {(const void *)icp_persistent_mid_kernel<512>, (const void *)icp_persistent_mid_kernel<768>,
+                              (const void *)icp_persistent_mid_kernel<1024>})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kPersistMidLdsMax);
         (void)hipGetLastError();
         return true;
     }();
     (void)attr;
-    icp_persistent_mid_kernel<<<grid, kMidThreads, lds_bytes, st>>>(args);
+    switch (mid_threads()) {
+    case 768: icp_persistent_mid_kernel<768><<<grid, 768, lds_bytes, st>>>(args); break;
+    case 1024: icp_persistent_mid_kernel<1024><<<grid, 1024, lds_bytes, st>>>(args); break;
+    default: icp_persistent_mid_kernel<512><<<grid, 512, lds_bytes, st>>>(args); break;
+    }
 }
 
 size_t persistent_static_lds()
@@ -1748,7 +1780,7 @@ size_t persistent_mid_static_lds()
 {
     static const size_t bytes = [] {
         hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, (const void *)icp_persistent_mid_kernel) != hipSuccess) {
+        if (hipFuncGetAttributes(&fa, (const void *)icp_persistent_mid_kernel<512>) != hipSuccess) {
             (void)hipGetLastError();
             return (size_t)32 * 1024; // (conservative)
         }
@@ -1831,6 +1863,14 @@ void launch_err_step(double *sums, double n_total, double threshold, int max_ite
     else
         err_step_kernel<<<1, 1, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, st_dev, hflag_dev, ticket,
                                          h_state_dev, h_trace_dev);
+}
+
+void launch_err_horn_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
+                          IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
+                          const double c[3], int shifted, int *amb_count, hipStream_t st)
+{
+    err_horn_step_kernel<<<1, 64, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, st_dev, hflag_dev, ticket,
+                                           h_state_dev, h_trace_dev, c[0], c[1], c[2], shifted, amb_count);
 }
 
 void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, double *py, double *pz, int n,

@@ -427,6 +427,10 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], int
 // or iter == max_iter; a recorded iteration is mirrored to mapped host memory (h_state, h_trace[iter]);
 // finally hflag[0..1] = (done, iter) and hflag[2] = ticket (system scope, mapped host memory)
 // partials (nullable): reduce_kernel<1>'s input (nblocks rows), folded into sums[kSumErr] first
+// launch_err_step (no partials) then launch_horn_step, in one single-thread launch
+void launch_err_horn_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
+                          IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
+                          const double c[3], int shifted, int *amb_count, hipStream_t st);
 void launch_err_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                      IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
                      hipStream_t st, const double *partials = nullptr, int nblocks = 0);

@@ -1713,7 +1713,8 @@ __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
 
 // one pass around shifts near the centroids: the centred sums follow as
 // S = sum (p - cp)(y - cy)^T - N dp dy^T etc. (horn_step), with N dp dy^T at rounding level
-__global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
+template <int kMomBatch>
+__global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st,
@@ -1725,8 +1726,40 @@ __global__ __launch_bounds__(kBlock) void shifted_moments_kernel(
     double a[17];
 #pragma unroll
     for (int k = 0; k < 17; ++k) a[k] = 0.0;
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-        shifted_moment_point(i, idx, m4, px, py, pz, yx, yy, yz, cp0, cp1, cp2, cy0, cy1, cy2, a, kpos, m4kd);
+    // The thread's points i, i + G, i + 2G, ... (G = the grid's threads) in that order, as
+    // shifted_moment_point takes them, but kMomBatch at a time with every load of the batch issued
+    // before the first sum: at C4 a thread has four points, and one by one their dependent
+    // (index -> model point) loads ran back to back.  Same sums, same order: bit-identical.
+    const int G = gridDim.x * kBlock;
+    for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += kMomBatch * G) {
+        int j[kMomBatch];
+#pragma unroll
+        for (int u = 0; u < kMomBatch; ++u) {
+            const int i = i0 + u * G;
+            j[u] = i < n ? (kpos ? kpos[i] : idx[i]) : 0;
+        }
+        double4 m[kMomBatch];
+        double qx[kMomBatch], qy[kMomBatch], qz[kMomBatch];
+#pragma unroll
+        for (int u = 0; u < kMomBatch; ++u) {
+            const int i = i0 + u * G;
+            const bool in = i < n;
+            m[u] = in ? (kpos ? m4kd[j[u]] : m4[j[u]]) : make_double4(0.0, 0.0, 0.0, 0.0);
+            qx[u] = in ? px[i] : 0.0;
+            qy[u] = in ? py[i] : 0.0;
+            qz[u] = in ? pz[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kMomBatch; ++u) {
+            const int i = i0 + u * G;
+            if (i < n) {
+                yx[i] = m[u].x;
+                yy[i] = m[u].y;
+                yz[i] = m[u].z;
+                shifted_moment_terms(qx[u], qy[u], qz[u], m[u], cp0, cp1, cp2, cy0, cy1, cy2, a);
+            }
+        }
+    }
     block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
 }
 
@@ -2381,8 +2414,22 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
                             double *partials, hipStream_t st, const int *kpos, const double4 *m4kd)
 {
-    shifted_moments_kernel<<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, partials,
-                                                             kpos, m4kd);
+    // points of a thread whose loads are issued together (A/B: ICP_MOM_BATCH = 1 | 2 | 4; same
+    // sums).  C4 (four points a thread): 23.5 / 20.5 / 21.2 us at 1 / 2 / 4 (profiles/r03bd/)
+    static const int batch = [] {
+        const char *e = getenv("ICP_MOM_BATCH");
+        const int v = e ? atoi(e) : 2;
+        return v == 1 || v == 4 ? v : 2;
+    }();
+    if (batch == 2)
+        shifted_moments_kernel<2><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev,
+                                                                    partials, kpos, m4kd);
+    else if (batch == 1)
+        shifted_moments_kernel<1><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev,
+                                                                    partials, kpos, m4kd);
+    else
+        shifted_moments_kernel<4><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev,
+                                                                    partials, kpos, m4kd);
 }
 
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,

@@ -296,6 +296,14 @@ for s in $STEPS; do
                    python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-cow --no-cases || exit 1
              done
            done ;;
+    shardab) for k in 1 2; do
+               for L in ${LIBS:-tree}; do
+                 lib=""; [ "$L" != tree ] && lib=iterative-closest-point_amd/build_ab/$L/libicp_hip.so
+                 ICP_AMD_LIB=$lib run shardab_${L}_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1
+                 cat $OUT/shardab_${L}_$k.log >> $OUT/shardab_all_$L.log
+               done
+             done ;;
+    c5shard) run c5shard 300 python tools/shard_probe.py --n 8388608 --worlds 8 --steps 5 --warmup 2 ;;
     *) echo "unknown step $s" ;;
     esac
 done
