@@ -113,7 +113,7 @@ def roofline(tag=None, n=1 << 20, world=1):
 
 
 # ---- the other captures: C3's one-launch registration, the grid variant's resolve ----------
-# profiles/<tag>_c3_kernel_stats.csv + <tag>_c3_pmc_traffic.json (+ <tag>_c3_stamps.log): rocprofv3
+# profiles/<tag>_c3_kernel_stats.csv + <tag>_c3_pmc_traffic.json (+ <tag>_c3_stamps.stamps): rocprofv3
 # kernel trace and FETCH_SIZE / WRITE_SIZE passes of `tools/configs_probe.py --configs C3_horse
 # --variants auto --reps 1` (BASELINE config C3: horse_ref vs horse_tr1, 50 iterations, one launch
 # of icp_persistent_mid_kernel per registration), and its ICP_PERSIST_STAMPS=1 phase timers.
@@ -177,10 +177,10 @@ def config_roofline(cfg, tag=None, n=1 << 20):
     if cfg == "c3":
         out["iterations_per_launch"] = C3_ITERATIONS
         out["pmc_bytes_per_iteration"] = b / C3_ITERATIONS
-        sp = os.path.join(PROFILES, f"{tag}_c3_stamps.log")
+        sp = os.path.join(PROFILES, f"{tag}_c3_stamps.stamps")
         if os.path.exists(sp):
             out["phases_us_per_registration"] = stamp_phases(sp)
-            out["phases_source"] = f"profiles/{tag}_c3_stamps.log (ICP_PERSIST_STAMPS=1, workgroup 0)"
+            out["phases_source"] = f"profiles/{tag}_c3_stamps.stamps (ICP_PERSIST_STAMPS=1, workgroup 0)"
     else:
         alg = 28.0 * n + 32.0 * n
         out["algorithmic_bytes"] = alg
