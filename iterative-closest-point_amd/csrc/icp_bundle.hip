@@ -53,6 +53,8 @@ constexpr int kBDmaPerWave = kBBlocksPerTile / 4;     // 2 wave-instructions per
 constexpr int kBVmcntDma = 0x0F70 | kBDmaPerWave;     // vmcnt(2): one tile's DMA may stay in flight
 constexpr int kBQG = 8;                               // 32-query groups per wave
 constexpr int kTaskQueues = 8, kTaskQueueStride = 32; // nn_bundle2_kernel's task queues (tctl)
+constexpr int kBundleDoneCtr = kTaskQueueStride * (kTaskQueues + 1); // tctl: bundle_candidates_kernel's done counter
+static_assert(kBundleDoneCtr < kBundleTctlInts, "tctl holds the done counter");
 constexpr int kBPendCap = 64;                         // deferred 32-bundle blocks per wave (LDS)
 // the same from the (clamped, scaled) queries a
 __device__ __forceinline__ GroupBound bundle_group(const double a[3], double dq, int mode, int gh)
@@ -740,10 +742,16 @@ __global__ __launch_bounds__(kBlock) void bundle_group_kernel(const BundleQuery 
 // margins).  A workgroup with a forced group takes every block.  Output: the candidate blocks in
 // increasing order, cand[w * nbb + e], e < cand_n[w].  all != 0: every block with a real point
 // (A/B: ICP_BUNDLE_CAND=0).
+template <int T>
+__device__ void bundle_tasks_body(const int *__restrict__ cand_n, int qblocks, int smax, int ch,
+                                  int *__restrict__ wsplit, int2 *__restrict__ tasks, int *__restrict__ tctl);
+
 __global__ __launch_bounds__(kBlock) void bundle_candidates_kernel(const double4 *__restrict__ gctr, int ng,
                                                                    const double4 *__restrict__ blk, int nbb, int all,
                                                                    int *__restrict__ cand, int *__restrict__ cand_n,
-                                                                   const int *__restrict__ stop)
+                                                                   const int *__restrict__ stop, int fuse_tasks,
+                                                                   int smax, int ch, int *__restrict__ wsplit,
+                                                                   int2 *__restrict__ tasks, int *__restrict__ tctl)
 {
     if (stop && *stop) return;
     __shared__ double s_wd[4];
@@ -805,6 +813,20 @@ __global__ __launch_bounds__(kBlock) void bundle_candidates_kernel(const double4
         __syncthreads(); // (s_cnt reused)
     }
     if (tid == 0) cand_n[w] = base;
+    if (!fuse_tasks) return;
+    // The task list in the same launch: the last workgroup to finish (one device atomic per
+    // workgroup on tctl's done counter, after a release fence) builds it, as bundle_tasks_kernel
+    // would in a launch of its own, then re-zeroes the counter for the next search.
+    __shared__ int s_last;
+    if (tid == 0) {
+        __threadfence(); // (release: this workgroup's cand / cand_n)
+        s_last = atomicAdd(tctl + kBundleDoneCtr, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence(); // (acquire: every workgroup's cand_n)
+    bundle_tasks_body<kBlock>(cand_n, (int)gridDim.x, smax, ch, wsplit, tasks, tctl);
+    if (tid == 0) tctl[kBundleDoneCtr] = 0;
 }
 
 #ifndef ICP_B2_WAVES
@@ -827,21 +849,23 @@ constexpr int kTaskBins = 1024;
 // 0.208 / 0.199 / 0.203 ms at 16 / 32 / 64 / 128 per task, the W = 8 shard's 22,984 in 0.112 /
 // 0.111 / 0.177 / 0.212 ms (profiles/r03t/): ch = the total / 1,024 (C4 56, the shard 23)
 constexpr int kB2TargetTasks = 1024, kB2ChMin = 8, kB2ChMax = 64;
-__global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restrict__ cand_n, int qblocks, int smax,
-                                                            int ch, int *__restrict__ wsplit,
-                                                            int2 *__restrict__ tasks, int *__restrict__ tctl,
-                                                            const int *__restrict__ stop)
+// (T threads: 1,024 in bundle_tasks_kernel, 256 in the last candidates workgroup)
+template <int T>
+__device__ void bundle_tasks_body(const int *__restrict__ cand_n, int qblocks, int smax, int ch,
+                                  int *__restrict__ wsplit, int2 *__restrict__ tasks, int *__restrict__ tctl)
 {
-    if (stop && *stop) return;
+    static_assert(kTaskBins % T == 0 && T % 64 == 0 && T <= 1024, "bins per thread");
+    constexpr int kPer = kTaskBins / T; // consecutive bins per thread in the scan
     __shared__ int s_hist[kTaskBins];
     __shared__ int s_total, s_ch;
+    __shared__ int s_wsum[T / 64];
     const int tid = threadIdx.x;
-    for (int i = tid; i < kTaskBins; i += 1024) s_hist[i] = 0;
+    for (int i = tid; i < kTaskBins; i += T) s_hist[i] = 0;
     if (tid == 0) s_total = 0;
     __syncthreads();
     if (ch <= 0) { // candidates per task: about kB2TargetTasks tasks in all, within [kB2ChMin, kB2ChMax]
         int c = 0;
-        for (int w = tid; w < qblocks; w += 1024) c += cand_n[w];
+        for (int w = tid; w < qblocks; w += T) c += cand_n[w];
         atomicAdd(&s_total, c);
         __syncthreads();
         if (tid == 0) {
@@ -856,18 +880,21 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
         const int per = (cand_n[w] + S - 1) / S;
         return kTaskBins - 1 - min(per, kTaskBins - 1);
     };
-    for (int w = tid; w < qblocks; w += 1024) {
+    for (int w = tid; w < qblocks; w += T) {
         const int S = split_of(w);
         wsplit[w] = S;
         atomicAdd(&s_hist[bin_of(w, S)], S);
     }
     __syncthreads();
-    { // exclusive scan of the bins: one bin per thread, wave scans, then the 16 wave totals
-        static_assert(kTaskBins == 1024, "one bin per thread");
-        __shared__ int s_wsum[16];
+    { // exclusive scan of the bins: kPer consecutive bins per thread, wave scans, then the wave totals
         const int lane = tid & 63, wv = tid >> 6;
-        const int v = s_hist[tid];
-        int x = v;
+        int v[kPer], sum = 0;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            v[i] = s_hist[kPer * tid + i];
+            sum += v[i];
+        }
+        int x = sum;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(x, o, 64);
@@ -877,17 +904,31 @@ __global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restric
         __syncthreads();
         int before = 0;
         for (int k = 0; k < wv; ++k) before += s_wsum[k];
-        s_hist[tid] = before + x - v;
-        if (tid == 1023) s_total = before + x;
+        int run = before + x - sum;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            s_hist[kPer * tid + i] = run;
+            run += v[i];
+        }
+        if (tid == T - 1) s_total = run;
         __syncthreads();
     }
-    for (int w = tid; w < qblocks; w += 1024) {
+    for (int w = tid; w < qblocks; w += T) {
         const int S = split_of(w);
         const int pos = atomicAdd(&s_hist[bin_of(w, S)], S);
         for (int sp = 0; sp < S; ++sp) tasks[pos + sp] = make_int2(w, sp | (S << 16));
     }
     if (tid == 0) tctl[0] = s_total;
     if (tid < kTaskQueues) tctl[kTaskQueueStride * (tid + 1)] = 0; // (the queues' counters)
+}
+
+__global__ __launch_bounds__(1024) void bundle_tasks_kernel(const int *__restrict__ cand_n, int qblocks, int smax,
+                                                            int ch, int *__restrict__ wsplit,
+                                                            int2 *__restrict__ tasks, int *__restrict__ tctl,
+                                                            const int *__restrict__ stop)
+{
+    if (stop && *stop) return;
+    bundle_tasks_body<1024>(cand_n, qblocks, smax, ch, wsplit, tasks, tctl);
 }
 
 // The filter proper, a persistent grid of the resident workgroups taking tasks off the list
@@ -1439,9 +1480,16 @@ static bool bundle_cand_all() // ICP_BUNDLE_CAND=0: every block a candidate (A/B
 void launch_bundle_candidates(const NNPlan &pl, const double4 *gctr, const double4 *blk, int nb_pad, int *cand,
                               int *cand_n, int *wsplit, int2 *tasks, int *tctl, hipStream_t st, const int *stop)
 {
+    // the task list in a launch of its own (bundle_tasks_kernel, 1,024 threads); ICP_BUNDLE_FUSE_TASKS=1
+    // has the candidates' last workgroup build it instead (256 threads): one launch fewer, but the
+    // W = 8 shard's candidates launch then took 16.2 us against 5.7 + 7.0 us for the two
+    // (profiles/r03bf/), so it is off
+    static const bool fuse = env_int("ICP_BUNDLE_FUSE_TASKS", 0) != 0;
     bundle_candidates_kernel<<<pl.qblocks, kBlock, 0, st>>>(gctr, 4 * pl.q_per_lane, blk, nb_pad >> 5,
-                                                            bundle_cand_all() ? 1 : 0, cand, cand_n, stop);
-    bundle_tasks_kernel<<<1, 1024, 0, st>>>(cand_n, pl.qblocks, pl.splits, pl.chunk, wsplit, tasks, tctl, stop);
+                                                            bundle_cand_all() ? 1 : 0, cand, cand_n, stop, fuse ? 1 : 0,
+                                                            pl.splits, pl.chunk, wsplit, tasks, tctl);
+    if (!fuse)
+        bundle_tasks_kernel<<<1, 1024, 0, st>>>(cand_n, pl.qblocks, pl.splits, pl.chunk, wsplit, tasks, tctl, stop);
 }
 
 void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bimg, int nb_pad, const int *cand,

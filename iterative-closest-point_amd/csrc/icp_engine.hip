@@ -772,7 +772,10 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             TRY(grow(ctx, &ctx->b_cand_n, &ctx->b_cand_n_cap, (size_t)pl.qblocks));
             TRY(grow(ctx, &ctx->b_wsplit, &ctx->b_wsplit_cap, (size_t)pl.qblocks));
             TRY(grow(ctx, &ctx->b_tasks, &ctx->b_tasks_cap, bundle2_task_count(pl)));
-            TRY(grow(ctx, &ctx->b_tctl, &ctx->b_tctl_cap, kBundleTctlInts));
+            if (ctx->b_tctl_cap < (size_t)kBundleTctlInts || !ctx->b_tctl) { // (the done counter starts at zero)
+                TRY(grow(ctx, &ctx->b_tctl, &ctx->b_tctl_cap, kBundleTctlInts));
+                HIPCHK(hipMemsetAsync(ctx->b_tctl, 0, sizeof(int) * kBundleTctlInts, ctx->st));
+            }
             TRY(grow(ctx, &ctx->b_gctr, &ctx->b_gctr_cap, nslots / 32));
             if (ctx->b_counters && ctx->b_counters_rows < bundle2_counter_rows(pl)) { // (per-wave rows)
                 HIPCHK(hipFree(ctx->b_counters));
@@ -1892,15 +1895,17 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // one iteration late (before this iteration's Horn solve, so a converged state is still
     // frozen at the same point).  Without one, err_step follows its own transform.
     const bool lag = ctx->comm != nullptr || ctx->world > 1;
-    // The O(N*M) kernel is timed (two events) every timing_stride-th iteration: every one for
-    // large searches; every 8th for small ones, where each event marker's ~4.5 us stream gap
-    // is a sizeable share of a ~70 us iteration (stats.nn_ms / nn_launches stays the mean of
-    // the timed launches).  ICP_NN_TIMING_STRIDE overrides.
+    // The O(N*M) kernel is timed (two events; on multi-rank runs two more around the
+    // all-reduce) every 8th iteration: each event marker leaves a ~4.4 us gap in the stream,
+    // which at the bundle filter's C4 iteration (~0.25 ms) is 3.5% per iteration for the filter's
+    // pair and ~11% of a W = 8 shard's 0.15 ms iteration for all four (profiles/r03bf/ kernel
+    // trace).  stats.nn_ms / nn_launches stays the mean of the timed launches.
+    // ICP_NN_TIMING_STRIDE overrides (1: every iteration, as before for searches of >= 2^32 pairs).
     static const int forced_stride = [] {
         const char *e = getenv("ICP_NN_TIMING_STRIDE");
         return e ? std::max(1, atoi(e)) : 0;
     }();
-    const int timing_stride = forced_stride ? forced_stride : ((double)n * (double)ctx->nm >= kTimedPairs ? 1 : 8);
+    const int timing_stride = forced_stride ? forced_stride : 8;
     // (partials: the residual's unreduced rows, folded in the same launch)
     // (horn: this iteration's Horn step in the same single-thread launch, right after it)
     auto enqueue_err_step = [&](int it, const double *partials = nullptr, bool horn = false) -> int {

@@ -200,7 +200,7 @@ constexpr int kBundleCounterFields = 12;
 bool bundle_v2();
 bool bundle_local(); // the local-frame pair test with a scene in slot order (ICP_BUNDLE_LOCAL=0: off)
 NNPlan plan_nn_bundle2(size_t np, int nb_pad);
-constexpr int kBundleTctlInts = 32 * 9;
+constexpr int kBundleTctlInts = 32 * 10; // (count, eight queue counters, the candidates' done counter: 128 B apart)
 size_t bundle2_slots(const NNPlan &pl);
 size_t bundle2_list_ints(const NNPlan &pl, int nb_pad);
 size_t bundle2_counter_rows(const NNPlan &pl);
@@ -222,7 +222,8 @@ void launch_bundle_groups(const void *qop, size_t nslots, void *gop, double4 *gc
 // cand (qblocks x nb_pad / 32 ints), cand_n (qblocks): each filter workgroup's candidate blocks;
 // then the task list: wsplit (qblocks: the partial sets of each query workgroup), tasks
 // (bundle2_task_count(plan) int2), tctl (kBundleTctlInts ints: the count, then the filter's
-// eight task-queue counters, 128 B apart)
+// eight task-queue counters, 128 B apart, then the candidates' done counter, which must be zero
+// when tctl is allocated: the last candidates workgroup builds the task list and re-zeroes it)
 void launch_bundle_candidates(const NNPlan &pl, const double4 *gctr, const double4 *blk, int nb_pad, int *cand,
                               int *cand_n, int *wsplit, int2 *tasks, int *tctl, hipStream_t st,
                               const int *stop = nullptr);

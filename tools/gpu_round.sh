@@ -304,6 +304,28 @@ for s in $STEPS; do
                done
              done ;;
     c5shard) run c5shard 300 python tools/shard_probe.py --n 8388608 --worlds 8 --steps 5 --warmup 2 ;;
+    fuseab) for k in 1 2; do
+              for f in 1 0; do
+                ICP_BUNDLE_FUSE_TASKS=$f run fuseab_${f}_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 20 || exit 1
+                cat $OUT/fuseab_${f}_$k.log >> $OUT/fuseab_all_$f.log
+                ICP_BUNDLE_FUSE_TASKS=$f run fusebench_${f}_$k 300 python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-cow --no-cases || exit 1
+                cat $OUT/fusebench_${f}_$k.log >> $OUT/fuseab_all_$f.log
+              done
+            done ;;
+    finw8) for k in 1 2; do
+             for r in 1 2 4; do
+               ICP_FIN16_ROUNDS=$r run finw8_${r}_$k 300 python tools/shard_probe.py --worlds 8 4 --steps 20 || exit 1
+               cat $OUT/finw8_${r}_$k.log >> $OUT/finw8_all_$r.log
+             done
+           done ;;
+    strideab) for k in 1 2; do
+                for r in 8 1; do
+                  ICP_NN_TIMING_STRIDE=$r run strideab_${r}_$k 300 python tools/shard_probe.py --worlds 1 8 --steps 40 || exit 1
+                  cat $OUT/strideab_${r}_$k.log >> $OUT/strideab_all_$r.log
+                  ICP_NN_TIMING_STRIDE=$r run stridebench_${r}_$k 300 python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-cow --no-cases || exit 1
+                  cat $OUT/stridebench_${r}_$k.log >> $OUT/strideab_all_$r.log
+                done
+              done ;;
     *) echo "unknown step $s" ;;
     esac
 done
