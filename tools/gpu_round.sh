@@ -326,6 +326,9 @@ for s in $STEPS; do
                   cat $OUT/stridebench_${r}_$k.log >> $OUT/strideab_all_$r.log
                 done
               done ;;
+    test_bf) ICP_AMD_LIB=iterative-closest-point_amd/build_ab/bf/libicp_hip.so run pytest_bf 600 python -u -m pytest \
+               tests/test_gpu_c4c5.py tests/test_gpu_parity.py tests/test_gpu_cert_stress.py -m gpu -x -q -rf \
+               --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
     esac
 done
