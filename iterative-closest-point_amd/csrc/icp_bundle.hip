@@ -829,9 +829,6 @@ __global__ __launch_bounds__(kBlock) void bundle_candidates_kernel(const double4
     if (tid == 0) tctl[kBundleDoneCtr] = 0;
 }
 
-#ifndef ICP_B2_BRANCHFREE
-#define ICP_B2_BRANCHFREE 0 // (A/B build: branch-free pair update)
-#endif
 #ifndef ICP_B2_WAVES
 #define ICP_B2_WAVES 4 // waves per SIMD the QG = 4 filter is compiled for (112 VGPRs, no spill)
 #endif
@@ -1096,18 +1093,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
         const float ma = fmin3(m0, m1, m2), sa = fminf(__builtin_amdgcn_fmed3f(m0, m1, m2), fmin3(s0, s1, s2));
         const float mb = fmin3(m3, m4, dd[15]), sb = fminf(__builtin_amdgcn_fmed3f(m3, m4, dd[15]), fminf(s3, s4));
         const float mn = fminf(ma, mb);
-#if ICP_B2_BRANCHFREE
-        // (A/B build: no wave-uniform branch per update, so that the next (group, bundle)'s MFMA
-        // can issue under this update's VALU; the updates below are the identity on lanes with
-        // mn >= second, and the row select on lanes with mn >= best: the same values)
-        {
-            int row = 0;
-#pragma unroll
-            for (int r = 15; r >= 0; --r)
-                row = dd[r] == mn ? (r & 3) + 8 * (r >> 2) : row;
-            bpos[q] = mn < best[q] ? blk * 32 + 4 * h + row : bpos[q];
-        }
-#else
         if (!__any(mn < second[q])) return;
         if (__any(mn < best[q])) {
             int row = 0;
@@ -1116,7 +1101,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
                 row = dd[r] == mn ? (r & 3) + 8 * (r >> 2) : row;
             bpos[q] = mn < best[q] ? blk * 32 + 4 * h + row : bpos[q];
         }
-#endif
         const float b0 = best[q], c0 = second[q];
         second[q] = fminf(__builtin_amdgcn_fmed3f(b0, ma, mb), fmin3(c0, sa, sb));
         best[q] = fmin3(b0, ma, mb);
