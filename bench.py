@@ -520,7 +520,10 @@ def main():
               "pmc_gbps": traffic / nn_s / 1e9 if traffic and nn_s > 0 else None,
               "peak_gbps": 8000.0,
               "pmc_hbm_frac": traffic / nn_s / 1e9 / 8000.0 if traffic and nn_s > 0 else None,
-              "note": "the O(N*M) filter is compute-bound: its HBM fraction is small by construction (§8d)"}
+              "note": ("the bundle filter is latency-bound (dependent L2/MALL operand loads -> MFMA -> ballot per "
+                       "fired block, DESIGN §3.1.1): neither HBM nor the matrix pipe is its limit"
+                       if level1 == "bundle" else
+                       "the O(N*M) filter is compute-bound: its HBM fraction is small by construction (§8d)")}
     dtype = {"mfma16": "f16 hi/lo-split MFMA filter (fp32 accumulate); fp64 certificate, resolve and reductions",
              "bundle": "f16 hi/lo-split MFMA bundle bound + pair filter (fp32 accumulate); fp64 certificate, "
                        "resolve and reductions",
