@@ -132,12 +132,18 @@ def cpu_baseline(m, p, sample=4096, seed=0):
     return out
 
 
-def rank_record(rank, info, filter_ms, allreduce_ms, n_local, iterations):
-    """One rank's entry of the line's per_rank: its level-1 filter time and per-iteration
-    all-reduce latency (HIP events on the engine stream), and what it ran on -- its RCCL
-    communicator's ncclCommCount / ncclCommUserRank (null / its own rank without RCCL) and the
-    PCI bus id of its device (icp_get_comm_info)."""
-    return {"rank": rank, "filter_ms": filter_ms, "allreduce_ms_per_iter": allreduce_ms,
+def rank_record(rank, info, filter_ms, allreduce_ms, n_local, iterations, ms_per_step=None, reg=None):
+    """One rank's entry of the line's per_rank: its own ms per iteration, its level-1 filter time
+    (HIP events on the engine stream), the rest of its iteration (tail_ms: the other launches and
+    the all-reduce), its per-iteration all-reduce latency, its registration cost (set_model ms,
+    whole-registration ms), and what it ran on -- its RCCL communicator's ncclCommCount /
+    ncclCommUserRank (null / its own rank without RCCL) and the PCI bus id of its device
+    (icp_get_comm_info)."""
+    return {"rank": rank, "ms_per_step": ms_per_step, "filter_ms": filter_ms,
+            "tail_ms": (ms_per_step - filter_ms) if ms_per_step is not None and filter_ms else None,
+            "allreduce_ms_per_iter": allreduce_ms,
+            "set_model_ms": reg["set_model_ms"] if reg else None,
+            "registration_ms": reg["registration_ms"] if reg else None,
             "n_scene_local": n_local, "iterations": iterations, "comm_count": info["comm_count"],
             "comm_rank": info["comm_rank"], "pci_bus_id": info["pci_bus_id"]}
 
@@ -168,6 +174,7 @@ def _cow_paths():
 
 
 BUNDLE_COUNT_STEPS = 3
+REGISTRATION_ITERS = 30  # BASELINE.json configs[3] / [4]: 30 iterations
 
 
 def bundle_v1():
@@ -240,6 +247,12 @@ def reference_cases_gpu(min_time=0.3):
     r = subprocess.run([exe, "--ref", ref, "--scene", scene, "--min-time", str(min_time), "--json"],
                        capture_output=True, text=True, timeout=600, check=True)
     cases = json.loads(r.stdout.strip().splitlines()[-1])["cases"]
+    # the reference's opti_gpu_loop re-uploads the model on every frame (compute.cu:160): the
+    # same case with icp_set_model inside each registration
+    r = subprocess.run([exe, "--ref", ref, "--scene", scene, "--min-time", str(min_time), "--json", "--cold",
+                        "--only", "opti_gpu_loop_cold"], capture_output=True, text=True, timeout=600, check=True)
+    cases.update(json.loads(r.stdout.strip().splitlines()[-1])["cases"])
+    REF_README_MS.setdefault("opti_gpu_loop_cold", REF_README_MS["opti_gpu_loop"])
     return {k: {"ms": v["ms"], "frame_rate": v["frame_rate"], "reference_ms": REF_README_MS.get(k),
                 "speedup_vs_reference": (REF_README_MS[k] / v["ms"]) if k in REF_README_MS else None}
             for k, v in cases.items()}
@@ -375,6 +388,41 @@ def csv_io(m):
             "load_mb_per_s": size / tl / 1e6, "roundtrip_rows": int(back.shape[0])}
 
 
+def registration(ctx, m, p_local, n_total, iters=30, reps=3):
+    """SURVEY §8d's clock: a whole registration from model upload through the last iteration's
+    err -- icp_set_model (host AoS in, every device image built), icp_set_scene, the first
+    (unseeded) iteration and the seeded ones.  Each rep re-uploads both clouds (set_model always
+    rebuilds), on the caller's context (one-time hipInit / RCCL init excluded, as §8d says).
+    The first iteration is timed by a separate run(1) after a fresh set_scene; the seeded ones
+    are the rest of the 30-iteration run."""
+    rows = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.set_model(m)
+        t1 = time.perf_counter()
+        ctx.set_scene(p_local, np_total=n_total)
+        t2 = time.perf_counter()
+        res, _ = ctx.run(iters, -1.0)
+        t3 = time.perf_counter()
+        ctx.set_scene(p_local, np_total=n_total)
+        t4 = time.perf_counter()
+        ctx.run(1, -1.0)
+        t5 = time.perf_counter()
+        rows.append((t1 - t0, t2 - t1, t3 - t2, t5 - t4, res.iterations))
+    a = np.median(np.array(rows, dtype=np.float64), axis=0)
+    set_model, set_scene, run_all, first, its = a
+    total = set_model + set_scene + run_all
+    return {"iterations": int(its), "reps": reps, "set_model_ms": set_model * 1e3, "set_scene_ms": set_scene * 1e3,
+            "first_iteration_ms": first * 1e3,
+            "seeded_iteration_ms": (run_all - first) * 1e3 / max(its - 1, 1),
+            "run_ms": run_all * 1e3, "registration_ms": total * 1e3,
+            "iterations_per_s_inclusive": its / total,
+            "set_model_ms_per_rep": [r[0] * 1e3 for r in rows],
+            "definition": "median over reps of wall time: set_model (host fp64 AoS -> every device image) + "
+                          f"set_scene + icp_run({iters}); first_iteration_ms = run(1) after a fresh set_scene "
+                          "(slot order, grid seeds, unseeded search); seeded = the rest of the run per iteration"}
+
+
 def cow_frame_rate(device, reps=20):
     """Reference headline: opti_gpu_loop frame_rate = complete cow registrations/s."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -407,6 +455,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cow", action="store_true")
     ap.add_argument("--no-cases", action="store_true", help="skip the reference's 14 benchmark cases")
+    ap.add_argument("--no-registration", dest="registration", action="store_false",
+                    help="skip the registration block (SURVEY §8d: set_model through the last iteration)")
     ap.add_argument("--rccl", action="store_true",
                     help="N=1: route the per-iteration sums through a 1-rank RCCL communicator, as N>1 does")
     args = ap.parse_args()
@@ -454,10 +504,6 @@ def main():
     ctx.set_nn_variant(variant)
     m, p = icp_amd.synthetic_pair(args.n, seed=42)
     b, c = icp_amd.shard_range(args.n, rank, world)
-    big = c >= 8192 and args.n >= 8192  # level1_kind's f16 MFMA threshold (AUTO: the bundle filter)
-    level1 = None if args.nn != "certified" else (
-        "bundle" if args.variant == "bundle" or (args.variant == "auto" and big) else
-        "mfma16" if args.variant == "mfma16" else ("mfma" if args.variant == "mfma" else None))
     ctx.set_model(m)
     ctx.set_scene(p[b:b + c], np_total=args.n)
 
@@ -469,12 +515,17 @@ def main():
     res, errs = ctx.run(args.steps, -1.0)
     barrier_sync()
     dt = time.perf_counter() - t0
+    dt_local = dt
     st = ctx.stats()
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    # the level-1 filter the engine ran (icp_stats.last_filter), not a guess from the sizes
+    level1 = icp_amd.FILTER_NAMES.get(st["last_filter"])
+    if level1 in ("valu", "fp64", "one_launch"):
+        level1 = None
     nn_avg_ms = st["nn_ms"] / max(st["nn_launches"], 1)
     ar_ms = st["allreduce_ms"] / st["allreduce_calls"] if st["allreduce_calls"] else None
     work = None
@@ -488,8 +539,11 @@ def main():
         work = {k: v / BUNDLE_COUNT_STEPS for k, v in bc.items() if not isinstance(v, dict)}
         work["us_per_wave_task"] = bc["us_per_wave_task"]
         ctx.set_bundle_counters(False)
+    # SURVEY §8d's clock: whole registrations from the model upload (every rank: icp_run
+    # all-reduces), untimed by the headline
+    reg = registration(ctx, m, p[b:b + c], args.n, iters=REGISTRATION_ITERS) if args.registration else None
     host_reduce = world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1"
-    per_rank = [rank_record(rank, ctx.comm_info(), nn_avg_ms, ar_ms, c, st["iterations"])]
+    per_rank = [rank_record(rank, ctx.comm_info(), nn_avg_ms, ar_ms, c, st["iterations"], dt_local * 1e3 / args.steps, reg)]
     if dist is not None:
         got = [None] * world
         dist.all_gather_object(got, per_rank[0])
@@ -530,9 +584,11 @@ def main():
              "mfma": "f32 MFMA filter; fp64 certificate, resolve and reductions"}.get(
         level1, "f64" if args.nn == "fp64" else "f32 VALU filter; fp64 certificate, resolve and reductions")
 
+    workload = {1 << 20: "C4", 1 << 23: "C5"}.get(args.n, "custom")
     if rank == 0:
         out = {
-            "metric": "ICP iterations/sec (synthetic 2^20-point pair, exact NN)",
+            "metric": f"ICP iterations/sec (synthetic {args.n}-point pair{', ' + workload if workload != 'custom' else ''}, "
+                      "exact NN)",
             "value": args.steps / dt,
             "unit": "ICP iterations/s",
             "n_gpus": world,
@@ -544,7 +600,7 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic (mt19937_64 seed 42, uniform [-1,1]^3; scene = 5deg rotation + translation)",
-            "config": {"workload": f"{ {1 << 20: 'C4', 1 << 23: 'C5'}.get(args.n, 'custom')} synthetic "
+            "config": {"workload": f"{workload} synthetic "
                                    f"{args.n}-pt model vs rigid-transformed copy, fixed iterations",
                        "n_model": args.n, "n_scene": args.n, "nn_mode": args.nn, "nn_variant": args.variant,
                        "parallelism": f"scene-sharded x{world}, model replicated, "
@@ -570,6 +626,15 @@ def main():
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
         }
+        if reg is not None:
+            regs = [r for r in per_rank if r.get("registration_ms")]
+            out["registration"] = dict(reg)
+            if world > 1:  # the job's registration: its slowest rank
+                worst = max(regs, key=lambda r: r["registration_ms"])
+                out["registration"].update({"rank0": reg["registration_ms"], "max_rank": worst["rank"],
+                                            "registration_ms": worst["registration_ms"],
+                                            "set_model_ms_max": max(r["set_model_ms"] for r in regs)})
+                out["registration"]["iterations_per_s_inclusive"] = reg["iterations"] / (worst["registration_ms"] * 1e-3)
         if level1 == "bundle" and nn_s > 0:
             out["roofline"].update(bundle_roofline(c, args.n, nn_s, work, v1=bundle_v1()))
         if level1 == "mfma16" and nn_s > 0:

@@ -78,8 +78,11 @@ typedef struct icp_result {
 } icp_result;
 
 typedef struct icp_stats {
-    double nn_ms;          /* summed device time of the NN search kernels (HIP events) */
-    long long nn_launches; /* number of NN searches timed                               */
+    double nn_ms;          /* summed device time of the timed NN searches' O(N*M)-class kernel (HIP
+                              events).  icp_run times iterations 1, 9, 17, ... of each run (an event
+                              pair costs the stream ~9 us; ICP_NN_TIMING_STRIDE changes the 8), the
+                              per-operation surface every search of >= 2^32 pairs               */
+    long long nn_launches; /* number of NN searches timed (samples, not every search)       */
     long long nn_pairs;    /* sum over searches of np_local * nm                        */
     long long ambiguous;   /* queries the fp32 certificate sent to fp64 resolution      */
     long long level1_queued; /* queries the MFMA certificate sent to the VALU filter     */
@@ -103,7 +106,17 @@ typedef struct icp_stats {
     long long cpu_rule_changed; /* ... whose CPU-rule answer differs from the squared rule's   */
     long long persistent_fallbacks; /* one-launch runs that found their grid not co-resident at
                                        the first barrier and ran the launch loop instead         */
+    int last_filter; /* ICP_FILTER_* of the last NN search's O(N*M)-class level (-1: none since the
+                        context was created or its stats reset)                                    */
 } icp_stats;
+/* icp_stats.last_filter: the search level that decided most queries */
+#define ICP_FILTER_VALU 0    /* fp32 direct-form filter on the vector ALUs */
+#define ICP_FILTER_MFMA 1    /* f32 MFMA expanded-form filter               */
+#define ICP_FILTER_MFMA16 2  /* f16 hi/lo MFMA filter over all N x M pairs  */
+#define ICP_FILTER_BUNDLE 3  /* f16 MFMA bundle bound + pair filter (nn_bundle2_kernel) */
+#define ICP_FILTER_GRID 4    /* exact fp64 grid search of every query       */
+#define ICP_FILTER_FP64 5    /* fp64 brute force                            */
+#define ICP_FILTER_ONE_LAUNCH 6 /* the one-launch registration's culled fp64 search */
 
 /* ---- context ------------------------------------------------------------ */
 /* Single-GPU context on HIP device `device` (replaces the stateless wrappers of
@@ -140,10 +153,12 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm);
 int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total);
 /* Copy this rank's current new_p (gpu.hh:88) back to the host. */
 int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
-/* icp_set_model, unless the resident model already holds exactly these nm points (memcmp
- * against the engine's host copy of the last model uploaded): the safe form of "upload the
- * model once" for wrappers that receive the model on every call (compute_Y_w_opti,
- * compute.cu:154-160, re-uploads per call).  *uploaded (nullable) = 1 if it uploaded. */
+/* icp_set_model, unless the resident model already holds exactly these nm points, bit for bit
+ * (models of <= 64k points: memcmp against the engine's host copy; larger ones: the upload is
+ * compared with the resident device copy, and becomes the new model if it differs): the safe
+ * form of "upload the model once" for wrappers that receive the model on every call
+ * (compute_Y_w_opti, compute.cu:154-160, re-uploads per call).  *uploaded (nullable) = 1 if
+ * the model changed. */
 int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded);
 /* Reference behaviour is to refuse np != nm (gpu.cc:54-57); 1 lifts that check. */
 int icp_set_allow_unequal(icp_ctx *ctx, int allow);
@@ -265,6 +280,10 @@ int icp_get_bundle_counters(icp_ctx *ctx, uint64_t out[16]);
  * it has none (plain or host all-reduce contexts); bus_id (nullable, len >= 16) = the PCI bus
  * id of its HIP device (hipDeviceGetPCIBusId), NUL-terminated. */
 int icp_get_comm_info(icp_ctx *ctx, int *comm_count, int *comm_rank, char *bus_id, int len);
+/* The bundle filter's kd order of the resident model (models of >= 8,192 points; built on the
+ * device by icp_set_model): kd_out[P] = the original index of kd position P (nm entries); 32
+ * consecutive positions form a bundle.  ICP_E_NO_MODEL if the model has no bundle images. */
+int icp_get_model_order(icp_ctx *ctx, int32_t *kd_out);
 
 #ifdef __cplusplus
 }

@@ -162,8 +162,14 @@ struct icp_ctx {
     // host copy of the model (AoS): kept when the one-launch paths can take it (small models),
     // downloaded on demand for the CPU rule's host fix-up, else empty (0.2 GB at 2^23 points)
     std::vector<double> model_host;
-    unsigned long long model_hash = 0; // of the last model uploaded (icp_ensure_model compares it)
     double rm = 0.0;         // max |centred fp32 model coordinate|
+    // the model's preparation on the device (icp_model.hip): stats scratch, results (device and
+    // pinned host), the kd builder's plan and scratch, the compare counter of icp_ensure_model
+    double *mstat_part = nullptr, *mstat_out = nullptr, *h_mstat = nullptr;
+    int *cmp_diff = nullptr;
+    KdPlan kd_plan;
+    char *kd_scratch = nullptr;
+    size_t kd_scratch_cap = 0;
     bool has_model = false;
 
     // scene (this rank's shard), its correspondences
@@ -479,32 +485,6 @@ int model_host_copy(icp_ctx *ctx, const double **out)
     return ICP_OK;
 }
 
-// 64-bit content hash of a model array (icp_ensure_model): two multiply-xorshift lanes over
-// the 8-byte words, folded with the length
-unsigned long long model_digest(const double *xyz, size_t count)
-{
-    unsigned long long a = 0x9e3779b97f4a7c15ull ^ count, b = 0xc2b2ae3d27d4eb4full;
-    size_t k = 0;
-    for (; k + 1 < count; k += 2) {
-        unsigned long long w0, w1;
-        std::memcpy(&w0, xyz + k, 8);
-        std::memcpy(&w1, xyz + k + 1, 8);
-        a = (a ^ w0) * 0xff51afd7ed558ccdull;
-        a ^= a >> 32;
-        b = (b ^ w1) * 0xc4ceb9fe1a85ec53ull;
-        b ^= b >> 29;
-    }
-    if (k < count) {
-        unsigned long long w;
-        std::memcpy(&w, xyz + k, 8);
-        a = (a ^ w) * 0xff51afd7ed558ccdull;
-    }
-    unsigned long long h = a ^ (b * 0x9e3779b97f4a7c15ull);
-    h ^= h >> 33;
-    h *= 0xff51afd7ed558ccdull;
-    return h ^ (h >> 33);
-}
-
 int ensure_reduction_space(icp_ctx *ctx)
 {
     if (ctx->partials) return ICP_OK;
@@ -686,6 +666,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
     TRY(ensure_queue(ctx, n));
     if (zero_counts) HIPCHK(hipMemsetAsync(ctx->amb_count, 0, sizeof(int) * 4, ctx->st));
     if (ctx->nn_mode == ICP_NN_FP64) {
+        ctx->stats.last_filter = ICP_FILTER_FP64;
         const NNPlan pl = plan_nn64(n, ctx->nm);
         const size_t need = (size_t)pl.splits * n * (sizeof(double) + sizeof(int));
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap, need));
@@ -699,6 +680,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         LAUNCHCHK("nn_fp64");
     } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
         // exact grid search for every query; over-budget boxes -> fp64 brute force per query
+        ctx->stats.last_filter = ICP_FILTER_GRID;
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
@@ -731,6 +713,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         }
         const bool sd = (seeded || gseed) && l1 >= 2;
         const bool v2 = l1 == 3 && bundle_v2();
+        ctx->stats.last_filter = l1 == 3 ? ICP_FILTER_BUNDLE : l1 == 2 ? ICP_FILTER_MFMA16 : ICP_FILTER_MFMA;
         const NNPlan pl = l1 == 3   ? (v2 ? plan_nn_bundle2(n, ctx->nb_pad) : plan_nn_bundle(n, ctx->nb_pad))
                           : l1 == 2 ? plan_nn_mfma16(n, ctx->nm_pad, sd)
                                     : plan_nn_mfma(n, ctx->nm_pad);
@@ -836,6 +819,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         LAUNCHCHK("nn_mfma");
         ctx->kpos_valid = kpos_out != nullptr;
     } else {
+        ctx->stats.last_filter = ICP_FILTER_VALU;
         const NNPlan pl = plan_nn32(n, ctx->nm_pad);
         const size_t need = (size_t)pl.splits * n * (2 * sizeof(float) + sizeof(int));
         TRY(grow(ctx, (char **)&ctx->part, &ctx->part_cap, need));
@@ -1049,6 +1033,7 @@ static int ctx_init(icp_ctx *ctx)
     ctx->n_cu = prop.multiProcessorCount;
     ctx->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
     ctx->lds_per_block = prop.sharedMemPerBlock;
+    ctx->stats.last_filter = -1;
     return ensure_reduction_space(ctx);
 }
 
@@ -1260,60 +1245,74 @@ int icp_set_allow_unequal(icp_ctx *ctx, int allow)
     return ICP_OK;
 }
 
-int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
+// The model's AoS copy -> ctx->stage (pageable host memory: the runtime's staged copy).
+static int stage_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
 {
-    if (!ctx || (!m_xyz && nm) || nm == 0) return ICP_E_ARG;
-    if (nm > (size_t)0x7fffffff - kTile32) return fail(ctx, ICP_E_ARG, "model too large");
-    HIPCHK(hipSetDevice(ctx->device));
-    // centring point c = model centroid (any c is valid for the certificate; the centroid
-    // keeps |coordinates| and hence the fp32 error bound small)
-    double s[3] = {0, 0, 0};
-    for (size_t j = 0; j < nm; ++j)
-        for (int k = 0; k < 3; ++k) s[k] += m_xyz[3 * j + k];
-    for (int k = 0; k < 3; ++k) ctx->c[k] = s[k] / (double)nm;
-    // centred fp32 model, padded to a whole number of LDS tiles with far points
-    const size_t nm_pad = (nm + kTile32 - 1) / kTile32 * kTile32;
-    std::vector<float4> h(nm_pad);
-    double rm = 0.0;
-    for (size_t j = 0; j < nm; ++j) {
-        float4 v;
-        v.x = (float)(m_xyz[3 * j] - ctx->c[0]);
-        v.y = (float)(m_xyz[3 * j + 1] - ctx->c[1]);
-        v.z = (float)(m_xyz[3 * j + 2] - ctx->c[2]);
-        v.w = 0.f;
-        if (!std::isfinite(v.x) || !std::isfinite(v.y) || !std::isfinite(v.z))
-            return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
-        rm = std::fmax(rm, std::fmax(std::fabs((double)v.x), std::fmax(std::fabs((double)v.y), std::fabs((double)v.z))));
-        h[j] = v;
+    TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * nm));
+    HIPCHK(hipMemcpyAsync(ctx->stage, m_xyz, sizeof(double) * 3 * nm, hipMemcpyHostToDevice, ctx->st));
+    return ICP_OK;
+}
+
+// ICP_KD_HOST=1: the bundle filter's kd order from the host statement of the rule
+// (bundle_kd_order, threaded nth_element) instead of the device build (A/B runs)
+static bool kd_host()
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_KD_HOST");
+        return e && atoi(e) == 1;
+    }();
+    return on;
+}
+
+// icp_set_model from the staged AoS copy: every image of the model is built on the device
+// (icp_model.hip); the host reads back 13 doubles and, for models that fit the one-launch
+// loops (<= 64k points), builds their Morton image.  Nothing of the context changes before the
+// model has passed its checks.
+static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm)
+{
+    const double *aos = ctx->stage;
+    if (!ctx->mstat_part) {
+        HIPCHK(hipMalloc((void **)&ctx->mstat_part, sizeof(double) * model_stats_scratch_doubles()));
+        HIPCHK(hipMalloc((void **)&ctx->mstat_out, sizeof(double) * 16));
+        HIPCHK(hipHostMalloc((void **)&ctx->h_mstat, sizeof(double) * 16, hipHostMallocDefault));
     }
+    // 1. sum, box, finiteness; the centring point c = the model's centroid (any c is valid for
+    // the certificate; the centroid keeps |coordinates| and hence the fp32 error bound small)
+    launch_model_stats(aos, (int)nm, ctx->mstat_part, ctx->mstat_out, ctx->st);
+    LAUNCHCHK("model_stats");
+    HIPCHK(hipMemcpyAsync(ctx->h_mstat, ctx->mstat_out, sizeof(double) * 10, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (ctx->h_mstat[9] != 0.0) return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
+    double c[3], lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        c[k] = ctx->h_mstat[k] / (double)nm;
+        lo[k] = ctx->h_mstat[3 + k];
+        hi[k] = ctx->h_mstat[6 + k];
+    }
+    // 2. the fp32 range around c (the certificate's rm) and the fp64 one (the f16 image's scale)
+    launch_model_range(aos, (int)nm, c, ctx->mstat_part, ctx->mstat_out, ctx->st);
+    LAUNCHCHK("model_range");
+    HIPCHK(hipMemcpyAsync(ctx->h_mstat, ctx->mstat_out, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (ctx->h_mstat[2] != 0.0) return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
+    const double rm = ctx->h_mstat[0], rm64 = ctx->h_mstat[1];
     if (rm > 1e15) return fail(ctx, ICP_E_RANGE, "model coordinates exceed 1e15 around the centroid");
-    for (size_t j = nm; j < nm_pad; ++j) h[j] = make_float4(1.0e18f, 1.0e18f, 1.0e18f, 0.f);
+    ctx->has_model = false; // (until every image below is built)
+    for (int k = 0; k < 3; ++k) ctx->c[k] = c[k];
     ctx->rm = rm;
+    // 3. the images: SoA fp64, the centred fp32 copy padded to whole LDS tiles with far points
+    // and its MFMA operand order, the f16 split image at S = 2^e with max |m - c| S in
+    // [2^11, 2^12), the double4 rows, the grid
+    const size_t nm_pad = (nm + kTile32 - 1) / kTile32 * kTile32;
+    TRY(grow_cloud(ctx, ctx->model, nm, true));
+    launch_aos_to_soa(aos, nm, ctx->model.x, ctx->model.y, ctx->model.z, ctx->st);
     TRY(grow(ctx, &ctx->m32, &ctx->m32_cap, nm_pad));
-    HIPCHK(hipMemcpyAsync(ctx->m32, h.data(), sizeof(float4) * nm_pad, hipMemcpyHostToDevice, ctx->st));
-    // MFMA operand image: point P = 64g + 16t + i, component k (mm, x, y, z) at float
-    // g*256 + k*64 + 4i + t  (lane l = 16k + i reads its 4 operands as one float4)
-    std::vector<float> hp(4 * nm_pad), hmm(nm_pad);
-    for (size_t P = 0; P < nm_pad; ++P) {
-        const float4 v = h[P];
-        const bool real = P < nm;
-        const float mmv = real ? (float)((double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z) : 1.0e30f;
-        const float comp[4] = {mmv, real ? v.x : 0.f, real ? v.y : 0.f, real ? v.z : 0.f};
-        const size_t g = P >> 6, t = (P >> 4) & 3, i = P & 15;
-        for (int k = 0; k < 4; ++k) hp[g * 256 + k * 64 + i * 4 + t] = comp[k];
-        hmm[P] = mmv;
-    }
     TRY(grow(ctx, &ctx->mperm, &ctx->mperm_cap, nm_pad));
     TRY(grow(ctx, &ctx->mm, &ctx->mm_cap, nm_pad));
-    HIPCHK(hipMemcpyAsync(ctx->mperm, hp.data(), sizeof(float) * 4 * nm_pad, hipMemcpyHostToDevice, ctx->st));
-    HIPCHK(hipMemcpyAsync(ctx->mm, hmm.data(), sizeof(float) * nm_pad, hipMemcpyHostToDevice, ctx->st));
-    // f16 split image: scale S = 2^e with max |m - c| * S in [2^11, 2^12)
-    double rm64 = 0.0;
-    for (size_t j = 0; j < nm; ++j)
-        for (int k = 0; k < 3; ++k) rm64 = std::fmax(rm64, std::fabs(m_xyz[3 * j + k] - ctx->c[k]));
+    launch_model_f32_images(aos, (int)nm, (int)nm_pad, ctx->c, ctx->m32, (float *)ctx->mperm, ctx->mm, ctx->st);
+    LAUNCHCHK("model_f32_images");
     ctx->scale16 = rm64 > 0.0 ? std::ldexp(1.0, (int)std::floor(std::log2(4096.0 / rm64))) : 1.0;
     while (rm64 * ctx->scale16 >= 4096.0) ctx->scale16 *= 0.5;
-    TRY(upload_cloud(ctx, ctx->model, m_xyz, nm, false));
     TRY(grow(ctx, &ctx->mimg16, &ctx->mimg16_cap, nm_pad * 32));
     TRY(grow(ctx, &ctx->mms16, &ctx->mms16_cap, nm_pad));
     launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, (int)nm_pad, ctx->c,
@@ -1321,8 +1320,8 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     LAUNCHCHK("build_mimage16");
     TRY(grow(ctx, &ctx->m4, &ctx->m4_cap, nm));
     launch_make_aos4(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->m4, ctx->st);
-    // uniform grid over the fp64 model for the exact resolver
-    ctx->grid = grid_params(m_xyz, nm);
+    // uniform grid over the fp64 model for the exact resolver (its box: step 1's)
+    ctx->grid = grid_params_box(lo, hi, nm);
     const long long ncell = grid_cells(ctx->grid);
     TRY(grow(ctx, &ctx->g_cid, &ctx->g_cid_cap, nm));
     TRY(grow(ctx, &ctx->g_count, &ctx->g_count_cap, (size_t)ncell + 1));
@@ -1333,52 +1332,32 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_cid, ctx->g_count,
                       ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->st);
     LAUNCHCHK("grid_build");
-    std::vector<double> pm;
-    if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel)) { // the one-launch loops' model image
-        pm = persist_model_image(m_xyz, nm, &ctx->pm_blocks);
-        TRY(grow(ctx, &ctx->pm_img, &ctx->pm_img_cap, pm.size()));
-        HIPCHK(hipMemcpyAsync(ctx->pm_img, pm.data(), sizeof(double) * pm.size(), hipMemcpyHostToDevice, ctx->st));
-        { // the mid-size search's stale-seed scale: a move beyond 2 diagonals of a median 16-point block
-            const size_t nb16 = (nm + 15) / 16;
-            std::vector<double> d2(nb16);
-            for (size_t b = 0; b < nb16; ++b) {
-                double acc = 0.0;
-                for (int k = 0; k < 3; ++k) {
-                    double lo = pm[k * nm + 16 * b], hi = lo;
-                    for (size_t j = 16 * b + 1; j < std::min(nm, 16 * b + 16); ++j) {
-                        lo = std::min(lo, pm[k * nm + j]);
-                        hi = std::max(hi, pm[k * nm + j]);
-                    }
-                    acc += (hi - lo) * (hi - lo);
-                }
-                d2[b] = acc;
-            }
-            std::nth_element(d2.begin(), d2.begin() + nb16 / 2, d2.end());
-            ctx->pm_seed_big = 4.0 * d2[nb16 / 2];
-        }
-    }
     for (int k = 0; k < 3; ++k) { // the model's box (the query orders: mid-size loop, bundle filter)
-        ctx->m_lo[k] = INFINITY;
-        ctx->m_hi[k] = -INFINITY;
+        ctx->m_lo[k] = lo[k];
+        ctx->m_hi[k] = hi[k];
     }
-    for (size_t j = 0; j < nm; ++j)
-        for (int k = 0; k < 3; ++k) {
-            ctx->m_lo[k] = std::min(ctx->m_lo[k], m_xyz[3 * j + k]);
-            ctx->m_hi[k] = std::max(ctx->m_hi[k], m_xyz[3 * j + k]);
-        }
     ctx->nb_pad = 0;
     ctx->b_rlmax = -1.0;
+    std::vector<int> kd_h; // (ICP_KD_HOST: alive until the closing sync)
     if (nm >= (size_t)kBundleMinModel) { // the bundle filter's kd images (icp_bundle.hip)
-        const std::vector<int> kd = bundle_kd_order(m_xyz, nm);
         const int nb_pad = bundle_pad(nm);
         TRY(grow(ctx, &ctx->b_kd, &ctx->b_kd_cap, nm));
+        if (kd_host()) {
+            kd_h = bundle_kd_order(m_xyz, nm);
+            HIPCHK(hipMemcpyAsync(ctx->b_kd, kd_h.data(), sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
+        } else {
+            kd_plan(nm, ctx->kd_plan); // (ctx-owned: outlives the stream's copy of it)
+            TRY(grow(ctx, &ctx->kd_scratch, &ctx->kd_scratch_cap, kd_order_scratch_bytes(ctx->kd_plan)));
+            if (launch_kd_order(ctx->model.x, ctx->model.y, ctx->model.z, ctx->kd_plan, ctx->kd_scratch,
+                                ctx->kd_scratch_cap, ctx->b_kd, ctx->st) != 0)
+                return fail(ctx, ICP_E_HIP, "icp_set_model: the kd order's build failed");
+        }
         const size_t nbx = (size_t)nb_pad + 32; // + the null block (icp_bundle.hip)
         TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, nbx * 32));
         TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, nbx * 1024));
         TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, nbx * 32));
         TRY(grow(ctx, &ctx->b_bctr, &ctx->b_bctr_cap, nbx));
         TRY(grow(ctx, &ctx->b_blk, &ctx->b_blk_cap, nbx / 32));
-        HIPCHK(hipMemcpyAsync(ctx->b_kd, kd.data(), sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
         launch_build_bundle_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
                                    ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_bctr, ctx->b_blk,
                                    ctx->st);
@@ -1396,18 +1375,41 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
         LAUNCHCHK("build_kd_tables");
         std::vector<float4> fr(nfr);
         HIPCHK(hipMemcpyAsync(fr.data(), ctx->b_frame, sizeof(float4) * nfr, hipMemcpyDeviceToHost, ctx->st));
-        HIPCHK(hipStreamSynchronize(ctx->st)); // (kd is freed on return)
+        HIPCHK(hipStreamSynchronize(ctx->st));
         double rl = 0.0;
         for (const float4 &f : fr) rl = std::max(rl, (double)f.w);
         ctx->b_rlmax = rl;
         ctx->nb_pad = nb_pad;
+    }
+    std::vector<double> pm;
+    if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel)) { // the one-launch loops' model image
+        pm = persist_model_image(m_xyz, nm, &ctx->pm_blocks);
+        TRY(grow(ctx, &ctx->pm_img, &ctx->pm_img_cap, pm.size()));
+        HIPCHK(hipMemcpyAsync(ctx->pm_img, pm.data(), sizeof(double) * pm.size(), hipMemcpyHostToDevice, ctx->st));
+        { // the mid-size search's stale-seed scale: a move beyond 2 diagonals of a median 16-point block
+            const size_t nb16 = (nm + 15) / 16;
+            std::vector<double> d2(nb16);
+            for (size_t b = 0; b < nb16; ++b) {
+                double acc = 0.0;
+                for (int k = 0; k < 3; ++k) {
+                    double blo = pm[k * nm + 16 * b], bhi = blo;
+                    for (size_t j = 16 * b + 1; j < std::min(nm, 16 * b + 16); ++j) {
+                        blo = std::min(blo, pm[k * nm + j]);
+                        bhi = std::max(bhi, pm[k * nm + j]);
+                    }
+                    acc += (bhi - blo) * (bhi - blo);
+                }
+                d2[b] = acc;
+            }
+            std::nth_element(d2.begin(), d2.begin() + nb16 / 2, d2.end());
+            ctx->pm_seed_big = 4.0 * d2[nb16 / 2];
+        }
     }
     HIPCHK(hipStreamSynchronize(ctx->st));
     if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel) || ctx->nn_rule == ICP_NN_RULE_CPU_SQRT)
         ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
     else
         std::vector<double>().swap(ctx->model_host);
-    ctx->model_hash = model_digest(m_xyz, 3 * nm);
     ctx->nm = nm;
     ctx->nm_pad = nm_pad;
     ctx->has_model = true;
@@ -1423,16 +1425,39 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     return ICP_OK;
 }
 
+int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
+{
+    if (!ctx || (!m_xyz && nm) || nm == 0) return ICP_E_ARG;
+    if (nm > (size_t)0x7fffffff - kTile32) return fail(ctx, ICP_E_ARG, "model too large");
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(stage_model(ctx, m_xyz, nm));
+    return set_model_staged(ctx, m_xyz, nm);
+}
+
 int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded)
 {
     if (!ctx || !m_xyz || nm == 0) return ICP_E_ARG;
     if (uploaded) *uploaded = 0;
+    if (nm > (size_t)0x7fffffff - kTile32) return fail(ctx, ICP_E_ARG, "model too large");
+    HIPCHK(hipSetDevice(ctx->device));
     if (ctx->has_model && ctx->nm == nm) {
-        // the kept copy compares exactly; a large model by its content hash
-        const bool same = ctx->model_host.size() == 3 * nm
-                              ? std::memcmp(ctx->model_host.data(), m_xyz, sizeof(double) * 3 * nm) == 0
-                              : model_digest(m_xyz, 3 * nm) == ctx->model_hash;
-        if (same) return ICP_OK;
+        if (ctx->model_host.size() == 3 * nm) { // the kept host copy compares exactly
+            if (std::memcmp(ctx->model_host.data(), m_xyz, sizeof(double) * 3 * nm) == 0) return ICP_OK;
+        } else { // a large model: its upload compared bit for bit with the resident copy on the device
+            if (!ctx->cmp_diff) HIPCHK(hipMalloc((void **)&ctx->cmp_diff, sizeof(int)));
+            TRY(stage_model(ctx, m_xyz, nm));
+            HIPCHK(hipMemsetAsync(ctx->cmp_diff, 0, sizeof(int), ctx->st));
+            launch_model_compare(ctx->stage, (int)nm, ctx->model.x, ctx->model.y, ctx->model.z, ctx->cmp_diff,
+                                 ctx->st);
+            LAUNCHCHK("model_compare");
+            int diff = 0;
+            HIPCHK(hipMemcpyAsync(&diff, ctx->cmp_diff, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            HIPCHK(hipStreamSynchronize(ctx->st));
+            if (diff == 0) return ICP_OK;
+            TRY(set_model_staged(ctx, m_xyz, nm)); // (staged already)
+            if (uploaded) *uploaded = 1;
+            return ICP_OK;
+        }
     }
     TRY(icp_set_model(ctx, m_xyz, nm));
     if (uploaded) *uploaded = 1;
@@ -1755,6 +1780,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
     const int iters = ctx->h_iter->iter;
     ctx->stats.nn_pairs += (long long)iters * (long long)n * (long long)ctx->nm;
     ctx->stats.persistent_runs += 1;
+    ctx->stats.last_filter = ICP_FILTER_ONE_LAUNCH;
     return finish_run(ctx, threshold, err_trace, res, wall0);
 }
 
@@ -1906,6 +1932,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         return e ? std::max(1, atoi(e)) : 0;
     }();
     const int timing_stride = forced_stride ? forced_stride : 8;
+    // iteration 0 of a run is not sampled (its search may be unseeded): 1, 9, 17, ...
+    const int timing_phase = timing_stride > 1 ? 1 : 0;
     // (partials: the residual's unreduced rows, folded in the same launch)
     // (horn: this iteration's Horn step in the same single-thread launch, right after it)
     auto enqueue_err_step = [&](int it, const double *partials = nullptr, bool horn = false) -> int {
@@ -1926,7 +1954,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         if (enqueued < max_iter && enqueued - waited <= kAhead + (lag ? 1 : 0)) {
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
-            const bool timed = enqueued % timing_stride == 0;
+            const bool timed = enqueued % timing_stride == timing_phase;
             // (the search of an iteration queued behind the converged one returns at once)
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
@@ -2068,7 +2096,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;
-            if (n && (waited - 1) % timing_stride == 0) { // (an empty shard records no events)
+            if (n && (waited - 1) % timing_stride == timing_phase) { // (an empty shard records no events)
                 if (hipEventElapsedTime(&ms, ctx->iter_ev[5 * slot], ctx->iter_ev[5 * slot + 1]) == hipSuccess) {
                     ctx->stats.nn_ms += ms;
                     ctx->stats.nn_launches += 1;
@@ -2498,6 +2526,16 @@ int icp_set_cert_audit(icp_ctx *ctx, int enable)
     return cert_audit_reset(ctx);
 }
 
+int icp_get_model_order(icp_ctx *ctx, int32_t *kd_out)
+{
+    if (!ctx || !kd_out) return ICP_E_ARG;
+    if (!ctx->has_model || ctx->nb_pad <= 0 || !ctx->b_kd) return fail(ctx, ICP_E_NO_MODEL, "no bundle kd order");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpyAsync(kd_out, ctx->b_kd, sizeof(int32_t) * ctx->nm, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    return ICP_OK;
+}
+
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out)
 {
     if (!ctx || !out) return ICP_E_ARG;
@@ -2526,6 +2564,7 @@ int icp_reset_stats(icp_ctx *ctx)
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->cert_audit) TRY(cert_audit_reset(ctx));
     ctx->stats = icp_stats{};
+    ctx->stats.last_filter = -1;
     return ICP_OK;
 }
 

@@ -402,13 +402,18 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const doub
 
 GridParams grid_params(const double *m_xyz, size_t nm)
 {
-    GridParams p{};
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (size_t j = 0; j < nm; ++j)
         for (int a = 0; a < 3; ++a) {
             lo[a] = std::min(lo[a], m_xyz[3 * j + a]);
             hi[a] = std::max(hi[a], m_xyz[3 * j + a]);
         }
+    return grid_params_box(lo, hi, nm);
+}
+
+GridParams grid_params_box(const double lo[3], const double hi[3], size_t nm)
+{
+    GridParams p{};
     double ext[3], emax = 0.0;
     for (int a = 0; a < 3; ++a) {
         ext[a] = hi[a] - lo[a];

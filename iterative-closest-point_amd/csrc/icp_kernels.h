@@ -276,6 +276,7 @@ struct GridView {
     double inv_h;
 };
 GridParams grid_params(const double *m_xyz, size_t nm); // host: bounding box, ~2 points/cell
+GridParams grid_params_box(const double lo[3], const double hi[3], size_t nm); // (from the model's box)
 long long grid_cells(const GridParams &p);
 size_t grid_scan_blocks(long long n);
 // cid[nm], count/start[ncells + 1], bsum[grid_scan_blocks(ncells + 1)], fill[ncells], pts[nm]
@@ -554,5 +555,34 @@ void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm,
 
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);
+
+// ---- the model's preparation on the device (icp_model.hip) ------------------------------------
+// out[10] = (sum x, sum y, sum z, lo xyz, hi xyz, non-finite coordinates) of n AoS points; out[3] =
+// (max |(float)(m - c)| over the fp32 values, max |m - c|, non-finite fp32 values): fixed-order
+// two-stage reductions; scratch: model_stats_scratch_doubles()
+size_t model_stats_scratch_doubles();
+void launch_model_stats(const double *aos, int n, double *scratch, double *out, hipStream_t st);
+void launch_model_range(const double *aos, int n, const double c[3], double *scratch, double *out, hipStream_t st);
+// m32 (centred fp32, nm_pad rows, padding = far points), mperm (the f32 MFMA operand order), mm
+void launch_model_f32_images(const double *aos, int nm, int nm_pad, const double c[3], float4 *m32, float *mperm,
+                             float *mm, hipStream_t st);
+// *diff += points of the AoS cloud that differ bit for bit from the resident SoA cloud
+void launch_model_compare(const double *aos, int n, const double *x, const double *y, const double *z, int *diff,
+                          hipStream_t st);
+// The bundle filter's kd order (bundle_kd_order's rule) built on the device.  The plan (the
+// ranges of every level: data-independent) is host data that must outlive the stream's copy.
+struct KdPlan {
+    struct Level {
+        int seg_off, nseg, mid_off, piece_off, npieces, seg_bits;
+    };
+    int nm = 0, rank_bits = 1, max_seg = 1, leaf_off = 0, nleaf = 0;
+    std::vector<Level> levels;
+    std::vector<int> ints;
+};
+void kd_plan(size_t nm, KdPlan &pl);
+size_t kd_order_scratch_bytes(const KdPlan &pl);
+// kd[P] = the original index of kd position P; 0 on success
+int launch_kd_order(const double *mx, const double *my, const double *mz, const KdPlan &pl, void *scratch,
+                    size_t bytes, int *kd, hipStream_t st);
 
 } // namespace icp

@@ -64,7 +64,7 @@ EXPORTED = [
     "icp_load_matrix", "icp_write_matrix", "icp_free", "icp_get_stats", "icp_reset_stats",
     "icp_ensure_model", "icp_subtract_col", "icp_get_indices", "icp_set_index_digest",
     "icp_get_index_digest", "icp_set_cert_audit", "icp_set_run_mode", "icp_set_nn_rule",
-    "icp_get_comm_info", "icp_set_bundle_counters", "icp_get_bundle_counters",
+    "icp_get_comm_info", "icp_set_bundle_counters", "icp_get_bundle_counters", "icp_get_model_order",
 ]
 
 
@@ -86,7 +86,12 @@ class Stats(C.Structure):
                 ("allreduce_calls", C.c_longlong), ("cert_max_err_ratio", C.c_double),
                 ("cert_min_margin", C.c_double), ("cert_audited", C.c_longlong),
                 ("persistent_runs", C.c_longlong), ("cpu_rule_ties", C.c_longlong),
-                ("cpu_rule_changed", C.c_longlong), ("persistent_fallbacks", C.c_longlong)]
+                ("cpu_rule_changed", C.c_longlong), ("persistent_fallbacks", C.c_longlong),
+                ("last_filter", C.c_int)]
+
+
+# icp_stats.last_filter (ICP_FILTER_*): the search level that decided most queries
+FILTER_NAMES = {-1: None, 0: "valu", 1: "mfma", 2: "mfma16", 3: "bundle", 4: "grid", 5: "fp64", 6: "one_launch"}
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
@@ -140,6 +145,7 @@ def lib() -> C.CDLL:
     L.icp_ensure_model.argtypes = [vp, dp, sz, C.POINTER(C.c_int)]
     L.icp_subtract_col.argtypes = [vp, dp, sz, dp, dp]
     L.icp_get_indices.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.icp_get_model_order.argtypes = [vp, C.POINTER(C.c_int32)]
     L.icp_set_index_digest.argtypes = [vp, sz]
     L.icp_get_index_digest.argtypes = [vp, C.POINTER(C.c_uint64), sz]
     L.icp_set_cert_audit.argtypes = [vp, C.c_int]
@@ -361,6 +367,12 @@ class Context:
         idx = np.empty(self._np_local, dtype=np.int32)
         self._check(lib().icp_get_indices(self._h, idx.ctypes.data_as(C.POINTER(C.c_int32))))
         return idx
+
+    def model_order(self, nm: int) -> np.ndarray:
+        """The bundle filter's kd order of the resident model (icp_get_model_order)."""
+        kd = np.empty(nm, dtype=np.int32)
+        self._check(lib().icp_get_model_order(self._h, kd.ctypes.data_as(C.POINTER(C.c_int32))))
+        return kd
 
     def set_index_digest(self, cap: int):
         self._check(lib().icp_set_index_digest(self._h, cap))
