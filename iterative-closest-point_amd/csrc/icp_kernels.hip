@@ -1243,33 +1243,43 @@ __global__ __launch_bounds__(kBlock) void nn_finalize_mfma16_kernel(
             ms[r] = INFINITY;
             mi[r] = -1;
         }
-        for (int sp = 0; sp < smax; ++sp) {
-            float pb[R], ps[R];
-            int pi[R];
+        // CH splits' loads of all R slots in flight together (8 per array): a shard's few query
+        // workgroups carry up to 32 partial sets each, and one split per round left the merge
+        // a chain of dependent loads (W = 8 shard: 16 us for 131k queries, profiles/r03bf/)
+        constexpr int CH = R >= 8 ? 1 : 8 / R;
+        for (int sp0 = 0; sp0 < smax; sp0 += CH) {
+            float pb[CH][R], ps[CH][R];
+            int pi[CH][R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const size_t o = (size_t)sp * np + (size_t)((blockIdx.x * R + r) * kBlock + threadIdx.x);
-                if (sp < S[r]) {
-                    pb[r] = part_best[o];
-                    ps[r] = part_second[o];
-                    pi[r] = part_idx[o];
-                }
-            }
+            for (int c = 0; c < CH; ++c)
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (sp >= S[r]) continue;
-                if (sp == 0) {
-                    mb[r] = pb[r];
-                    ms[r] = ps[r];
-                    mi[r] = pi[r];
-                } else if (pb[r] < mb[r]) {
-                    ms[r] = fminf(mb[r], ps[r]);
-                    mb[r] = pb[r];
-                    mi[r] = pi[r];
-                } else {
-                    ms[r] = fminf(ms[r], pb[r]);
+                for (int r = 0; r < R; ++r) {
+                    const int sp = sp0 + c;
+                    const size_t o = (size_t)sp * np + (size_t)((blockIdx.x * R + r) * kBlock + threadIdx.x);
+                    if (sp < S[r]) {
+                        pb[c][r] = part_best[o];
+                        ps[c][r] = part_second[o];
+                        pi[c][r] = part_idx[o];
+                    }
                 }
-            }
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int sp = sp0 + c;
+                    if (sp >= S[r]) continue;
+                    if (sp == 0) {
+                        mb[r] = pb[c][r];
+                        ms[r] = ps[c][r];
+                        mi[r] = pi[c][r];
+                    } else if (pb[c][r] < mb[r]) {
+                        ms[r] = fminf(mb[r], ps[c][r]);
+                        mb[r] = pb[c][r];
+                        mi[r] = pi[c][r];
+                    } else {
+                        ms[r] = fminf(ms[r], pb[c][r]);
+                    }
+                }
         }
     }
 #pragma unroll
