@@ -573,9 +573,9 @@ void launch_model_compare(const double *aos, int n, const double *x, const doubl
 // ranges of every level: data-independent) is host data that must outlive the stream's copy.
 struct KdPlan {
     struct Level {
-        int seg_off, nseg, mid_off, piece_off, npieces, seg_bits;
+        int seg_off, nseg, mid_off; // its ranges' first positions and splits (-1: not split here)
     };
-    int nm = 0, rank_bits = 1, max_seg = 1, leaf_off = 0, nleaf = 0;
+    int nm = 0, max_seg = 1, leaf_off = 0, nleaf = 0; // (leaves: ranges of <= 1,024 points)
     std::vector<Level> levels;
     std::vector<int> ints;
 };

@@ -14,17 +14,20 @@
 //    block equal the host rule's exactly; the order inside a bundle is the rank order of its last
 //    split (every image and bound is built from the sets, and every result is the exact first
 //    minimum by original index).
-//    - ranks: for each axis a stable radix sort of the coordinate's ordered bits gives every point
-//      its rank in (coordinate, index) order, a 32-bit key that orders exactly like the host's
-//      comparator;
-//    - ranges of more than 1,024 points ("global levels"): per level, the active ranges' boxes
-//      (one workgroup per 4,096-point piece, 64-bit atomics on the ordered bits), then one radix
-//      sort of (range << rank bits | rank on the range's axis): each range becomes sorted along
-//      its axis and the split is a position;
-//    - ranges of at most 1,024 points (the 32-point splits): one workgroup per range, in LDS
-//      (a counting rank per level).
+//    - three lists, the points in (coordinate, index) order along x, y and z (stable radix
+//      sorts of the coordinates' ordered bits);
+//    - ranges of more than 1,024 points ("global levels"): per level each active range takes
+//      the widest extent of its three lists' end points, its left part is the first mid - lo of
+//      that axis's list, and all three lists are partitioned stably inside the range (flags, one
+//      exclusive scan of the three flag counts, one scatter): every list stays sorted inside
+//      every range;
+//    - ranges of at most 1,024 points (the 32-point splits): one workgroup per range, the same
+//      steps in LDS.
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -42,11 +45,6 @@ __device__ __forceinline__ unsigned long long ord_bits(double v)
     if (v == 0.0) v = 0.0;
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-__device__ __forceinline__ double ord_value(unsigned long long k)
-{
-    const unsigned long long b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
-    return __longlong_as_double((long long)b);
 }
 
 // Stage 1 of the stats: per workgroup (sum x, y, z; lo x, y, z; hi x, y, z; non-finite
@@ -129,10 +127,8 @@ __global__ __launch_bounds__(kBlock) void model_range_kernel(const double *__res
 
 // Stage 2: one workgroup folds G rows of K (kinds: 0 sum, 1 min, 2 max) in a fixed order.
 template <int K>
-__global__ __launch_bounds__(kBlock) void stats_fold_kernel(const double *__restrict__ part, int G,
-                                                            const int *__restrict__ kinds_unused, double *__restrict__ out)
+__global__ __launch_bounds__(kBlock) void stats_fold_kernel(const double *__restrict__ part, int G, double *__restrict__ out)
 {
-    (void)kinds_unused;
     __shared__ double sh[kBlock][K];
     auto kind = [](int k) { return K == 10 ? (k < 3 ? 0 : k < 6 ? 1 : k < 9 ? 2 : 0) : (k < 2 ? 2 : 0); };
     double v[K];
@@ -198,7 +194,12 @@ __global__ __launch_bounds__(kBlock) void model_compare_kernel(const double *__r
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(diff, (int)__popcll(m));
 }
 
-// ---- kd order ---------------------------------------------------------------------------
+// ---- kd order -----------------------------------------------------------------------------
+// Presorted construction: A_a (a = x, y, z) holds the points sorted by (coordinate a, index)
+// (a stable radix sort of the coordinate's ordered bits from the identity order).  Every split
+// keeps all three lists sorted inside every range by partitioning them stably, so a range's
+// extent along a is the difference of its A_a end points (the host rule's max - min) and its
+// split is a position of A_axis: the first (mid - lo) of it go left.
 
 __global__ __launch_bounds__(kBlock) void kd_axis_keys_kernel(const double *__restrict__ v, int n,
                                                               unsigned long long *__restrict__ key, int *__restrict__ val)
@@ -210,121 +211,146 @@ __global__ __launch_bounds__(kBlock) void kd_axis_keys_kernel(const double *__re
     }
 }
 
-__global__ __launch_bounds__(kBlock) void kd_rank_kernel(const int *__restrict__ sorted, int n, int *__restrict__ rank)
-{
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    if (k < n) rank[sorted[k]] = k;
-}
-
-// boxes of the active ranges: one workgroup per piece (range, begin, end) of <= kKdPiece points;
-// box = 3 min then 3 max ordered bits per range (initialised to ~0 / 0)
-constexpr int kKdPiece = 4096;
-__global__ __launch_bounds__(kBlock) void kd_box_init_kernel(unsigned long long *__restrict__ box, int nseg)
-{
-    const int k = blockIdx.x * kBlock + threadIdx.x;
-    if (k < 6 * nseg) box[k] = k % 6 < 3 ? ~0ull : 0ull;
-}
-
-__global__ __launch_bounds__(kBlock) void kd_box_kernel(const int *__restrict__ pieces, const int *__restrict__ perm,
-                                                        const double *__restrict__ x, const double *__restrict__ y,
-                                                        const double *__restrict__ z,
-                                                        unsigned long long *__restrict__ box)
-{
-    const int seg = pieces[3 * blockIdx.x], b = pieces[3 * blockIdx.x + 1], e = pieces[3 * blockIdx.x + 2];
-    unsigned long long lo[3] = {~0ull, ~0ull, ~0ull}, hi[3] = {0ull, 0ull, 0ull};
-    for (int pos = b + threadIdx.x; pos < e; pos += kBlock) {
-        const int id = perm ? perm[pos] : pos;
-        const unsigned long long k[3] = {ord_bits(x[id]), ord_bits(y[id]), ord_bits(z[id])};
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = min(lo[a], k[a]);
-            hi[a] = max(hi[a], k[a]);
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1)
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = min(lo[a], (unsigned long long)__shfl_xor((long long)lo[a], off, 64));
-            hi[a] = max(hi[a], (unsigned long long)__shfl_xor((long long)hi[a], off, 64));
-        }
-    __shared__ unsigned long long sh[kBlock / 64][6];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0)
-        for (int a = 0; a < 3; ++a) {
-            sh[wave][a] = lo[a];
-            sh[wave][3 + a] = hi[a];
-        }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        const int k = threadIdx.x;
-        unsigned long long v = sh[0][k];
-        for (int w = 1; w < kBlock / 64; ++w) v = k < 3 ? min(v, sh[w][k]) : max(v, sh[w][k]);
-        if (k < 3) atomicMin(box + 6 * (size_t)seg + k, v);
-        else atomicMax(box + 6 * (size_t)seg + k, v);
-    }
-}
-
 // the host rule's axis: the widest extent hi - lo, the first of equal ones
-__device__ __forceinline__ int widest_axis(const double lo[3], const double hi[3])
+__device__ __forceinline__ int widest_axis3(const double (&ext)[3])
 {
     int ax = 0;
     for (int a = 1; a < 3; ++a)
-        if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        if (ext[a] > ext[ax]) ax = a;
     return ax;
 }
 
-// sort keys of one global level: (range << rank_bits) | rank on the range's axis (active ranges)
-// or | the position within the range (ranges that no longer split here keep their order)
-__global__ __launch_bounds__(kBlock) void kd_level_keys_kernel(int n, const int *__restrict__ seg_lo,
-                                                               const int *__restrict__ seg_mid, int nseg,
-                                                               const unsigned long long *__restrict__ box,
-                                                               const int *__restrict__ rank, const int *__restrict__ perm,
-                                                               int rank_bits, unsigned long long *__restrict__ key,
-                                                               int *__restrict__ val)
+__device__ __forceinline__ int seg_of(const int *__restrict__ lo, int nseg, int pos) // last range with lo <= pos
 {
-    const int pos = blockIdx.x * kBlock + threadIdx.x;
-    if (pos >= n) return;
-    int l = 0, h = nseg - 1; // last range with lo <= pos
+    int l = 0, h = nseg - 1;
     while (l < h) {
         const int m = (l + h + 1) >> 1;
-        if (seg_lo[m] <= pos) l = m;
+        if (lo[m] <= pos) l = m;
         else h = m - 1;
     }
-    const int id = perm ? perm[pos] : pos;
-    unsigned long long low;
-    if (seg_mid[l] >= 0) {
-        double lo[3], hi[3];
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = ord_value(box[6 * (size_t)l + a]);
-            hi[a] = ord_value(box[6 * (size_t)l + 3 + a]);
-        }
-        low = (unsigned long long)rank[(size_t)widest_axis(lo, hi) * n + id];
-    } else {
-        low = (unsigned long long)(pos - seg_lo[l]);
-    }
-    key[pos] = ((unsigned long long)l << rank_bits) | low;
-    val[pos] = id;
+    return l;
 }
 
-// The 32-point splits of one range of at most 1,024 points, in LDS: per level each range of
-// more than 32 points takes its box (one wave per range), its axis, and its points' counting
-// ranks along it; the range [lo, hi) then splits at lo + 32 ceil(units / 2).
+struct KdLists {
+    const int *a[3];
+};
+
+// per active range: its axis (from the three lists' end points)
+__global__ __launch_bounds__(kBlock) void kd_range_axis_kernel(const int *__restrict__ seg_lo,
+                                                               const int *__restrict__ seg_mid, int nseg, int n,
+                                                               KdLists A, const double *__restrict__ x,
+                                                               const double *__restrict__ y,
+                                                               const double *__restrict__ z, int *__restrict__ axis)
+{
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= nseg || seg_mid[s] < 0) return;
+    const int lo = seg_lo[s], hi = s + 1 < nseg ? seg_lo[s + 1] : n;
+    const double *c[3] = {x, y, z};
+    double ext[3];
+    for (int a = 0; a < 3; ++a) ext[a] = c[a][A.a[a][hi - 1]] - c[a][A.a[a][lo]];
+    axis[s] = widest_axis3(ext);
+}
+
+// flag[id] = 1 for the left part of every active range (the first mid - lo of its axis list)
+__global__ __launch_bounds__(kBlock) void kd_flag_kernel(const int *__restrict__ seg_lo, const int *__restrict__ seg_mid,
+                                                         int nseg, int n, KdLists A, const int *__restrict__ axis,
+                                                         unsigned char *__restrict__ flag)
+{
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const int s = seg_of(seg_lo, nseg, p), mid = seg_mid[s];
+    if (mid < 0) return;
+    flag[A.a[axis[s]][p]] = p < mid ? 1 : 0;
+}
+
+// the scans' input: at position p, the flags of the three lists' points (no array: a transform
+// iterator over the positions, one exclusive scan of the three counts together)
+struct Cnt3 {
+    int c[3];
+};
+struct Cnt3Sum {
+    __host__ __device__ Cnt3 operator()(const Cnt3 &x, const Cnt3 &y) const
+    {
+        return Cnt3{{x.c[0] + y.c[0], x.c[1] + y.c[1], x.c[2] + y.c[2]}};
+    }
+};
+struct FlagsAt {
+    KdLists A;
+    const unsigned char *flag;
+    __host__ __device__ Cnt3 operator()(int p) const
+    {
+        return Cnt3{{(int)flag[A.a[0][p]], (int)flag[A.a[1][p]], (int)flag[A.a[2][p]]}};
+    }
+};
+
+inline auto flags_at(const FlagsAt &f)
+{
+    return rocprim::make_transform_iterator(rocprim::counting_iterator<int>(0), f);
+}
+
+// the stable partition of each list inside every active range (S: the exclusive scan of the
+// three flag counts)
+__global__ __launch_bounds__(kBlock) void kd_partition_kernel(const int *__restrict__ seg_lo,
+                                                              const int *__restrict__ seg_mid, int nseg, int n, KdLists A,
+                                                              const unsigned char *__restrict__ flag,
+                                                              const Cnt3 *__restrict__ S, int *__restrict__ d0,
+                                                              int *__restrict__ d1, int *__restrict__ d2)
+{
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const int s = seg_of(seg_lo, nseg, p), mid = seg_mid[s], lo = seg_lo[s];
+    int *d[3] = {d0, d1, d2};
+    const Cnt3 sp = S[p], sl = S[lo];
+    for (int a = 0; a < 3; ++a) {
+        const int id = A.a[a][p];
+        int dest = p;
+        if (mid >= 0) {
+            const int left_before = sp.c[a] - sl.c[a];
+            dest = flag[id] ? lo + left_before : mid + (p - lo - left_before);
+        }
+        d[a][dest] = id;
+    }
+}
+
+// loc[id] = the point's position in list x inside its leaf (the leaf kernel's local number)
+__global__ __launch_bounds__(kBlock) void kd_local_kernel(const int *__restrict__ leaf_lo, int nleaf, int n,
+                                                          const int *__restrict__ A0, int *__restrict__ loc)
+{
+    const int p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    loc[A0[p]] = p - leaf_lo[seg_of(leaf_lo, nleaf, p)];
+}
+
+// The 32-point splits of one leaf range (<= 1,024 points) in LDS: the three lists as local
+// numbers, each level's flags, and the partitions by block-wide exclusive scans.
 constexpr int kKdLeaf = 1024;
-__global__ __launch_bounds__(kBlock) void kd_leaf_kernel(const int *__restrict__ leaf_lo, const int *__restrict__ perm,
-                                                         const int *__restrict__ rank, int n, const double *__restrict__ x,
+__global__ __launch_bounds__(kBlock) void kd_leaf_kernel(const int *__restrict__ leaf_lo, KdLists A,
+                                                         const int *__restrict__ loc, const double *__restrict__ x,
                                                          const double *__restrict__ y, const double *__restrict__ z,
                                                          int *__restrict__ kd)
 {
-    __shared__ int s_id[2][kKdLeaf];
-    __shared__ int s_key[kKdLeaf];
-    __shared__ int s_rlo[kKdLeaf / 32 + 2], s_rhi[kKdLeaf / 32 + 2], s_rmid[kKdLeaf / 32 + 2], s_rax[kKdLeaf / 32 + 2];
+    constexpr int kMaxR = kKdLeaf / 32 + 2;
+    __shared__ int s_id[kKdLeaf];                 // local number -> point
+    __shared__ short s_A[2][3][kKdLeaf];          // the lists as local numbers (double-buffered)
+    __shared__ int s_S[3][kKdLeaf];               // exclusive scans of the flags along each list
+    __shared__ unsigned char s_flag[kKdLeaf];     // per local number
+    __shared__ int s_rlo[kMaxR], s_rhi[kMaxR], s_rmid[kMaxR], s_rax[kMaxR];
+    __shared__ int s_wsum[3][kBlock / 64];
     __shared__ int s_nr, s_active;
     const int L0 = leaf_lo[blockIdx.x], cnt = leaf_lo[blockIdx.x + 1] - L0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < cnt; i += kBlock) s_id[0][i] = perm ? perm[L0 + i] : L0 + i;
+    for (int i = tid; i < cnt; i += kBlock) {
+        s_id[i] = A.a[0][L0 + i];
+        s_A[0][0][i] = (short)i;
+        s_A[0][1][i] = (short)loc[A.a[1][L0 + i]];
+        s_A[0][2][i] = (short)loc[A.a[2][L0 + i]];
+    }
     if (tid == 0) {
         s_rlo[0] = 0;
         s_rhi[0] = cnt;
         s_nr = 1;
     }
+    const double *coord[3] = {x, y, z};
     int cur = 0;
     for (;;) {
         __syncthreads();
@@ -345,48 +371,73 @@ __global__ __launch_bounds__(kBlock) void kd_leaf_kernel(const int *__restrict__
         __syncthreads();
         if (!s_active) break;
         const int nr = s_nr;
-        for (int r = wave; r < nr; r += kBlock / 64) {
-            if (s_rmid[r] < 0) continue;
-            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (int i = s_rlo[r] + lane; i < s_rhi[r]; i += 64) {
-                const int id = s_id[cur][i];
-                const double v[3] = {x[id], y[id], z[id]};
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = fmin(lo[a], v[a]);
-                    hi[a] = fmax(hi[a], v[a]);
-                }
-            }
-            for (int off = 32; off > 0; off >>= 1)
-                for (int a = 0; a < 3; ++a) {
-                    lo[a] = fmin(lo[a], __shfl_xor(lo[a], off, 64));
-                    hi[a] = fmax(hi[a], __shfl_xor(hi[a], off, 64));
-                }
-            if (lane == 0) s_rax[r] = widest_axis(lo, hi);
+        if (tid < nr && s_rmid[tid] >= 0) {
+            const int lo = s_rlo[tid], hi = s_rhi[tid];
+            double ext[3];
+            for (int a = 0; a < 3; ++a)
+                ext[a] = coord[a][s_id[s_A[cur][a][hi - 1]]] - coord[a][s_id[s_A[cur][a][lo]]];
+            s_rax[tid] = widest_axis3(ext);
         }
         __syncthreads();
-        // each point's range: ranges are contiguous and sorted
-        for (int i = tid; i < cnt; i += kBlock) {
-            int r = 0;
-            while (s_rhi[r] <= i) ++r;
-            s_key[i] = s_rmid[r] >= 0 ? rank[(size_t)s_rax[r] * n + s_id[cur][i]] : 0;
+        auto range_of = [&](int p) {
+            int l = 0, h = nr - 1;
+            while (l < h) {
+                const int m = (l + h + 1) >> 1;
+                if (s_rlo[m] <= p) l = m;
+                else h = m - 1;
+            }
+            return l;
+        };
+        for (int p = tid; p < cnt; p += kBlock) {
+            const int r = range_of(p);
+            if (s_rmid[r] >= 0) s_flag[s_A[cur][s_rax[r]][p]] = p < s_rmid[r] ? 1 : 0;
         }
         __syncthreads();
-        for (int i = tid; i < cnt; i += kBlock) {
-            int r = 0;
-            while (s_rhi[r] <= i) ++r;
-            if (s_rmid[r] < 0) {
-                s_id[cur ^ 1][i] = s_id[cur][i];
-                continue;
+        // block-wide exclusive scans of the flags along each list: 4 consecutive positions a thread
+        int f[3][4], t[3];
+        for (int a = 0; a < 3; ++a) {
+            t[a] = 0;
+            for (int k = 0; k < 4; ++k) {
+                const int p = 4 * tid + k;
+                f[a][k] = p < cnt ? s_flag[s_A[cur][a][p]] : 0;
+                t[a] += f[a][k];
             }
-            const int k = s_key[i], lo = s_rlo[r], hi = s_rhi[r];
-            int c = 0;
-            for (int f = lo; f < hi; ++f) c += s_key[f] < k ? 1 : 0;
-            s_id[cur ^ 1][lo + c] = s_id[cur][i];
+        }
+        int incl[3] = {t[0], t[1], t[2]};
+        for (int o = 1; o < 64; o <<= 1)
+            for (int a = 0; a < 3; ++a) {
+                const int v = __shfl_up(incl[a], o, 64);
+                if (lane >= o) incl[a] += v;
+            }
+        if (lane == 63)
+            for (int a = 0; a < 3; ++a) s_wsum[a][wave] = incl[a];
+        __syncthreads();
+        for (int a = 0; a < 3; ++a) {
+            int base = incl[a] - t[a];
+            for (int w = 0; w < wave; ++w) base += s_wsum[a][w];
+            for (int k = 0; k < 4; ++k) {
+                const int p = 4 * tid + k;
+                if (p < cnt) s_S[a][p] = base;
+                base += f[a][k];
+            }
+        }
+        __syncthreads();
+        for (int p = tid; p < cnt; p += kBlock) {
+            const int r = range_of(p), mid = s_rmid[r], lo = s_rlo[r];
+            for (int a = 0; a < 3; ++a) {
+                const short v = s_A[cur][a][p];
+                int dest = p;
+                if (mid >= 0) {
+                    const int left_before = s_S[a][p] - s_S[a][lo];
+                    dest = s_flag[v] ? lo + left_before : mid + (p - lo - left_before);
+                }
+                s_A[cur ^ 1][a][dest] = v;
+            }
         }
         __syncthreads();
         if (tid == 0) { // the next level's ranges
             int m = 0;
-            int nlo[kKdLeaf / 32 + 2], nhi[kKdLeaf / 32 + 2];
+            int nlo[kMaxR], nhi[kMaxR];
             for (int r = 0; r < s_nr; ++r) {
                 if (s_rmid[r] >= 0) {
                     nlo[m] = s_rlo[r];
@@ -406,14 +457,7 @@ __global__ __launch_bounds__(kBlock) void kd_leaf_kernel(const int *__restrict__
         }
         cur ^= 1;
     }
-    for (int i = tid; i < cnt; i += kBlock) kd[L0 + i] = s_id[cur][i];
-}
-
-int bits_for(size_t v) // bits to hold values 0 .. v - 1
-{
-    int b = 0;
-    while (b < 63 && ((size_t)1 << b) < v) ++b;
-    return std::max(b, 1);
+    for (int i = tid; i < cnt; i += kBlock) kd[L0 + i] = s_id[s_A[cur][0][i]];
 }
 
 } // namespace
@@ -425,13 +469,13 @@ size_t model_stats_scratch_doubles() { return (size_t)kStatBlocks * 10 + 16; }
 void launch_model_stats(const double *aos, int n, double *scratch, double *out, hipStream_t st)
 {
     model_stats_kernel<<<kStatBlocks, kBlock, 0, st>>>(aos, n, scratch);
-    stats_fold_kernel<10><<<1, kBlock, 0, st>>>(scratch, kStatBlocks, nullptr, out);
+    stats_fold_kernel<10><<<1, kBlock, 0, st>>>(scratch, kStatBlocks, out);
 }
 
 void launch_model_range(const double *aos, int n, const double c[3], double *scratch, double *out, hipStream_t st)
 {
     model_range_kernel<<<kStatBlocks, kBlock, 0, st>>>(aos, n, c[0], c[1], c[2], scratch);
-    stats_fold_kernel<3><<<1, kBlock, 0, st>>>(scratch, kStatBlocks, nullptr, out);
+    stats_fold_kernel<3><<<1, kBlock, 0, st>>>(scratch, kStatBlocks, out);
 }
 
 void launch_model_f32_images(const double *aos, int nm, int nm_pad, const double c[3], float4 *m32, float *mperm,
@@ -472,18 +516,6 @@ void kd_plan(size_t nm, KdPlan &pl)
         pl.ints.insert(pl.ints.end(), lo.begin(), lo.end());
         L.mid_off = (int)pl.ints.size();
         pl.ints.insert(pl.ints.end(), mid.begin(), mid.end());
-        L.piece_off = (int)pl.ints.size();
-        L.npieces = 0;
-        for (size_t s = 0; s < lo.size(); ++s) {
-            if (mid[s] < 0) continue;
-            for (int b = lo[s]; b < hi[s]; b += kKdPiece) {
-                pl.ints.push_back((int)s);
-                pl.ints.push_back(b);
-                pl.ints.push_back(std::min(hi[s], b + kKdPiece));
-                ++L.npieces;
-            }
-        }
-        L.seg_bits = bits_for(lo.size());
         pl.levels.push_back(L);
         std::vector<int> nlo, nhi;
         for (size_t s = 0; s < lo.size(); ++s) {
@@ -506,19 +538,63 @@ void kd_plan(size_t nm, KdPlan &pl)
     pl.ints.push_back((int)nm);
     pl.max_seg = 1;
     for (const auto &L : pl.levels) pl.max_seg = std::max(pl.max_seg, L.nseg);
-    pl.rank_bits = bits_for(nm);
 }
+
+namespace {
+struct KdScratch { // carve of the kd builder's scratch
+    unsigned long long *k0, *k1;
+    int *A[2][3], *axis, *loc, *plan;
+    Cnt3 *S;
+    unsigned char *flag;
+    void *temp;
+    size_t temp_bytes, used;
+};
+
+size_t scan_temp_bytes(int n)
+{
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const unsigned long long *)nullptr,
+                                             (unsigned long long *)nullptr, (const int *)nullptr, (int *)nullptr, n, 0,
+                                             64);
+    (void)rocprim::exclusive_scan(nullptr, b, flags_at(FlagsAt{}), (Cnt3 *)nullptr, Cnt3{{0, 0, 0}}, (size_t)n,
+                                  Cnt3Sum{});
+    return std::max(a, b);
+}
+
+KdScratch kd_carve(const KdPlan &pl, void *base)
+{
+    const size_t n = (size_t)std::max(pl.nm, 1);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    KdScratch k{};
+    char *p = (char *)base;
+    k.k0 = (unsigned long long *)p;
+    k.k1 = k.k0 + n;
+    p += al(2 * n * sizeof(unsigned long long));
+    for (int b = 0; b < 2; ++b)
+        for (int a = 0; a < 3; ++a) {
+            k.A[b][a] = (int *)p;
+            p += al(n * sizeof(int));
+        }
+    k.S = (Cnt3 *)p;
+    p += al(n * sizeof(Cnt3));
+    k.axis = (int *)p;
+    p += al((size_t)pl.max_seg * sizeof(int));
+    k.loc = (int *)p;
+    p += al(n * sizeof(int));
+    k.plan = (int *)p;
+    p += al(pl.ints.size() * sizeof(int));
+    k.flag = (unsigned char *)p;
+    p += al(n);
+    k.temp = p;
+    k.used = (size_t)(p - (char *)base);
+    return k;
+}
+} // namespace
 
 size_t kd_order_scratch_bytes(const KdPlan &pl)
 {
-    const size_t n = (size_t)std::max(pl.nm, 1);
-    size_t temp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned long long *)nullptr,
-                                             (unsigned long long *)nullptr, (const int *)nullptr, (int *)nullptr,
-                                             (int)n, 0, 64);
-    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    return al(2 * n * sizeof(unsigned long long)) + al(2 * n * sizeof(int)) + al(3 * n * sizeof(int)) +
-           al((size_t)pl.max_seg * 6 * sizeof(unsigned long long)) + al(pl.ints.size() * sizeof(int)) + al(temp);
+    const KdScratch k = kd_carve(pl, nullptr);
+    return k.used + ((scan_temp_bytes(std::max(pl.nm, 1)) + 255) & ~(size_t)255);
 }
 
 int launch_kd_order(const double *mx, const double *my, const double *mz, const KdPlan &pl, void *scratch,
@@ -526,45 +602,38 @@ int launch_kd_order(const double *mx, const double *my, const double *mz, const 
 {
     const int n = pl.nm;
     if (n <= 0) return 0;
-    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    char *p = (char *)scratch;
-    unsigned long long *k0 = (unsigned long long *)p, *k1 = k0 + n;
-    p += al(2 * (size_t)n * sizeof(unsigned long long));
-    int *v0 = (int *)p, *v1 = v0 + n;
-    p += al(2 * (size_t)n * sizeof(int));
-    int *rank = (int *)p;
-    p += al(3 * (size_t)n * sizeof(int));
-    unsigned long long *box = (unsigned long long *)p;
-    p += al((size_t)pl.max_seg * 6 * sizeof(unsigned long long));
-    int *plan = (int *)p;
-    p += al(pl.ints.size() * sizeof(int));
-    void *temp = p;
-    const size_t used = (size_t)(p - (char *)scratch);
-    if (used > bytes) return -1;
-    size_t temp_bytes = bytes - used;
+    KdScratch k = kd_carve(pl, scratch);
+    if (k.used > bytes) return -1;
+    k.temp_bytes = bytes - k.used;
     // (the plan is a caller-owned vector that outlives the stream's copy: KdPlan::ints)
-    if (hipMemcpyAsync(plan, pl.ints.data(), pl.ints.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess)
+    if (hipMemcpyAsync(k.plan, pl.ints.data(), pl.ints.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess)
         return -1;
     const int g = (n + kBlock - 1) / kBlock;
     const double *axes[3] = {mx, my, mz};
-    for (int a = 0; a < 3; ++a) { // rank of every point along each axis, (coordinate, index) order
-        kd_axis_keys_kernel<<<g, kBlock, 0, st>>>(axes[a], n, k0, v0);
-        if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, v1, n, 0, 64, st) != hipSuccess)
-            return -1;
-        kd_rank_kernel<<<g, kBlock, 0, st>>>(v1, n, rank + (size_t)a * n);
-    }
-    const int *perm = nullptr; // (identity before the first level)
-    for (const KdPlan::Level &L : pl.levels) {
-        kd_box_init_kernel<<<(6 * L.nseg + kBlock - 1) / kBlock, kBlock, 0, st>>>(box, L.nseg);
-        kd_box_kernel<<<L.npieces, kBlock, 0, st>>>(plan + L.piece_off, perm, mx, my, mz, box);
-        kd_level_keys_kernel<<<g, kBlock, 0, st>>>(n, plan + L.seg_off, plan + L.mid_off, L.nseg, box, rank, perm,
-                                                   pl.rank_bits, k0, v0);
-        if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, v1, n, 0, pl.rank_bits + L.seg_bits, st) !=
+    int *ids = k.A[1][0]; // (the identity order, sorted three times)
+    for (int a = 0; a < 3; ++a) { // list a: the points in (coordinate a, index) order
+        kd_axis_keys_kernel<<<g, kBlock, 0, st>>>(axes[a], n, k.k0, ids);
+        if (hipcub::DeviceRadixSort::SortPairs(k.temp, k.temp_bytes, k.k0, k.k1, ids, k.A[0][a], n, 0, 64, st) !=
             hipSuccess)
             return -1;
-        perm = v1;
     }
-    kd_leaf_kernel<<<pl.nleaf, kBlock, 0, st>>>(plan + pl.leaf_off, perm, rank, n, mx, my, mz, kd);
+    int cur = 0;
+    for (const KdPlan::Level &L : pl.levels) {
+        const KdLists A{{k.A[cur][0], k.A[cur][1], k.A[cur][2]}};
+        const int *lo = k.plan + L.seg_off, *mid = k.plan + L.mid_off;
+        kd_range_axis_kernel<<<(L.nseg + kBlock - 1) / kBlock, kBlock, 0, st>>>(lo, mid, L.nseg, n, A, mx, my, mz,
+                                                                               k.axis);
+        kd_flag_kernel<<<g, kBlock, 0, st>>>(lo, mid, L.nseg, n, A, k.axis, k.flag);
+        if (rocprim::exclusive_scan(k.temp, k.temp_bytes, flags_at(FlagsAt{A, k.flag}), k.S, Cnt3{{0, 0, 0}}, (size_t)n,
+                                    Cnt3Sum{}, st) != hipSuccess)
+            return -1;
+        kd_partition_kernel<<<g, kBlock, 0, st>>>(lo, mid, L.nseg, n, A, k.flag, k.S, k.A[cur ^ 1][0], k.A[cur ^ 1][1],
+                                                  k.A[cur ^ 1][2]);
+        cur ^= 1;
+    }
+    const KdLists A{{k.A[cur][0], k.A[cur][1], k.A[cur][2]}};
+    kd_local_kernel<<<g, kBlock, 0, st>>>(k.plan + pl.leaf_off, pl.nleaf, n, A.a[0], k.loc);
+    kd_leaf_kernel<<<pl.nleaf, kBlock, 0, st>>>(k.plan + pl.leaf_off, A, k.loc, mx, my, mz, kd);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
