@@ -216,6 +216,26 @@ def bundle_roofline(n_local, n_model, t_kernel, work, v1=False):
             "pairs_per_s": n_local * n_model / t_kernel}
 
 
+def grid_roofline(n_local, n_model, avg_ms, traffic, traffic_src, explicit_variant):
+    """The seeded grid search's pass over every query (nn_grid_resolve_kernel<4, false>, all-mode:
+    the dominant kernel of an AUTO iteration once icp_run's policy takes the grid) against HBM.
+    Algorithmic bytes per launch: per query its fp64 position (24 B), seed distance (8 B), index
+    in and out (8 B) and kd position out (4 B); per model point its 32-byte grid record and ~2 B
+    of the cell table, each once."""
+    gbytes = 44.0 * n_local + 34.0 * n_model
+    t = avg_ms * 1e-3
+    ach = gbytes / t / 1e9 if t > 0 else 0.0
+    return {"bound": "hbm", "kernel": "nn_grid_resolve_kernel<4, false> (seeded, every query)",
+            "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
+            "traffic": traffic, "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src, "avg_launch_ms": avg_ms, "bytes_per_launch": gbytes,
+            "bytes_definition": "algorithmic: 44 B per query (fp64 xyz, seed distance, index in/out, kd "
+                                "position out) + 34 B per model point (32-byte grid record + cell table), once",
+            "path": "ICP_NN_VARIANT_GRID" if explicit_variant else
+                    "AUTO: icp_run's policy (seeded iterations once the scene is near the model)",
+            "note": "latency-bound gather: each query walks the grid rows of its box (dependent loads)"}
+
+
 def full_nxm_rate(device, m, p, steps=5, warmup=2):
     """The full N x M f16 filter (ICP_NN_VARIANT_MFMA16, nn_mfma16r_kernel<8>) on the same C4
     iterations, for comparison with the bundle filter: same results bit for bit."""
@@ -561,10 +581,11 @@ def main():
     kernel = {"mfma16": k16, "mfma": "nn_mfma_kernel",
               "bundle": "nn_bundle_kernel" if bundle_v1() else "nn_bundle2_kernel"}.get(
         level1, "nn_fp64_kernel" if args.nn == "fp64" else "nn_filter_kernel")
-    if args.variant == "grid":
+    if level1 == "grid":
         # timed iterations are seeded (warm-up leaves every query a correspondence): the seeded
-        # resolve (launch_nn_grid_resolve_all) scans each query's complete candidate box
-        kernel = "nn_grid_resolve_kernel"
+        # resolve (launch_nn_grid_resolve_all) scans each query's complete candidate box; AUTO
+        # takes it by icp_run's policy once the scene is near the model
+        kernel = "nn_grid_resolve_kernel<4>"
     traffic, traffic_src = pmc_traffic(kernel) if world == 1 and args.n == 1 << 20 else (None, None)
     nn_s = nn_avg_ms * 1e-3
     compulsory = 16.0 * c + 12.0 * args.n  # §8d: fp32 xyz in (scene shard + model), int32 index out
@@ -656,17 +677,12 @@ def main():
                 out["streaming"] = {"source": f"profiles/{rf['tag']}_bench_kernel_stats.csv + "
                                               f"profiles/{rf['tag']}_pmc_traffic.json (tools/roofline.py)",
                                     "kernels": {k: v for k, v in rf["kernels"].items() if k in keep}}
-        if args.variant == "grid":
-            # no brute-force filter: the seeded resolve reads each query (24 B) and its previous
-            # correspondence (4 B, rewritten in place) and scans the model's 32-byte grid records
-            # in the query's candidate box; algorithmic bytes = 28 per query + the records once
-            gbytes = 28.0 * c + 32.0 * args.n
-            ach = gbytes / (nn_avg_ms * 1e-3) / 1e9 if nn_avg_ms > 0 else 0.0
-            out["roofline"] = {"bound": "hbm", "kernel": kernel, "achieved": ach, "peak": 8000.0,
-                               "unit": "GB/s", "frac": ach / 8000.0, "traffic": None,
-                               "avg_launch_ms": nn_avg_ms, "bytes_per_launch": gbytes,
-                               "note": "latency-bound gather search; compulsory bytes only"}
-            out["dtype"] = "f64"
+        if level1 == "grid":
+            out["roofline"] = grid_roofline(c, args.n, nn_avg_ms, traffic, traffic_src, args.variant == "grid")
+            out["dtype"] = ("f64 (exact grid search of every query)" if args.variant == "grid" else
+                            "f64 exact grid search in the seeded iterations (icp_run's policy); the first searches: "
+                            "f16 hi/lo-split MFMA bundle bound + pair filter (fp32 accumulate) with the fp64 "
+                            "certificate; fp64 reductions")
         if world == 1 and not args.no_cow:
             out["cow_frame_rate"] = cow_frame_rate(local)
         if world == 1 and not args.no_cases:

@@ -571,6 +571,28 @@ static int grid_budget(const icp_ctx *ctx)
     return (int)std::min<size_t>(std::max<size_t>(kGridBudget, ctx->nm / 4), (size_t)1 << 16);
 }
 
+// icp_run's search policy for AUTO at the bundle filter's sizes (run_loop); ICP_GRID_AUTO=0 keeps
+// every seeded search on the bundle cascade (A/B)
+static bool grid_auto()
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_GRID_AUTO");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+// the seeded grid search of a sparse scene in slot order, each XCD on a contiguous eighth of it
+// (launch_nn_grid_resolve_all); ICP_GRID_XCD=0: the plain block order (A/B)
+static bool grid_xcd()
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_GRID_XCD");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 // The bundle filter's processing order of the n queries in q (a Morton order over the model's
 // box, launch_query_order): computed once per cloud -- an icp_run's scene moves rigidly, so its
 // first order stays spatially coherent -- and again after set_scene / closest_matrix uploads.
@@ -646,6 +668,46 @@ static int scene_to_slot_order(icp_ctx *ctx)
 
 constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger model: nn_resolve, 256 per query)
 
+// The seeded grid search of a scene stored in slot order: every query walks the complete box
+// around its seed (the previous correspondence) with a few lanes, if it has at most kSeededBox
+// cells; the queries with a bigger box go to the resolver with a whole wave each (flattened scan,
+// loads in flight: a big box is one query's long chain of dependent loads in the first pass),
+// and what is over the cell budget to the fp64 brute force.  Every level returns the exact first
+// minimum.  kpos is kept when the bundle's kd tables exist (the moments then gather from the
+// kd-ordered model).
+constexpr int kSeededBox = 125;
+static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop, const double *seedd,
+                              hipEvent_t ev1)
+{
+    const int inline_nm = ctx->nm <= kInlineFallbackModel ? (int)ctx->nm : 0;
+    TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
+    TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
+    TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
+    TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
+    int *kpos_out = nullptr;
+    if (ctx->nn_rule == ICP_NN_RULE_SQUARED && ctx->m4kd && ctx->kd_of) {
+        TRY(grow(ctx, &ctx->kpos, &ctx->kpos_cap, n));
+        kpos_out = ctx->kpos;
+    }
+    // (an XCD a contiguous eighth of the slot order: measured faster for sparse shards, slower
+    // for a whole scene -- C4 W = 8 shard 36.8 against 41.5 us, W = 1 140 against 126 us, r04k)
+    launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), kSeededBox, ctx->idx,
+                               ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0,
+                               grid_xcd() && 4 * n <= ctx->nm, ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, kpos_out,
+                               ctx->kd_of, seedd);
+    if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st)); // (the timed kernel: the pass over every query)
+    launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
+                           grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
+                           ctx->fb_T, ctx->st, stop, inline_nm, kpos_out, ctx->kd_of, 64);
+    if (!inline_nm)
+        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32, ctx->model.x,
+                          ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st, stop, kpos_out,
+                          ctx->kd_of);
+    LAUNCHCHK("grid_seeded_search");
+    ctx->kpos_valid = kpos_out != nullptr;
+    return ICP_OK;
+}
+
 // Launches the complete NN search of the n queries in q against the resident model ->
 // ctx->idx, with no host synchronisation: every level is sized on the device.  Queue sizes:
 // amb_count [0] queue of the VALU certificate, [1] grid -> fp64 brute-force fallback,
@@ -654,7 +716,7 @@ constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger mod
 // zero_counts = false: amb_count is already zero (icp_run: horn_step clears it)
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
                     bool zero_counts = true, bool seeds_ready = false, const int *stop = nullptr,
-                    bool slot_order = false, bool records_ready = false)
+                    bool slot_order = false, bool records_ready = false, bool grid_seeded = false)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     ctx->kpos_valid = false;
@@ -678,6 +740,14 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
         launch_nn_finalize64(pb, pi, pl.splits, (int)n, ctx->idx, ctx->st, stop);
         LAUNCHCHK("nn_fp64");
+    } else if (seeded && slot_order && (grid_seeded || ctx->nn_variant == ICP_NN_VARIANT_GRID)) {
+        // (icp_run's seeded search of a scene in slot order; AUTO takes it by icp_run's policy,
+        // run_loop)
+        ctx->stats.last_filter = ICP_FILTER_GRID;
+        if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
+        // (the policy's searches: the last transform wrote each point's seed distance)
+        TRY(grid_seeded_search(ctx, q, n, stop, grid_seeded && ctx->b_seedd ? ctx->b_seedd : nullptr, ev1));
+        return ICP_OK;
     } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
         // exact grid search for every query; over-budget boxes -> fp64 brute force per query
         ctx->stats.last_filter = ICP_FILTER_GRID;
@@ -686,7 +756,8 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
         if (seeded) // (icp_run: the previous correspondence is each query's candidate; no ring search)
             launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), grid_budget(ctx), ctx->idx,
-                                       ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop);
+                                       ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0,
+                                       slot_order && grid_xcd());
         else
             launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx,
                                   ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st);
@@ -1884,6 +1955,26 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }
     if (want_slot_order(ctx, n)) TRY(scene_to_slot_order(ctx));
     const int *digest_order = ctx->scene_slot ? ctx->s_order : nullptr;
+    // The search policy of AUTO at the bundle filter's sizes (the scene in slot order): a seeded
+    // search takes the grid (grid_seeded_search) instead of the bundle cascade when the last
+    // transform the host has seen left at most n/32 points farther than 1.5 grid cells from their
+    // correspondence (the queries whose box exceeds kSeededBox cells: the second, per-wave pass).  The decision for
+    // iteration k + 1 is taken when k is enqueued (k's transform writes the bundle's records and
+    // seeds only if k + 1 is a bundle search), on the count of an iteration one or two behind;
+    // the first two searches are the bundle cascade's.  Both paths return the exact first
+    // minimum, so the trajectory is the same whichever runs.  ICP_GRID_AUTO=0: always the bundle.
+    const bool grid_policy = ctx->scene_slot && ctx->nn_mode == ICP_NN_CERTIFIED &&
+                             ctx->nn_variant == ICP_NN_VARIANT_AUTO && level1_kind(ctx, n) == 3 && grid_auto();
+    const int far_thr = std::max(16, (int)(n >> 5));
+    bool grid_next = false; // the path of the search after the one being enqueued
+    int far_obs = -1;       // far_acc of the last iteration the host has seen
+    SeedArgs sa_grid;       // a transform before a grid search: its seed distances only
+    if (grid_policy) {
+        const double h = 1.0 / ctx->grid.inv_h;
+        sa.far_acc = sa_grid.far_acc = &ctx->iter_state->far_acc;
+        sa.far_d2 = sa_grid.far_d2 = 2.25 * h * h;
+        sa_grid.seedd = sa.seedd; // (grid_seeded_search reads them: no gather of the seed point)
+    }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     // mid-size single-rank runs: iterations >= 2 end in ONE fused launch (moments ... error step)
     static const int forced_mode = [] {
@@ -1955,10 +2046,13 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == timing_phase;
+            const bool grid_cur = enqueued > 0 && grid_next; // (decided with the previous transform)
+            grid_next = grid_policy && enqueued >= 1 && far_obs >= 0 && far_obs <= far_thr;
             // (the search of an iteration queued behind the converged one returns at once)
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
-                                timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, fuse_seeds && enqueued > 0,
-                                &sd->done, ctx->scene_slot, sa.qop && enqueued > 0)); // (run_init zeroed the counters)
+                                timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false,
+                                fuse_seeds && enqueued > 0 && !grid_cur, &sd->done, ctx->scene_slot,
+                                sa.qop && enqueued > 0 && !grid_cur, grid_cur)); // (run_init zeroed the counters)
             if (enqueued == 0 && sa.seedd && ctx->scene_slot && transform_records) {
                 // a scene in slot order: from here on each transform writes the next search's
                 // slot records and group bounds in order (the first search sized the buffers;
@@ -2072,7 +2166,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             if (!horn_fused) launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
             launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, need_p32 ? P.f : nullptr,
-                                     red_target(ctx, n, ctx->sums + kSumErr), sa, ctx->st);
+                                     red_target(ctx, n, ctx->sums + kSumErr), grid_next ? sa_grid : sa, ctx->st);
             if (!need_p32) ctx->p32_stale = true;
             const bool fold_err = !lag && red_blocks(n) > 1; // (folded by the error step's launch)
             if (!fold_err) red_finish(ctx, n, 1, ctx->sums + kSumErr);
@@ -2093,6 +2187,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             return wr;
         }
         ++waited;
+        if (grid_policy) { // (mirrored by the error step of that iteration)
+            far_obs = ctx->h_iter->far_acc;
+            static const bool dbg = getenv("ICP_DEBUG_POLICY") != nullptr;
+            if (dbg) fprintf(stderr, "[policy] waited %d far %d thr %d next_grid %d\n", waited, far_obs, far_thr, (int)grid_next);
+        }
         const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;

@@ -207,13 +207,52 @@ __device__ __forceinline__ void scan_box_flat(const double q[3], const int c0[3]
     }
 }
 
+// scan_box with the loads batched: a lane first reads the (start, end) of up to kR of its rows
+// together, then walks each run kU points at a time with their loads in flight together (the
+// same points, so the same (D64, index) minimum): the per-query chain of dependent loads -- the
+// seeded resolver is latency-bound -- falls from ~1 per point to ~1 per kU points
+template <int G>
+__device__ __forceinline__ void scan_box_batched(const double q[3], const int c0[3], const int c1[3],
+                                                 const GridView &gv, int sub, double &best, int &bi)
+{
+    constexpr int kR = 8, kU = 4;
+    const int ny = c1[1] - c0[1] + 1;
+    const int nrows = ny * (c1[2] - c0[2] + 1);
+    for (int r0 = sub; r0 < nrows; r0 += kR * G) {
+        int k0[kR], k1[kR];
+#pragma unroll
+        for (int u = 0; u < kR; ++u) {
+            const int r = r0 + u * G;
+            k0[u] = 0;
+            k1[u] = 0;
+            if (r < nrows) {
+                const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                const int row = (cz * gv.g[1] + cy) * gv.g[0];
+                k0[u] = gv.start[row + c0[0]];
+                k1[u] = gv.start[row + c1[0] + 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kR; ++u)
+            for (int k = k0[u]; k < k1[u]; k += kU) {
+                double4 m[kU];
+#pragma unroll
+                for (int v = 0; v < kU; ++v)
+                    if (k + v < k1[u]) m[v] = gv.pts[k + v];
+#pragma unroll
+                for (int v = 0; v < kU; ++v)
+                    if (k + v < k1[u]) lex_min(best, bi, d64g(q[0], q[1], q[2], m[v].x, m[v].y, m[v].z), (int)m[v].w);
+            }
+    }
+}
+
 // resolver box scan: flattened (default) or one x-run per lane (ICP_GRID_SCAN=rows, for A/B)
 template <int G, bool FLAT>
 __device__ __forceinline__ void scan_box_sel(const double q[3], const int c0[3], const int c1[3],
                                              const GridView &gv, int sub, double &best, int &bi)
 {
     if constexpr (FLAT) scan_box_flat<G>(q, c0, c1, gv, sub, best, bi);
-    else scan_box<G>(q, c0, c1, gv, sub, best, bi);
+    else scan_box_batched<G>(q, c0, c1, gv, sub, best, bi);
 }
 
 template <int G = kGroup> __device__ __forceinline__ void group_lex_min(double &best, int &bi)
@@ -250,8 +289,14 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count,
     int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out, const int *__restrict__ stop,
-    int inline_nm, int n_all, int *__restrict__ kpos, const int *__restrict__ kd_of)
+    int inline_nm, int n_all, int *__restrict__ kpos, const int *__restrict__ kd_of, int xcd_remap,
+    int *far_count, int *__restrict__ far_list, int *__restrict__ far_hint, const double *__restrict__ seedd)
 {
+    // seedd (all-mode, nullable): each query's seed distance D64(q, m[idx]) as the last transform
+    // computed it (the same arithmetic on the same values): no dependent gather of the seed point
+    // far_count (all-mode, nullable): a query whose box exceeds `budget` is queued with its seed
+    // as the hint (far_list, far_hint) for a second pass with a whole wave per query and a
+    // larger budget, instead of the brute force
     // (kpos, nullable: the resolved queries' kd positions, kd_of[index], next to idx)
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     // list == nullptr: every query t = 0 .. n_all-1, its candidate the previous correspondence
@@ -259,7 +304,12 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const int count = list ? *count_ptr : n_all;
     const int sub = threadIdx.x & (G - 1);
     const int groups = gridDim.x * (kBlock / G);
-    for (int t = (blockIdx.x * kBlock + threadIdx.x) / G; t < count; t += groups) {
+    // xcd_remap (every query of a scene in slot order): workgroup b takes block (b % 8) * (B / 8) +
+    // b / 8 of the queries, so that the round-robin dispatch hands each XCD -- its own L2 -- a
+    // contiguous eighth of the slot (Morton) order: one region of space instead of all of it
+    const int bx = xcd_remap && (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                                     : blockIdx.x;
+    for (int t = (bx * kBlock + threadIdx.x) / G; t < count; t += groups) {
         const int j = list ? list[t] : t;
         const int h = list ? hint[t] : idx[t];
         bool ok = h >= 0;
@@ -268,8 +318,12 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
         double best = 0.0;
         int bi = h;
         if (ok) {
-            const double4 mh = m4[h];
-            best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
+            if (seedd && !list) {
+                best = seedd[t];
+            } else {
+                const double4 mh = m4[h];
+                best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
+            }
             // a non-finite seed distance (a NaN / inf query) bounds no box: such a query goes
             // to the brute-force levels and their first-minimum rule (index 0 for NaN)
             ok = best == best && best < INFINITY && complete_box(q, best, gv, budget, c0, c1);
@@ -281,6 +335,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
                 idx[j] = bi;
                 if (kpos) kpos[j] = kd_of[bi];
             }
+        } else if (far_count) { // (uniform per group: handed on below)
         } else if (inline_nm > 0) { // small model: the exact fp64 scan of every point, right here
             best = INFINITY;
             bi = -1;
@@ -294,8 +349,14 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
                 if (kpos) kpos[j] = kd_of[bi < 0 ? 0 : bi];
             } // (no comparison held: a NaN query -> index 0)
         }
+        const bool far = far_count && !ok && sub == 0;
+        const int fs = wave_append(far_count ? far_count : fb_count, far);
+        if (far) {
+            far_list[fs] = j;
+            far_hint[fs] = h;
+        }
         // queue for nn_resolve -- or, scanned inline, only counted (the fallback statistic)
-        const bool fb = !ok && sub == 0;
+        const bool fb = !far_count && !ok && sub == 0;
         const int slot = wave_append(fb_count, fb);
         if (fb && inline_nm == 0) {
             fb_list[slot] = j;
@@ -522,7 +583,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st, const int *stop, int inline_nm,
-                            int *kpos, const int *kd_of)
+                            int *kpos, const int *kd_of, int group)
 {
     // lanes per queued query, measured: a whole wave for searches of 8,192 to 2^18 queries (horse /
     // bunny surfaces: big boxes of dense surface cells; 64 lanes 4,289 vs 16 lanes 3,231 it/s
@@ -532,7 +593,9 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
         const char *e = getenv("ICP_GRID_RGROUP");
         return e ? atoi(e) : 0;
     }();
-    const int g = forced == 4 || forced == 16 || forced == 64 ? forced : (max_items >= 8192 && max_items < (1 << 18) ? 64 : 16);
+    const int g = forced == 4 || forced == 16 || forced == 64 ? forced
+                  : group == 4 || group == 16 || group == 64 ? group
+                                                             : (max_items >= 8192 && max_items < (1 << 18) ? 64 : 16);
     const int per_block = kBlock / g;
     // (a grid-stride over the device-side count: the cap bounds the launch when the queue is a
     // small share of max_items; ICP_GRID_RBLOCKS overrides it for A/B)
@@ -544,7 +607,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
 #define RESOLVE(GG, F)                                                                                  \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx, \
                                                              fb_count, fb_list, T_in, T_out, stop, inline_nm, 0, \
-                                                             kpos, kd_of)
+                                                             kpos, kd_of, 0, nullptr, nullptr, nullptr, nullptr)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE(4, true);
         else if (g == 64) RESOLVE(64, true);
@@ -559,7 +622,8 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
 
 void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const double *pz, const double4 *m4,
                                 const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list, double *fb_T,
-                                hipStream_t st, const int *stop, int inline_nm)
+                                hipStream_t st, const int *stop, int inline_nm, bool xcd_remap, int *far_count,
+                                int *far_list, int *far_hint, int *kpos, const int *kd_of, const double *seedd)
 {
     // lanes per query as the unseeded search (launch_nn_grid_search): many queries a few lanes
     // each, few queries 16 lanes each; ICP_GRID_GROUP overrides (4 | 16)
@@ -569,11 +633,13 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
     }();
     const int g = forced == 4 || forced == 16 ? forced : (n >= (1 << 16) ? 4 : 16);
     const int per_block = kBlock / g;
-    const int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
+    int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
+    if (xcd_remap) blocks = (blocks + 7) / 8 * 8; // (whole eighths; the extra workgroups find no query)
 #define RESOLVE_ALL(GG, F)                                                                                       \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(nullptr, nullptr, nullptr, px, py, pz, m4, gv, budget, \
                                                              idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n, \
-                                                             nullptr, nullptr)
+                                                             kpos, kd_of, xcd_remap ? 1 : 0, far_count, far_list, far_hint, \
+                                                             seedd)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE_ALL(4, true);
         else RESOLVE_ALL(16, true);

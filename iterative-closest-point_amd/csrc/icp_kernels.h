@@ -295,14 +295,21 @@ void launch_nn_grid_seed(int np, const double *px, const double *py, const doubl
 // exactly in place (no fallback queue, no nn_resolve launch)
 // seeded grid variant: every query's previous correspondence (idx[t]) as the candidate, its
 // complete box scanned (no ring search); idx is overwritten with the exact answer
+// xcd_remap (a scene stored in slot order): each XCD takes a contiguous eighth of the queries;
+// far_count (nullable): a box over `budget` goes to (far_list, far_hint = its seed) for
+// launch_nn_grid_resolve instead of fb_list; kpos (nullable) = kd_of[idx] of the answered queries;
+// seedd (nullable): each query's seed distance D64(p_t, m[idx_t]) (SeedArgs::seedd, the transform's)
 void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const double *pz, const double4 *m4,
                                 const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list, double *fb_T,
-                                hipStream_t st, const int *stop = nullptr, int inline_nm = 0);
+                                hipStream_t st, const int *stop = nullptr, int inline_nm = 0, bool xcd_remap = false,
+                                int *far_count = nullptr, int *far_list = nullptr, int *far_hint = nullptr,
+                                int *kpos = nullptr, const int *kd_of = nullptr, const double *seedd = nullptr);
 void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list, const int *hint,
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st, const int *stop = nullptr,
-                            int inline_nm = 0, int *kpos = nullptr, const int *kd_of = nullptr);
+                            int inline_nm = 0, int *kpos = nullptr, const int *kd_of = nullptr,
+                            int group = 0); // (lanes per query: 0 = by max_items)
 
 // The reference CPU rule's near ties (icp_grid.hip): queries whose squared-rule winner idx[j]
 // has another point within the window are appended to out[*count] (count zeroed by the caller).
@@ -389,6 +396,10 @@ struct SeedArgs {
     // >= 0: the records are the local pair test's (icp_bundle_rec.h; its R = max block radius),
     // and seed16 receives each point's shift s0 (float bits) instead of the f16 seed
     double local_r = -1.0;
+    // (nullable) += the moved points farther than sqrt(far_d2) from their correspondence: the
+    // next seeded grid search's queries with a big box (icp_run's search policy)
+    int *far_acc = nullptr;
+    double far_d2 = 0.0;
 };
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
@@ -408,6 +419,9 @@ struct IterState {
     long long nn_counts[4]; // sums of amb_count[0..3] over the recorded searches
     double shift_p[3]; // one-pass moments: the next iteration's shifts (~ its centroids)
     double shift_y[3];
+    int far_acc;       // points the last transform left farther than SeedArgs::far_d2 from their
+                       // correspondence (zeroed by each Horn step; the host reads the mirror)
+    int pad_;
 };
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,

@@ -1896,6 +1896,21 @@ __global__ __launch_bounds__(kBlock) void norms_kernel(
     block_sum_store<2>(a, partials + (size_t)blockIdx.x * 2);
 }
 
+// a workgroup's count into *acc: one atomic, and only when it is not zero (a same-address
+// atomic per workgroup would serialise ~1,000 of them a launch)
+__device__ __forceinline__ void far_to_acc(int far, int *acc)
+{
+    __shared__ int s_far[kBlock / 64];
+    for (int o = 32; o >= 1; o >>= 1) far += __shfl_xor(far, o, 64);
+    if ((threadIdx.x & 63) == 0) s_far[threadIdx.x >> 6] = far;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += s_far[w];
+        if (tot) atomicAdd(acc, tot);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
@@ -1914,6 +1929,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     if (sdone) return;
     const Xform xf = sxf;
     double a[1] = {0.0};
+    int far = 0; // (sa.far_acc: this thread's moved points beyond sqrt(far_d2) of their correspondence)
     if (sa.qop && write_p) {
         // slot records (a scene in slot order): whole waves run to n rounded up to 64 (the
         // stride is a multiple of 64), so that each 32-slot group's lanes are all present for
@@ -1932,6 +1948,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
                 if (p32)
                     p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
                 const double dx = q0 - y0, dy = q1 - y1, dz = q2 - y2;
+                far += ((dx * dx + dy * dy) + dz * dz > sa.far_d2) ? 1 : 0;
                 double4 raw;
                 if (sa.local_r >= 0.0) { // (the local pair test: the shift is the finalize's seed)
                     float s0;
@@ -1953,6 +1970,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
             bundle_group_store(r, i, sa.nslots, (half8_t *)sa.gop, sa.gctr);
         }
         block_sum_store<1>(a, partials + blockIdx.x);
+        if (sa.far_acc) far_to_acc(far, sa.far_acc);
         return;
     }
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
@@ -1971,13 +1989,16 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
             if (sa.seed16)
                 sa.seed16[i] = mfma16_seed_value(q0, q1, q2, yx[i], yy[i], yz[i], sa.c[0], sa.c[1], sa.c[2],
                                                  sa.scale);
-            if (sa.seedd) { // (bundle_prep_kernel's seed distance, in its arithmetic: no gather there)
+            if (sa.seedd || sa.far_acc) { // (bundle_prep_kernel's seed distance, in its arithmetic)
                 const double dx = q0 - yx[i], dy = q1 - yy[i], dz = q2 - yz[i];
-                sa.seedd[i] = (dx * dx + dy * dy) + dz * dz;
+                const double d2 = (dx * dx + dy * dy) + dz * dz;
+                if (sa.seedd) sa.seedd[i] = d2;
+                far += d2 > sa.far_d2 ? 1 : 0;
             }
         }
     }
     block_sum_store<1>(a, partials + blockIdx.x);
+    if (sa.far_acc) far_to_acc(far, sa.far_acc);
 }
 
 // out[k] = sum_b partials[b*K + k], one workgroup, fixed order (deterministic): thread t

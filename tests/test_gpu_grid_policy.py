@@ -1,0 +1,106 @@
+"""icp_run's search policy at the bundle filter's sizes (icp_engine.hip run_loop) and the seeded
+grid search it switches to (grid_seeded_search: the per-query walk of boxes up to 125 cells, a
+whole wave per query for bigger ones, fp64 brute force over the cell budget).
+
+With the AUTO variant and the scene in slot order, a seeded search takes the grid when the last
+transform the host has seen left few points far from their correspondence, else the bundle
+cascade.  Both return the exact first minimum, so:
+  * the AUTO run's per-iteration index digests equal the explicit bundle variant's (which never
+    takes the grid) at every iteration, and its final cloud is bit-identical;
+  * the policy engages on a well-aligned pair (last_filter == grid) and stays on the bundle
+    cascade while the scene is far from the model;
+  * the second pass (big boxes) gives the same answers: clustered clouds (many points a cell)
+    and a sparse shard, against the oracle.
+Sizes: 2^16 x 2^16 (>= 2^31 pairs, > 49,152 queries: the slot-order path).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 1 << 16
+
+
+@pytest.fixture(scope="module")
+def amd(icp_lib):
+    if icp_lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    return icp_lib
+
+
+def run(amd, m, p, iters, variant, digest=True):
+    with amd.Context(0) as ctx:
+        ctx.set_nn_variant(variant)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        if digest:
+            ctx.set_index_digest(iters)
+        res, errs = ctx.run(iters, -1.0)
+        out = dict(errs=errs, res=res, scene=ctx.get_scene(), idx=ctx.get_indices(), stats=ctx.stats())
+        if digest:
+            out["dig"] = ctx.index_digest(iters)
+    return out
+
+
+def rotation(deg, axis=(1.0, 2.0, 3.0)):
+    a = np.asarray(axis) / np.linalg.norm(axis)
+    t = np.deg2rad(deg)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return np.eye(3) + np.sin(t) * K + (1 - np.cos(t)) * K @ K
+
+
+def test_policy_engages_and_matches_bundle(amd):
+    m, p = amd.synthetic_pair(N, seed=42)
+    a = run(amd, m, p, 20, amd.VARIANT_AUTO)
+    b = run(amd, m, p, 20, amd.VARIANT_BUNDLE)
+    assert amd.FILTER_NAMES[a["stats"]["last_filter"]] == "grid"  # the tiles ran the last searches
+    assert amd.FILTER_NAMES[b["stats"]["last_filter"]] == "bundle"
+    assert np.array_equal(a["dig"], b["dig"])
+    assert np.array_equal(a["errs"], b["errs"])
+    assert np.array_equal(a["scene"], b["scene"])
+
+
+def test_policy_stays_on_bundle_far_from_the_model(amd):
+    """A 60-degree rotation: the first iterations move points by many grid cells."""
+    rng = np.random.default_rng(3)
+    m = rng.uniform(-1, 1, size=(N, 3))
+    p = m @ rotation(60.0).T + np.array([0.3, -0.2, 0.1])
+    a = run(amd, m, p, 4, amd.VARIANT_AUTO)
+    b = run(amd, m, p, 4, amd.VARIANT_BUNDLE)
+    assert amd.FILTER_NAMES[a["stats"]["last_filter"]] == "bundle"
+    assert np.array_equal(a["dig"], b["dig"])
+    assert np.array_equal(a["scene"], b["scene"])
+
+
+@pytest.mark.parametrize("case", ["clustered", "shard"])
+def test_seeded_grid_against_oracle(amd, oracle, case):
+    """Dense clusters (hundreds of points a cell region: big boxes for the second pass) and an
+    8-way shard's sparse queries; the grid variant's seeded searches against the oracle."""
+    rng = np.random.default_rng(5)
+    if case == "clustered":
+        centres = rng.uniform(-1, 1, size=(64, 3))
+        m = centres[rng.integers(0, 64, N)] + rng.normal(scale=0.01, size=(N, 3))
+        p = m @ rotation(1.0).T + 0.002
+        scene = p
+        total = N
+    else:
+        m = rng.uniform(-1, 1, size=(N * 8, 3))
+        p = m @ rotation(1.0).T + 0.001
+        scene = p[:N]  # (queries at an eighth of the model's density: an 8-way shard's)
+        total = N
+    with amd.Context(0) as ctx:
+        ctx.set_nn_variant(amd.VARIANT_GRID)
+        ctx.set_allow_unequal(True)
+        ctx.set_model(m)
+        ctx.set_scene(scene, np_total=total)
+        ctx.run(3, -1.0)  # the last two searches seeded
+        got = ctx.get_indices()
+        cur = ctx.get_scene()
+        ctx.run(1, -1.0)  # one more seeded search, on `cur`
+        got2 = ctx.get_indices()
+        st = ctx.stats()
+    sel = np.sort(rng.choice(scene.shape[0], 512, replace=False))
+    _, ref = oracle.closest_blocked(cur[sel], m)
+    assert np.array_equal(got2[sel], ref)
+    assert got.min() >= 0 and got.max() < m.shape[0]
+    assert st["level1_queued"] >= 0

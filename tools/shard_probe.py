@@ -52,6 +52,7 @@ def main():
         row = {"world": w, "shard_points": c, "ms_per_iter": dt * 1e3, "filter_ms": nn,
                "other_ms": dt * 1e3 - nn, "grid_fallback_per_iter": st["grid_fallback"] / a.steps,
                "level1_queued_per_iter": st["level1_queued"] / a.steps,
+               "last_filter": icp_amd.FILTER_NAMES.get(st["last_filter"]),
                "projected_efficiency": (base / (w * dt)) if base else None}
         rows.append(row)
         print(json.dumps(row), flush=True)
