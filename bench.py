@@ -37,10 +37,14 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "iterative-closest-point_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import numpy as np  # noqa: E402
 
 import icp_amd  # noqa: E402
+import roofline as RF  # noqa: E402
+
+GRID_SEEDED_KERNEL = "nn_grid_seeded_kernel"  # (tools/roofline.py GRID_KERNELS: its algorithmic bytes)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32 MFMA peak
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
@@ -217,20 +221,22 @@ def bundle_roofline(n_local, n_model, t_kernel, work, v1=False):
 
 
 def grid_roofline(n_local, n_model, avg_ms, traffic, traffic_src, explicit_variant):
-    """The seeded grid search's pass over every query (nn_grid_resolve_kernel<4, false>, all-mode:
-    the dominant kernel of an AUTO iteration once icp_run's policy takes the grid) against HBM.
-    Algorithmic bytes per launch: per query its fp64 position (24 B), seed distance (8 B), index
-    in and out (8 B) and kd position out (4 B); per model point its 32-byte grid record and ~2 B
-    of the cell table, each once."""
-    gbytes = 44.0 * n_local + 34.0 * n_model
+    """The seeded grid search's pass over every query (nn_grid_seeded_kernel: the dominant kernel
+    of an AUTO iteration once icp_run's policy takes the grid) against HBM.  Algorithmic bytes per
+    launch: per query its fp64 position (24 B), seed distance (8 B), index in and out (8 B) and
+    its correspondence's fp64 coordinates out (24 B); per model point its 32-byte grid record and
+    ~2 B of the cell table, each once."""
+    bq, bm = RF.GRID_KERNELS[GRID_SEEDED_KERNEL]
+    gbytes = bq * n_local + bm * n_model
     t = avg_ms * 1e-3
     ach = gbytes / t / 1e9 if t > 0 else 0.0
-    return {"bound": "hbm", "kernel": "nn_grid_resolve_kernel<4, false> (seeded, every query)",
+    return {"bound": "hbm", "kernel": f"{GRID_SEEDED_KERNEL} (seeded, every query)",
             "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
             "traffic": traffic, "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src, "avg_launch_ms": avg_ms, "bytes_per_launch": gbytes,
-            "bytes_definition": "algorithmic: 44 B per query (fp64 xyz, seed distance, index in/out, kd "
-                                "position out) + 34 B per model point (32-byte grid record + cell table), once",
+            "bytes_definition": f"algorithmic: {bq:.0f} B per query (fp64 xyz, seed distance, index in/out, "
+                                f"correspondence xyz out) + {bm:.0f} B per model point (32-byte grid record + "
+                                "cell table), once",
             "path": "ICP_NN_VARIANT_GRID" if explicit_variant else
                     "AUTO: icp_run's policy (seeded iterations once the scene is near the model)",
             "note": "latency-bound gather: each query walks the grid rows of its box (dependent loads)"}
@@ -326,7 +332,7 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
         st = ctx.stats()
     return {"iterations_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps,
             "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1), "brute_force_fallbacks": st["grid_fallback"],
-            "final_err": float(errs[-1]), "kernel": "nn_grid_resolve_kernel (seeded, every query)",
+            "final_err": float(errs[-1]), "kernel": f"{GRID_SEEDED_KERNEL} (seeded, every query)",
             "roofline": committed_config_roofline("grid")}
 
 
@@ -585,7 +591,7 @@ def main():
         # timed iterations are seeded (warm-up leaves every query a correspondence): the seeded
         # resolve (launch_nn_grid_resolve_all) scans each query's complete candidate box; AUTO
         # takes it by icp_run's policy once the scene is near the model
-        kernel = "nn_grid_resolve_kernel<4>"
+        kernel = GRID_SEEDED_KERNEL
     traffic, traffic_src = pmc_traffic(kernel) if world == 1 and args.n == 1 << 20 else (None, None)
     nn_s = nn_avg_ms * 1e-3
     compulsory = 16.0 * c + 12.0 * args.n  # §8d: fp32 xyz in (scene shard + model), int32 index out

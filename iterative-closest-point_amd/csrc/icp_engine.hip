@@ -315,6 +315,9 @@ struct icp_ctx {
     int *kd_of = nullptr, *kpos = nullptr;
     size_t m4kd_cap = 0, kd_of_cap = 0, kpos_cap = 0;
     bool kpos_valid = false;
+    // y_ready: the last search over the resident scene also wrote Y = m[idx] (the shifted moments
+    // then stream it instead of gathering)
+    bool y_ready = false;
     bool scene_slot = false;
     bool p32_stale = false; // the scene's fp32 copy was not kept by the last icp_run (its path never read it)
     int *s_order = nullptr;
@@ -583,14 +586,14 @@ static bool grid_auto()
 }
 
 // the seeded grid search of a sparse scene in slot order, each XCD on a contiguous eighth of it
-// (launch_nn_grid_resolve_all); ICP_GRID_XCD=0: the plain block order (A/B)
-static bool grid_xcd()
+// (launch_nn_grid_resolve_all); ICP_GRID_XCD=0: the plain block order, =2: every scene (A/B)
+static int grid_xcd()
 {
-    static const bool on = [] {
+    static const int mode = [] {
         const char *e = getenv("ICP_GRID_XCD");
-        return !(e && atoi(e) == 0);
+        return e ? atoi(e) : 1;
     }();
-    return on;
+    return mode;
 }
 
 // The bundle filter's processing order of the n queries in q (a Morton order over the model's
@@ -691,20 +694,32 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     }
     // (an XCD a contiguous eighth of the slot order: measured faster for sparse shards, slower
     // for a whole scene -- C4 W = 8 shard 36.8 against 41.5 us, W = 1 140 against 126 us, r04k)
-    launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), kSeededBox, ctx->idx,
-                               ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0,
-                               grid_xcd() && 4 * n <= ctx->nm, ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, kpos_out,
-                               ctx->kd_of, seedd);
+    const bool xcd = grid_xcd() == 2 || (grid_xcd() == 1 && 4 * n <= ctx->nm);
+    // with the seed distances (the policy's searches): every level also writes each answered
+    // query's correspondence y = m[idx] (the moments then stream y: no gather)
+    const DevCloud &Y = ctx->Y;
+    const bool y_out = seedd && Y.x && Y.cap >= n;
+    double *yx = y_out ? Y.x : nullptr, *yy = y_out ? Y.y : nullptr, *yz = y_out ? Y.z : nullptr;
+    if (y_out) {
+        kpos_out = nullptr;
+        launch_nn_grid_seeded((int)n, q.x, q.y, q.z, grid_view(ctx), kSeededBox, seedd, ctx->m4, ctx->idx, yx, yy,
+                              yz, ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, stop, xcd, ctx->st);
+    } else {
+        launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), kSeededBox, ctx->idx,
+                                   ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0, xcd,
+                                   ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, kpos_out, ctx->kd_of, seedd);
+    }
     if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st)); // (the timed kernel: the pass over every query)
     launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                            grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
-                           ctx->fb_T, ctx->st, stop, inline_nm, kpos_out, ctx->kd_of, 64);
+                           ctx->fb_T, ctx->st, stop, inline_nm, kpos_out, ctx->kd_of, 64, yx, yy, yz);
     if (!inline_nm)
         launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32, ctx->model.x,
                           ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st, stop, kpos_out,
-                          ctx->kd_of);
+                          ctx->kd_of, yx, yy, yz);
     LAUNCHCHK("grid_seeded_search");
     ctx->kpos_valid = kpos_out != nullptr;
+    ctx->y_ready = y_out;
     return ICP_OK;
 }
 
@@ -716,10 +731,12 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
 // zero_counts = false: amb_count is already zero (icp_run: horn_step clears it)
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
                     bool zero_counts = true, bool seeds_ready = false, const int *stop = nullptr,
-                    bool slot_order = false, bool records_ready = false, bool grid_seeded = false)
+                    bool slot_order = false, bool records_ready = false, bool grid_seeded = false,
+                    const double *seedd = nullptr)
 {
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     ctx->kpos_valid = false;
+    ctx->y_ready = false;
     if (!n) return ICP_OK;
     int *kpos_out = nullptr; // (the local bundle filter: each writer of idx also writes kpos)
     // small models: the grid resolver scans its rare leftovers exactly in place (no fp64
@@ -745,8 +762,9 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         // run_loop)
         ctx->stats.last_filter = ICP_FILTER_GRID;
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
-        // (the policy's searches: the last transform wrote each point's seed distance)
-        TRY(grid_seeded_search(ctx, q, n, stop, grid_seeded && ctx->b_seedd ? ctx->b_seedd : nullptr, ev1));
+        // (seedd: the last transform wrote each point's seed distance -- the policy's searches, and
+        // the grid variant's after its first iteration)
+        TRY(grid_seeded_search(ctx, q, n, stop, seedd, ev1));
         return ICP_OK;
     } else if (ctx->nn_variant == ICP_NN_VARIANT_GRID) {
         // exact grid search for every query; over-budget boxes -> fp64 brute force per query
@@ -757,7 +775,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         if (seeded) // (icp_run: the previous correspondence is each query's candidate; no ring search)
             launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), grid_budget(ctx), ctx->idx,
                                        ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0,
-                                       slot_order && grid_xcd());
+                                       slot_order && grid_xcd() != 0);
         else
             launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx,
                                   ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st);
@@ -1954,6 +1972,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         }
     }
     if (want_slot_order(ctx, n)) TRY(scene_to_slot_order(ctx));
+    if (ctx->scene_slot && ctx->nn_variant == ICP_NN_VARIANT_GRID && ctx->nn_mode == ICP_NN_CERTIFIED && !sa.seedd) {
+        // the grid variant's seeded searches read the transform's seed distances too
+        TRY(grow(ctx, &ctx->b_seedd, &ctx->b_seedd_cap, n));
+        sa.seedd = ctx->b_seedd;
+    }
     const int *digest_order = ctx->scene_slot ? ctx->s_order : nullptr;
     // The search policy of AUTO at the bundle filter's sizes (the scene in slot order): a seeded
     // search takes the grid (grid_seeded_search) instead of the bundle cascade when the last
@@ -2049,10 +2072,13 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             const bool grid_cur = enqueued > 0 && grid_next; // (decided with the previous transform)
             grid_next = grid_policy && enqueued >= 1 && far_obs >= 0 && far_obs <= far_thr;
             // (the search of an iteration queued behind the converged one returns at once)
+            // (the seed distances the last transform of this run wrote, for a grid search)
+            const double *gseedd = enqueued > 0 && (grid_cur || ctx->nn_variant == ICP_NN_VARIANT_GRID) ? sa.seedd
+                                                                                                        : nullptr;
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false,
                                 fuse_seeds && enqueued > 0 && !grid_cur, &sd->done, ctx->scene_slot,
-                                sa.qop && enqueued > 0 && !grid_cur, grid_cur)); // (run_init zeroed the counters)
+                                sa.qop && enqueued > 0 && !grid_cur, grid_cur, gseedd)); // (run_init zeroed the counters)
             if (enqueued == 0 && sa.seedd && ctx->scene_slot && transform_records) {
                 // a scene in slot order: from here on each transform writes the next search's
                 // slot records and group bounds in order (the first search sized the buffers;
@@ -2143,7 +2169,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             } else {
                 launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
                                        red_target(ctx, n, ctx->sums), ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr,
-                                       ctx->m4kd);
+                                       ctx->m4kd, ctx->y_ready);
                 if (!lag && red_blocks(n) > 1) { // the fold and the Horn step in one launch
                     launch_reduce_horn(ctx->partials, red_blocks(n), ctx->sums, N, ctx->c, 1, ctx->amb_count, sd,
                                        ctx->st);

@@ -290,7 +290,8 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
     const double4 *__restrict__ m4, GridView gv, int budget, int *__restrict__ idx, int *fb_count,
     int *__restrict__ fb_list, const double *__restrict__ T_in, double *__restrict__ T_out, const int *__restrict__ stop,
     int inline_nm, int n_all, int *__restrict__ kpos, const int *__restrict__ kd_of, int xcd_remap,
-    int *far_count, int *__restrict__ far_list, int *__restrict__ far_hint, const double *__restrict__ seedd)
+    int *far_count, int *__restrict__ far_list, int *__restrict__ far_hint, const double *__restrict__ seedd,
+    double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz)
 {
     // seedd (all-mode, nullable): each query's seed distance D64(q, m[idx]) as the last transform
     // computed it (the same arithmetic on the same values): no dependent gather of the seed point
@@ -334,6 +335,12 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
             if (sub == 0) {
                 idx[j] = bi;
                 if (kpos) kpos[j] = kd_of[bi];
+                if (yx) { // (y nullable: the winner's coordinates for the moments)
+                    const double4 w = m4[bi];
+                    yx[j] = w.x;
+                    yy[j] = w.y;
+                    yz[j] = w.z;
+                }
             }
         } else if (far_count) { // (uniform per group: handed on below)
         } else if (inline_nm > 0) { // small model: the exact fp64 scan of every point, right here
@@ -347,6 +354,12 @@ __global__ __launch_bounds__(kBlock) void nn_grid_resolve_kernel(
             if (sub == 0) {
                 idx[j] = bi < 0 ? 0 : bi;
                 if (kpos) kpos[j] = kd_of[bi < 0 ? 0 : bi];
+                if (yx) {
+                    const double4 w = m4[bi < 0 ? 0 : bi];
+                    yx[j] = w.x;
+                    yy[j] = w.y;
+                    yz[j] = w.z;
+                }
             } // (no comparison held: a NaN query -> index 0)
         }
         const bool far = far_count && !ok && sub == 0;
@@ -456,6 +469,123 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const doub
             group_lex_min<G>(best, bi);
         }
         if (sub == 0) idx[j] = bi >= 0 ? bi : j % nm;
+    }
+}
+
+// (D64, index) first minimum that also carries the winner's position k in pts.  The seed enters
+// as (best, bi) with no position; the scan meets the seed point itself (it lies in its own box)
+// and then takes its position (the equal-index case), so a scanned winner always has one.
+__device__ __forceinline__ void lex_min_pos(double &best, int &bi, int &bk, double d, int mi, int k)
+{
+    if (d < best || (d == best && (unsigned)mi <= (unsigned)bi)) {
+        best = d;
+        bi = mi;
+        bk = k;
+    }
+}
+
+template <int G> __device__ __forceinline__ void group_lex_min_pos(double &best, int &bi, int &bk)
+{
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(best, o, G);
+        const int oi = __shfl_xor(bi, o, G);
+        const int ok = __shfl_xor(bk, o, G);
+        if (ob < best || (ob == best && (unsigned)oi < (unsigned)bi)) {
+            best = ob;
+            bi = oi;
+            bk = ok;
+        } else if (ob == best && oi == bi) {
+            bk = max(bk, ok); // (the same point: its position, or -1 where a lane never met it)
+        }
+    }
+}
+
+// The seeded search of every query of a scene in slot order (icp_run's grid iterations,
+// grid_seeded_search): each query's box comes from its seed distance seedd[t] -- the last
+// transform's D64(q, m[idx[t]]), the same arithmetic on the same values, so the seed point is met
+// with d == best -- and G lanes scan its x-runs, KR run bounds read together and then the lane's
+// points as one flat sequence, KU loads in flight.  The winner's index goes to idx and its
+// coordinates to y (the correspondence cloud the moments then stream: no gather there), re-read
+// from pts at the position the scan met it (an L2 hit).
+// A box over `budget` cells (or a non-finite seed) queues the query for the second pass.
+template <int G, int KR, int KU, int W>
+__global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
+    int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
+    int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
+    double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
+    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap)
+{
+    if (stop && *stop) return; // a frozen (converged) ICP iteration
+    const int sub = threadIdx.x & (G - 1);
+    const int groups = gridDim.x * (kBlock / G);
+    const int bx = xcd_remap && (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                                     : blockIdx.x;
+    for (int t = (bx * kBlock + threadIdx.x) / G; t < n; t += groups) {
+        const int h = idx[t];
+        const double q[3] = {px[t], py[t], pz[t]};
+        double best = seedd[t];
+        int bi = h, bk = -1, c0[3], c1[3];
+        // (a non-finite seed distance -- a NaN / inf query -- bounds no box: second pass, then
+        // the brute force and its first-minimum rule)
+        const bool ok = h >= 0 && best == best && best < INFINITY && complete_box(q, best, gv, budget, c0, c1);
+        if (ok) {
+            const int ny = c1[1] - c0[1] + 1;
+            const int nrows = ny * (c1[2] - c0[2] + 1);
+            for (int r0 = sub; r0 < nrows; r0 += KR * G) {
+                int k0[KR], pre[KR + 1];
+                pre[0] = 0;
+#pragma unroll
+                for (int u = 0; u < KR; ++u) {
+                    const int r = r0 + u * G;
+                    int a = 0, b = 0;
+                    if (r < nrows) {
+                        const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                        const int row = (cz * gv.g[1] + cy) * gv.g[0];
+                        a = gv.start[row + c0[0]];
+                        b = gv.start[row + c1[0] + 1];
+                    }
+                    k0[u] = a;
+                    pre[u + 1] = pre[u] + (b - a);
+                }
+                const int total = pre[KR];
+                for (int f0 = 0; f0 < total; f0 += KU) { // the lane's runs as one sequence
+                    int k[KU];
+#pragma unroll
+                    for (int v = 0; v < KU; ++v) {
+                        const int f = f0 + v;
+                        int p = k0[0] + f;
+#pragma unroll
+                        for (int u = 1; u < KR; ++u)
+                            if (f >= pre[u]) p = k0[u] + (f - pre[u]);
+                        k[v] = f < total ? p : -1;
+                    }
+                    double4 m[KU];
+#pragma unroll
+                    for (int v = 0; v < KU; ++v)
+                        if (k[v] >= 0) m[v] = gv.pts[k[v]];
+#pragma unroll
+                    for (int v = 0; v < KU; ++v)
+                        if (k[v] >= 0)
+                            lex_min_pos(best, bi, bk, d64g(q[0], q[1], q[2], m[v].x, m[v].y, m[v].z), (int)m[v].w,
+                                        k[v]);
+                }
+            }
+            group_lex_min_pos<G>(best, bi, bk);
+            if (sub == 0) { // (bk >= 0: the seed point lies in its box; pts[bk] was just read)
+                const double4 w = bk >= 0 ? gv.pts[bk] : m4[bi];
+                idx[t] = bi;
+                yx[t] = w.x;
+                yy[t] = w.y;
+                yz[t] = w.z;
+            }
+        }
+        const bool far = !ok && sub == 0;
+        const int fs = wave_append(far_count, far);
+        if (far) {
+            far_list[fs] = t;
+            far_hint[fs] = h;
+        }
     }
 }
 
@@ -583,7 +713,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const double *px, const double *py, const double *pz, const double4 *m4,
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st, const int *stop, int inline_nm,
-                            int *kpos, const int *kd_of, int group)
+                            int *kpos, const int *kd_of, int group, double *yx, double *yy, double *yz)
 {
     // lanes per queued query, measured: a whole wave for searches of 8,192 to 2^18 queries (horse /
     // bunny surfaces: big boxes of dense surface cells; 64 lanes 4,289 vs 16 lanes 3,231 it/s
@@ -607,7 +737,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
 #define RESOLVE(GG, F)                                                                                  \
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(count_ptr, list, hint, px, py, pz, m4, gv, budget, idx, \
                                                              fb_count, fb_list, T_in, T_out, stop, inline_nm, 0, \
-                                                             kpos, kd_of, 0, nullptr, nullptr, nullptr, nullptr)
+                                                             kpos, kd_of, 0, nullptr, nullptr, nullptr, nullptr, yx, yy, yz)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE(4, true);
         else if (g == 64) RESOLVE(64, true);
@@ -639,7 +769,7 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
     nn_grid_resolve_kernel<GG, F><<<blocks, kBlock, 0, st>>>(nullptr, nullptr, nullptr, px, py, pz, m4, gv, budget, \
                                                              idx, fb_count, fb_list, nullptr, fb_T, stop, inline_nm, n, \
                                                              kpos, kd_of, xcd_remap ? 1 : 0, far_count, far_list, far_hint, \
-                                                             seedd)
+                                                             seedd, nullptr, nullptr, nullptr)
     if (grid_flat_scan(g)) {
         if (g == 4) RESOLVE_ALL(4, true);
         else RESOLVE_ALL(16, true);
@@ -648,6 +778,53 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
         else RESOLVE_ALL(16, false);
     }
 #undef RESOLVE_ALL
+}
+
+void launch_nn_grid_seeded(int n, const double *px, const double *py, const double *pz, const GridView &gv,
+                           int budget, const double *seedd, const double4 *m4, int *idx, double *yx, double *yy,
+                           double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
+                           hipStream_t st)
+{
+    // (lanes per query, run bounds read together, point loads in flight[, waves per SIMD forced]):
+    // ICP_GRID_SEEDED="G,KR,KU" picks one of the instantiated forms for A/B.  Default 2,2,2 (70
+    // VGPRs, 7 waves per SIMD), measured at C4 W = 1 (profiles/r04r): 106 us against 132 (4,2,4),
+    // 112 (4,2,2), 145 (4,1,4); forcing 8 waves spills (2,2,2,8: 110; 4,2,4,8: 199)
+    static const int form = [] {
+        const char *e = getenv("ICP_GRID_SEEDED");
+        if (!e) return 7;
+        const std::string s(e);
+        const char *forms[] = {"4,2,4", "4,1,4", "4,4,4", "2,2,4", "2,4,4", "1,4,4", "4,2,2", "2,2,2",
+                               "4,2,4,8", "4,1,4,8", "4,2,2,8", "2,2,2,8", "2,2,4,8", "1,4,4,8", "1,2,2,8"};
+        for (int i = 0; i < (int)(sizeof(forms) / sizeof(forms[0])); ++i)
+            if (s == forms[i]) return i;
+        return 0;
+    }();
+    static const int G_of[] = {4, 4, 4, 2, 2, 1, 4, 2, 4, 4, 4, 2, 2, 1, 1};
+    const int per_block = kBlock / G_of[form];
+    int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
+    if (xcd_remap) blocks = (blocks + 7) / 8 * 8; // (whole eighths; the extra workgroups find no query)
+#define SEEDED(GG, R, U, W)                                                                                       \
+    nn_grid_seeded_kernel<GG, R, U, W><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, \
+                                                                  yy, yz, far_count, far_list, far_hint, stop,         \
+                                                                  xcd_remap ? 1 : 0)
+    switch (form) {
+    case 1: SEEDED(4, 1, 4, 1); break;
+    case 2: SEEDED(4, 4, 4, 1); break;
+    case 3: SEEDED(2, 2, 4, 1); break;
+    case 4: SEEDED(2, 4, 4, 1); break;
+    case 5: SEEDED(1, 4, 4, 1); break;
+    case 6: SEEDED(4, 2, 2, 1); break;
+    case 7: SEEDED(2, 2, 2, 1); break;
+    case 8: SEEDED(4, 2, 4, 8); break;
+    case 9: SEEDED(4, 1, 4, 8); break;
+    case 10: SEEDED(4, 2, 2, 8); break;
+    case 11: SEEDED(2, 2, 2, 8); break;
+    case 12: SEEDED(2, 2, 4, 8); break;
+    case 13: SEEDED(1, 4, 4, 8); break;
+    case 14: SEEDED(1, 2, 2, 8); break;
+    default: SEEDED(4, 2, 4, 1); break;
+    }
+#undef SEEDED
 }
 
 // ---- the reference CPU path's rule (ICP_NN_RULE_CPU_SQRT) ------------------------------------

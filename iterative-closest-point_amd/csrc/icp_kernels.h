@@ -251,7 +251,8 @@ void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *
                        const float4 *p32, const double *px, const double *py, const double *pz,
                        const float4 *m32, const double *mx, const double *my, const double *mz,
                        int nm, int max_items, int *idx, hipStream_t st, const int *stop = nullptr,
-                       int *kpos = nullptr, const int *kd_of = nullptr); // (kpos[j] = kd_of[idx[j]])
+                       int *kpos = nullptr, const int *kd_of = nullptr, // (kpos[j] = kd_of[idx[j]])
+                       double *yx = nullptr, double *yy = nullptr, double *yz = nullptr); // (y[j] = m[idx[j]])
 // fp64 brute force: partial (best d64, argbest) per (split, query), then merge.
 void launch_nn_fp64(const double *px, const double *py, const double *pz, int np,
                     const double *mx, const double *my, const double *mz, int nm,
@@ -309,7 +310,18 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
                             const GridView &gv, int budget, int *idx, int *fb_count, int *fb_list,
                             const double *T_in, double *T_out, hipStream_t st, const int *stop = nullptr,
                             int inline_nm = 0, int *kpos = nullptr, const int *kd_of = nullptr,
-                            int group = 0); // (lanes per query: 0 = by max_items)
+                            int group = 0, // (lanes per query: 0 = by max_items)
+                            double *yx = nullptr, double *yy = nullptr, double *yz = nullptr); // (y[j] = m[idx[j]])
+// icp_run's seeded search of every query of a scene in slot order (the policy's grid
+// iterations): the box of query t from its seed distance seedd[t] = D64(p_t, m[idx_t]) (the last
+// transform's), scanned by a few lanes; idx[t] and the correspondence y_t = m[idx_t] written for
+// every answered query; a box over `budget` cells (or a non-finite seed) goes to (far_list,
+// far_hint = its seed) at *far_count for launch_nn_grid_resolve.  xcd_remap: each XCD takes a
+// contiguous eighth of the queries.
+void launch_nn_grid_seeded(int n, const double *px, const double *py, const double *pz, const GridView &gv,
+                           int budget, const double *seedd, const double4 *m4, int *idx, double *yx, double *yy,
+                           double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
+                           hipStream_t st);
 
 // The reference CPU rule's near ties (icp_grid.hip): queries whose squared-rule winner idx[j]
 // has another point within the window are appended to out[*count] (count zeroed by the caller).
@@ -429,7 +441,7 @@ struct IterState {
 void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
                             double *partials, hipStream_t st, const int *kpos = nullptr,
-                            const double4 *m4kd = nullptr);
+                            const double4 *m4kd = nullptr, bool y_ready = false); // (y_ready: y = m[idx] already)
 // (1 thread) NN queue sizes amb_count[0..3] -> nn_counts (unless done), then zeroed for the next
 // search; then, unless done, the Horn solve (icp_horn.h) from the reduced sums -- two-pass
 // sums (Σp, Σy, centred S, d_caps, sp) or, if shifted, launch_shifted_moments' -- and the

@@ -1492,7 +1492,8 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
     const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
     const float4 *__restrict__ m32, const double *__restrict__ mx, const double *__restrict__ my,
     const double *__restrict__ mz, int nm, int *__restrict__ idx, const int *__restrict__ stop,
-    int *__restrict__ kpos, const int *__restrict__ kd_of)
+    int *__restrict__ kpos, const int *__restrict__ kd_of, double *__restrict__ yx, double *__restrict__ yy,
+    double *__restrict__ yz)
 {
     __shared__ double shd[kBlock];
     if (stop && *stop) return; // a frozen (converged) ICP iteration (uniform: before any barrier)
@@ -1537,6 +1538,11 @@ __global__ __launch_bounds__(kBlock) void nn_resolve_kernel(
             const int w = shi[0] == 0x7fffffff ? 0 : shi[0];
             idx[j] = w;
             if (kpos) kpos[j] = kd_of[w];
+            if (yx) { // (the correspondence for moments that stream y)
+                yx[j] = mx[w];
+                yy[j] = my[w];
+                yz[j] = mz[w];
+            }
         }
         __syncthreads();
     }
@@ -1723,7 +1729,7 @@ __global__ __launch_bounds__(kBlock) void gather_moments_kernel(
 
 // one pass around shifts near the centroids: the centred sums follow as
 // S = sum (p - cp)(y - cy)^T - N dp dy^T etc. (horn_step), with N dp dy^T at rounding level
-template <int kMomBatch>
+template <int kMomBatch, bool YIN>
 __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
@@ -1743,10 +1749,12 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     const int G = gridDim.x * kBlock;
     for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += kMomBatch * G) {
         int j[kMomBatch];
+        if constexpr (!YIN) {
 #pragma unroll
-        for (int u = 0; u < kMomBatch; ++u) {
-            const int i = i0 + u * G;
-            j[u] = i < n ? (kpos ? kpos[i] : idx[i]) : 0;
+            for (int u = 0; u < kMomBatch; ++u) {
+                const int i = i0 + u * G;
+                j[u] = i < n ? (kpos ? kpos[i] : idx[i]) : 0;
+            }
         }
         double4 m[kMomBatch];
         double qx[kMomBatch], qy[kMomBatch], qz[kMomBatch];
@@ -1754,7 +1762,10 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
         for (int u = 0; u < kMomBatch; ++u) {
             const int i = i0 + u * G;
             const bool in = i < n;
-            m[u] = in ? (kpos ? m4kd[j[u]] : m4[j[u]]) : make_double4(0.0, 0.0, 0.0, 0.0);
+            if constexpr (YIN) // (the search wrote y = m[idx]: the same values, streamed)
+                m[u] = in ? make_double4(yx[i], yy[i], yz[i], 0.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+            else
+                m[u] = in ? (kpos ? m4kd[j[u]] : m4[j[u]]) : make_double4(0.0, 0.0, 0.0, 0.0);
             qx[u] = in ? px[i] : 0.0;
             qy[u] = in ? py[i] : 0.0;
             qz[u] = in ? pz[i] : 0.0;
@@ -1763,9 +1774,11 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
         for (int u = 0; u < kMomBatch; ++u) {
             const int i = i0 + u * G;
             if (i < n) {
-                yx[i] = m[u].x;
-                yy[i] = m[u].y;
-                yz[i] = m[u].z;
+                if constexpr (!YIN) {
+                    yx[i] = m[u].x;
+                    yy[i] = m[u].y;
+                    yz[i] = m[u].z;
+                }
                 shifted_moment_terms(qx[u], qy[u], qz[u], m[u], cp0, cp1, cp2, cy0, cy1, cy2, a);
             }
         }
@@ -2401,14 +2414,14 @@ void launch_nn_resolve(const int *amb_count, const int *amb_list, const double *
                        const float4 *p32, const double *px, const double *py, const double *pz,
                        const float4 *m32, const double *mx, const double *my, const double *mz,
                        int nm, int max_items, int *idx, hipStream_t st, const int *stop, int *kpos,
-                       const int *kd_of)
+                       const int *kd_of, double *yx, double *yy, double *yz)
 {
     // (one workgroup per CU, grid-striding over the device-side count: the launch is on every
     // search's path and usually finds nothing to do -- 2,048 idle workgroups cost ~4.6 us)
     int grid = max_items < 256 ? max_items : 256;
     if (grid < 1) grid = 1;
     nn_resolve_kernel<<<grid, kBlock, 0, st>>>(amb_count, amb_list, amb_T, p32, px, py, pz, m32, mx,
-                                                my, mz, nm, idx, stop, kpos, kd_of);
+                                                my, mz, nm, idx, stop, kpos, kd_of, yx, yy, yz);
 }
 
 void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm, int *idx_out, double *y_aos,
@@ -2443,7 +2456,7 @@ int red_blocks(size_t n) { return n <= (size_t)kRedSingle ? 1 : grid_for(n, kRed
 
 void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
-                            double *partials, hipStream_t st, const int *kpos, const double4 *m4kd)
+                            double *partials, hipStream_t st, const int *kpos, const double4 *m4kd, bool y_ready)
 {
     // points of a thread whose loads are issued together (A/B: ICP_MOM_BATCH = 1 | 2 | 4; same
     // sums).  C4 (four points a thread): 23.5 / 20.5 / 21.2 us at 1 / 2 / 4 (profiles/r03bd/)
@@ -2452,15 +2465,19 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
         const int v = e ? atoi(e) : 2;
         return v == 1 || v == 4 ? v : 2;
     }();
-    if (batch == 2)
-        shifted_moments_kernel<2><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev,
-                                                                    partials, kpos, m4kd);
-    else if (batch == 1)
-        shifted_moments_kernel<1><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev,
-                                                                    partials, kpos, m4kd);
-    else
-        shifted_moments_kernel<4><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev,
-                                                                    partials, kpos, m4kd);
+#define MOMENTS(B, Y)                                                                                         \
+    shifted_moments_kernel<B, Y><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, \
+                                                                   partials, kpos, m4kd)
+    if (y_ready) {
+        if (batch == 1) MOMENTS(1, true);
+        else if (batch == 4) MOMENTS(4, true);
+        else MOMENTS(2, true);
+    } else {
+        if (batch == 1) MOMENTS(1, false);
+        else if (batch == 4) MOMENTS(4, false);
+        else MOMENTS(2, false);
+    }
+#undef MOMENTS
 }
 
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,

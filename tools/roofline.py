@@ -121,7 +121,20 @@ def roofline(tag=None, n=1 << 20, world=1):
 # --variant grid` at C4 (nn_grid_resolve_kernel: the seeded exact grid search of every query).
 C3_KERNEL = "icp_persistent_mid_kernel"
 C3_ITERATIONS = 50
-GRID_KERNEL = "nn_grid_resolve_kernel"
+# the grid capture's kernel and its algorithmic bytes (per query, per model point): the seeded
+# kernel (round 4: fp64 query 24 B + seed distance 8 + index in 4 / out 4 + correspondence out 24;
+# 32-byte grid record + cell table 2) or, in captures before it, the generic resolver's all-mode
+# (query 24 + index in/out; 32-byte record) -- its JSON keyed without the template argument
+GRID_KERNELS = {"nn_grid_seeded_kernel": (64.0, 34.0), "nn_grid_resolve_kernel<4>": (28.0, 32.0)}
+GRID_KERNEL = "nn_grid_seeded_kernel"
+
+
+def grid_kernel_keys(times, pmc):
+    """(kernel name in the trace, its key in the PMC JSON, bytes per query, bytes per model point)"""
+    for k, (bq, bm) in GRID_KERNELS.items():
+        if k in times:
+            return k, (k if k in pmc else k.split("<")[0]), bq, bm
+    raise KeyError(f"none of {list(GRID_KERNELS)} in the kernel trace")
 # workgroup 0's phase timers of the one-launch kernels (icp_iter.hip persist_stamp tags): time
 # accumulated into the tag that ENDS each interval
 STAMP_PHASES = {0: "iteration turnaround", 1: "nn search", 2: "local sums + publish", 3: "grid barrier wait",
@@ -159,15 +172,18 @@ def stamp_phases(path):
 
 def config_roofline(cfg, tag=None, n=1 << 20):
     """cfg "c3": bytes per registration of the one-launch kernel, its rate and HBM fraction, bytes
-    per iteration, the phase split; cfg "grid": the seeded grid resolve at C4 (n queries, n model
-    points) against its algorithmic bytes 28 n + 32 n."""
+    per iteration, the phase split; cfg "grid": the seeded grid search at C4 (n queries, n model
+    points) against its algorithmic bytes (GRID_KERNELS)."""
     tag = tag or newest_config_tag(cfg)
     if tag is None:
         return None
     times = kernel_times(os.path.join(PROFILES, f"{tag}_{cfg}_kernel_stats.csv"))
     pmc = json.load(open(os.path.join(PROFILES, f"{tag}_{cfg}_pmc_traffic.json")))["kernels"]
-    k = C3_KERNEL if cfg == "c3" else GRID_KERNEL
-    t, p = times[k], pmc[k]
+    if cfg == "c3":
+        k = kp = C3_KERNEL
+    else:
+        k, kp, bq, bm = grid_kernel_keys(times, pmc)
+    t, p = times[k], pmc[kp]
     sec = t["avg_ms"] * 1e-3
     b = p["traffic_bytes_per_launch"]
     out = {"tag": tag, "kernel": k, "source": f"profiles/{tag}_{cfg}_kernel_stats.csv + profiles/{tag}_{cfg}_pmc_traffic.json",
@@ -182,7 +198,7 @@ def config_roofline(cfg, tag=None, n=1 << 20):
             out["phases_us_per_registration"] = stamp_phases(sp)
             out["phases_source"] = f"profiles/{tag}_c3_stamps.stamps (ICP_PERSIST_STAMPS=1, workgroup 0)"
     else:
-        alg = 28.0 * n + 32.0 * n
+        alg = bq * n + bm * n
         out["algorithmic_bytes"] = alg
         out["algorithmic_gbps"] = alg / sec / 1e9
         out["hbm_frac"] = out["algorithmic_gbps"] / HBM_PEAK_GBS

@@ -1,0 +1,23 @@
+# A/B of the seeded grid kernel's forms (ICP_GRID_SEEDED = "G,KR,KU[,waves]") and of the XCD
+# block remap (ICP_GRID_XCD = 0 | 1 | 2) on the C4 bench iteration and the 8-way shard probe.
+#   tools/seeded_ab.sh TAG "form1 form2 ..."
+set -u
+O=gpurun_out/${1:-ab}; mkdir -p $O; export TMPDIR=/tmp
+FORMS=${2:-"4,2,4 4,1,4 4,2,2 2,2,2 4,2,4,8 4,2,2,8 2,2,2,8 1,2,2,8"}
+line() { python3 -c "
+import json,sys
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d=json.loads(l); r=d['per_rank'][0]
+        print(f\"{sys.argv[2]:>14s} it/s {d['value']:8.1f} ms/step {d['ms_per_step']*1e3:7.1f}us grid {r['filter_ms']*1e3:7.1f}us tail {r['tail_ms']*1e3:6.1f}us\")
+" $1 "$2"; }
+for f in $FORMS; do
+  ICP_GRID_SEEDED=$f timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_$f.log 2>&1 || exit 1
+  line $O/b_$f.log "$f" | tee -a $O/summary.txt
+done
+for x in 0 2; do
+  ICP_GRID_XCD=$x timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_xcd$x.log 2>&1 || exit 1
+  line $O/b_xcd$x.log "xcd=$x" | tee -a $O/summary.txt
+done
+timeout -k 10 200 python3 tools/shard_probe.py --worlds 1 8 --steps 30 > $O/shard.log 2>&1 || exit 1
+echo done
