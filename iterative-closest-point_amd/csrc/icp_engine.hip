@@ -194,6 +194,8 @@ struct icp_ctx {
     GridParams grid{};
     int *g_cid = nullptr, *g_count = nullptr, *g_start = nullptr, *g_bsum = nullptr, *g_fill = nullptr;
     double4 *g_pts = nullptr;
+    float4 *g_pts32 = nullptr; // (the fp32 image of g_pts: the seeded grid search's prefilter)
+    size_t g_pts32_cap = 0;
     size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
@@ -318,6 +320,9 @@ struct icp_ctx {
     // y_ready: the last search over the resident scene also wrote Y = m[idx] (the shifted moments
     // then stream it instead of gathering)
     bool y_ready = false;
+    // arrival counters of the passes that end in their own last workgroup (StepFold): [0] the
+    // moments + Horn step, [1] the transform + error step; zero between launches
+    unsigned *fold_ticket = nullptr;
     bool scene_slot = false;
     bool p32_stale = false; // the scene's fp32 copy was not kept by the last icp_run (its path never read it)
     int *s_order = nullptr;
@@ -555,6 +560,9 @@ GridView grid_view(const icp_ctx *ctx)
         gv.lo[a] = ctx->grid.lo[a];
     }
     gv.inv_h = ctx->grid.inv_h;
+    gv.pts32 = ctx->g_pts32;
+    for (int a = 0; a < 3; ++a) gv.c32[a] = ctx->grid.c32[a];
+    gv.em32 = ctx->grid.em32;
     return gv;
 }
 
@@ -710,7 +718,10 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
                                    ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, kpos_out, ctx->kd_of, seedd);
     }
     if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st)); // (the timed kernel: the pass over every query)
-    launch_nn_grid_resolve(ctx->amb_count + 2, (int)n, ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
+    // the second pass: a whole wave per queued query, grid-striding over the device-side count
+    // (sized for a few thousand -- the policy keeps the queue short; a launch of 4,096 idle
+    // workgroups cost ~6 us a search, r04q)
+    launch_nn_grid_resolve(ctx->amb_count + 2, (int)std::min<size_t>(n, 4096), ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                            grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
                            ctx->fb_T, ctx->st, stop, inline_nm, kpos_out, ctx->kd_of, 64, yx, yy, yz);
     if (!inline_nm)
@@ -1274,10 +1285,10 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
-                    (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts,
+                    (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts, (void *)ctx->g_pts32,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
-                    (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest,
+                    (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest, (void *)ctx->fold_ticket,
                     (void *)ctx->cert_audit, (void *)ctx->pers_part, (void *)ctx->pers_sync,
                     (void *)ctx->pers_stamps, (void *)ctx->pm_img, (void *)ctx->b_img, (void *)ctx->b_pimg, (void *)ctx->b_kd_orig,
                     (void *)ctx->b_bctr, (void *)ctx->b_blk, (void *)ctx->b_gctr, (void *)ctx->b_cand,
@@ -1418,8 +1429,9 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm)
     TRY(grow(ctx, &ctx->g_bsum, &ctx->g_bsum_cap, grid_scan_blocks(ncell + 1)));
     TRY(grow(ctx, &ctx->g_fill, &ctx->g_fill_cap, (size_t)ncell));
     TRY(grow(ctx, &ctx->g_pts, &ctx->g_pts_cap, nm));
+    TRY(grow(ctx, &ctx->g_pts32, &ctx->g_pts32_cap, nm));
     launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_cid, ctx->g_count,
-                      ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->st);
+                      ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->g_pts32, ctx->st);
     LAUNCHCHK("grid_build");
     for (int k = 0; k < 3; ++k) { // the model's box (the query orders: mid-size loop, bundle filter)
         ctx->m_lo[k] = lo[k];
@@ -1999,6 +2011,18 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         sa_grid.seedd = sa.seedd; // (grid_seeded_search reads them: no gather of the seed point)
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
+    // one rank, partials over several workgroups: the moments end in the Horn step and the
+    // transform in the error step, each in its own last workgroup (StepFold: one launch fewer
+    // each, bit-identical).  ICP_FUSED_STEPS=0: the separate fold launches (A/B)
+    static const bool fused_steps_env = [] {
+        const char *e = getenv("ICP_FUSED_STEPS");
+        return !(e && atoi(e) == 0);
+    }();
+    const bool fused_steps = fused_steps_env && !lag_run(ctx) && red_blocks(n) > 1;
+    if (fused_steps && !ctx->fold_ticket) {
+        HIPCHK(hipMalloc((void **)&ctx->fold_ticket, 2 * sizeof(unsigned)));
+        HIPCHK(hipMemsetAsync(ctx->fold_ticket, 0, 2 * sizeof(unsigned), ctx->st));
+    }
     // mid-size single-rank runs: iterations >= 2 end in ONE fused launch (moments ... error step)
     static const int forced_mode = [] {
         const char *e = getenv("ICP_RUN_MODE");
@@ -2167,10 +2191,21 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 ++enqueued;
                 continue;
             } else {
+                StepFold mf;
+                if (fused_steps) { // (+ reduce_horn_kernel's fold and Horn step, in the last workgroup)
+                    mf.ticket = ctx->fold_ticket;
+                    mf.sums = ctx->sums;
+                    mf.N = N;
+                    for (int a = 0; a < 3; ++a) mf.c[a] = ctx->c[a];
+                    mf.cnt = ctx->amb_count;
+                    mf.s = sd;
+                }
                 launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
                                        red_target(ctx, n, ctx->sums), ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr,
-                                       ctx->m4kd, ctx->y_ready);
-                if (!lag && red_blocks(n) > 1) { // the fold and the Horn step in one launch
+                                       ctx->m4kd, ctx->y_ready, mf);
+                if (fused_steps) {
+                    horn_fused = true;
+                } else if (!lag && red_blocks(n) > 1) { // the fold and the Horn step in one launch
                     launch_reduce_horn(ctx->partials, red_blocks(n), ctx->sums, N, ctx->c, 1, ctx->amb_count, sd,
                                        ctx->st);
                     horn_fused = true;
@@ -2191,14 +2226,32 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             // 4. Horn solve (gpu.cc:106-146) on the device
             if (!horn_fused) launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
+            const SeedArgs &sa_t = grid_next ? sa_grid : sa;
+            StepFold ef;
+            const bool err_fused = fused_steps && !sa_t.qop; // (the slot-record form keeps its own launch)
+            if (err_fused) { // (+ reduce_err_kernel's fold and error step, in the last workgroup)
+                const int sl = enqueued % kRing;
+                slot_ticket[sl] = ++ctx->flag_ticket;
+                ef.ticket = ctx->fold_ticket + 1;
+                ef.sums = ctx->sums;
+                ef.N = N;
+                ef.s = sd;
+                ef.threshold = threshold;
+                ef.max_iter = max_iter;
+                ef.err_trace = ctx->err_trace_dev;
+                ef.hflag = ctx->d_flags + 4 * sl;
+                ef.hticket = slot_ticket[sl];
+                ef.h_state = ctx->d_iter_mirror;
+                ef.h_trace = ctx->d_trace;
+            }
             launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, need_p32 ? P.f : nullptr,
-                                     red_target(ctx, n, ctx->sums + kSumErr), grid_next ? sa_grid : sa, ctx->st);
+                                     red_target(ctx, n, ctx->sums + kSumErr), sa_t, ctx->st, ef);
             if (!need_p32) ctx->p32_stale = true;
             const bool fold_err = !lag && red_blocks(n) > 1; // (folded by the error step's launch)
             if (!fold_err) red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
-            if (!lag) TRY(enqueue_err_step(enqueued, fold_err ? ctx->partials : nullptr));
+            if (!lag && !err_fused) TRY(enqueue_err_step(enqueued, fold_err ? ctx->partials : nullptr));
             ++enqueued;
             if (lag && enqueued == max_iter) { // the last residual has no next iteration to ride on
                 TRY(allreduce(ctx, ctx->sums + kSumErr, 1));

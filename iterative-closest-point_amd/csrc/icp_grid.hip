@@ -113,12 +113,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_add_kernel(int *__restrict_
 __global__ __launch_bounds__(kBlock) void grid_scatter_kernel(
     const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
     int nm, const int *__restrict__ cid, const int *__restrict__ start, int *__restrict__ fill,
-    double4 *__restrict__ pts)
+    double4 *__restrict__ pts, float4 *__restrict__ pts32, double c0, double c1, double c2)
 {
     for (int i = blockIdx.x * kBlock + threadIdx.x; i < nm; i += gridDim.x * kBlock) {
         const int c = cid[i];
         const int pos = start[c] + atomicAdd(fill + c, 1); // order within a cell is irrelevant
-        pts[pos] = make_double4(mx[i], my[i], mz[i], (double)i);
+        const double x = mx[i], y = my[i], z = mz[i];
+        pts[pos] = make_double4(x, y, z, (double)i);
+        // (the fp32 image: offsets from the box centre, the index's bits in w)
+        if (pts32) pts32[pos] = make_float4((float)(x - c0), (float)(y - c1), (float)(z - c2), __int_as_float(i));
     }
 }
 
@@ -589,6 +592,122 @@ __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
     }
 }
 
+// The fp32 prefilter's candidate bound.  Query and model coordinates enter as fp32 offsets from
+// the box centre c: q32 = fl32(q - c), m32 = fl32(m - c), each axis off by at most e = eq + em
+// (eq = 2^-23 max_a |q_a - c_a|, em = GridView::em32).  For a model point with D64(q, m) <= best:
+// |v| = |q - m| <= sqrt(best) (1 + 2^-51) =: r (D64 >= |v|^2 (1 - 3 2^-53)), each computed fp32
+// difference |dx| <= (|v_x| + e)(1 + 2^-24), and so d32 = (dx^2 + dy^2) + dz^2 <=
+// (sum_a (|v_a| + e)^2)(1 + 2^-24)^4 <= (r + sqrt(3) e)^2 (1 + 2^-21).  A point with d32 above the
+// bound below is therefore strictly farther than best and cannot be the first minimum; the rest
+// (the candidates: the seed and the few points as close) are decided in fp64.
+__device__ __forceinline__ float seeded_bound32(double best, double e)
+{
+    const double s = sqrt(best) * (1.0 + 0x1.0p-50) + 1.7320508075688774 * e;
+    return (float)(s * s * (1.0 + 0x1.0p-20)) * (1.0f + 0x1.0p-22f); // (rounded up past fl32's halving)
+}
+
+// nn_grid_seeded_kernel with the box's points read from the fp32 image (16 B a point instead of
+// 32) and tested against seeded_bound32: a candidate that is the current winner itself (the seed,
+// index == bi: its D64 is best) only records its position; any other candidate is evaluated in
+// fp64 from pts (the same position) with the exact (D64, index) rule.  Same answers as the fp64
+// scan: every point that can be the first minimum is a candidate.
+template <int G, int KR, int KU>
+__global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
+    int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
+    int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
+    double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
+    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap)
+{
+    if (stop && *stop) return; // a frozen (converged) ICP iteration
+    const int sub = threadIdx.x & (G - 1);
+    const int groups = gridDim.x * (kBlock / G);
+    const int bx = xcd_remap && (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                                     : blockIdx.x;
+    for (int t = (bx * kBlock + threadIdx.x) / G; t < n; t += groups) {
+        const int h = idx[t];
+        const double q[3] = {px[t], py[t], pz[t]};
+        double best = seedd[t];
+        int bi = h, bk = -1, c0[3], c1[3];
+        const bool ok = h >= 0 && best == best && best < INFINITY && complete_box(q, best, gv, budget, c0, c1);
+        if (ok) {
+            const double o0 = q[0] - gv.c32[0], o1 = q[1] - gv.c32[1], o2 = q[2] - gv.c32[2];
+            const float q0 = (float)o0, q1 = (float)o1, q2 = (float)o2;
+            const double e = std::ldexp(fmax(fabs(o0), fmax(fabs(o1), fabs(o2))), -23) + gv.em32;
+            // (T stays the seed's bound: a closer winner found on the way leaves a few more
+            // candidates, not a wrong answer)
+            const float T = seeded_bound32(best, e);
+            const int ny = c1[1] - c0[1] + 1;
+            const int nrows = ny * (c1[2] - c0[2] + 1);
+            for (int r0 = sub; r0 < nrows; r0 += KR * G) {
+                int k0[KR], pre[KR + 1];
+                pre[0] = 0;
+#pragma unroll
+                for (int u = 0; u < KR; ++u) {
+                    const int r = r0 + u * G;
+                    int a = 0, b = 0;
+                    if (r < nrows) {
+                        const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                        const int row = (cz * gv.g[1] + cy) * gv.g[0];
+                        a = gv.start[row + c0[0]];
+                        b = gv.start[row + c1[0] + 1];
+                    }
+                    k0[u] = a;
+                    pre[u + 1] = pre[u] + (b - a);
+                }
+                const int total = pre[KR];
+                for (int f0 = 0; f0 < total; f0 += KU) { // the lane's runs as one sequence
+                    int k[KU];
+#pragma unroll
+                    for (int v = 0; v < KU; ++v) {
+                        const int f = f0 + v;
+                        int p = k0[0] + f;
+#pragma unroll
+                        for (int u = 1; u < KR; ++u)
+                            if (f >= pre[u]) p = k0[u] + (f - pre[u]);
+                        k[v] = f < total ? p : -1;
+                    }
+                    float4 m[KU];
+#pragma unroll
+                    for (int v = 0; v < KU; ++v)
+                        if (k[v] >= 0) m[v] = gv.pts32[k[v]];
+#pragma unroll
+                    for (int v = 0; v < KU; ++v) {
+                        if (k[v] < 0) continue;
+                        const float dx = q0 - m[v].x, dy = q1 - m[v].y, dz = q2 - m[v].z;
+                        if ((dx * dx + dy * dy) + dz * dz > T) continue; // (strictly farther than best)
+                        const int mi = __float_as_int(m[v].w);
+                        if (mi == bi) {
+                            bk = k[v]; // (the current winner itself)
+                        } else {
+                            const double4 w = gv.pts[k[v]];
+                            const double d = d64g(q[0], q[1], q[2], w.x, w.y, w.z);
+                            if (d < best || (d == best && (unsigned)mi < (unsigned)bi)) {
+                                best = d;
+                                bi = mi;
+                                bk = k[v];
+                            }
+                        }
+                    }
+                }
+            }
+            group_lex_min_pos<G>(best, bi, bk);
+            if (sub == 0) { // (bk >= 0: the seed point lies in its box)
+                const double4 w = bk >= 0 ? gv.pts[bk] : m4[bi];
+                idx[t] = bi;
+                yx[t] = w.x;
+                yy[t] = w.y;
+                yz[t] = w.z;
+            }
+        }
+        const bool far = !ok && sub == 0;
+        const int fs = wave_append(far_count, far);
+        if (far) {
+            far_list[fs] = t;
+            far_hint[fs] = h;
+        }
+    }
+}
+
 } // namespace
 
 GridParams grid_params(const double *m_xyz, size_t nm)
@@ -610,7 +729,11 @@ GridParams grid_params_box(const double lo[3], const double hi[3], size_t nm)
         ext[a] = hi[a] - lo[a];
         emax = std::max(emax, ext[a]);
         p.lo[a] = lo[a];
+        p.c32[a] = lo[a] + 0.5 * ext[a];
     }
+    // |fl32(fl64(m - c)) - (m - c)| <= 2^-24 |m - c| (1 + 2^-28) with |m - c| <= ext / 2 (1 + 2^-50):
+    // ext * 2^-23 bounds it with room (a non-finite box: every point stays a candidate)
+    p.em32 = std::isfinite(emax) ? std::ldexp(emax, -23) : INFINITY;
     if (!(emax > 0.0) || !std::isfinite(emax)) { // one point (or all equal): a single cell
         p.g[0] = p.g[1] = p.g[2] = 1;
         p.inv_h = 1.0;
@@ -654,7 +777,7 @@ size_t grid_scan_blocks(long long n) { return (size_t)((n + kScanChunk - 1) / kS
 
 void launch_grid_build(const double *mx, const double *my, const double *mz, int nm,
                        const GridParams &p, int *cid, int *count, int *start, int *bsum, int *fill,
-                       double4 *pts, hipStream_t st)
+                       double4 *pts, float4 *pts32, hipStream_t st)
 {
     const long long ncell = grid_cells(p);
     GridView gv{};
@@ -672,7 +795,8 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
     scan_local_kernel<<<nb, kScanThreads, 0, st>>>(count, n, start, bsum);
     scan_blocks_kernel<<<1, 1, 0, st>>>(bsum, nb);
     scan_add_kernel<<<nb, kScanThreads, 0, st>>>(start, n, bsum);
-    grid_scatter_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, cid, start, fill, pts);
+    grid_scatter_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, cid, start, fill, pts, pts32, p.c32[0], p.c32[1],
+                                                   p.c32[2]);
 }
 
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
@@ -785,44 +909,44 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
                            double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
                            hipStream_t st)
 {
-    // (lanes per query, run bounds read together, point loads in flight[, waves per SIMD forced]):
-    // ICP_GRID_SEEDED="G,KR,KU" picks one of the instantiated forms for A/B.  Default 2,2,2 (70
-    // VGPRs, 7 waves per SIMD), measured at C4 W = 1 (profiles/r04r): 106 us against 132 (4,2,4),
-    // 112 (4,2,2), 145 (4,1,4); forcing 8 waves spills (2,2,2,8: 110; 4,2,4,8: 199)
+    // (lanes per query, run bounds read together, point loads in flight; "f": the fp32 image with
+    // the fp64 decision for candidates, nn_grid_seeded32_kernel): ICP_GRID_SEEDED picks one of the
+    // instantiated forms for A/B.  fp64 forms measured at C4 W = 1 (profiles/r04r): 2,2,2 (70 VGPRs,
+    // 7 waves per SIMD) 106 us against 132 (4,2,4), 112 (4,2,2), 145 (4,1,4); forcing 8 waves
+    // spills (2,2,2 at 8 waves: 110 us; 4,2,4: 199)
+    struct Form {
+        const char *name;
+        int g;
+    };
+    static const Form forms[] = {{"2,2,2", 2}, {"4,2,2", 4}, {"4,2,4", 4}, {"2,2,4", 2},  {"f2,2,4", 2},
+                                 {"f2,2,2", 2}, {"f4,2,4", 4}, {"f2,4,4", 2}, {"f4,2,2", 4}, {"f2,2,8", 2},
+                                 {"f1,4,4", 1}};
     static const int form = [] {
         const char *e = getenv("ICP_GRID_SEEDED");
-        if (!e) return 7;
-        const std::string s(e);
-        const char *forms[] = {"4,2,4", "4,1,4", "4,4,4", "2,2,4", "2,4,4", "1,4,4", "4,2,2", "2,2,2",
-                               "4,2,4,8", "4,1,4,8", "4,2,2,8", "2,2,2,8", "2,2,4,8", "1,4,4,8", "1,2,2,8"};
+        if (!e) return 0;
         for (int i = 0; i < (int)(sizeof(forms) / sizeof(forms[0])); ++i)
-            if (s == forms[i]) return i;
+            if (std::string(e) == forms[i].name) return i;
         return 0;
     }();
-    static const int G_of[] = {4, 4, 4, 2, 2, 1, 4, 2, 4, 4, 4, 2, 2, 1, 1};
-    const int per_block = kBlock / G_of[form];
+    const int f = form >= 4 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
+    const int per_block = kBlock / forms[f].g;
     int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
     if (xcd_remap) blocks = (blocks + 7) / 8 * 8; // (whole eighths; the extra workgroups find no query)
-#define SEEDED(GG, R, U, W)                                                                                       \
-    nn_grid_seeded_kernel<GG, R, U, W><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, \
-                                                                  yy, yz, far_count, far_list, far_hint, stop,         \
-                                                                  xcd_remap ? 1 : 0)
-    switch (form) {
-    case 1: SEEDED(4, 1, 4, 1); break;
-    case 2: SEEDED(4, 4, 4, 1); break;
-    case 3: SEEDED(2, 2, 4, 1); break;
-    case 4: SEEDED(2, 4, 4, 1); break;
-    case 5: SEEDED(1, 4, 4, 1); break;
-    case 6: SEEDED(4, 2, 2, 1); break;
-    case 7: SEEDED(2, 2, 2, 1); break;
-    case 8: SEEDED(4, 2, 4, 8); break;
-    case 9: SEEDED(4, 1, 4, 8); break;
-    case 10: SEEDED(4, 2, 2, 8); break;
-    case 11: SEEDED(2, 2, 2, 8); break;
-    case 12: SEEDED(2, 2, 4, 8); break;
-    case 13: SEEDED(1, 4, 4, 8); break;
-    case 14: SEEDED(1, 2, 2, 8); break;
-    default: SEEDED(4, 2, 4, 1); break;
+#define SEEDED(K, ...)                                                                                       \
+    K<__VA_ARGS__><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz, far_count, \
+                                              far_list, far_hint, stop, xcd_remap ? 1 : 0)
+    switch (f) {
+    case 1: SEEDED(nn_grid_seeded_kernel, 4, 2, 2, 1); break;
+    case 2: SEEDED(nn_grid_seeded_kernel, 4, 2, 4, 1); break;
+    case 3: SEEDED(nn_grid_seeded_kernel, 2, 2, 4, 1); break;
+    case 4: SEEDED(nn_grid_seeded32_kernel, 2, 2, 4); break;
+    case 5: SEEDED(nn_grid_seeded32_kernel, 2, 2, 2); break;
+    case 6: SEEDED(nn_grid_seeded32_kernel, 4, 2, 4); break;
+    case 7: SEEDED(nn_grid_seeded32_kernel, 2, 4, 4); break;
+    case 8: SEEDED(nn_grid_seeded32_kernel, 4, 2, 2); break;
+    case 9: SEEDED(nn_grid_seeded32_kernel, 2, 2, 8); break;
+    case 10: SEEDED(nn_grid_seeded32_kernel, 1, 4, 4); break;
+    default: SEEDED(nn_grid_seeded_kernel, 2, 2, 2, 1); break;
     }
 #undef SEEDED
 }

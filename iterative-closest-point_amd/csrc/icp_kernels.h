@@ -268,6 +268,8 @@ struct GridParams {
     int g[3];
     double lo[3];
     double inv_h;
+    double c32[3]; // the box centre: the fp32 image's origin
+    double em32;   // bound on a model coordinate's error in the fp32 image
 };
 struct GridView {
     const double4 *pts; // model points sorted by cell: (x, y, z, original index)
@@ -275,6 +277,9 @@ struct GridView {
     int g[3];
     double lo[3];
     double inv_h;
+    const float4 *pts32 = nullptr; // (nullable) pts as fp32 offsets from c32, the index's bits in w
+    double c32[3] = {0.0, 0.0, 0.0};
+    double em32 = 0.0;
 };
 GridParams grid_params(const double *m_xyz, size_t nm); // host: bounding box, ~2 points/cell
 GridParams grid_params_box(const double lo[3], const double hi[3], size_t nm); // (from the model's box)
@@ -283,7 +288,7 @@ size_t grid_scan_blocks(long long n);
 // cid[nm], count/start[ncells + 1], bsum[grid_scan_blocks(ncells + 1)], fill[ncells], pts[nm]
 void launch_grid_build(const double *mx, const double *my, const double *mz, int nm,
                        const GridParams &p, int *cid, int *count, int *start, int *bsum, int *fill,
-                       double4 *pts, hipStream_t st);
+                       double4 *pts, float4 *pts32, hipStream_t st); // (pts32 nullable)
 // For queued query list[t] (t < *count_ptr) with candidate hint[t]: exact fp64 first minimum
 // over the grid box that must contain every point at least as close as the candidate ->
 // idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its window T_in[t]
@@ -341,6 +346,27 @@ void launch_nn_cpu_rule_window(int n, const double *px, const double *py, const 
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, int *idx, int *fb_count, int *fb_list, double *fb_T, hipStream_t st);
 
+struct IterState;
+// A pass's fold and step in its own last workgroup (icp_fold.h last_arrival; one rank, partial
+// rows of red_blocks(n) workgroups): the moments' reduce_kernel<17> + Horn step, or the
+// transform's reduce_kernel<1> + error step -- the same trees and bodies as the separate launches
+// (bit-identical), one launch fewer each.  ticket: the kernel kind's arrival counter (zero at rest).
+struct StepFold {
+    unsigned *ticket = nullptr; // nullptr: not fused (the caller launches the fold)
+    double *sums = nullptr;     // the folded sums (as reduce_horn / reduce_err write them)
+    double N = 0.0;
+    double c[3] = {0.0, 0.0, 0.0}; // (the Horn step's fp32-image centre)
+    int *cnt = nullptr;            // (the Horn step's NN queue counters)
+    IterState *s = nullptr;
+    // the error step's outputs
+    double threshold = 0.0;
+    int max_iter = 0;
+    double *err_trace = nullptr;
+    int *hflag = nullptr;
+    int hticket = 0;
+    IterState *h_state = nullptr;
+    double *h_trace = nullptr;
+};
 // ---- streaming reductions (deterministic two-stage, fp64) --------------------------
 int red_blocks(size_t n);
 // y = m[idx]; partial [sum p (3), sum y (3)]
@@ -416,7 +442,8 @@ struct SeedArgs {
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, const SeedArgs &sa, hipStream_t st);
+                              double *partials, const SeedArgs &sa, hipStream_t st,
+                              const StepFold &fold = StepFold{}); // (fold.ticket: + the fold and the error step)
 
 // ---- device-resident ICP iteration (icp_iter.hip) -----------------------------------
 // `stop` (NN launchers): when non-null and *stop != 0 the kernels return at once -- the
@@ -441,7 +468,8 @@ struct IterState {
 void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
                             double *partials, hipStream_t st, const int *kpos = nullptr,
-                            const double4 *m4kd = nullptr, bool y_ready = false); // (y_ready: y = m[idx] already)
+                            const double4 *m4kd = nullptr, bool y_ready = false, // (y_ready: y = m[idx] already)
+                            const StepFold &fold = StepFold{}); // (fold.ticket: + the fold and the Horn step)
 // (1 thread) NN queue sizes amb_count[0..3] -> nn_counts (unless done), then zeroed for the next
 // search; then, unless done, the Horn solve (icp_horn.h) from the reduced sums -- two-pass
 // sums (Σp, Σy, centred S, d_caps, sp) or, if shifted, launch_shifted_moments' -- and the

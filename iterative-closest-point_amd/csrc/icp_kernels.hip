@@ -28,6 +28,7 @@
 // ---------------------------------------------------------------------------------
 #include "icp_kernels.h"
 #include "icp_device.h"
+#include "icp_fold.h"
 #include "icp_mfma16.h"
 #include "icp_bundle_rec.h"
 
@@ -1734,9 +1735,10 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st,
-    double *__restrict__ partials, const int *__restrict__ kpos, const double4 *__restrict__ m4kd)
+    double *__restrict__ partials, const int *__restrict__ kpos, const double4 *__restrict__ m4kd, StepFold fold)
 {
-    if (st->done) return; // a frozen (converged) ICP iteration: its sums are never used
+    const bool frozen = st->done != 0; // a frozen (converged) ICP iteration: its sums are never used
+    if (frozen && !fold.ticket) return; // (fused: every workgroup still arrives; the Horn step runs)
     const double cp0 = st->shift_p[0], cp1 = st->shift_p[1], cp2 = st->shift_p[2];
     const double cy0 = st->shift_y[0], cy1 = st->shift_y[1], cy2 = st->shift_y[2];
     double a[17];
@@ -1747,7 +1749,7 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     // before the first sum: at C4 a thread has four points, and one by one their dependent
     // (index -> model point) loads ran back to back.  Same sums, same order: bit-identical.
     const int G = gridDim.x * kBlock;
-    for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += kMomBatch * G) {
+    for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < (frozen ? 0 : n); i0 += kMomBatch * G) {
         int j[kMomBatch];
         if constexpr (!YIN) {
 #pragma unroll
@@ -1783,7 +1785,17 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
             }
         }
     }
-    block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
+    if (!fold.ticket) {
+        block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
+        return;
+    }
+    // fused: reduce_horn_kernel's fold and Horn step in the last workgroup to arrive
+    block_sum_publish<17>(a, partials + (size_t)blockIdx.x * 17);
+    if (!last_arrival(fold.ticket)) return;
+    __shared__ double s_sum[17];
+    tail_fold<17>(partials, (int)gridDim.x, s_sum);
+    if (threadIdx.x < 17) fold.sums[threadIdx.x] = s_sum[threadIdx.x];
+    if (threadIdx.x == 0) horn_step_body(s_sum, fold.N, fold.c[0], fold.c[1], fold.c[2], 1, fold.cnt, fold.s);
 }
 
 // stride 1: SoA rows; stride 3 with x, y, z = p, p + 1, p + 2: an AoS cloud (e.g. mapped host)
@@ -1928,7 +1940,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
     int n, Xform xfv, const Xform *__restrict__ xfd, const int *__restrict__ done, int write_p,
-    float4 *__restrict__ p32, double *__restrict__ partials, SeedArgs sa)
+    float4 *__restrict__ p32, double *__restrict__ partials, SeedArgs sa, StepFold fold)
 {
     // xfd / done (device-resident loop): the transform comes from the device Horn solve, and
     // nothing is applied once the loop has converged.  One load per workgroup, via LDS.
@@ -1939,7 +1951,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         sxf = xfd ? *xfd : xfv;
     }
     __syncthreads();
-    if (sdone) return;
+    if (sdone && !fold.ticket) return; // (fused: every workgroup still arrives; the error step runs)
     const Xform xf = sxf;
     double a[1] = {0.0};
     int far = 0; // (sa.far_acc: this thread's moved points beyond sqrt(far_d2) of their correspondence)
@@ -1986,7 +1998,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         if (sa.far_acc) far_to_acc(far, sa.far_acc);
         return;
     }
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    for (int i = blockIdx.x * kBlock + threadIdx.x; i < (sdone ? 0 : n); i += gridDim.x * kBlock) {
         double q0, q1, q2;
         transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
         a[0] += residual2(yx[i], yy[i], yz[i], q0, q1, q2);
@@ -2010,8 +2022,23 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
             }
         }
     }
-    block_sum_store<1>(a, partials + blockIdx.x);
+    if (!fold.ticket) {
+        block_sum_store<1>(a, partials + blockIdx.x);
+        if (sa.far_acc) far_to_acc(far, sa.far_acc);
+        return;
+    }
+    // fused: reduce_err_kernel's fold and error step in the last workgroup to arrive (the far
+    // count is added first: the error step mirrors the loop state, far_acc included, to the host)
     if (sa.far_acc) far_to_acc(far, sa.far_acc);
+    block_sum_publish<1>(a, partials + blockIdx.x);
+    if (!last_arrival(fold.ticket)) return;
+    __shared__ double loc[1];
+    tail_fold<1>(partials, (int)gridDim.x, loc);
+    if (threadIdx.x == 0) {
+        fold.sums[kSumErr] = loc[0];
+        err_step_body(fold.sums, fold.N, fold.threshold, fold.max_iter, fold.err_trace, fold.s, fold.hflag,
+                      fold.hticket, fold.h_state, fold.h_trace);
+    }
 }
 
 // out[k] = sum_b partials[b*K + k], one workgroup, fixed order (deterministic): thread t
@@ -2456,7 +2483,8 @@ int red_blocks(size_t n) { return n <= (size_t)kRedSingle ? 1 : grid_for(n, kRed
 
 void launch_shifted_moments(const int *idx, const double4 *m4, const double *px, const double *py,
                             const double *pz, int n, double *yx, double *yy, double *yz, const IterState *st_dev,
-                            double *partials, hipStream_t st, const int *kpos, const double4 *m4kd, bool y_ready)
+                            double *partials, hipStream_t st, const int *kpos, const double4 *m4kd, bool y_ready,
+                            const StepFold &fold)
 {
     // points of a thread whose loads are issued together (A/B: ICP_MOM_BATCH = 1 | 2 | 4; same
     // sums).  C4 (four points a thread): 23.5 / 20.5 / 21.2 us at 1 / 2 / 4 (profiles/r03bd/)
@@ -2467,7 +2495,7 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
     }();
 #define MOMENTS(B, Y)                                                                                         \
     shifted_moments_kernel<B, Y><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, \
-                                                                   partials, kpos, m4kd)
+                                                                   partials, kpos, m4kd, fold)
     if (y_ready) {
         if (batch == 1) MOMENTS(1, true);
         else if (batch == 4) MOMENTS(4, true);
@@ -2574,15 +2602,16 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                           double *partials, hipStream_t st)
 {
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
-                                                            write_p, p32, partials, SeedArgs{});
+                                                            write_p, p32, partials, SeedArgs{}, StepFold{});
 }
 
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
-                              double *partials, const SeedArgs &sa, hipStream_t st)
+                              double *partials, const SeedArgs &sa, hipStream_t st, const StepFold &fold)
 {
+    // (the slot-record form ends without the fused step: its caller launches the error step)
     transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done, 1,
-                                                            p32, partials, sa);
+                                                            p32, partials, sa, sa.qop ? StepFold{} : fold);
 }
 
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st)

@@ -3,7 +3,16 @@
 #   tools/seeded_ab.sh TAG "form1 form2 ..."
 set -u
 O=gpurun_out/${1:-ab}; mkdir -p $O; export TMPDIR=/tmp
-FORMS=${2:-"4,2,4 4,1,4 4,2,2 2,2,2 4,2,4,8 4,2,2,8 2,2,2,8 1,2,2,8"}
+FORMS=${2:-"2,2,2 f2,2,4 f2,2,2 f4,2,4 f2,4,4 f4,2,2 f2,2,8 f1,4,4"}
+# the whole GPU suite on the defaults, then the exactness of the other forms (the policy
+# tests compare bit for bit)
+timeout -k 10 500 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 \
+  || { echo "GPU tests failed"; tail -15 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+for f in $FORMS; do
+  ICP_GRID_SEEDED=$f timeout -k 10 200 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_gpu_grid_policy.py > $O/t_$f.log 2>&1 || { echo "form $f: tests failed"; tail -5 $O/t_$f.log; exit 1; }
+done
 line() { python3 -c "
 import json,sys
 for l in open(sys.argv[1]):
@@ -15,6 +24,8 @@ for f in $FORMS; do
   ICP_GRID_SEEDED=$f timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_$f.log 2>&1 || exit 1
   line $O/b_$f.log "$f" | tee -a $O/summary.txt
 done
+ICP_FUSED_STEPS=0 timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_unfused.log 2>&1 || exit 1
+line $O/b_unfused.log "unfused" | tee -a $O/summary.txt
 for x in 0 2; do
   ICP_GRID_XCD=$x timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_xcd$x.log 2>&1 || exit 1
   line $O/b_xcd$x.log "xcd=$x" | tee -a $O/summary.txt
