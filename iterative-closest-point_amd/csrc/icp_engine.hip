@@ -2011,14 +2011,14 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         sa_grid.seedd = sa.seedd; // (grid_seeded_search reads them: no gather of the seed point)
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
-    // one rank, partials over several workgroups: the moments end in the Horn step and the
-    // transform in the error step, each in its own last workgroup (StepFold: one launch fewer
-    // each, bit-identical).  ICP_FUSED_STEPS=0: the separate fold launches (A/B)
+    // partials over several workgroups: the moments and the transform fold their partials in their
+    // own last workgroup (StepFold), and on one rank go on there to the Horn step / the error
+    // step -- one launch fewer each, bit-identical.  ICP_FUSED_STEPS=0: the separate launches (A/B)
     static const bool fused_steps_env = [] {
         const char *e = getenv("ICP_FUSED_STEPS");
         return !(e && atoi(e) == 0);
     }();
-    const bool fused_steps = fused_steps_env && !lag_run(ctx) && red_blocks(n) > 1;
+    const bool fused_steps = fused_steps_env && red_blocks(n) > 1;
     if (fused_steps && !ctx->fold_ticket) {
         HIPCHK(hipMalloc((void **)&ctx->fold_ticket, 2 * sizeof(unsigned)));
         HIPCHK(hipMemsetAsync(ctx->fold_ticket, 0, 2 * sizeof(unsigned), ctx->st));
@@ -2192,9 +2192,10 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 continue;
             } else {
                 StepFold mf;
-                if (fused_steps) { // (+ reduce_horn_kernel's fold and Horn step, in the last workgroup)
+                if (fused_steps) { // (+ the fold, and on one rank the Horn step, in the last workgroup)
                     mf.ticket = ctx->fold_ticket;
                     mf.sums = ctx->sums;
+                    mf.step = !lag;
                     mf.N = N;
                     for (int a = 0; a < 3; ++a) mf.c[a] = ctx->c[a];
                     mf.cnt = ctx->amb_count;
@@ -2204,7 +2205,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                        red_target(ctx, n, ctx->sums), ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr,
                                        ctx->m4kd, ctx->y_ready, mf);
                 if (fused_steps) {
-                    horn_fused = true;
+                    horn_fused = !lag; // (multi-rank: the all-reduce, then the lagged error + Horn step below)
                 } else if (!lag && red_blocks(n) > 1) { // the fold and the Horn step in one launch
                     launch_reduce_horn(ctx->partials, red_blocks(n), ctx->sums, N, ctx->c, 1, ctx->amb_count, sd,
                                        ctx->st);
@@ -2229,7 +2230,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             const SeedArgs &sa_t = grid_next ? sa_grid : sa;
             StepFold ef;
             const bool err_fused = fused_steps && !sa_t.qop; // (the slot-record form keeps its own launch)
-            if (err_fused) { // (+ reduce_err_kernel's fold and error step, in the last workgroup)
+            if (err_fused && lag) { // (the fold only: the residual rides on the next all-reduce)
+                ef.ticket = ctx->fold_ticket + 1;
+                ef.sums = ctx->sums;
+                ef.step = false;
+            } else if (err_fused) { // (+ reduce_err_kernel's fold and error step, in the last workgroup)
                 const int sl = enqueued % kRing;
                 slot_ticket[sl] = ++ctx->flag_ticket;
                 ef.ticket = ctx->fold_ticket + 1;
@@ -2248,7 +2253,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                      red_target(ctx, n, ctx->sums + kSumErr), sa_t, ctx->st, ef);
             if (!need_p32) ctx->p32_stale = true;
             const bool fold_err = !lag && red_blocks(n) > 1; // (folded by the error step's launch)
-            if (!fold_err) red_finish(ctx, n, 1, ctx->sums + kSumErr);
+            if (!fold_err && !err_fused) red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
             if (!lag && !err_fused) TRY(enqueue_err_step(enqueued, fold_err ? ctx->partials : nullptr));

@@ -353,7 +353,8 @@ struct IterState;
 // (bit-identical), one launch fewer each.  ticket: the kernel kind's arrival counter (zero at rest).
 struct StepFold {
     unsigned *ticket = nullptr; // nullptr: not fused (the caller launches the fold)
-    double *sums = nullptr;     // the folded sums (as reduce_horn / reduce_err write them)
+    double *sums = nullptr;     // the folded sums (as reduce_horn / reduce_err / reduce_kernel write them)
+    bool step = true;           // false: the fold only (a multi-rank run: the all-reduce and the steps follow)
     double N = 0.0;
     double c[3] = {0.0, 0.0, 0.0}; // (the Horn step's fp32-image centre)
     int *cnt = nullptr;            // (the Horn step's NN queue counters)

@@ -1795,7 +1795,7 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     __shared__ double s_sum[17];
     tail_fold<17>(partials, (int)gridDim.x, s_sum);
     if (threadIdx.x < 17) fold.sums[threadIdx.x] = s_sum[threadIdx.x];
-    if (threadIdx.x == 0) horn_step_body(s_sum, fold.N, fold.c[0], fold.c[1], fold.c[2], 1, fold.cnt, fold.s);
+    if (fold.step && threadIdx.x == 0) horn_step_body(s_sum, fold.N, fold.c[0], fold.c[1], fold.c[2], 1, fold.cnt, fold.s);
 }
 
 // stride 1: SoA rows; stride 3 with x, y, z = p, p + 1, p + 2: an AoS cloud (e.g. mapped host)
@@ -2036,8 +2036,9 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     tail_fold<1>(partials, (int)gridDim.x, loc);
     if (threadIdx.x == 0) {
         fold.sums[kSumErr] = loc[0];
-        err_step_body(fold.sums, fold.N, fold.threshold, fold.max_iter, fold.err_trace, fold.s, fold.hflag,
-                      fold.hticket, fold.h_state, fold.h_trace);
+        if (fold.step)
+            err_step_body(fold.sums, fold.N, fold.threshold, fold.max_iter, fold.err_trace, fold.s, fold.hflag,
+                          fold.hticket, fold.h_state, fold.h_trace);
     }
 }
 
