@@ -70,7 +70,7 @@ __device__ __forceinline__ void horn_step_body(const double *__restrict__ sums, 
 
 __device__ __forceinline__ void err_step_body(const double *__restrict__ sums, double N, double threshold, int max_iter,
                               double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag, int ticket,
-                              IterState *h_state, double *h_trace)
+                              IterState *h_state, double *h_trace, bool far_coherent = false)
 {
     if (!s->done) {
         const double e = sums[kSumErr];
@@ -79,11 +79,12 @@ __device__ __forceinline__ void err_step_body(const double *__restrict__ sums, d
         h_trace[s->iter] = err; // mapped host copies: the run's result needs no copy back
         s->iter += 1;
         if (err < threshold || s->iter >= max_iter) s->done = 1; // gpu.cc:79-80
-        // (agent-scope loads: a fused transform's workgroups added to s->far_acc in this launch)
         const int *src = (const int *)s;
         int *dst = (int *)h_state;
-        for (size_t k = 0; k < sizeof(IterState) / sizeof(int); ++k)
-            dst[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (size_t k = 0; k < sizeof(IterState) / sizeof(int); ++k) dst[k] = src[k];
+        // (far_coherent: s is global and this launch's workgroups added to s->far_acc -- a fused
+        // transform -- so its count is read at agent scope; s may be an LDS copy otherwise)
+        if (far_coherent) h_state->far_acc = __hip_atomic_load(&s->far_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // (done, iter) to the host (mapped memory), then the ticket the host spins on
     __hip_atomic_store(hflag, s->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

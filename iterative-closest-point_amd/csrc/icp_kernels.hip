@@ -2038,7 +2038,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         fold.sums[kSumErr] = loc[0];
         if (fold.step)
             err_step_body(fold.sums, fold.N, fold.threshold, fold.max_iter, fold.err_trace, fold.s, fold.hflag,
-                          fold.hticket, fold.h_state, fold.h_trace);
+                          fold.hticket, fold.h_state, fold.h_trace, true);
     }
 }
 
