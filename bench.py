@@ -62,14 +62,17 @@ REF_README_MS = {
 }
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, cfg=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950 correction)."""
+    (written by tools/pmc_summary.py from separate FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE
+    doubled per the gfx950 correction): profiles/<tag>_pmc_traffic.json for this bench at C4 on
+    one GPU, profiles/<tag>_<cfg>_pmc_traffic.json for another workload (cfg "c5shard": rank 0's
+    shard of the 8-way C5, tools/gpu_round.sh c5pmc)."""
     import glob
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
     from roofline import _tag_key
-    paths = glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))
+    paths = glob.glob(os.path.join(ROOT, "profiles", f"*_{cfg}_pmc_traffic.json" if cfg else "*_pmc_traffic.json"))
+    if not cfg:  # (this bench's own captures: <tag>_pmc_traffic.json, no workload label)
+        paths = [f for f in paths if os.path.basename(f).count("_") == 2]
     for path in sorted(paths, key=lambda f: _tag_key(os.path.basename(f).split("_")[0]), reverse=True):
         try:
             k = json.load(open(path))["kernels"].get(kernel)
@@ -592,7 +595,9 @@ def main():
         # resolve (launch_nn_grid_resolve_all) scans each query's complete candidate box; AUTO
         # takes it by icp_run's policy once the scene is near the model
         kernel = GRID_SEEDED_KERNEL
-    traffic, traffic_src = pmc_traffic(kernel) if world == 1 and args.n == 1 << 20 else (None, None)
+    # the capture of this workload's kernels: C4 on one GPU, or rank 0's shard of the 8-way C5
+    traffic_cfg = {(1 << 20, 1): "", (1 << 23, 8): "c5shard"}.get((args.n, world))
+    traffic, traffic_src = pmc_traffic(kernel, traffic_cfg) if traffic_cfg is not None else (None, None)
     nn_s = nn_avg_ms * 1e-3
     compulsory = 16.0 * c + 12.0 * args.n  # §8d: fp32 xyz in (scene shard + model), int32 index out
     nn_hbm = {"compulsory_bytes": compulsory,

@@ -75,6 +75,17 @@ for s in $STEPS; do
             run sqs2 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE \
                 --output-format csv -d "$OUT/sqs2" -o sq -- python3 tools/nn_probe.py --variant mfma16 --icp 4 ;;
     cfg16) for c in 21 22 24 41 42; do ICP_MFMA16_CFG=$c run probe16_$c 300 python3 tools/nn_probe.py --variant mfma16; done ;;
+    c5pmc) # rank 0's shard of the 8-way C5 (1-rank RCCL): kernel trace + FETCH / WRITE passes
+           run rocprof_c5shard 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5shard" -o c5shard -- \
+               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 10 --warmup 2 &&
+           run pmc_c5shard_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_c5shard1" -o fetch -- \
+               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 3 --warmup 2 &&
+           run pmc_c5shard_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_c5shard2" -o write -- \
+               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 3 --warmup 2 ;;
+    c5dist8) # the 8-rank C5 flow rehearsed on one GPU (8 processes, sums through gloo)
+           ICP_BENCH_HOST_REDUCE=1 run bench_c5_dist8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+               --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 8 --points 8388608 --steps 10 --warmup 2 \
+               --no-cpu-baseline --no-cow --no-cases ;;
     shard) run shard_c4 600 python tools/shard_probe.py --worlds 1 2 4 8 &&
            run shard_c5 600 python tools/shard_probe.py --n 8388608 --worlds 8 --steps 5 --warmup 2 ;;
     profshard) run rocprof_shard8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_shard8" -o shard -- \
