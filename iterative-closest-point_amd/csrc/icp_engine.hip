@@ -683,14 +683,14 @@ constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger mod
 // around its seed (the previous correspondence) with a few lanes, if it has at most kSeededBox
 // cells; the queries with a bigger box go to the resolver with a whole wave each (flattened scan,
 // loads in flight: a big box is one query's long chain of dependent loads in the first pass),
-// and what is over the cell budget to the fp64 brute force.  Every level returns the exact first
-// minimum.  kpos is kept when the bundle's kd tables exist (the moments then gather from the
-// kd-ordered model).
+// which scans what is over the cell budget over every model point in place.  Every level returns
+// the exact first minimum.  With the seed distances (seedd) the passes also write each query's
+// correspondence y (the moments stream it); without them kpos is kept when the bundle's kd tables
+// exist (the moments then gather from the kd-ordered model).
 constexpr int kSeededBox = 125;
 static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop, const double *seedd,
                               hipEvent_t ev1)
 {
-    const int inline_nm = ctx->nm <= kInlineFallbackModel ? (int)ctx->nm : 0;
     TRY(grow(ctx, &ctx->amb1, &ctx->amb1_cap, n));
     TRY(grow(ctx, &ctx->amb1_hint, &ctx->amb1_hint_cap, n));
     TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
@@ -721,13 +721,13 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     // the second pass: a whole wave per queued query, grid-striding over the device-side count
     // (sized for a few thousand -- the policy keeps the queue short; a launch of 4,096 idle
     // workgroups cost ~6 us a search, r04q)
+    // A box over the budget (grid_budget: 65,536 cells at C4 -- a non-finite query, or one about a
+    // model extent away) is scanned in place over every model point by its wave (the exact fp64
+    // first minimum), instead of a brute-force launch that nearly always finds nothing to do
+    // (~5 us a search)
     launch_nn_grid_resolve(ctx->amb_count + 2, (int)std::min<size_t>(n, 4096), ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                            grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
-                           ctx->fb_T, ctx->st, stop, inline_nm, kpos_out, ctx->kd_of, 64, yx, yy, yz);
-    if (!inline_nm)
-        launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32, ctx->model.x,
-                          ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st, stop, kpos_out,
-                          ctx->kd_of, yx, yy, yz);
+                           ctx->fb_T, ctx->st, stop, (int)ctx->nm, kpos_out, ctx->kd_of, 64, yx, yy, yz);
     LAUNCHCHK("grid_seeded_search");
     ctx->kpos_valid = kpos_out != nullptr;
     ctx->y_ready = y_out;
