@@ -259,6 +259,19 @@ int icp_set_index_digest(icp_ctx *ctx, size_t cap);
 /* Test instrumentation: 1 = audit every f16-certified query (extra fp64 work per query and
  * three atomics; results in icp_stats.cert_*), 0 = off (the default). */
 int icp_set_cert_audit(icp_ctx *ctx, int enable);
+/* Test instrumentation of the bundle filter's exclusions (a model with its bundle images, a
+ * resident scene with correspondences): `groups` 32-query groups of the scene, each query's
+ * correspondence as its seed, against every bundle.  max_err_ratio = max over the evaluated
+ * (query, bundle) pairs of |V^ - (V - mu_q - mu_c)| / (mu_q + mu_c) (the exclusion is sound
+ * while < 1); over the excluded pairs near the bound, violations counts a bundle holding a
+ * point at least as close as the seed (0 when sound) and min_gap the smallest relative D64 gap
+ * (D64 min - D_seed) / D_seed.  Synchronous; ICP_E_NO_MODEL without bundle images or seeds. */
+typedef struct icp_bundle_audit_result {
+    double max_err_ratio;
+    double min_gap;
+    long long pairs, excluded, checked, violations;
+} icp_bundle_audit_result;
+int icp_bundle_audit(icp_ctx *ctx, int groups, icp_bundle_audit_result *out);
 int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap);
 
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out);

@@ -1252,6 +1252,105 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QG == 4 
     }
 }
 
+// Bundle-bound audit (icp_bundle_audit; tests only).  For the sampled 32-query groups (the
+// resident scene's queries j0 .. j0 + 31 with their current correspondences as seeds, records
+// built as bundle_record builds them) against every bundle of the model: V^ from the same
+// v_mfma_f32_32x32x16_f16 on the same operands as the stream (A = the bundle image, B = the
+// query operand), against V = |q^ - c^|^2 - (d' + r')^2 in fp64 from the values the operands
+// represent.  The margins folded into the operands make V^ = V - mu_q - mu_c + eps, and the
+// exclusion V^ > 0 => V > 0 is sound while |eps| < mu_q + mu_c: the kernel records
+// max |eps| / (mu_q + mu_c) over every evaluated pair.  For the excluded pairs near the bound
+// (V^ > 0 but |q^ - c^| < 2 (d' + r')) it also checks the geometry the exclusion claims: every
+// point of the bundle strictly farther (D64) than the seed.  out[0]: the max ratio, out[1]: the
+// min (D64 min - D_seed) / D_seed over the checked pairs (as bits: both non-negative unless a
+// violation, which cnt[2] counts); cnt: pairs, excluded, violations, checked.
+__global__ __launch_bounds__(64) void bundle_audit_kernel(
+    const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz,
+    const int *__restrict__ idx, const double4 *__restrict__ m4, int n, int gstride, const half8_t *__restrict__ bimg,
+    const double4 *__restrict__ bctr, const int *__restrict__ kd_orig, int nm, int nblk, double cx, double cy,
+    double cz, double scale, unsigned long long *__restrict__ out, unsigned long long *__restrict__ cnt)
+{
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * gstride * 32 + (lane & 31);
+    const bool valid = j < n;
+    double p[3] = {0.0, 0.0, 0.0}, D = 0.0;
+    if (valid) {
+        p[0] = px[j];
+        p[1] = py[j];
+        p[2] = pz[j];
+        const double4 mh = m4[idx[j]];
+        const double dx = p[0] - mh.x, dy = p[1] - mh.y, dz = p[2] - mh.z;
+        D = (dx * dx + dy * dy) + dz * dz; // (the transform's seed distance, bundle_record's D)
+    }
+    double a[3];
+    a[0] = fmin(fmax((p[0] - cx) * scale, -kF16QueryClamp), kF16QueryClamp);
+    a[1] = fmin(fmax((p[1] - cy) * scale, -kF16QueryClamp), kF16QueryClamp);
+    a[2] = fmin(fmax((p[2] - cz) * scale, -kF16QueryClamp), kF16QueryClamp);
+    const double eq = 0x1.0p-20 * ((fabs(a[0]) + fabs(a[1])) + fabs(a[2])) + 0x1.0p-22;
+    const double dq = (sqrt(D) * scale * (1.0 + 0x1.0p-40) + 1e-300 + eq) * (1.0 + 0x1.0p-20) + 0x1.0p-20;
+    const bool normal = valid && fabs(a[0]) <= kBQueryMax && fabs(a[1]) <= kBQueryMax && fabs(a[2]) <= kBQueryMax &&
+                        dq <= kBSeedMax;
+    const half8_t qf = bundle_query_frag(a, dq, valid ? (normal ? kBqNormal : kBqForced) : kBqNever, lane >> 5);
+    double qh[3];
+    for (int k = 0; k < 3; ++k) {
+        _Float16 hi, lo;
+        split_f16(a[k], hi, lo);
+        qh[k] = (double)hi + (double)lo;
+    }
+    const double qq = (qh[0] * qh[0] + qh[1] * qh[1]) + qh[2] * qh[2];
+    const double muq = 0x1.0p-16 * (qq + dq * dq) + 0x1.0p-4;
+    const f32x16_t zero = {};
+    double worst = 0.0, gap = INFINITY;
+    unsigned long long pairs = 0, excl = 0, viol = 0, checked = 0;
+    for (int g = blockIdx.y; g < nblk; g += gridDim.y) {
+        const f32x16_t d = __builtin_amdgcn_mfma_f32_32x32x16_f16(bimg[(size_t)g * 64 + lane], qf, zero, 0, 0, 0);
+        if (!normal) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int b = g * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); // (this lane's column: its query)
+            const double4 c = bctr[b];
+            if (!(c.w >= 0.0 && c.w < INFINITY)) continue; // (padding / a bundle searched always)
+            const double e0 = qh[0] - c.x, e1 = qh[1] - c.y, e2 = qh[2] - c.z;
+            const double dist2 = (e0 * e0 + e1 * e1) + e2 * e2, s = dq + c.w;
+            const double V = dist2 - s * s;
+            const double muc = 0x1.0p-16 * ((c.x * c.x + c.y * c.y + c.z * c.z) + c.w * c.w) + 0x1.0p-4;
+            const double Vh = (double)d[r];
+            worst = fmax(worst, fabs(Vh - (V - muq - muc)) / (muq + muc));
+            ++pairs;
+            if (!(Vh > 0.0)) continue;
+            ++excl;
+            if (dist2 >= 4.0 * s * s) continue; // (far bundles: the margin is the whole distance)
+            ++checked;
+            double dmin = INFINITY;
+            for (int k = 0; k < kBundle; ++k) {
+                const int o = kd_orig[(size_t)b * kBundle + k];
+                if (o < 0 || o >= nm) continue;
+                const double4 m = m4[o];
+                const double fx = p[0] - m.x, fy = p[1] - m.y, fz = p[2] - m.z;
+                dmin = fmin(dmin, (fx * fx + fy * fy) + fz * fz);
+            }
+            if (!(dmin > D)) ++viol;
+            else gap = fmin(gap, (dmin - D) / fmax(D, 1e-300));
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        worst = fmax(worst, __shfl_xor(worst, o, 64));
+        gap = fmin(gap, __shfl_xor(gap, o, 64));
+        pairs += __shfl_xor(pairs, o, 64);
+        excl += __shfl_xor(excl, o, 64);
+        viol += __shfl_xor(viol, o, 64);
+        checked += __shfl_xor(checked, o, 64);
+    }
+    if (lane == 0) { // (non-negative doubles order as their bits)
+        atomicMax(out, (unsigned long long)__double_as_longlong(worst));
+        atomicMin(out + 1, (unsigned long long)__double_as_longlong(gap));
+        atomicAdd(cnt, pairs);
+        atomicAdd(cnt + 1, excl);
+        atomicAdd(cnt + 2, viol);
+        atomicAdd(cnt + 3, checked);
+    }
+}
+
 } // namespace
 
 int bundle_pad(size_t nm) // bundles, padded to whole LDS tiles
@@ -1328,6 +1427,18 @@ void launch_build_bundle_images(const double *mx, const double *my, const double
                                                                    scale, (half8_t *)bimg, bctr);
     const int nbb = nb_pad >> 5;
     build_block_bounds_kernel<<<(nbb + 1 + kBlock - 1) / kBlock, kBlock, 0, st>>>(bctr, nbb, blk);
+}
+
+void launch_bundle_audit(const double *px, const double *py, const double *pz, const int *idx, const double4 *m4,
+                         int n, int groups, const void *bimg, const double4 *bctr, const int *kd_orig, int nm,
+                         int nb_pad, const double c[3], double scale, unsigned long long *out,
+                         unsigned long long *cnt, hipStream_t st)
+{
+    const int ng = std::max(1, std::min(groups, (n + 31) / 32));
+    const int gstride = std::max(1, (n + 32 * ng - 1) / (32 * ng)); // (groups spread over the scene)
+    const int nblk = nb_pad >> 5;
+    bundle_audit_kernel<<<dim3(ng, 64), 64, 0, st>>>(px, py, pz, idx, m4, n, gstride, (const half8_t *)bimg, bctr,
+                                                    kd_orig, nm, nblk, c[0], c[1], c[2], scale, out, cnt);
 }
 
 void launch_build_kd_tables(const double4 *m4, const int *kd_orig, int nm, double4 *m4kd, int *kd_of, hipStream_t st)

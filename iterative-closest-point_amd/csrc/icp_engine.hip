@@ -2709,6 +2709,41 @@ int icp_set_cert_audit(icp_ctx *ctx, int enable)
     return cert_audit_reset(ctx);
 }
 
+int icp_bundle_audit(icp_ctx *ctx, int groups, icp_bundle_audit_result *out)
+{
+    if (!ctx || !out || groups < 1) return ICP_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    const DevCloud &P = ctx->scene;
+    if (!ctx->b_img || !ctx->b_bctr || !ctx->b_kd_orig || ctx->nb_pad <= 0 || !P.n || !ctx->seeds_valid)
+        return fail(ctx, ICP_E_NO_MODEL, "icp_bundle_audit: needs the bundle images and a scene with correspondences");
+    unsigned long long *buf = nullptr;
+    HIPCHK(hipMalloc((void **)&buf, 6 * sizeof(unsigned long long)));
+    const double inf = INFINITY;
+    unsigned long long init[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+    std::memcpy(&init[1], &inf, sizeof(double));
+    int rc = ICP_OK;
+    if (hipMemcpyAsync(buf, init, sizeof(init), hipMemcpyHostToDevice, ctx->st) != hipSuccess) rc = ICP_E_HIP;
+    if (rc == ICP_OK) {
+        launch_bundle_audit(P.x, P.y, P.z, ctx->idx, ctx->m4, (int)P.n, groups, ctx->b_img, ctx->b_bctr, ctx->b_kd_orig,
+                            (int)ctx->nm, ctx->nb_pad, ctx->c, ctx->scale16, buf, buf + 2, ctx->st);
+        unsigned long long h[6];
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(h, buf, sizeof(h), hipMemcpyDeviceToHost, ctx->st) != hipSuccess ||
+            hipStreamSynchronize(ctx->st) != hipSuccess) {
+            rc = ICP_E_HIP;
+        } else {
+            std::memcpy(&out->max_err_ratio, &h[0], sizeof(double));
+            std::memcpy(&out->min_gap, &h[1], sizeof(double));
+            out->pairs = (long long)h[2];
+            out->excluded = (long long)h[3];
+            out->violations = (long long)h[4];
+            out->checked = (long long)h[5];
+        }
+    }
+    (void)hipFree(buf);
+    return rc == ICP_OK ? ICP_OK : fail(ctx, rc, "icp_bundle_audit: HIP error");
+}
+
 int icp_get_model_order(icp_ctx *ctx, int32_t *kd_out)
 {
     if (!ctx || !kd_out) return ICP_E_ARG;

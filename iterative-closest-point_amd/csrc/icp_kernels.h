@@ -178,6 +178,14 @@ void launch_build_local_images(const double *mx, const double *my, const double 
 void launch_build_bundle_images(const double *mx, const double *my, const double *mz, int nm, const int *kd,
                                 int nb_pad, const double c[3], double scale, void *bimg, void *pimg, int *kd_orig,
                                 double4 *bctr, double4 *blk, hipStream_t st);
+// the bundle bound's audit (tests: icp_bundle_audit): `groups` 32-query groups of the scene with
+// their correspondences as seeds against every bundle; out[0] max |eps| / (mu_q + mu_c) and
+// out[1] the min relative D64 gap of the checked excluded pairs, as double bits (init 0 / +inf);
+// cnt: pairs, excluded, violations, checked (init 0)
+void launch_bundle_audit(const double *px, const double *py, const double *pz, const int *idx, const double4 *m4,
+                         int n, int groups, const void *bimg, const double4 *bctr, const int *kd_orig, int nm,
+                         int nb_pad, const double c[3], double scale, unsigned long long *out,
+                         unsigned long long *cnt, hipStream_t st);
 NNPlan plan_nn_bundle(size_t np, int nb_pad);
 // Seeded search (prev: each query's seed index, seed16 its f16 shift): partial (best, second,
 // original index) per (split, query) in the format of launch_nn_mfma16 (same finalize).

@@ -65,6 +65,7 @@ EXPORTED = [
     "icp_ensure_model", "icp_subtract_col", "icp_get_indices", "icp_set_index_digest",
     "icp_get_index_digest", "icp_set_cert_audit", "icp_set_run_mode", "icp_set_nn_rule",
     "icp_get_comm_info", "icp_set_bundle_counters", "icp_get_bundle_counters", "icp_get_model_order",
+    "icp_bundle_audit",
 ]
 
 
@@ -88,6 +89,11 @@ class Stats(C.Structure):
                 ("persistent_runs", C.c_longlong), ("cpu_rule_ties", C.c_longlong),
                 ("cpu_rule_changed", C.c_longlong), ("persistent_fallbacks", C.c_longlong),
                 ("last_filter", C.c_int)]
+
+
+class BundleAudit(C.Structure):
+    _fields_ = [("max_err_ratio", C.c_double), ("min_gap", C.c_double), ("pairs", C.c_longlong),
+                ("excluded", C.c_longlong), ("checked", C.c_longlong), ("violations", C.c_longlong)]
 
 
 # icp_stats.last_filter (ICP_FILTER_*): the search level that decided most queries
@@ -149,6 +155,7 @@ def lib() -> C.CDLL:
     L.icp_set_index_digest.argtypes = [vp, sz]
     L.icp_get_index_digest.argtypes = [vp, C.POINTER(C.c_uint64), sz]
     L.icp_set_cert_audit.argtypes = [vp, C.c_int]
+    L.icp_bundle_audit.argtypes = [vp, C.c_int, C.POINTER(BundleAudit)]
     L.icp_get_stats.argtypes = [vp, C.POINTER(Stats)]
     L.icp_reset_stats.argtypes = [vp]
     L.icp_set_bundle_counters.argtypes = [vp, C.c_int]
@@ -380,6 +387,14 @@ class Context:
 
     def set_cert_audit(self, on: bool):
         self._check(lib().icp_set_cert_audit(self._h, 1 if on else 0))
+
+    def bundle_audit(self, groups: int = 64) -> dict:
+        """The bundle bound's exclusions checked on `groups` 32-query groups of the resident
+        scene (icp_bundle_audit): max MFMA error over its margin, and the excluded bundles'
+        geometry (violations must be 0)."""
+        out = BundleAudit()
+        self._check(lib().icp_bundle_audit(self._h, int(groups), C.byref(out)))
+        return {f: getattr(out, f) for f, _ in BundleAudit._fields_}
 
     def index_digest(self, k: int | None = None) -> np.ndarray:
         """(k, 3) uint64: per icp_run iteration (sum idx, sum (j+1) idx[j], #{idx[j] == j})."""

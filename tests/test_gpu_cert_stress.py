@@ -17,6 +17,8 @@ must show the winner's filter error below its bound on every certified query:
 
 The audit's two figures (max |G^ - G64| / delta_b, min certified margin) are printed and
 written to gpurun_out/cert_stress.json when that directory exists; DESIGN.md §3.1 quotes them.
+Behind the bundle bound, icp_bundle_audit also checks its exclusions on every scene: the MFMA's
+bound value against its folded margins, and the geometry of the excluded bundles near the bound.
 """
 import json
 import os
@@ -125,7 +127,9 @@ def run(amd, nn_mode, variant, m, q, iters):
         ctx.reset_stats()
         ctx.set_scene(q)
         res, errs = ctx.run(iters, -1.0)
-        return idx0, st0, res, errs, ctx.get_scene(), ctx.get_indices(), ctx.stats()
+        # the bundle bound's exclusions audited against the last correspondences as seeds
+        audit = ctx.bundle_audit(64) if variant == amd.VARIANT_BUNDLE else None
+        return idx0, st0, res, errs, ctx.get_scene(), ctx.get_indices(), ctx.stats(), audit
 
 
 @pytest.mark.parametrize("variant", ["mfma16", "bundle"])
@@ -154,6 +158,19 @@ def test_f16_certificate_adversarial(amd, name, variant):
     if name != "clusters":
         assert d[1]["cert_audited"] > 0 and d[6]["cert_audited"] > 0
     if variant != "mfma16":
+        #  the bundle exclusions keep their margin: the MFMA's V^ off the value its
+        # operands represent by less than the folded margins mu_q + mu_c on every evaluated
+        # (query, bundle) pair, and no excluded bundle near the bound holds a point as close as
+        # the seed
+        au = d[7]
+        print(name, "bundle audit", json.dumps(au))
+        assert au["violations"] == 0, au
+        if au["pairs"]:
+            assert au["max_err_ratio"] < 1.0, au
+        if name not in ("clusters", "far_queries"):
+            assert au["pairs"] > 0 and au["checked"] > 0, au
+        AUDIT.setdefault("bundle_audit", {})[name] = au
+        _dump()
         return
     AUDIT[name] = {"unseeded": {k: d[1][k] for k in ("cert_max_err_ratio", "cert_min_margin", "cert_audited",
                                                      "level1_queued", "grid_fallback")},
@@ -161,6 +178,10 @@ def test_f16_certificate_adversarial(amd, name, variant):
                                                     "level1_queued", "grid_fallback")},
                    "n_model": int(m.shape[0]), "n_queries": int(q.shape[0])}
     print(name, json.dumps(AUDIT[name]))
+    _dump()
+
+
+def _dump():
     out = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(out):
         with open(os.path.join(out, "cert_stress.json"), "w") as fh:
