@@ -2011,15 +2011,20 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         sa_grid.seedd = sa.seedd; // (grid_seeded_search reads them: no gather of the seed point)
     }
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
-    // partials over several workgroups: the moments and the transform fold their partials in their
-    // own last workgroup (StepFold), and on one rank go on there to the Horn step / the error
-    // step -- one launch fewer each, bit-identical.  ICP_FUSED_STEPS=0: the separate launches (A/B)
-    static const bool fused_steps_env = [] {
+    // partials over several workgroups: the moments and / or the transform may fold their
+    // partials in their own last workgroup (StepFold), and on one rank go on there to the Horn
+    // step / the error step -- one launch fewer each, bit-identical.  ICP_FUSED_STEPS = bit 0:
+    // the moments, bit 1: the transform; 0 (the default): the separate launches.  Measured at C4
+    // (profiles/r04r): both fused 0.183 ms per iteration against 0.164 separate -- the last
+    // workgroup's fold reads the rows coherently (sc1: past L2), and the moments kernel with the
+    // Horn solve inlined holds 128 VGPRs
+    static const int fused_steps_env = [] {
         const char *e = getenv("ICP_FUSED_STEPS");
-        return !(e && atoi(e) == 0);
+        return e ? atoi(e) & 3 : 0;
     }();
-    const bool fused_steps = fused_steps_env && red_blocks(n) > 1;
-    if (fused_steps && !ctx->fold_ticket) {
+    const bool fused_moments = (fused_steps_env & 1) && red_blocks(n) > 1;
+    const bool fused_steps = (fused_steps_env & 2) && red_blocks(n) > 1; // (the transform's)
+    if ((fused_steps || fused_moments) && !ctx->fold_ticket) {
         HIPCHK(hipMalloc((void **)&ctx->fold_ticket, 2 * sizeof(unsigned)));
         HIPCHK(hipMemsetAsync(ctx->fold_ticket, 0, 2 * sizeof(unsigned), ctx->st));
     }
@@ -2192,7 +2197,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 continue;
             } else {
                 StepFold mf;
-                if (fused_steps) { // (+ the fold, and on one rank the Horn step, in the last workgroup)
+                if (fused_moments) { // (+ the fold, and on one rank the Horn step, in the last workgroup)
                     mf.ticket = ctx->fold_ticket;
                     mf.sums = ctx->sums;
                     mf.step = !lag;
@@ -2204,7 +2209,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 launch_shifted_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd,
                                        red_target(ctx, n, ctx->sums), ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr,
                                        ctx->m4kd, ctx->y_ready, mf);
-                if (fused_steps) {
+                if (fused_moments) {
                     horn_fused = !lag; // (multi-rank: the all-reduce, then the lagged error + Horn step below)
                 } else if (!lag && red_blocks(n) > 1) { // the fold and the Horn step in one launch
                     launch_reduce_horn(ctx->partials, red_blocks(n), ctx->sums, N, ctx->c, 1, ctx->amb_count, sd,

@@ -919,8 +919,8 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
         int g;
     };
     static const Form forms[] = {{"2,2,2", 2}, {"4,2,2", 4}, {"4,2,4", 4}, {"2,2,4", 2},  {"f2,2,4", 2},
-                                 {"f2,2,2", 2}, {"f4,2,4", 4}, {"f2,4,4", 2}, {"f4,2,2", 4}, {"f2,2,8", 2},
-                                 {"f1,4,4", 1}};
+                                 {"f2,2,2", 2}, {"f4,2,4", 4}, {"f2,4,4", 2}, {"f4,2,2", 4}, {"4,1,2", 4},
+                                 {"f4,1,2", 4}};
     static const int form = [] {
         const char *e = getenv("ICP_GRID_SEEDED");
         if (!e) return 0;
@@ -944,8 +944,8 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     case 6: SEEDED(nn_grid_seeded32_kernel, 4, 2, 4); break;
     case 7: SEEDED(nn_grid_seeded32_kernel, 2, 4, 4); break;
     case 8: SEEDED(nn_grid_seeded32_kernel, 4, 2, 2); break;
-    case 9: SEEDED(nn_grid_seeded32_kernel, 2, 2, 8); break;
-    case 10: SEEDED(nn_grid_seeded32_kernel, 1, 4, 4); break;
+    case 9: SEEDED(nn_grid_seeded_kernel, 4, 1, 2, 1); break;
+    case 10: SEEDED(nn_grid_seeded32_kernel, 4, 1, 2); break;
     default: SEEDED(nn_grid_seeded_kernel, 2, 2, 2, 1); break;
     }
 #undef SEEDED

@@ -19,7 +19,7 @@ namespace {
 
 // one pass around shifts near the centroids: the centred sums follow as
 // S = sum (p - cp)(y - cy)^T - N dp dy^T etc. (horn_step), with N dp dy^T at rounding level
-template <int kMomBatch, bool YIN>
+template <int kMomBatch, bool YIN, bool FOLD>
 __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
     double *__restrict__ partials, const int *__restrict__ kpos, const double4 *__restrict__ m4kd, StepFold fold)
 {
     const bool frozen = st->done != 0; // a frozen (converged) ICP iteration: its sums are never used
-    if (frozen && !fold.ticket) return; // (fused: every workgroup still arrives; the Horn step runs)
+    if (frozen && !FOLD) return; // (fused: every workgroup still arrives; the Horn step runs)
     const double cp0 = st->shift_p[0], cp1 = st->shift_p[1], cp2 = st->shift_p[2];
     const double cy0 = st->shift_y[0], cy1 = st->shift_y[1], cy2 = st->shift_y[2];
     double a[17];
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
             }
         }
     }
-    if (!fold.ticket) {
+    if constexpr (!FOLD) {
         block_sum_store<17>(a, partials + (size_t)blockIdx.x * 17);
         return;
     }
@@ -102,6 +102,9 @@ __device__ __forceinline__ void far_to_acc(int far, int *acc)
     }
 }
 
+// QOP: the form that also writes the next bundle search's slot records (sa.qop); without it the
+// kernel carries none of their registers (the plain pass streams at a higher occupancy)
+template <bool FOLD, bool QOP>
 __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
@@ -117,11 +120,11 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         sxf = xfd ? *xfd : xfv;
     }
     __syncthreads();
-    if (sdone && !fold.ticket) return; // (fused: every workgroup still arrives; the error step runs)
+    if (sdone && !FOLD) return; // (fused: every workgroup still arrives; the error step runs)
     const Xform xf = sxf;
     double a[1] = {0.0};
     int far = 0; // (sa.far_acc: this thread's moved points beyond sqrt(far_d2) of their correspondence)
-    if (sa.qop && write_p) {
+    if (QOP && sa.qop && write_p) {
         // slot records (a scene in slot order): whole waves run to n rounded up to 64 (the
         // stride is a multiple of 64), so that each 32-slot group's lanes are all present for
         // its bound; the lanes past n build the padding's never-firing records
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
             }
         }
     }
-    if (!fold.ticket) {
+    if constexpr (!FOLD) {
         block_sum_store<1>(a, partials + blockIdx.x);
         if (sa.far_acc) far_to_acc(far, sa.far_acc);
         return;
@@ -222,18 +225,24 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
         const int v = e ? atoi(e) : 2;
         return v == 1 || v == 4 ? v : 2;
     }();
-#define MOMENTS(B, Y)                                                                                         \
-    shifted_moments_kernel<B, Y><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, \
-                                                                   partials, kpos, m4kd, fold)
+#define MOMENTS(B, Y, F)                                                                                      \
+    shifted_moments_kernel<B, Y, F><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, \
+                                                                      partials, kpos, m4kd, fold)
+#define MOMENTS_Y(B, Y)                                                                                       \
+    do {                                                                                                      \
+        if (fold.ticket) MOMENTS(B, Y, true);                                                                 \
+        else MOMENTS(B, Y, false);                                                                            \
+    } while (0)
     if (y_ready) {
-        if (batch == 1) MOMENTS(1, true);
-        else if (batch == 4) MOMENTS(4, true);
-        else MOMENTS(2, true);
+        if (batch == 1) MOMENTS_Y(1, true);
+        else if (batch == 4) MOMENTS_Y(4, true);
+        else MOMENTS_Y(2, true);
     } else {
-        if (batch == 1) MOMENTS(1, false);
-        else if (batch == 4) MOMENTS(4, false);
-        else MOMENTS(2, false);
+        if (batch == 1) MOMENTS_Y(1, false);
+        else if (batch == 4) MOMENTS_Y(4, false);
+        else MOMENTS_Y(2, false);
     }
+#undef MOMENTS_Y
 #undef MOMENTS
 }
 
@@ -241,7 +250,7 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                           const double *yz, int n, Xform xf, int write_p, float4 *p32,
                           double *partials, hipStream_t st)
 {
-    transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
+    transform_err_kernel<false, false><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, nullptr, nullptr,
                                                             write_p, p32, partials, SeedArgs{}, StepFold{});
 }
 
@@ -250,8 +259,15 @@ void launch_transform_err_dev(double *px, double *py, double *pz, const double *
                               double *partials, const SeedArgs &sa, hipStream_t st, const StepFold &fold)
 {
     // (the slot-record form ends without the fused step: its caller launches the error step)
-    transform_err_kernel<<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done, 1,
-                                                            p32, partials, sa, sa.qop ? StepFold{} : fold);
+    if (sa.qop)
+        transform_err_kernel<false, true><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done,
+                                                                            1, p32, partials, sa, StepFold{});
+    else if (fold.ticket)
+        transform_err_kernel<true, false><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done,
+                                                                            1, p32, partials, sa, fold);
+    else
+        transform_err_kernel<false, false><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf,
+                                                                             done, 1, p32, partials, sa, StepFold{});
 }
 
 } // namespace icp

@@ -20,12 +20,26 @@ for l in open(sys.argv[1]):
         d=json.loads(l); r=d['per_rank'][0]
         print(f\"{sys.argv[2]:>14s} it/s {d['value']:8.1f} ms/step {d['ms_per_step']*1e3:7.1f}us grid {r['filter_ms']*1e3:7.1f}us tail {r['tail_ms']*1e3:6.1f}us\")
 " $1 "$2"; }
+shard8() { python3 -c "
+import json,sys
+for l in open(sys.argv[1]):
+    if l.startswith('{'):
+        d=json.loads(l)
+        if d['world'] == 8:
+            print(f\"{sys.argv[2]:>14s} W=8 ms/iter {d['ms_per_iter']*1e3:7.1f}us grid {d['filter_ms']*1e3:7.1f}us other {d['other_ms']*1e3:6.1f}us\")
+" $1 "$2"; }
 for f in $FORMS; do
   ICP_GRID_SEEDED=$f timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_$f.log 2>&1 || exit 1
   line $O/b_$f.log "$f" | tee -a $O/summary.txt
+  ICP_GRID_SEEDED=$f timeout -k 10 120 python3 tools/shard_probe.py --worlds 8 --steps 30 > $O/s_$f.log 2>&1 || exit 1
+  shard8 $O/s_$f.log "$f" | tee -a $O/summary.txt
 done
-ICP_FUSED_STEPS=0 timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_unfused.log 2>&1 || exit 1
-line $O/b_unfused.log "unfused" | tee -a $O/summary.txt
+for fs in ${FUSED:-1 2 3}; do
+  ICP_FUSED_STEPS=$fs timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_fused$fs.log 2>&1 || exit 1
+  line $O/b_fused$fs.log "fused=$fs" | tee -a $O/summary.txt
+  ICP_FUSED_STEPS=$fs timeout -k 10 120 python3 tools/shard_probe.py --worlds 8 --steps 30 > $O/s_fused$fs.log 2>&1 || exit 1
+  shard8 $O/s_fused$fs.log "fused=$fs" | tee -a $O/summary.txt
+done
 for x in 0 2; do
   ICP_GRID_XCD=$x timeout -k 10 120 python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-cow --no-cases --no-registration > $O/b_xcd$x.log 2>&1 || exit 1
   line $O/b_xcd$x.log "xcd=$x" | tee -a $O/summary.txt
