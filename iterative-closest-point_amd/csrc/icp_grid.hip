@@ -921,14 +921,18 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     static const Form forms[] = {{"2,2,2", 2}, {"4,2,2", 4}, {"4,2,4", 4}, {"2,2,4", 2},  {"f2,2,4", 2},
                                  {"f2,2,2", 2}, {"f4,2,4", 4}, {"f2,4,4", 2}, {"f4,2,2", 4}, {"4,1,2", 4},
                                  {"f4,1,2", 4}};
-    static const int form = [] {
+    static const int forced = [] {
         const char *e = getenv("ICP_GRID_SEEDED");
-        if (!e) return 0;
+        if (!e) return -1;
         for (int i = 0; i < (int)(sizeof(forms) / sizeof(forms[0])); ++i)
             if (std::string(e) == forms[i].name) return i;
-        return 0;
+        return -1;
     }();
-    const int f = form >= 4 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
+    // by size (profiles/r04r): a whole scene two lanes a query (fp64 scan); a shard (a few
+    // queries a SIMD: the per-query chain is the time) four lanes a query with the fp32 image
+    // (C4 W = 8: 36.5 against 48.1 us)
+    const int form = forced >= 0 ? forced : n >= (1 << 19) ? 0 : 8;
+    const int f = form >= 4 && form != 9 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
     const int per_block = kBlock / forms[f].g;
     int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
     if (xcd_remap) blocks = (blocks + 7) / 8 * 8; // (whole eighths; the extra workgroups find no query)
