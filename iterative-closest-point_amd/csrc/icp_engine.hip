@@ -222,6 +222,11 @@ struct icp_ctx {
     size_t seed16_cap = 0;
     bool last_search_timed = false; // the per-operation search recorded its events
     bool seeds_valid = false;   // idx holds the previous search over the resident scene
+    // seedd_valid: b_seedd holds D64(p_j, m[idx_j]) of the resident scene (the last icp_run took
+    // the search policy, whose every transform writes it), and last_far that run's last far count
+    // (SeedArgs::far_acc): the next run's policy starts from them instead of two bundle searches
+    bool seedd_valid = false;
+    int last_far = -1;
     int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
     int *fb_list = nullptr;                           // queries the grid hands back
     double *fb_T = nullptr;
@@ -1515,6 +1520,7 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm)
     ctx->nm_pad = nm_pad;
     ctx->has_model = true;
     ctx->seeds_valid = false;
+    ctx->seedd_valid = false;
     // the scene's fp32 copy depends on c: refresh it
     if (ctx->has_scene && ctx->scene.n) {
         launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1],
@@ -1579,6 +1585,7 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     ctx->np_total = np_total;
     ctx->has_scene = true;
     ctx->seeds_valid = false;
+    ctx->seedd_valid = false;
     ctx->q_order_src = nullptr; // new contents: a new query order
     ctx->scene_slot = false;    // (in the caller's order)
     ctx->p32_stale = false;
@@ -1878,6 +1885,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
     ctx->pers_epoch_base += (unsigned)__atomic_load_n(ctx->h_flags + 7, __ATOMIC_ACQUIRE);
     ctx->pers_sync_valid = true;
     ctx->seeds_valid = true;
+    ctx->seedd_valid = false; // (the one-launch loop keeps no seed distances)
     const int iters = ctx->h_iter->iter;
     ctx->stats.nn_pairs += (long long)iters * (long long)n * (long long)ctx->nm;
     ctx->stats.persistent_runs += 1;
@@ -2001,8 +2009,12 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     const bool grid_policy = ctx->scene_slot && ctx->nn_mode == ICP_NN_CERTIFIED &&
                              ctx->nn_variant == ICP_NN_VARIANT_AUTO && level1_kind(ctx, n) == 3 && grid_auto();
     const int far_thr = std::max(16, (int)(n >> 5));
-    bool grid_next = false; // the path of the search after the one being enqueued
-    int far_obs = -1;       // far_acc of the last iteration the host has seen
+    // a run that continues the last one (the same resident scene, its seed distances written by
+    // that run's last transform) starts from that run's last far count: its first searches need
+    // not be the bundle cascade's
+    const bool carry = grid_policy && ctx->seeds_valid && ctx->seedd_valid;
+    int far_obs = carry ? ctx->last_far : -1; // far_acc of the last iteration the host has seen
+    bool grid_next = carry && far_obs >= 0 && far_obs <= far_thr; // the path of the next search
     SeedArgs sa_grid;       // a transform before a grid search: its seed distances only
     if (grid_policy) {
         const double h = 1.0 / ctx->grid.inv_h;
@@ -2098,12 +2110,15 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == timing_phase;
-            const bool grid_cur = enqueued > 0 && grid_next; // (decided with the previous transform)
-            grid_next = grid_policy && enqueued >= 1 && far_obs >= 0 && far_obs <= far_thr;
+            const bool grid_cur = grid_next; // (decided with the previous transform, or carried over)
+            grid_next = grid_policy && far_obs >= 0 && far_obs <= far_thr;
             // (the search of an iteration queued behind the converged one returns at once)
-            // (the seed distances the last transform of this run wrote, for a grid search)
-            const double *gseedd = enqueued > 0 && (grid_cur || ctx->nn_variant == ICP_NN_VARIANT_GRID) ? sa.seedd
-                                                                                                        : nullptr;
+            // (the seed distances the last transform wrote -- of this run, or of the last one when
+            // carried over -- for a grid search)
+            const double *gseedd = (enqueued > 0 || (carry && grid_cur)) &&
+                                           (grid_cur || ctx->nn_variant == ICP_NN_VARIANT_GRID)
+                                       ? sa.seedd
+                                       : nullptr;
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false,
                                 fuse_seeds && enqueued > 0 && !grid_cur, &sd->done, ctx->scene_slot,
@@ -2315,8 +2330,12 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         if (seeds_at_start) HIPCHK(hipMemcpyAsync(ctx->idx, bk + n * 40, n * sizeof(int), hipMemcpyDeviceToDevice, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
         ctx->seeds_valid = seeds_at_start;
+        ctx->seedd_valid = false;
         return kTailAborted;
     }
+    // (every transform of a policy run wrote the seed distances; the next run may start from them)
+    ctx->seedd_valid = grid_policy && sa.seedd != nullptr;
+    ctx->last_far = far_obs;
     return finish_run(ctx, threshold, err_trace, res, wall0);
 }
 
@@ -2434,6 +2453,7 @@ int icp_closest_matrix(icp_ctx *ctx, const double *p_xyz, size_t np, double *y_x
         return closest_lds(ctx, p_xyz, np, y_xyz_out, idx_out);
     TRY(upload_cloud(ctx, ctx->qa, p_xyz, np, true));
     ctx->seeds_valid = false; // idx is about to hold other queries' correspondences
+    ctx->seedd_valid = false;
     ctx->q_order_src = nullptr;
     TRY(nn_search(ctx, ctx->qa, np));
     TRY(cpu_rule_fixup(ctx, ctx->qa, np, nullptr));

@@ -104,3 +104,28 @@ def test_seeded_grid_against_oracle(amd, oracle, case):
     assert np.array_equal(got2[sel], ref)
     assert got.min() >= 0 and got.max() < m.shape[0]
     assert st["level1_queued"] >= 0
+
+
+def test_policy_carries_over_to_the_next_run(amd):
+    """A run that continues the last one on the same scene starts from that run's far count and
+    seed distances (grid searches from its first iteration): the same trajectory as the bundle
+    cascade's, and a fresh scene starts over."""
+    m, p = amd.synthetic_pair(N, seed=42)
+    out = {}
+    for name, variant in (("auto", amd.VARIANT_AUTO), ("bundle", amd.VARIANT_BUNDLE)):
+        with amd.Context(0) as ctx:
+            ctx.set_nn_variant(variant)
+            ctx.set_model(m)
+            ctx.set_scene(p)
+            ctx.run(12, -1.0)
+            ctx.reset_stats()
+            ctx.set_index_digest(6)
+            res, errs = ctx.run(6, -1.0)
+            out[name] = dict(errs=errs, dig=ctx.index_digest(6), scene=ctx.get_scene(), st=ctx.stats())
+    a, b = out["auto"], out["bundle"]
+    assert amd.FILTER_NAMES[a["st"]["last_filter"]] == "grid"
+    # (no bundle search in the continued run: the level-1 queue stays empty)
+    assert a["st"]["level1_queued"] == 0, a["st"]
+    assert np.array_equal(a["dig"], b["dig"])
+    assert np.array_equal(a["errs"], b["errs"])
+    assert np.array_equal(a["scene"], b["scene"])
