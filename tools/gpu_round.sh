@@ -79,9 +79,9 @@ for s in $STEPS; do
            run rocprof_c5shard 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5shard" -o c5shard -- \
                python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 10 --warmup 2 &&
            run pmc_c5shard_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_c5shard1" -o fetch -- \
-               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 3 --warmup 2 &&
+               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 4 --warmup 8 &&
            run pmc_c5shard_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_c5shard2" -o write -- \
-               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 3 --warmup 2 ;;
+               python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 4 --warmup 8 ;;
     c5dist8) # the 8-rank C5 flow rehearsed on one GPU (8 processes, sums through gloo)
            ICP_BENCH_HOST_REDUCE=1 run bench_c5_dist8 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
                --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 8 --points 8388608 --steps 10 --warmup 2 \

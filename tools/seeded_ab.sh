@@ -3,7 +3,7 @@
 #   tools/seeded_ab.sh TAG "form1 form2 ..."
 set -u
 O=gpurun_out/${1:-ab}; mkdir -p $O; export TMPDIR=/tmp
-FORMS=${2:-"2,2,2 f2,2,4 f2,2,2 f4,2,4 f2,4,4 f4,2,2 f2,2,8 f1,4,4"}
+FORMS=${FORMS:-${2:-"2,2,2 f2,2,2 4,2,2 f4,2,2 4,1,2 f4,1,2"}}
 # the whole GPU suite on the defaults, then the exactness of the other forms (the policy
 # tests compare bit for bit)
 timeout -k 10 500 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 \
