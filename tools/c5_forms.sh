@@ -2,7 +2,8 @@
 #   tools/c5_forms.sh TAG "form1 form2 ..."
 set -u
 O=gpurun_out/${1:-c5f}; mkdir -p $O; export TMPDIR=/tmp
-for f in ${2:-"2,2,2 f2,2,2 f4,2,2 4,2,2"}; do
+FORMS=${2:-"2,2,2 f2,2,2 f4,2,2 4,2,2"}
+for f in $FORMS; do
   ICP_GRID_SEEDED=$f timeout -k 10 200 python3 tools/shard_probe.py --n 8388608 --worlds 8 --steps 12 --warmup 8 > $O/c5_$f.log 2>&1 || exit 1
   python3 -c "
 import json,sys
