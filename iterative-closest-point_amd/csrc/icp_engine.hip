@@ -716,7 +716,8 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     if (y_out) {
         kpos_out = nullptr;
         launch_nn_grid_seeded((int)n, q.x, q.y, q.z, grid_view(ctx), kSeededBox, seedd, ctx->m4, ctx->idx, yx, yy,
-                              yz, ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, stop, xcd, ctx->st);
+                              yz, ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, stop, xcd, ctx->st,
+                              (long long)ctx->nm);
     } else {
         launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), kSeededBox, ctx->idx,
                                    ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0, xcd,

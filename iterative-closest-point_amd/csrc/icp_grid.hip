@@ -907,7 +907,7 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
 void launch_nn_grid_seeded(int n, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, const double *seedd, const double4 *m4, int *idx, double *yx, double *yy,
                            double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
-                           hipStream_t st)
+                           hipStream_t st, long long nm_hint)
 {
     // (lanes per query, run bounds read together, point loads in flight; "f": the fp32 image with
     // the fp64 decision for candidates, nn_grid_seeded32_kernel): ICP_GRID_SEEDED picks one of the
@@ -921,17 +921,16 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     static const Form forms[] = {{"2,2,2", 2}, {"4,2,2", 4}, {"4,2,4", 4}, {"2,2,4", 2},  {"f2,2,4", 2},
                                  {"f2,2,2", 2}, {"f4,2,4", 4}, {"f2,4,4", 2}, {"f4,2,2", 4}, {"4,1,2", 4},
                                  {"f4,1,2", 4}};
-    static const int forced = [] {
-        const char *e = getenv("ICP_GRID_SEEDED");
-        if (!e) return -1;
+    // (read at every launch, not cached: the tests switch forms inside one process)
+    int forced = -1;
+    if (const char *e = getenv("ICP_GRID_SEEDED"))
         for (int i = 0; i < (int)(sizeof(forms) / sizeof(forms[0])); ++i)
-            if (std::string(e) == forms[i].name) return i;
-        return -1;
-    }();
-    // by size (profiles/r04r): a whole scene two lanes a query (fp64 scan); a shard (a few
-    // queries a SIMD: the per-query chain is the time) four lanes a query with the fp32 image
-    // (C4 W = 8: 36.5 against 48.1 us)
-    const int form = forced >= 0 ? forced : n >= (1 << 19) ? 0 : 8;
+            if (std::string(e) == forms[i].name) forced = i;
+    // by size (profiles/r04s-u): two lanes a query for a whole scene against a model of its size
+    // (C4 W = 1: 105 against 112 us for 4,2,2); four where a SIMD holds few queries or the model
+    // is denser than the scene -- each query's chain of dependent loads is then the time
+    // (C4 W = 8: 31.2 against 45.3 us, W = 2: 67.1 against 82.4; C5's shard: 208 against 240)
+    const int form = forced >= 0 ? forced : (n >= (1 << 19) && nm_hint < 2 * (long long)n) ? 0 : 1;
     const int f = form >= 4 && form != 9 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
     const int per_block = kBlock / forms[f].g;
     int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));

@@ -334,7 +334,7 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
 void launch_nn_grid_seeded(int n, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, const double *seedd, const double4 *m4, int *idx, double *yx, double *yy,
                            double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
-                           hipStream_t st);
+                           hipStream_t st, long long nm_hint); // (nm_hint: the model's points, for the form)
 
 // The reference CPU rule's near ties (icp_grid.hip): queries whose squared-rule winner idx[j]
 // has another point within the window are appended to out[*count] (count zeroed by the caller).

@@ -127,3 +127,17 @@ def test_policy_carries_over_to_the_next_run(amd):
     assert np.array_equal(a["dig"], b["dig"])
     assert np.array_equal(a["errs"], b["errs"])
     assert np.array_equal(a["scene"], b["scene"])
+
+
+@pytest.mark.parametrize("form", ["f4,2,2", "f2,2,2", "2,2,2", "4,1,2"])
+def test_seeded_forms_match_bundle(amd, form, monkeypatch):
+    """Every instantiated form of the seeded grid kernel (ICP_GRID_SEEDED, read at each launch),
+    the fp32-image forms included, returns the bundle cascade's indices bit for bit over a run."""
+    monkeypatch.setenv("ICP_GRID_SEEDED", form)
+    m, p = amd.synthetic_pair(N, seed=42)
+    a = run(amd, m, p, 16, amd.VARIANT_AUTO)
+    monkeypatch.delenv("ICP_GRID_SEEDED")
+    b = run(amd, m, p, 16, amd.VARIANT_BUNDLE)
+    assert amd.FILTER_NAMES[a["stats"]["last_filter"]] == "grid"
+    assert np.array_equal(a["dig"], b["dig"])
+    assert np.array_equal(a["scene"], b["scene"])
