@@ -708,150 +708,6 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
     }
 }
 
-// Inclusive scan of v over the 64 lanes of a wave (Hillis-Steele, shuffles)
-__device__ __forceinline__ int wave_incl_scan(int v)
-{
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
-    }
-    return v;
-}
-
-// The number of lanes whose (non-decreasing) incl is <= x: the lane that holds item x of the
-// concatenation of the lanes' runs (x < incl[63]); 63 at most
-__device__ __forceinline__ int wave_owner(int incl, int x)
-{
-    int o = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1)
-        if (__shfl(incl, o + step - 1, 64) <= x) o += step;
-    return o;
-}
-
-// The seeded search with the wave's work balanced over its lanes (one wave a workgroup, 64
-// queries, one per lane).  nn_grid_seeded_kernel gives each query's rows and points to its own
-// lanes, so a wave runs as many load rounds as its busiest query needs (per the SQ counters at
-// C4: 75 vector loads a wave where ~20 carry data).  Here the wave's x-runs are numbered query
-// after query (a scan of the queries' row counts) and taken 64 at a time, one per lane; their
-// points are numbered run after run (a scan of the run lengths) and taken 64 at a time, one
-// per lane: every load round is full.  A lane finds its run's / point's owner by a binary
-// search of the scan over the lanes.  The points of one query are consecutive lanes of a round,
-// so a segmented (D64, index) minimum over the lanes leaves the query's round minimum in the
-// segment's last lane, which folds it into the query's running minimum in LDS (one writer per
-// query per round; the wave's rounds are ordered by its own barrier).  The seed point lies in
-// its box and is met with d == best (seedd), so the query's final key is the first minimum's
-// (index, position in pts); its coordinates are re-read for y.
-__global__ __launch_bounds__(64) void nn_grid_seeded_wave_kernel(
-    int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
-    int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
-    double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
-    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap)
-{
-    if (stop && *stop) return; // a frozen (converged) ICP iteration
-    __shared__ double s_d[64];
-    __shared__ unsigned long long s_key[64]; // (index << 32) | position in pts: the min is the first index
-    const int lane = threadIdx.x;
-    const int bx = xcd_remap && (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
-                                                     : blockIdx.x;
-    for (int base = bx * 64; base < n; base += gridDim.x * 64) {
-        const int t = base + lane;
-        const bool in = t < n;
-        int h = -1;
-        double q[3] = {0.0, 0.0, 0.0}, best = 0.0;
-        if (in) {
-            h = idx[t];
-            q[0] = px[t];
-            q[1] = py[t];
-            q[2] = pz[t];
-            best = seedd[t];
-        }
-        int c0[3] = {0, 0, 0}, c1[3] = {-1, -1, -1};
-        // (a non-finite seed distance -- a NaN / inf query -- bounds no box: the second pass)
-        const bool ok = in && h >= 0 && best == best && best < INFINITY && complete_box(q, best, gv, budget, c0, c1);
-        const bool far = in && !ok;
-        const int fs = wave_append(far_count, far);
-        if (far) {
-            far_list[fs] = t;
-            far_hint[fs] = h;
-        }
-        s_d[lane] = best;
-        s_key[lane] = ~0ull;
-        const int ny = ok ? c1[1] - c0[1] + 1 : 0;
-        const int nrows = ok ? ny * (c1[2] - c0[2] + 1) : 0;
-        const int rincl = wave_incl_scan(nrows);
-        const int R = __shfl(rincl, 63, 64), rbase = rincl - nrows;
-        __syncthreads();
-        for (int r0 = 0; r0 < R; r0 += 64) {
-            const int j = r0 + lane; // this lane's x-run
-            const int owner = wave_owner(rincl, j);
-            const int o_rbase = __shfl(rbase, owner, 64), o_ny = __shfl(ny, owner, 64);
-            const int o_x0 = __shfl(c0[0], owner, 64), o_x1 = __shfl(c1[0], owner, 64);
-            const int o_y0 = __shfl(c0[1], owner, 64), o_z0 = __shfl(c0[2], owner, 64);
-            int k0 = 0, len = 0;
-            if (j < R) {
-                const int r = j - o_rbase;
-                const int cy = o_y0 + r % o_ny, cz = o_z0 + r / o_ny;
-                const int row = (cz * gv.g[1] + cy) * gv.g[0];
-                k0 = gv.start[row + o_x0];
-                len = gv.start[row + o_x1 + 1] - k0;
-            }
-            const int pincl = wave_incl_scan(len);
-            const int P = __shfl(pincl, 63, 64), pbase = pincl - len;
-            for (int f0 = 0; f0 < P; f0 += 64) {
-                const int f = f0 + lane; // this lane's point
-                const int rl = wave_owner(pincl, f);
-                const int k = __shfl(k0, rl, 64) + (f - __shfl(pbase, rl, 64));
-                const int qo = __shfl(owner, rl, 64); // its query's lane
-                const double a0 = __shfl(q[0], qo, 64), a1 = __shfl(q[1], qo, 64), a2 = __shfl(q[2], qo, 64);
-                const bool valid = f < P;
-                double d = INFINITY;
-                unsigned long long key = ~0ull;
-                int seg = -1;
-                if (valid) {
-                    const double4 m = gv.pts[k];
-                    d = d64g(a0, a1, a2, m.x, m.y, m.z);
-                    key = ((unsigned long long)(unsigned)(int)m.w << 32) | (unsigned)k;
-                    seg = qo;
-                }
-                // segmented lexicographic minimum (segments: runs of equal seg, the invalid tail -1)
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const double od = __shfl_up(d, o, 64);
-                    const unsigned long long ok2 = __shfl_up(key, o, 64);
-                    const int os = __shfl_up(seg, o, 64);
-                    if (lane >= o && os == seg && (od < d || (od == d && ok2 < key))) {
-                        d = od;
-                        key = ok2;
-                    }
-                }
-                const int nseg = __shfl_down(seg, 1, 64);
-                if (valid && (lane == 63 || nseg != seg)) { // the segment's last lane: its query's round minimum
-                    const double bd = s_d[qo];
-                    const unsigned long long bk = s_key[qo];
-                    if (d < bd || (d == bd && key < bk)) {
-                        s_d[qo] = d;
-                        s_key[qo] = key;
-                    }
-                }
-                __syncthreads(); // (one wave: this round's minima before the next round reads them)
-            }
-        }
-        if (ok) {
-            const unsigned long long k = s_key[lane];
-            const int bi = k == ~0ull ? h : (int)(k >> 32);
-            const double4 w = k == ~0ull ? m4[h] : gv.pts[(unsigned)k];
-            idx[t] = bi;
-            yx[t] = w.x;
-            yy[t] = w.y;
-            yz[t] = w.z;
-        }
-        __syncthreads(); // (s_d / s_key are re-initialised for the next 64 queries)
-    }
-}
-
 } // namespace
 
 GridParams grid_params(const double *m_xyz, size_t nm)
@@ -1064,7 +920,7 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     };
     static const Form forms[] = {{"2,2,2", 2}, {"4,2,2", 4}, {"4,2,4", 4}, {"2,2,4", 2},  {"f2,2,4", 2},
                                  {"f2,2,2", 2}, {"f4,2,4", 4}, {"f2,4,4", 2}, {"f4,2,2", 4}, {"4,1,2", 4},
-                                 {"f4,1,2", 4}, {"w", 1}};
+                                 {"f4,1,2", 4}};
     // (read at every launch, not cached: the tests switch forms inside one process)
     int forced = -1;
     if (const char *e = getenv("ICP_GRID_SEEDED"))
@@ -1075,14 +931,7 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     // is denser than the scene -- each query's chain of dependent loads is then the time
     // (C4 W = 8: 31.2 against 45.3 us, W = 2: 67.1 against 82.4; C5's shard: 208 against 240)
     const int form = forced >= 0 ? forced : (n >= (1 << 19) && nm_hint < 2 * (long long)n) ? 0 : 1;
-    const int f = form >= 4 && form != 9 && form != 11 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
-    if (f == 11) { // the balanced wave form: one 64-lane workgroup per 64 queries
-        int blocks = std::max(1, std::min((n + 63) / 64, 65536));
-        if (xcd_remap) blocks = (blocks + 7) / 8 * 8;
-        nn_grid_seeded_wave_kernel<<<blocks, 64, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz,
-                                                           far_count, far_list, far_hint, stop, xcd_remap ? 1 : 0);
-        return;
-    }
+    const int f = form >= 4 && form != 9 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
     const int per_block = kBlock / forms[f].g;
     int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
     if (xcd_remap) blocks = (blocks + 7) / 8 * 8; // (whole eighths; the extra workgroups find no query)

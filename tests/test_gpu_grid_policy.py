@@ -129,7 +129,7 @@ def test_policy_carries_over_to_the_next_run(amd):
     assert np.array_equal(a["scene"], b["scene"])
 
 
-@pytest.mark.parametrize("form", ["f4,2,2", "f2,2,2", "2,2,2", "4,1,2", "w"])
+@pytest.mark.parametrize("form", ["f4,2,2", "f2,2,2", "2,2,2", "4,1,2"])
 def test_seeded_forms_match_bundle(amd, form, monkeypatch):
     """Every instantiated form of the seeded grid kernel (ICP_GRID_SEEDED, read at each launch),
     the fp32-image forms included, returns the bundle cascade's indices bit for bit over a run."""
