@@ -31,6 +31,28 @@ __device__ __forceinline__ void block_sum_store(double (&a)[K], double *out)
     }
 }
 
+// a[k] += row b's k-th value for this thread's rows b = t, t + kBlock, ... in that order (the
+// reduce_kernel fold), four rows' loads issued before their sums: the same sums in the same
+// order, one memory round trip per four rows instead of one per row
+template <int K> __device__ __forceinline__ void fold_rows(const double *__restrict__ part, int nblocks, double (&a)[K])
+{
+    constexpr int kRows = 4;
+    for (int b0 = threadIdx.x; b0 < nblocks; b0 += kRows * kBlock) {
+        double v[kRows][K];
+#pragma unroll
+        for (int u = 0; u < kRows; ++u) {
+            const int b = b0 + u * kBlock;
+#pragma unroll
+            for (int k = 0; k < K; ++k) v[u][k] = b < nblocks ? part[(size_t)b * K + k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kRows; ++u)
+            if (b0 + u * kBlock < nblocks)
+#pragma unroll
+                for (int k = 0; k < K; ++k) a[k] += v[u][k];
+    }
+}
+
 __device__ __forceinline__ void shifted_moment_terms(double px, double py, double pz, const double4 &m, double cp0,
                                                      double cp1, double cp2, double cy0, double cy1, double cy2,
                                                      double (&a)[17]);

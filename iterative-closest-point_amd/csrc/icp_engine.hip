@@ -501,7 +501,7 @@ int model_host_copy(icp_ctx *ctx, const double **out)
 int ensure_reduction_space(icp_ctx *ctx)
 {
     if (ctx->partials) return ICP_OK;
-    HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocks * kRedMaxK));
+    HIPCHK(hipMalloc((void **)&ctx->partials, sizeof(double) * kRedMaxBlocksCap * kRedMaxK));
     HIPCHK(hipMalloc((void **)&ctx->sums, sizeof(double) * 32));
     HIPCHK(hipHostMalloc((void **)&ctx->h_sums, sizeof(double) * 32, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void **)&ctx->h_amb, sizeof(int) * 4, hipHostMallocDefault));

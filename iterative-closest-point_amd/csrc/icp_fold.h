@@ -140,11 +140,17 @@ template <int K, int S = K> __device__ __forceinline__ void tail_fold(const doub
     double a[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-        double v[K];
-        load_row<K, S>(part, nblocks, b, v);
+    constexpr int kRows = K <= 2 ? 4 : 1; // (narrow rows: four rows' loads in flight, the same sums in order)
+    for (int b0 = threadIdx.x; b0 < nblocks; b0 += kRows * kBlock) {
+        double v[kRows][K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) a[k] += v[k];
+        for (int u = 0; u < kRows; ++u)
+            if (b0 + u * kBlock < nblocks) load_row<K, S>(part, nblocks, b0 + u * kBlock, v[u]);
+#pragma unroll
+        for (int u = 0; u < kRows; ++u)
+            if (b0 + u * kBlock < nblocks)
+#pragma unroll
+                for (int k = 0; k < K; ++k) a[k] += v[u][k];
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {

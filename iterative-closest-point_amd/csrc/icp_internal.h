@@ -23,6 +23,7 @@ constexpr int kTileSmall = 128; // ... for small models (more model splits per s
 constexpr int kTile64 = 512;  // model points per LDS tile, fp64 path (16 KiB)
 constexpr int kSub = 32;      // sub-block granularity of the running-argmin bookkeeping
 constexpr int kRedMaxBlocks = 1024; // max workgroups of a streaming reduction pass
+constexpr int kRedMaxBlocksCap = 4096; // (the partials buffer's rows: ICP_RED_BLOCKS up to this)
 constexpr int kRedSingle = 4096;    // up to this many points: a single-workgroup pass
 constexpr int kRedMaxK = 17;        // max sums per workgroup of a streaming reduction pass
 

@@ -37,10 +37,7 @@ __global__ __launch_bounds__(kBlock) void reduce_horn_kernel(const double *__res
     double a[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) a[k] += partials[(size_t)b * K + k];
-    }
+    fold_rows<K>(partials, nblocks, a);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
 #pragma unroll

@@ -1862,10 +1862,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double *__restrict
     double a[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = 0.0;
-    for (int b = threadIdx.x; b < nblocks; b += kBlock) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) a[k] += partials[(size_t)b * K + k];
-    }
+    fold_rows<K>(partials, nblocks, a);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
 #pragma unroll
@@ -2288,7 +2285,16 @@ void launch_nn_finalize64(const double *part_best, const int *part_idx, int spli
 
 // up to kRedSingle points one workgroup does the whole pass (and writes the final sums
 // itself, see the engine's red_target): a launch less per reduction for small clouds
-int red_blocks(size_t n) { return n <= (size_t)kRedSingle ? 1 : grid_for(n, kRedMaxBlocks); }
+// (ICP_RED_BLOCKS: the cap for A/B runs, at most kRedMaxBlocksCap; it changes the sums' order)
+int red_blocks(size_t n)
+{
+    static const int cap = [] {
+        const char *e = getenv("ICP_RED_BLOCKS");
+        const int v = e ? atoi(e) : kRedMaxBlocks;
+        return v >= 64 && v <= kRedMaxBlocksCap ? v : kRedMaxBlocks;
+    }();
+    return n <= (size_t)kRedSingle ? 1 : grid_for(n, cap);
+}
 
 
 void launch_gather_moments(const int *idx, const double4 *m4, const double *px, const double *py,
