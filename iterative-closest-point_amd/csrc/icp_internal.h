@@ -22,7 +22,10 @@ constexpr int kTile32 = 1024; // model points per LDS tile, fp32 filter (16 KiB)
 constexpr int kTileSmall = 128; // ... for small models (more model splits per search)
 constexpr int kTile64 = 512;  // model points per LDS tile, fp64 path (16 KiB)
 constexpr int kSub = 32;      // sub-block granularity of the running-argmin bookkeeping
-constexpr int kRedMaxBlocks = 1024; // max workgroups of a streaming reduction pass
+// max workgroups of a streaming reduction pass: one a CU.  The folds (one row per thread) cost
+// less than the streaming loses at four waves a CU (profiles/r04w: C4 W = 1 0.156-0.159 ms per
+// iteration at 256 against 0.161 at 1,024, 0.175 at 2,048, 0.194 at 128; W = 8 0.0645 against 0.0688)
+constexpr int kRedMaxBlocks = 256;
 constexpr int kRedMaxBlocksCap = 4096; // (the partials buffer's rows: ICP_RED_BLOCKS up to this)
 constexpr int kRedSingle = 4096;    // up to this many points: a single-workgroup pass
 constexpr int kRedMaxK = 17;        // max sums per workgroup of a streaming reduction pass
