@@ -2009,7 +2009,12 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // minimum, so the trajectory is the same whichever runs.  ICP_GRID_AUTO=0: always the bundle.
     const bool grid_policy = ctx->scene_slot && ctx->nn_mode == ICP_NN_CERTIFIED &&
                              ctx->nn_variant == ICP_NN_VARIANT_AUTO && level1_kind(ctx, n) == 3 && grid_auto();
-    const int far_thr = std::max(16, (int)(n >> 5));
+    static const int far_shift = [] { // ICP_GRID_FAR_SHIFT: the threshold n >> shift (A/B)
+        const char *e = getenv("ICP_GRID_FAR_SHIFT");
+        const int v = e ? atoi(e) : 5;
+        return v >= 0 && v <= 20 ? v : 5;
+    }();
+    const int far_thr = std::max(16, (int)(n >> far_shift));
     // a run that continues the last one (the same resident scene, its seed distances written by
     // that run's last transform) starts from that run's last far count: its first searches need
     // not be the bundle cascade's
