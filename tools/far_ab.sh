@@ -2,7 +2,8 @@
 # (30 steps after 3 warm-up) with its registration block, and the W = 8 shard.
 set -u
 O=gpurun_out/${1:-farab}; mkdir -p $O; export TMPDIR=/tmp
-for v in ${2:-"5 3 2 1 0"}; do
+VALS=${2:-"5 3 2 1 0"}
+for v in $VALS; do
   ICP_GRID_FAR_SHIFT=$v timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-cow --no-cases > $O/b_$v.log 2>&1 || exit 1
   python3 - "$O/b_$v.log" "shift=$v" <<'PY' | tee -a $O/summary.txt
 import json, sys
