@@ -104,7 +104,7 @@ __device__ __forceinline__ void far_to_acc(int far, int *acc)
 
 // QOP: the form that also writes the next bundle search's slot records (sa.qop); without it the
 // kernel carries none of their registers (the plain pass streams at a higher occupancy)
-template <bool FOLD, bool QOP>
+template <bool FOLD, bool QOP, int KB = 1>
 __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz,
     const double *__restrict__ yx, const double *__restrict__ yy, const double *__restrict__ yz,
@@ -167,27 +167,46 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
         if (sa.far_acc) far_to_acc(far, sa.far_acc);
         return;
     }
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < (sdone ? 0 : n); i += gridDim.x * kBlock) {
-        double q0, q1, q2;
-        transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
-        a[0] += residual2(yx[i], yy[i], yz[i], q0, q1, q2);
-        if (write_p) {
-            px[i] = q0;
-            py[i] = q1;
-            pz[i] = q2;
-            if (p32)
-                p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]),
-                                     (float)(q2 - xf.c[2]), 0.0f);
-            // the next seeded f16 search's seed: the new position against this iteration's
-            // correspondence (y = m[idx], exactly what mfma16_seed_kernel would gather)
-            if (sa.seed16)
-                sa.seed16[i] = mfma16_seed_value(q0, q1, q2, yx[i], yy[i], yz[i], sa.c[0], sa.c[1], sa.c[2],
-                                                 sa.scale);
-            if (sa.seedd || sa.far_acc) { // (bundle_prep_kernel's seed distance, in its arithmetic)
-                const double dx = q0 - yx[i], dy = q1 - yy[i], dz = q2 - yz[i];
-                const double d2 = (dx * dx + dy * dy) + dz * dz;
-                if (sa.seedd) sa.seedd[i] = d2;
-                far += d2 > sa.far_d2 ? 1 : 0;
+    // the thread's points i, i + G, i + 2G, ... in that order, KB at a time with every load of the
+    // batch issued before the first transform (the same sums in the same order)
+    const int G = gridDim.x * kBlock;
+    for (int i0 = blockIdx.x * kBlock + threadIdx.x; i0 < (sdone ? 0 : n); i0 += KB * G) {
+        double p0[KB], p1[KB], p2[KB], y0[KB], y1[KB], y2[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int i = i0 + u * G;
+            const bool in = i < n;
+            p0[u] = in ? px[i] : 0.0;
+            p1[u] = in ? py[i] : 0.0;
+            p2[u] = in ? pz[i] : 0.0;
+            y0[u] = in ? yx[i] : 0.0;
+            y1[u] = in ? yy[i] : 0.0;
+            y2[u] = in ? yz[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int i = i0 + u * G;
+            if (i >= n) continue;
+            double q0, q1, q2;
+            transform_point(xf, p0[u], p1[u], p2[u], q0, q1, q2);
+            a[0] += residual2(y0[u], y1[u], y2[u], q0, q1, q2);
+            if (write_p) {
+                px[i] = q0;
+                py[i] = q1;
+                pz[i] = q2;
+                if (p32)
+                    p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
+                // the next seeded f16 search's seed: the new position against this iteration's
+                // correspondence (y = m[idx], exactly what mfma16_seed_kernel would gather)
+                if (sa.seed16)
+                    sa.seed16[i] = mfma16_seed_value(q0, q1, q2, y0[u], y1[u], y2[u], sa.c[0], sa.c[1], sa.c[2],
+                                                     sa.scale);
+                if (sa.seedd || sa.far_acc) { // (bundle_prep_kernel's seed distance, in its arithmetic)
+                    const double dx = q0 - y0[u], dy = q1 - y1[u], dz = q2 - y2[u];
+                    const double d2 = (dx * dx + dy * dy) + dz * dz;
+                    if (sa.seedd) sa.seedd[i] = d2;
+                    far += d2 > sa.far_d2 ? 1 : 0;
+                }
             }
         }
     }
@@ -254,6 +273,18 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
                                                             write_p, p32, partials, SeedArgs{}, StepFold{});
 }
 
+// points of a thread whose loads are issued together in the plain transform (ICP_TR_BATCH = 1 | 2 |
+// 4; the same sums)
+static int transform_batch()
+{
+    static const int b = [] {
+        const char *e = getenv("ICP_TR_BATCH");
+        const int v = e ? atoi(e) : 1;
+        return v == 2 || v == 4 ? v : 1;
+    }();
+    return b;
+}
+
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,
                               const double *yz, int n, const Xform *xf, const int *done, float4 *p32,
                               double *partials, const SeedArgs &sa, hipStream_t st, const StepFold &fold)
@@ -265,6 +296,12 @@ void launch_transform_err_dev(double *px, double *py, double *pz, const double *
     else if (fold.ticket)
         transform_err_kernel<true, false><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done,
                                                                             1, p32, partials, sa, fold);
+    else if (transform_batch() == 4)
+        transform_err_kernel<false, false, 4><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf,
+                                                                                done, 1, p32, partials, sa, StepFold{});
+    else if (transform_batch() == 2)
+        transform_err_kernel<false, false, 2><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf,
+                                                                                done, 1, p32, partials, sa, StepFold{});
     else
         transform_err_kernel<false, false><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf,
                                                                              done, 1, p32, partials, sa, StepFold{});
