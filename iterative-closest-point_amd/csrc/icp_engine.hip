@@ -285,6 +285,10 @@ struct icp_ctx {
     double4 *b_bctr = nullptr, *b_blk = nullptr; // per bundle / per 32-bundle block: centre, radius
     int *b_kd = nullptr;                      // the kd order (upload staging)
     int nb_pad = 0;                           // bundles (whole LDS tiles)
+    // the bundle filter's kd order and images are built at their first use (ensure_bundle):
+    // pending from icp_set_model on until then (a run whose searches all take the grid never
+    // builds them)
+    bool bundle_pending = false;
     size_t b_img_cap = 0, b_pimg_cap = 0, b_kd_orig_cap = 0, b_bctr_cap = 0, b_blk_cap = 0, b_kd_cap = 0;
     int *q_order = nullptr;                   // the bundle filter's query order (launch_query_order)
     int *q_pos = nullptr;                     // its inverse (query j's slot)
@@ -536,12 +540,15 @@ int ensure_queue(icp_ctx *ctx, size_t n)
     return ICP_OK;
 }
 
+int ensure_bundle(icp_ctx *ctx); // (the bundle filter's images at their first use; below)
+
 // level-1 filter of a certified search: 0 = none (VALU filter only), 1 = f32 MFMA, 2 = f16 MFMA
 int level1_kind(const icp_ctx *ctx, size_t n)
 {
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA) return 1;
     if (ctx->nn_variant == ICP_NN_VARIANT_MFMA16) return 2;
-    if (ctx->nn_variant == ICP_NN_VARIANT_BUNDLE) return ctx->nb_pad > 0 ? 3 : 2;
+    const bool bundle = ctx->nb_pad > 0 || ctx->bundle_pending; // (built, or built at first use)
+    if (ctx->nn_variant == ICP_NN_VARIANT_BUNDLE) return bundle ? 3 : 2;
     if (ctx->nn_variant == ICP_NN_VARIANT_VALU || ctx->nn_variant == ICP_NN_VARIANT_GRID) return 0;
     // measured crossover (tools/configs_probe.py, 50-iteration registrations of synthetic n x n
     // pairs): VALU wins at 4,096 (2.4 vs 8.9 ms), the f16 MFMA filter from 8,192 (3.3 vs 3.7
@@ -551,7 +558,7 @@ int level1_kind(const icp_ctx *ctx, size_t n)
     // (16,384 x 16,384: 73 against 25 us), so the bundle filter takes searches from 2^31 pairs
     // (tools/bundle_probe.py, profiles/r03f/)
     if (n >= 8192 && ctx->nm >= 8192)
-        return ctx->nb_pad > 0 && (double)n * (double)ctx->nm >= 2147483648.0 ? 3 : 2;
+        return bundle && (double)n * (double)ctx->nm >= 2147483648.0 ? 3 : 2;
     return 0;
 }
 
@@ -811,6 +818,24 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         }();
         // (the bundle bound needs every query's seed: without the grid, the full f16 pass)
         if (l1 == 3 && !seeded && !(grid_seed && ctx->g_pts)) l1 = 2;
+        if (l1 == 3 && !seeded && slot_order && ctx->bundle_pending && ctx->nn_variant == ICP_NN_VARIANT_AUTO) {
+            // an icp_run's unseeded first search while the bundle images are still pending: the
+            // exact grid search (ring seed, then the complete box), as the grid variant runs it.
+            // The run's policy then keeps to the grid until its far count says otherwise, and a
+            // registration that stays near the model never builds the bundle images (§3.6)
+            ctx->stats.last_filter = ICP_FILTER_GRID;
+            TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
+            TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
+            if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
+            launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1,
+                                  ctx->fb_list, ctx->fb_T, ctx->st);
+            if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
+            launch_nn_resolve(ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, q.f, q.x, q.y, q.z, ctx->m32, ctx->model.x,
+                              ctx->model.y, ctx->model.z, (int)ctx->nm, (int)n, ctx->idx, ctx->st, stop);
+            LAUNCHCHK("nn_grid_search (first)");
+            return ICP_OK;
+        }
+        if (l1 == 3) TRY(ensure_bundle(ctx)); // (built at their first use)
         const bool gseed = l1 >= 2 && !seeded && grid_seed && ctx->g_pts;
         if (gseed) {
             launch_nn_grid_seed((int)n, q.x, q.y, q.z, grid_view(ctx), (int)ctx->nm, ctx->idx, ctx->st);
@@ -1106,6 +1131,59 @@ int check_ready(icp_ctx *ctx, bool need_scene)
         return fail(ctx, ICP_E_NO_MODEL, "model/scene not set (icp_set_model / icp_set_scene)");
     HIPCHK(hipSetDevice(ctx->device));
     return ensure_reduction_space(ctx);
+}
+
+// The bundle filter's kd order, images, block frames and kd tables for the resident model (§3.6),
+// with kd_h (nullable) a host-built kd order (ICP_KD_HOST).  Synchronous (the frames' max R_B).
+static int build_bundle(icp_ctx *ctx, const int *kd_h)
+{
+    const size_t nm = ctx->nm;
+    const int nb_pad = bundle_pad(nm);
+    TRY(grow(ctx, &ctx->b_kd, &ctx->b_kd_cap, nm));
+    if (kd_h) {
+        HIPCHK(hipMemcpyAsync(ctx->b_kd, kd_h, sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
+    } else {
+        kd_plan(nm, ctx->kd_plan); // (ctx-owned: outlives the stream's copy of it)
+        TRY(grow(ctx, &ctx->kd_scratch, &ctx->kd_scratch_cap, kd_order_scratch_bytes(ctx->kd_plan)));
+        if (launch_kd_order(ctx->model.x, ctx->model.y, ctx->model.z, ctx->kd_plan, ctx->kd_scratch,
+                            ctx->kd_scratch_cap, ctx->b_kd, ctx->st) != 0)
+            return fail(ctx, ICP_E_HIP, "the bundle kd order's build failed");
+    }
+    const size_t nbx = (size_t)nb_pad + 32; // + the null block (icp_bundle.hip)
+    TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, nbx * 32));
+    TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, nbx * 1024));
+    TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, nbx * 32));
+    TRY(grow(ctx, &ctx->b_bctr, &ctx->b_bctr_cap, nbx));
+    TRY(grow(ctx, &ctx->b_blk, &ctx->b_blk_cap, nbx / 32));
+    launch_build_bundle_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
+                               ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_bctr, ctx->b_blk, ctx->st);
+    LAUNCHCHK("build_bundle_images");
+    // the local pair test's image and block frames, and max R_B (the certificate's R)
+    const size_t nfr = nbx / 32;
+    TRY(grow(ctx, &ctx->b_pimg_l, &ctx->b_pimg_l_cap, nbx * 1024));
+    TRY(grow(ctx, &ctx->b_frame, &ctx->b_frame_cap, nfr));
+    launch_build_local_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
+                              ctx->scale16, ctx->b_pimg_l, ctx->b_frame, ctx->st);
+    LAUNCHCHK("build_local_images");
+    TRY(grow(ctx, &ctx->m4kd, &ctx->m4kd_cap, nm));
+    TRY(grow(ctx, &ctx->kd_of, &ctx->kd_of_cap, nm));
+    launch_build_kd_tables(ctx->m4, ctx->b_kd_orig, (int)nm, ctx->m4kd, ctx->kd_of, ctx->st);
+    LAUNCHCHK("build_kd_tables");
+    std::vector<float4> fr(nfr);
+    HIPCHK(hipMemcpyAsync(fr.data(), ctx->b_frame, sizeof(float4) * nfr, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    double rl = 0.0;
+    for (const float4 &f : fr) rl = std::max(rl, (double)f.w);
+    ctx->b_rlmax = rl;
+    ctx->nb_pad = nb_pad;
+    ctx->bundle_pending = false;
+    return ICP_OK;
+}
+
+// the bundle filter's images, built now if they are pending (the first search that needs them)
+int ensure_bundle(icp_ctx *ctx)
+{
+    return ctx->bundle_pending ? build_bundle(ctx, nullptr) : ICP_OK;
 }
 
 } // namespace
@@ -1446,47 +1524,14 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm)
     ctx->nb_pad = 0;
     ctx->b_rlmax = -1.0;
     std::vector<int> kd_h; // (ICP_KD_HOST: alive until the closing sync)
-    if (nm >= (size_t)kBundleMinModel) { // the bundle filter's kd images (icp_bundle.hip)
-        const int nb_pad = bundle_pad(nm);
-        TRY(grow(ctx, &ctx->b_kd, &ctx->b_kd_cap, nm));
+    ctx->bundle_pending = false;
+    if (nm >= (size_t)kBundleMinModel) { // the bundle filter's kd images (icp_bundle.hip): at first use
         if (kd_host()) {
-            kd_h = bundle_kd_order(m_xyz, nm);
-            HIPCHK(hipMemcpyAsync(ctx->b_kd, kd_h.data(), sizeof(int) * nm, hipMemcpyHostToDevice, ctx->st));
+            kd_h = bundle_kd_order(m_xyz, nm); // (the host build needs the caller's array: now)
+            TRY(build_bundle(ctx, kd_h.data()));
         } else {
-            kd_plan(nm, ctx->kd_plan); // (ctx-owned: outlives the stream's copy of it)
-            TRY(grow(ctx, &ctx->kd_scratch, &ctx->kd_scratch_cap, kd_order_scratch_bytes(ctx->kd_plan)));
-            if (launch_kd_order(ctx->model.x, ctx->model.y, ctx->model.z, ctx->kd_plan, ctx->kd_scratch,
-                                ctx->kd_scratch_cap, ctx->b_kd, ctx->st) != 0)
-                return fail(ctx, ICP_E_HIP, "icp_set_model: the kd order's build failed");
+            ctx->bundle_pending = true;
         }
-        const size_t nbx = (size_t)nb_pad + 32; // + the null block (icp_bundle.hip)
-        TRY(grow(ctx, &ctx->b_img, &ctx->b_img_cap, nbx * 32));
-        TRY(grow(ctx, &ctx->b_pimg, &ctx->b_pimg_cap, nbx * 1024));
-        TRY(grow(ctx, &ctx->b_kd_orig, &ctx->b_kd_orig_cap, nbx * 32));
-        TRY(grow(ctx, &ctx->b_bctr, &ctx->b_bctr_cap, nbx));
-        TRY(grow(ctx, &ctx->b_blk, &ctx->b_blk_cap, nbx / 32));
-        launch_build_bundle_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
-                                   ctx->scale16, ctx->b_img, ctx->b_pimg, ctx->b_kd_orig, ctx->b_bctr, ctx->b_blk,
-                                   ctx->st);
-        LAUNCHCHK("build_bundle_images");
-        // the local pair test's image and block frames, and max R_B (the certificate's R)
-        const size_t nfr = nbx / 32;
-        TRY(grow(ctx, &ctx->b_pimg_l, &ctx->b_pimg_l_cap, nbx * 1024));
-        TRY(grow(ctx, &ctx->b_frame, &ctx->b_frame_cap, nfr));
-        launch_build_local_images(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->b_kd, nb_pad, ctx->c,
-                                  ctx->scale16, ctx->b_pimg_l, ctx->b_frame, ctx->st);
-        LAUNCHCHK("build_local_images");
-        TRY(grow(ctx, &ctx->m4kd, &ctx->m4kd_cap, nm));
-        TRY(grow(ctx, &ctx->kd_of, &ctx->kd_of_cap, nm));
-        launch_build_kd_tables(ctx->m4, ctx->b_kd_orig, (int)nm, ctx->m4kd, ctx->kd_of, ctx->st);
-        LAUNCHCHK("build_kd_tables");
-        std::vector<float4> fr(nfr);
-        HIPCHK(hipMemcpyAsync(fr.data(), ctx->b_frame, sizeof(float4) * nfr, hipMemcpyDeviceToHost, ctx->st));
-        HIPCHK(hipStreamSynchronize(ctx->st));
-        double rl = 0.0;
-        for (const float4 &f : fr) rl = std::max(rl, (double)f.w);
-        ctx->b_rlmax = rl;
-        ctx->nb_pad = nb_pad;
     }
     std::vector<double> pm;
     if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel)) { // the one-launch loops' model image
@@ -2117,7 +2162,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == timing_phase;
             const bool grid_cur = grid_next; // (decided with the previous transform, or carried over)
-            grid_next = grid_policy && far_obs >= 0 && far_obs <= far_thr;
+            // (nothing observed yet: the grid while the bundle images are still pending)
+            grid_next = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : ctx->bundle_pending);
             // (the search of an iteration queued behind the converged one returns at once)
             // (the seed distances the last transform wrote -- of this run, or of the last one when
             // carried over -- for a grid search)
@@ -2745,6 +2791,7 @@ int icp_bundle_audit(icp_ctx *ctx, int groups, icp_bundle_audit_result *out)
     if (!ctx || !out || groups < 1) return ICP_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     const DevCloud &P = ctx->scene;
+    TRY(ensure_bundle(ctx));
     if (!ctx->b_img || !ctx->b_bctr || !ctx->b_kd_orig || ctx->nb_pad <= 0 || !P.n || !ctx->seeds_valid)
         return fail(ctx, ICP_E_NO_MODEL, "icp_bundle_audit: needs the bundle images and a scene with correspondences");
     unsigned long long *buf = nullptr;
@@ -2778,8 +2825,9 @@ int icp_bundle_audit(icp_ctx *ctx, int groups, icp_bundle_audit_result *out)
 int icp_get_model_order(icp_ctx *ctx, int32_t *kd_out)
 {
     if (!ctx || !kd_out) return ICP_E_ARG;
-    if (!ctx->has_model || ctx->nb_pad <= 0 || !ctx->b_kd) return fail(ctx, ICP_E_NO_MODEL, "no bundle kd order");
     HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->has_model) TRY(ensure_bundle(ctx));
+    if (!ctx->has_model || ctx->nb_pad <= 0 || !ctx->b_kd) return fail(ctx, ICP_E_NO_MODEL, "no bundle kd order");
     HIPCHK(hipMemcpyAsync(kd_out, ctx->b_kd, sizeof(int32_t) * ctx->nm, hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
