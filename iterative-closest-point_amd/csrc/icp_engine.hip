@@ -708,7 +708,9 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
     TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
     int *kpos_out = nullptr;
-    if (ctx->nn_rule == ICP_NN_RULE_SQUARED && ctx->m4kd && ctx->kd_of) {
+    // (kd tables of the current model only: nb_pad > 0 -- set_model resets it, and pending bundle
+    // images leave the last model's tables in place)
+    if (ctx->nn_rule == ICP_NN_RULE_SQUARED && ctx->m4kd && ctx->kd_of && ctx->nb_pad > 0) {
         TRY(grow(ctx, &ctx->kpos, &ctx->kpos_cap, n));
         kpos_out = ctx->kpos;
     }
