@@ -23,6 +23,9 @@ Algorithmic bytes per scene point (fp64 SoA clouds):
     p 24 + Y 24 + write p 24 + the next search's 64 B slot record + seed16 4 = 140 (no fp32 copy;
     captures up to r03z ran the 92 B form: p 24 + Y 24 + write p 24 + p32 16 + seed16 4)
   NN filter: SURVEY §8d compulsory 12 N + 12 M + 4 N (fp32 xyz in, int32 index out)
+From profiles/r04x on (every C4 search the seeded grid search, which writes Y; no bundle record):
+  shifted_moments_kernel: p 24 + Y 24 = 48 (the search wrote Y: no index, no gather)
+  transform_err_kernel: p 24 + Y 24 + write p 24 + the next search's seed distance 8 = 80
 """
 from __future__ import annotations
 
@@ -45,8 +48,11 @@ BYTES_PER_POINT = {"shifted_moments_kernel": 84, "gather_moments_kernel": 84, "c
 
 
 def bytes_per_point(kernel, tag):
-    """BYTES_PER_POINT, with the form of transform_err_kernel the capture ran: the slot-record
-    form (140 B) from profiles/r03ac on, the fp32-copy form (92 B) before it."""
+    """BYTES_PER_POINT, with the form of the kernels the capture ran: from r04x the grid search's
+    (moments streaming Y: 48 B, transform writing the seed distance: 80 B); the slot-record
+    transform (140 B) from r03ac; the fp32-copy transform (92 B) before it."""
+    if _tag_key(tag) >= _tag_key("r04x") and kernel in ("shifted_moments_kernel", "transform_err_kernel"):
+        return {"shifted_moments_kernel": 48, "transform_err_kernel": 80}[kernel]
     if kernel == "transform_err_kernel" and _tag_key(tag) < _tag_key("r03ac"):
         return 92
     return BYTES_PER_POINT[kernel]
