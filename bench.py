@@ -336,7 +336,8 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
     return {"iterations_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps,
             "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1), "brute_force_fallbacks": st["grid_fallback"],
             "final_err": float(errs[-1]), "kernel": f"{GRID_SEEDED_KERNEL} (seeded, every query)",
-            "roofline": committed_config_roofline("grid")}
+            "roofline": grid_roofline(p.shape[0], m.shape[0], st["nn_ms"] / max(st["nn_launches"], 1),
+                                      *pmc_traffic(GRID_SEEDED_KERNEL), True)}
 
 
 def baseline_configs(device, reps=3):
