@@ -2051,8 +2051,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // transform the host has seen left at most n/32 points farther than 1.5 grid cells from their
     // correspondence (the queries whose box exceeds kSeededBox cells: the second, per-wave pass).  The decision for
     // iteration k + 1 is taken when k is enqueued (k's transform writes the bundle's records and
-    // seeds only if k + 1 is a bundle search), on the count of an iteration one or two behind;
-    // the first two searches are the bundle cascade's.  Both paths return the exact first
+    // seeds only if k + 1 is a bundle search), on the count of an iteration one or two behind.
+    // Before any count is seen: the count the last run ended with when this run continues it
+    // (carry), else the grid while the bundle images are still unbuilt (bundle_pending: the
+    // first search is then the unseeded grid search, nn_search_begin), else the bundle cascade.
+    // A far count above the threshold builds the bundle images (ensure_bundle).  Both paths return the exact first
     // minimum, so the trajectory is the same whichever runs.  ICP_GRID_AUTO=0: always the bundle.
     const bool grid_policy = ctx->scene_slot && ctx->nn_mode == ICP_NN_CERTIFIED &&
                              ctx->nn_variant == ICP_NN_VARIANT_AUTO && level1_kind(ctx, n) == 3 && grid_auto();

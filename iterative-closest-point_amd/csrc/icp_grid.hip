@@ -38,12 +38,17 @@ __device__ __forceinline__ double d64g(double px, double py, double pz, double m
     return (dx * dx + dy * dy) + dz * dz; // cpu.cc:17-19 order, no FMA (-ffp-contract=off)
 }
 
-__device__ __forceinline__ int cell1(double x, double lo, double inv_h, int g)
+// the cell of a coordinate t in cell units (t = (x - lo) inv_h), clamped to [0, g - 1]: monotone in t
+__device__ __forceinline__ int cellt(double t, int g)
 {
-    const double t = (x - lo) * inv_h;
     if (!(t > 0.0)) return 0;
     if (t >= (double)(g - 1)) return g - 1;
     return (int)t;
+}
+
+__device__ __forceinline__ int cell1(double x, double lo, double inv_h, int g)
+{
+    return cellt((x - lo) * inv_h, g);
 }
 
 __global__ __launch_bounds__(kBlock) void grid_count_kernel(
@@ -284,6 +289,58 @@ __device__ __forceinline__ bool complete_box(const double q[3], double r2, const
     return cells <= budget;
 }
 
+// The box's rows trimmed to the sphere (round 4): the x-cells of row (cy, cz) that can hold a
+// point m with D64(q, m) <= best, narrowed from [x0, x1] (false: the row holds none).  fp32 in
+// cell units, with an absolute slack sigma = 2^-8 cells that covers every error below:
+//  - u = (q - lo) inv_h, v = (m - lo) inv_h (reals); tq = fl32(fl64((q - lo) inv_h)) is within
+//    2^-10 of u while |tq| <= 2^13 (else no trim), and a model point's fp64 cell
+//    coordinate t' (cell1's) within 2^-38 of v (|t'| <= g <= 2^12);
+//  - a point in cell c <= g - 2 has t' < c + 1 (not clamped from above), one in cell c >= 1 has
+//    t' >= c; so |u_y - v_y| >= gy = max(tq_y - (c + 1), c - tq_y) - sigma (each term where it
+//    applies), and 0 if negative;
+//  - |u - v| <= rho = sqrt(best) inv_h (1 + 2^-50) (D64 >= |q - m|^2 (1 - 6 2^-53)); rho32 >= rho;
+//    rem = rho32^2 (1 + 2^-20) - (gy^2 + gz^2) >= (u_x - v_x)^2 despite fp32 rounding (the factor
+//    covers it when gy^2 + gz^2 <= rho^2; otherwise the row holds no such point), and
+//    rx = sqrt(rem) (1 + 2^-18) >= |u_x - v_x| (sqrt within a few ulps);
+//  - so t'_x lies in [tq_x - rx - sigma, tq_x + rx + sigma] (the fp32 sums' rounding is within
+//    sigma), and cellt, being monotone, puts m between the cells of the two ends.
+// Any upper bound of the first minimum's distance may serve as best (a lane's running minimum):
+// every point that can be the first minimum, or tie with it, stays in its row's range.
+__device__ __forceinline__ bool trim_row(const double q[3], double best, const GridView &gv, int cy, int cz,
+                                         int &x0, int &x1)
+{
+    // (tq recomputed at every row: the opaque copies keep the compiler from hoisting it out of the
+    // row loop, where three more live registers cost the kernel a wave per SIMD)
+    float tq[3];
+    bool on = true;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        double qa = q[a];
+        asm volatile("" : "+v"(qa));
+        const double t = (qa - gv.lo[a]) * gv.inv_h;
+        on = on && fabs(t) <= 8192.0;
+        tq[a] = (float)t;
+    }
+    if (!on) return true;
+    constexpr float sigma = 0x1.0p-8f;
+    const float rho = (float)(sqrt(best) * gv.inv_h) * (1.0f + 0x1.0p-20f);
+    float gap[2];
+#pragma unroll
+    for (int a = 1; a < 3; ++a) {
+        const int c = a == 1 ? cy : cz;
+        float d = 0.0f;
+        if (c <= gv.g[a] - 2) d = fmaxf(d, tq[a] - (float)(c + 1));
+        if (c >= 1) d = fmaxf(d, (float)c - tq[a]);
+        gap[a - 1] = fmaxf(d - sigma, 0.0f);
+    }
+    const float rem = rho * rho * (1.0f + 0x1.0p-20f) - (gap[0] * gap[0] + gap[1] * gap[1]);
+    if (!(rem >= 0.0f)) return false;
+    const float rx = sqrtf(rem) * (1.0f + 0x1.0p-18f);
+    x0 = max(x0, cellt((double)(tq[0] - rx - sigma), gv.g[0]));
+    x1 = min(x1, cellt((double)(tq[0] + rx + sigma), gv.g[0]));
+    return x0 <= x1;
+}
+
 // One G-lane group per queued query (grid-stride over *count; the trip count is uniform
 // within a group, so a group is always entirely active).
 template <int G, bool FLAT>
@@ -517,7 +574,7 @@ __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
     int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
     int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
     double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
-    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap)
+    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap, int trim)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
@@ -542,11 +599,12 @@ __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
                 for (int u = 0; u < KR; ++u) {
                     const int r = r0 + u * G;
                     int a = 0, b = 0;
-                    if (r < nrows) {
-                        const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                    int x0 = c0[0], x1 = c1[0];
+                    const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                    if (r < nrows && (!trim || trim_row(q, best, gv, cy, cz, x0, x1))) {
                         const int row = (cz * gv.g[1] + cy) * gv.g[0];
-                        a = gv.start[row + c0[0]];
-                        b = gv.start[row + c1[0] + 1];
+                        a = gv.start[row + x0];
+                        b = gv.start[row + x1 + 1];
                     }
                     k0[u] = a;
                     pre[u + 1] = pre[u] + (b - a);
@@ -616,7 +674,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
     int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
     int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
     double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
-    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap)
+    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap, int trim)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
@@ -645,11 +703,12 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
                 for (int u = 0; u < KR; ++u) {
                     const int r = r0 + u * G;
                     int a = 0, b = 0;
-                    if (r < nrows) {
-                        const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                    int x0 = c0[0], x1 = c1[0];
+                    const int cy = c0[1] + r % ny, cz = c0[2] + r / ny;
+                    if (r < nrows && (!trim || trim_row(q, best, gv, cy, cz, x0, x1))) {
                         const int row = (cz * gv.g[1] + cy) * gv.g[0];
-                        a = gv.start[row + c0[0]];
-                        b = gv.start[row + c1[0] + 1];
+                        a = gv.start[row + x0];
+                        b = gv.start[row + x1 + 1];
                     }
                     k0[u] = a;
                     pre[u + 1] = pre[u] + (b - a);
@@ -935,9 +994,15 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     const int per_block = kBlock / forms[f].g;
     int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
     if (xcd_remap) blocks = (blocks + 7) / 8 * 8; // (whole eighths; the extra workgroups find no query)
+    // ICP_GRID_TRIM=1: the box's rows trimmed to the seed's sphere (trim_row).  Exact, and it scans
+    // ~14% fewer cells at C4, but measured no faster there (109.7 against 109.9 us) and slower at
+    // the W = 8 shard (37.0 against 33.4 us: its ALU sits in each query's dependent chain), so the
+    // whole box stays the default (profiles/r04z/trim)
+    const char *te = getenv("ICP_GRID_TRIM");
+    const int trim = te && std::string(te) == "1" ? 1 : 0;
 #define SEEDED(K, ...)                                                                                       \
     K<__VA_ARGS__><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz, far_count, \
-                                              far_list, far_hint, stop, xcd_remap ? 1 : 0)
+                                              far_list, far_hint, stop, xcd_remap ? 1 : 0, trim)
     switch (f) {
     case 1: SEEDED(nn_grid_seeded_kernel, 4, 2, 2, 1); break;
     case 2: SEEDED(nn_grid_seeded_kernel, 4, 2, 4, 1); break;

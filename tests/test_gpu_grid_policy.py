@@ -129,14 +129,18 @@ def test_policy_carries_over_to_the_next_run(amd):
     assert np.array_equal(a["scene"], b["scene"])
 
 
-@pytest.mark.parametrize("form", ["f4,2,2", "f2,2,2", "2,2,2", "4,1,2"])
-def test_seeded_forms_match_bundle(amd, form, monkeypatch):
+@pytest.mark.parametrize("form,trim", [("f4,2,2", "0"), ("f2,2,2", "0"), ("2,2,2", "0"), ("4,1,2", "0"),
+                                       ("2,2,2", "1"), ("f4,2,2", "1"), ("4,2,2", "1")])
+def test_seeded_forms_match_bundle(amd, form, trim, monkeypatch):
     """Every instantiated form of the seeded grid kernel (ICP_GRID_SEEDED, read at each launch),
-    the fp32-image forms included, returns the bundle cascade's indices bit for bit over a run."""
+    the fp32-image forms included, with and without the rows trimmed to the seed's sphere
+    (ICP_GRID_TRIM, trim_row), returns the bundle cascade's indices bit for bit over a run."""
     monkeypatch.setenv("ICP_GRID_SEEDED", form)
+    monkeypatch.setenv("ICP_GRID_TRIM", trim)
     m, p = amd.synthetic_pair(N, seed=42)
     a = run(amd, m, p, 16, amd.VARIANT_AUTO)
     monkeypatch.delenv("ICP_GRID_SEEDED")
+    monkeypatch.delenv("ICP_GRID_TRIM")
     b = run(amd, m, p, 16, amd.VARIANT_BUNDLE)
     assert amd.FILTER_NAMES[a["stats"]["last_filter"]] == "grid"
     assert np.array_equal(a["dig"], b["dig"])
