@@ -1678,9 +1678,15 @@ static int moments_phase(icp_ctx *ctx, size_t n)
 // drains without the ticket (an earlier failure), report instead of spinning forever.
 static int wait_flag(icp_ctx *ctx, const int *flag, int ticket)
 {
+    // The stream is queried (a drained stream without the flag is a failure) only once a wait has
+    // lasted 20 ms, then every 20 ms: hipStreamQuery puts a marker at the stream's tail, right
+    // behind the last error step enqueued, and the next search then started 5.6 us late -- every
+    // iteration, with the spin's query every 1,024 pauses (profiles/r04z/gaps*)
+    auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
     for (unsigned spin = 1;; ++spin) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == ticket) return ICP_OK;
-        if ((spin & 1023u) == 0) {
+        if ((spin & 1023u) == 0 && std::chrono::steady_clock::now() >= next) {
+            next = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
             const hipError_t q = hipStreamQuery(ctx->st);
             if (q == hipErrorNotReady) continue;
             if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == ticket) return ICP_OK;
@@ -1856,8 +1862,12 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
         HIPCHK(hipStreamSynchronize(ctx->st));
     } else { // workgroup 0's last store (h_flags[7] = barriers used, a release after the run's
              // mirrored state); an aborted launch never writes it and ends with the stream
+        // (the stream queried after 2 ms, then every 2 ms: each query leaves a marker behind the
+        // launch, which the next launch waits for -- see wait_flag)
+        auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
         for (unsigned spin = 1; __atomic_load_n(ctx->h_flags + 7, __ATOMIC_ACQUIRE) == 0; ++spin) {
-            if ((spin & 1023u) == 0) {
+            if ((spin & 1023u) == 0 && std::chrono::steady_clock::now() >= next) {
+                next = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
                 const hipError_t q = hipStreamQuery(ctx->st);
                 if (q == hipErrorNotReady) continue;
                 if (q != hipSuccess) return fail(ctx, ICP_E_HIP, std::string("icp_run: ") + hipGetErrorString(q));
