@@ -227,6 +227,10 @@ struct icp_ctx {
     // (SeedArgs::far_acc): the next run's policy starts from them instead of two bundle searches
     bool seedd_valid = false;
     int last_far = -1;
+    // second_pass_items (icp_run's policy searches): the grid of the seeded search's second pass
+    // is sized for this many queued queries (0: min(n, 4096)) -- the far count the host last saw
+    int second_pass_items = 0;
+    int last_q2 = -1; // the last run's last observed second-pass queue (IterState::queued2)
     int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
     int *fb_list = nullptr;                           // queries the grid hands back
     double *fb_T = nullptr;
@@ -740,10 +744,21 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     // model extent away) is scanned in place over every model point by its wave (the exact fp64
     // first minimum), instead of a brute-force launch that nearly always finds nothing to do
     // (~5 us a search)
-    launch_nn_grid_resolve(ctx->amb_count + 2, (int)std::min<size_t>(n, 4096), ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
+    // (sized by the queue the host last saw when icp_run's policy runs the search -- at C4 it is
+    // empty after the first seeded search (profiles/r04z/far_counts.log): an empty queue then costs
+    // ~1.5 us instead of the ~4 us of 1,024 idle workgroups; more queries than the grid's waves
+    // are taken in turns)
+    const int sp_items = ctx->second_pass_items > 0 ? std::min(ctx->second_pass_items, 4096) : 4096;
+    launch_nn_grid_resolve(ctx->amb_count + 2, (int)std::min<size_t>(n, sp_items), ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                            grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
                            ctx->fb_T, ctx->st, stop, (int)ctx->nm, kpos_out, ctx->kd_of, 64, yx, yy, yz);
     LAUNCHCHK("grid_seeded_search");
+    static const bool dbg_far = getenv("ICP_DEBUG_FAR") != nullptr; // (diagnostics: synchronises)
+    if (dbg_far) {
+        int h[4];
+        HIPCHK(hipMemcpy(h, ctx->amb_count, sizeof(h), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[far] second pass %d fallback %d\n", h[2], h[1]);
+    }
     ctx->kpos_valid = kpos_out != nullptr;
     ctx->y_ready = y_out;
     return ICP_OK;
@@ -2080,6 +2095,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // not be the bundle cascade's
     const bool carry = grid_policy && ctx->seeds_valid && ctx->seedd_valid;
     int far_obs = carry ? ctx->last_far : -1; // far_acc of the last iteration the host has seen
+    int q2_obs = carry ? ctx->last_q2 : -1;   // queued2 of the last iteration the host has seen
     bool grid_next = carry && far_obs >= 0 && far_obs <= far_thr; // the path of the next search
     SeedArgs sa_grid;       // a transform before a grid search: its seed distances only
     if (grid_policy) {
@@ -2186,6 +2202,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                            (grid_cur || ctx->nn_variant == ICP_NN_VARIANT_GRID)
                                        ? sa.seedd
                                        : nullptr;
+            // (the second pass's grid: for four times the last queue seen, at least 256 queries)
+            ctx->second_pass_items = grid_policy && q2_obs >= 0 ? std::max(256, 4 * q2_obs) : 0;
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false,
                                 fuse_seeds && enqueued > 0 && !grid_cur, &sd->done, ctx->scene_slot,
@@ -2360,6 +2378,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         ++waited;
         if (grid_policy) { // (mirrored by the error step of that iteration)
             far_obs = ctx->h_iter->far_acc;
+            q2_obs = ctx->h_iter->queued2;
             static const bool dbg = getenv("ICP_DEBUG_POLICY") != nullptr;
             if (dbg) fprintf(stderr, "[policy] waited %d far %d thr %d next_grid %d\n", waited, far_obs, far_thr, (int)grid_next);
         }
@@ -2403,6 +2422,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // (every transform of a policy run wrote the seed distances; the next run may start from them)
     ctx->seedd_valid = grid_policy && sa.seedd != nullptr;
     ctx->last_far = far_obs;
+    ctx->last_q2 = q2_obs;
+    ctx->second_pass_items = 0;
     return finish_run(ctx, threshold, err_trace, res, wall0);
 }
 

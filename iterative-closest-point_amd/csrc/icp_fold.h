@@ -20,6 +20,7 @@ __device__ __forceinline__ void horn_step_body(const double *__restrict__ sums, 
     const int qc[4] = {cnt[0], cnt[1], cnt[2], cnt[3]};
     for (int k = 0; k < 4; ++k) cnt[k] = 0;
     s->far_acc = 0; // (this iteration's transform counts afresh)
+    s->queued2 = qc[2];
     if (s->done) return;
     for (int k = 0; k < 4; ++k) s->nn_counts[k] += qc[k];
     double mu_p[3], mu_y[3], S[9], d_caps, sp;

@@ -469,7 +469,9 @@ struct IterState {
     double shift_y[3];
     int far_acc;       // points the last transform left farther than SeedArgs::far_d2 from their
                        // correspondence (zeroed by each Horn step; the host reads the mirror)
-    int pad_;
+    int queued2;       // amb_count[2] of the last search (the seeded grid search's second pass),
+                       // copied by the Horn step before it zeroes the counters (the host sizes
+                       // the next second pass by it)
 };
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,

@@ -20,7 +20,7 @@ namespace {
 // one pass around shifts near the centroids: the centred sums follow as
 // S = sum (p - cp)(y - cy)^T - N dp dy^T etc. (horn_step), with N dp dy^T at rounding level
 template <int kMomBatch, bool YIN, bool FOLD>
-__global__ __launch_bounds__(kBlock, 4) void shifted_moments_kernel(
+__global__ __launch_bounds__(kBlock, kMomBatch >= 8 ? 1 : 4) void shifted_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
     const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st,
@@ -242,7 +242,7 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
     static const int batch = [] {
         const char *e = getenv("ICP_MOM_BATCH");
         const int v = e ? atoi(e) : 2;
-        return v == 1 || v == 4 ? v : 2;
+        return v == 1 || v == 4 || v == 8 ? v : 2;
     }();
 #define MOMENTS(B, Y, F)                                                                                      \
     shifted_moments_kernel<B, Y, F><<<red_blocks(n), kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, \
@@ -255,6 +255,7 @@ void launch_shifted_moments(const int *idx, const double4 *m4, const double *px,
     if (y_ready) {
         if (batch == 1) MOMENTS_Y(1, true);
         else if (batch == 4) MOMENTS_Y(4, true);
+        else if (batch == 8) MOMENTS_Y(8, true);
         else MOMENTS_Y(2, true);
     } else {
         if (batch == 1) MOMENTS_Y(1, false);
@@ -274,13 +275,14 @@ void launch_transform_err(double *px, double *py, double *pz, const double *yx, 
 }
 
 // points of a thread whose loads are issued together in the plain transform (ICP_TR_BATCH = 1 | 2 |
-// 4; the same sums)
+// 4 | 8; the same sums).  C4 W = 1: 155.4-155.7 us per iteration at 2 against 157.3-159.0 at 1,
+// 156.6-160.7 at 4 and 8; the W = 8 shard alike (profiles/r04z/trb_ab.txt)
 static int transform_batch()
 {
     static const int b = [] {
         const char *e = getenv("ICP_TR_BATCH");
-        const int v = e ? atoi(e) : 1;
-        return v == 2 || v == 4 ? v : 1;
+        const int v = e ? atoi(e) : 2;
+        return v == 1 || v == 4 || v == 8 ? v : 2;
     }();
     return b;
 }
@@ -296,6 +298,9 @@ void launch_transform_err_dev(double *px, double *py, double *pz, const double *
     else if (fold.ticket)
         transform_err_kernel<true, false><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf, done,
                                                                             1, p32, partials, sa, fold);
+    else if (transform_batch() == 8)
+        transform_err_kernel<false, false, 8><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf,
+                                                                                done, 1, p32, partials, sa, StepFold{});
     else if (transform_batch() == 4)
         transform_err_kernel<false, false, 4><<<red_blocks(n), kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, Xform{}, xf,
                                                                                 done, 1, p32, partials, sa, StepFold{});
