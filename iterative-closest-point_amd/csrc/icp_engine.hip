@@ -238,6 +238,8 @@ struct icp_ctx {
 
     // reductions
     double *partials = nullptr;
+    double *err_part = nullptr; // (multi-rank icp_run: the transform's residual partials, run_loop)
+    size_t err_part_cap = 0;
     double *sums = nullptr;
     double *h_sums = nullptr; // pinned
     int *h_amb = nullptr;     // pinned
@@ -1384,7 +1386,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
-                    (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials,
+                    (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials, (void *)ctx->err_part,
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts, (void *)ctx->g_pts32,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
@@ -2118,6 +2120,15 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }();
     const bool fused_moments = (fused_steps_env & 1) && red_blocks(n) > 1;
     const bool fused_steps = (fused_steps_env & 2) && red_blocks(n) > 1; // (the transform's)
+    // multi-rank runs: the transform's residual partials wait in err_part, and the next
+    // iteration's moments fold folds them too (launch_reduce_pair: one launch fewer an iteration,
+    // the same bits); the last iteration folds its own before the final all-reduce
+    static const bool err_pair_env = [] { // ICP_ERR_PAIR=0: the separate residual fold (A/B)
+        const char *e = getenv("ICP_ERR_PAIR");
+        return !(e && e[0] == '0');
+    }();
+    const bool err_pair = err_pair_env && lag_run(ctx) && red_blocks(n) > 1 && !fused_steps && !fused_moments;
+    if (err_pair) TRY(grow(ctx, &ctx->err_part, &ctx->err_part_cap, (size_t)kRedMaxBlocksCap));
     if ((fused_steps || fused_moments) && !ctx->fold_ticket) {
         HIPCHK(hipMalloc((void **)&ctx->fold_ticket, 2 * sizeof(unsigned)));
         HIPCHK(hipMemsetAsync(ctx->fold_ticket, 0, 2 * sizeof(unsigned), ctx->st));
@@ -2315,6 +2326,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     launch_reduce_horn(ctx->partials, red_blocks(n), ctx->sums, N, ctx->c, 1, ctx->amb_count, sd,
                                        ctx->st);
                     horn_fused = true;
+                } else if (err_pair) { // (+ the previous transform's residual, into sums[kSumErr])
+                    launch_reduce_pair(ctx->partials, ctx->err_part, red_blocks(n), ctx->sums, ctx->st);
                 } else {
                     red_finish(ctx, n, 17, ctx->sums);
                 }
@@ -2355,15 +2368,17 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 ef.h_trace = ctx->d_trace;
             }
             launch_transform_err_dev(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, need_p32 ? P.f : nullptr,
-                                     red_target(ctx, n, ctx->sums + kSumErr), sa_t, ctx->st, ef);
+                                     err_pair ? ctx->err_part : red_target(ctx, n, ctx->sums + kSumErr), sa_t,
+                                     ctx->st, ef);
             if (!need_p32) ctx->p32_stale = true;
             const bool fold_err = !lag && red_blocks(n) > 1; // (folded by the error step's launch)
-            if (!fold_err && !err_fused) red_finish(ctx, n, 1, ctx->sums + kSumErr);
+            if (!fold_err && !err_fused && !err_pair) red_finish(ctx, n, 1, ctx->sums + kSumErr);
             LAUNCHCHK("transform_err");
             // 6. err = (e + e) / np; stop after the iteration with err < threshold (gpu.cc:76-80)
             if (!lag && !err_fused) TRY(enqueue_err_step(enqueued, fold_err ? ctx->partials : nullptr));
             ++enqueued;
             if (lag && enqueued == max_iter) { // the last residual has no next iteration to ride on
+                if (err_pair) launch_reduce(ctx->err_part, red_blocks(n), 1, ctx->sums + kSumErr, ctx->st);
                 TRY(allreduce(ctx, ctx->sums + kSumErr, 1));
                 TRY(enqueue_err_step(enqueued - 1));
             }

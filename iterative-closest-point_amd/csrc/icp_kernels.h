@@ -619,6 +619,9 @@ void launch_nn_exact_few(const double *q_aos, int nq, const double4 *m4, int nm,
                          hipStream_t st);
 
 // out[k] = sum_b partials[b*K + k], fixed order, one workgroup
+// the moments' 17 sums and the previous transform's residual (out[17]) in one launch, each column
+// bit-identical to its own launch_reduce
+void launch_reduce_pair(const double *part17, const double *part1, int nblocks, double *out, hipStream_t st);
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);
 
 // ---- the model's preparation on the device (icp_model.hip) ------------------------------------

@@ -2388,6 +2388,47 @@ void launch_norms(const double *yx, const double *yy, const double *yz, const do
 
 
 
+// reduce_kernel<17> of the moments' partials into out[0..16] and reduce_kernel<1> of the last
+// transform's residual partials into out[17], in one launch: each column is folded by the same
+// rows per thread and the same tree as in its own launch, so both results are bit-identical
+// (the multi-rank loop: one launch fewer per iteration)
+__global__ __launch_bounds__(kBlock) void reduce_pair_kernel(const double *__restrict__ part17,
+                                                            const double *__restrict__ part1, int nblocks,
+                                                            double *__restrict__ out)
+{
+    __shared__ double sh[kBlock / 64][18];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[17], e[1] = {0.0};
+#pragma unroll
+    for (int k = 0; k < 17; ++k) a[k] = 0.0;
+    fold_rows<17>(part17, nblocks, a);
+    fold_rows<1>(part1, nblocks, e);
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) e[0] += __shfl_xor(e[0], o, 64);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 17; ++k) sh[wave][k] = a[k];
+        sh[wave][17] = e[0];
+    }
+    __syncthreads();
+    if (threadIdx.x < 18) {
+        double r = sh[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) r += sh[w][threadIdx.x];
+        out[threadIdx.x] = r;
+    }
+}
+
+void launch_reduce_pair(const double *part17, const double *part1, int nblocks, double *out, hipStream_t st)
+{
+    reduce_pair_kernel<<<1, kBlock, 0, st>>>(part17, part1, nblocks, out);
+}
+
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st)
 {
     switch (K) {
