@@ -72,10 +72,13 @@ def test_policy_stays_on_bundle_far_from_the_model(amd):
     assert np.array_equal(a["scene"], b["scene"])
 
 
+@pytest.mark.parametrize("trim", ["0", "1"])
 @pytest.mark.parametrize("case", ["clustered", "shard"])
-def test_seeded_grid_against_oracle(amd, oracle, case):
+def test_seeded_grid_against_oracle(amd, oracle, case, trim, monkeypatch):
     """Dense clusters (hundreds of points a cell region: big boxes for the second pass) and an
-    8-way shard's sparse queries; the grid variant's seeded searches against the oracle."""
+    8-way shard's sparse queries; the grid variant's seeded searches against the oracle, with
+    the whole box and with its rows trimmed to the seed's sphere (ICP_GRID_TRIM)."""
+    monkeypatch.setenv("ICP_GRID_TRIM", trim)
     rng = np.random.default_rng(5)
     if case == "clustered":
         centres = rng.uniform(-1, 1, size=(64, 3))
