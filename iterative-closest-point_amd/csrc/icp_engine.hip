@@ -230,8 +230,6 @@ struct icp_ctx {
     // second_pass_items (icp_run's policy searches): the grid of the seeded search's second pass
     // is sized for this many queued queries (0: min(n, 4096)) -- the far count the host last saw
     int second_pass_items = 0;
-    int second_pass_q2 = -1;          // the last queue seen (-1: none): the drain's condition
-    unsigned *drain_ticket = nullptr; // nn_grid_seeded_kernel<..., DRAIN>'s arrival counter
     int last_q2 = -1; // the last run's last observed second-pass queue (IterState::queued2)
     int *amb1_hint = nullptr, *amb_hint = nullptr;    // candidates of the level-1 / level-2 queues
     int *fb_list = nullptr;                           // queries the grid hands back
@@ -730,29 +728,11 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     const DevCloud &Y = ctx->Y;
     const bool y_out = seedd && Y.x && Y.cap >= n;
     double *yx = y_out ? Y.x : nullptr, *yy = y_out ? Y.y : nullptr, *yz = y_out ? Y.z : nullptr;
-    // ICP_GRID_DRAIN=1: when the last queue the host saw held at most 32 queries, the search's own
-    // last workgroup resolves the queue and no second launch follows (SeededDrain)
-    // (=2, for the tests: at every seeded search, whatever the queue)
-    const char *drain_e = getenv("ICP_GRID_DRAIN"); // (read at every search: the tests switch it)
-    const int drain_env = drain_e ? atoi(drain_e) : 0;
-    const bool drain = y_out && (drain_env == 2 || (drain_env == 1 && ctx->second_pass_q2 >= 0 &&
-                                                    ctx->second_pass_q2 <= 32));
-    if (drain && !ctx->drain_ticket) {
-        HIPCHK(hipMalloc((void **)&ctx->drain_ticket, sizeof(unsigned)));
-        HIPCHK(hipMemsetAsync(ctx->drain_ticket, 0, sizeof(unsigned), ctx->st));
-    }
     if (y_out) {
         kpos_out = nullptr;
-        SeededDrain dr;
-        if (drain) {
-            dr.ticket = ctx->drain_ticket;
-            dr.budget = grid_budget(ctx);
-            dr.nm = (int)ctx->nm;
-            dr.fb_count = ctx->amb_count + 1;
-        }
         launch_nn_grid_seeded((int)n, q.x, q.y, q.z, grid_view(ctx), kSeededBox, seedd, ctx->m4, ctx->idx, yx, yy,
                               yz, ctx->amb_count + 2, ctx->amb1, ctx->amb1_hint, stop, xcd, ctx->st,
-                              (long long)ctx->nm, dr);
+                              (long long)ctx->nm);
     } else {
         launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), kSeededBox, ctx->idx,
                                    ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0, xcd,
@@ -771,7 +751,7 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     // ~1.5 us instead of the ~4 us of 1,024 idle workgroups; more queries than the grid's waves
     // are taken in turns)
     const int sp_items = ctx->second_pass_items > 0 ? std::min(ctx->second_pass_items, 4096) : 4096;
-    if (!drain) launch_nn_grid_resolve(ctx->amb_count + 2, (int)std::min<size_t>(n, sp_items), ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
+    launch_nn_grid_resolve(ctx->amb_count + 2, (int)std::min<size_t>(n, sp_items), ctx->amb1, ctx->amb1_hint, q.x, q.y, q.z, ctx->m4,
                            grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1, ctx->fb_list, nullptr,
                            ctx->fb_T, ctx->st, stop, (int)ctx->nm, kpos_out, ctx->kd_of, 64, yx, yy, yz);
     LAUNCHCHK("grid_seeded_search");
@@ -1406,7 +1386,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     for (void *p : {(void *)ctx->m32, (void *)ctx->mperm, (void *)ctx->mm, (void *)ctx->mimg16,
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
-                    (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials, (void *)ctx->err_part, (void *)ctx->drain_ticket,
+                    (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials, (void *)ctx->err_part,
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
                     (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts, (void *)ctx->g_pts32,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
@@ -2235,7 +2215,6 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                        : nullptr;
             // (the second pass's grid: for four times the last queue seen, at least 256 queries)
             ctx->second_pass_items = grid_policy && q2_obs >= 0 ? std::max(256, 4 * q2_obs) : 0;
-            ctx->second_pass_q2 = grid_policy ? q2_obs : -1;
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
                                 timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false,
                                 fuse_seeds && enqueued > 0 && !grid_cur, &sd->done, ctx->scene_slot,
@@ -2460,7 +2439,6 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     ctx->last_far = far_obs;
     ctx->last_q2 = q2_obs;
     ctx->second_pass_items = 0;
-    ctx->second_pass_q2 = -1;
     return finish_run(ctx, threshold, err_trace, res, wall0);
 }
 

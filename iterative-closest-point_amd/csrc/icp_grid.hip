@@ -24,7 +24,6 @@
 #include <cstdlib>
 #include <string>
 
-#include "icp_fold.h"
 #include "icp_kernels.h"
 
 namespace icp {
@@ -169,10 +168,11 @@ __device__ __forceinline__ void scan_box(const double q[3], const int c0[3], con
 // not depend on each other, so kU of them are in flight at once.  Rows are taken G at a time:
 // lane s reads row s's run [k0, k0 + len), an inclusive scan of len numbers the points, and
 // point f's row is found by a binary search of the scan over the group's lanes (shuffles).
-template <int G, int kU = 4>
+template <int G>
 __device__ __forceinline__ void scan_box_flat(const double q[3], const int c0[3], const int c1[3],
                                               const GridView &gv, int sub, double &best, int &bi)
 {
+    constexpr int kU = 4;
     const int ny = c1[1] - c0[1] + 1;
     const int nrows = ny * (c1[2] - c0[2] + 1);
     for (int r0 = 0; r0 < nrows; r0 += G) {
@@ -569,13 +569,12 @@ template <int G> __device__ __forceinline__ void group_lex_min_pos(double &best,
 // coordinates to y (the correspondence cloud the moments then stream: no gather there), re-read
 // from pts at the position the scan met it (an L2 hit).
 // A box over `budget` cells (or a non-finite seed) queues the query for the second pass.
-template <int G, int KR, int KU, int W, bool DRAIN = false>
+template <int G, int KR, int KU, int W>
 __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
     int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
     int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
     double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
-    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap, int trim,
-    SeededDrain drain)
+    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap, int trim)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
@@ -645,54 +644,8 @@ __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
         const bool far = !ok && sub == 0;
         const int fs = wave_append(far_count, far);
         if (far) {
-            if constexpr (DRAIN) { // (write-through: the last workgroup may sit on another XCD)
-                __hip_atomic_store(far_list + fs, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(far_hint + fs, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                far_list[fs] = t;
-                far_hint[fs] = h;
-            }
-        }
-    }
-    if constexpr (DRAIN) {
-        // the last workgroup to finish resolves the queue, a wave a query: every append (agent-
-        // scope atomic count, write-through entries) landed before its workgroup arrived
-        if (!last_arrival(drain.ticket)) return;
-        const int count = __hip_atomic_load(far_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int lane = threadIdx.x & 63;
-        for (int s = threadIdx.x >> 6; s < count; s += kBlock / 64) {
-            const int j = __hip_atomic_load(far_list + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int h = __hip_atomic_load(far_hint + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double q[3] = {px[j], py[j], pz[j]};
-            double best = INFINITY;
-            int bi = h, c0[3], c1[3];
-            bool ok = h >= 0;
-            if (ok) {
-                const double4 mh = m4[h];
-                best = d64g(q[0], q[1], q[2], mh.x, mh.y, mh.z);
-                ok = best == best && best < INFINITY && complete_box(q, best, gv, drain.budget, c0, c1);
-            }
-            if (ok) {
-                scan_box_flat<64, 1>(q, c0, c1, gv, lane, best, bi); // (one load a lane: the main loop's registers)
-                group_lex_min<64>(best, bi);
-            } else { // (the exact fp64 scan of every model point; a NaN query -> index 0)
-                best = INFINITY;
-                bi = -1;
-                for (int k = lane; k < drain.nm; k += 64) {
-                    const double4 m = m4[k];
-                    lex_min(best, bi, d64g(q[0], q[1], q[2], m.x, m.y, m.z), k);
-                }
-                group_lex_min<64>(best, bi);
-                bi = bi < 0 ? 0 : bi;
-                if (lane == 0 && drain.fb_count) atomicAdd(drain.fb_count, 1);
-            }
-            if (lane == 0) {
-                const double4 w = m4[bi];
-                idx[j] = bi;
-                yx[j] = w.x;
-                yy[j] = w.y;
-                yz[j] = w.z;
-            }
+            far_list[fs] = t;
+            far_hint[fs] = h;
         }
     }
 }
@@ -721,8 +674,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
     int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
     int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
     double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
-    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap, int trim,
-    SeededDrain)
+    int *__restrict__ far_list, int *__restrict__ far_hint, const int *__restrict__ stop, int xcd_remap, int trim)
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
@@ -1014,7 +966,7 @@ void launch_nn_grid_resolve_all(int n, const double *px, const double *py, const
 void launch_nn_grid_seeded(int n, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, const double *seedd, const double4 *m4, int *idx, double *yx, double *yy,
                            double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
-                           hipStream_t st, long long nm_hint, const SeededDrain &drain)
+                           hipStream_t st, long long nm_hint)
 {
     // (lanes per query, run bounds read together, point loads in flight; "f": the fp32 image with
     // the fp64 decision for candidates, nn_grid_seeded32_kernel): ICP_GRID_SEEDED picks one of the
@@ -1050,13 +1002,7 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     const int trim = te && std::string(te) == "1" ? 1 : 0;
 #define SEEDED(K, ...)                                                                                       \
     K<__VA_ARGS__><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz, far_count, \
-                                              far_list, far_hint, stop, xcd_remap ? 1 : 0, trim, drain)
-    if (drain.ticket) { // (the queue resolved in the launch: the fp64 form of this many lanes;
-                        // 7 waves a SIMD, as the plain form -- the drain's code spills 4 registers)
-        if (forms[f].g == 2) SEEDED(nn_grid_seeded_kernel, 2, 2, 2, 7, true);
-        else SEEDED(nn_grid_seeded_kernel, 4, 2, 2, 7, true);
-        return;
-    }
+                                              far_list, far_hint, stop, xcd_remap ? 1 : 0, trim)
     switch (f) {
     case 1: SEEDED(nn_grid_seeded_kernel, 4, 2, 2, 1); break;
     case 2: SEEDED(nn_grid_seeded_kernel, 4, 2, 4, 1); break;

@@ -331,20 +331,10 @@ void launch_nn_grid_resolve(const int *count_ptr, int max_items, const int *list
 // every answered query; a box over `budget` cells (or a non-finite seed) goes to (far_list,
 // far_hint = its seed) at *far_count for launch_nn_grid_resolve.  xcd_remap: each XCD takes a
 // contiguous eighth of the queries.
-// drain.ticket != nullptr: the queued queries are resolved by the launch's last workgroup to
-// finish (a whole wave each, as launch_nn_grid_resolve with group 64 and inline_nm = nm would),
-// so that no second launch follows; for a queue the host expects to be empty or nearly so
-struct SeededDrain {
-    unsigned *ticket = nullptr; // arrival counter (zero between launches)
-    int budget = 0;             // the second pass's cell budget (grid_budget)
-    int nm = 0;                 // model points: a box over the budget is scanned over all of them
-    int *fb_count = nullptr;    // statistics: the queries scanned over every model point
-};
 void launch_nn_grid_seeded(int n, const double *px, const double *py, const double *pz, const GridView &gv,
                            int budget, const double *seedd, const double4 *m4, int *idx, double *yx, double *yy,
                            double *yz, int *far_count, int *far_list, int *far_hint, const int *stop, bool xcd_remap,
-                           hipStream_t st, long long nm_hint, // (nm_hint: the model's points, for the form)
-                           const SeededDrain &drain = SeededDrain{});
+                           hipStream_t st, long long nm_hint); // (nm_hint: the model's points, for the form)
 
 // The reference CPU rule's near ties (icp_grid.hip): queries whose squared-rule winner idx[j]
 // has another point within the window are appended to out[*count] (count zeroed by the caller).

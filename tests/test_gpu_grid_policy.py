@@ -72,15 +72,13 @@ def test_policy_stays_on_bundle_far_from_the_model(amd):
     assert np.array_equal(a["scene"], b["scene"])
 
 
-@pytest.mark.parametrize("trim,drain", [("0", "0"), ("1", "0"), ("0", "2")])
+@pytest.mark.parametrize("trim", ["0", "1"])
 @pytest.mark.parametrize("case", ["clustered", "shard"])
-def test_seeded_grid_against_oracle(amd, oracle, case, trim, drain, monkeypatch):
+def test_seeded_grid_against_oracle(amd, oracle, case, trim, monkeypatch):
     """Dense clusters (hundreds of points a cell region: big boxes for the second pass) and an
     8-way shard's sparse queries; the grid variant's seeded searches against the oracle, with
-    the whole box, with its rows trimmed to the seed's sphere (ICP_GRID_TRIM), and with the
-    queue resolved by the search's last workgroup (ICP_GRID_DRAIN)."""
+    the whole box and with its rows trimmed to the seed's sphere (ICP_GRID_TRIM)."""
     monkeypatch.setenv("ICP_GRID_TRIM", trim)
-    monkeypatch.setenv("ICP_GRID_DRAIN", drain)
     rng = np.random.default_rng(5)
     if case == "clustered":
         centres = rng.uniform(-1, 1, size=(64, 3))
@@ -134,21 +132,18 @@ def test_policy_carries_over_to_the_next_run(amd):
     assert np.array_equal(a["scene"], b["scene"])
 
 
-@pytest.mark.parametrize("form,trim,drain", [("f4,2,2", "0", "0"), ("f2,2,2", "0", "0"), ("2,2,2", "0", "0"),
-                                             ("4,1,2", "0", "0"), ("2,2,2", "1", "0"), ("f4,2,2", "1", "0"),
-                                             ("4,2,2", "1", "0"), ("2,2,2", "0", "1"), ("4,2,2", "0", "2")])
-def test_seeded_forms_match_bundle(amd, form, trim, drain, monkeypatch):
+@pytest.mark.parametrize("form,trim", [("f4,2,2", "0"), ("f2,2,2", "0"), ("2,2,2", "0"), ("4,1,2", "0"),
+                                       ("2,2,2", "1"), ("f4,2,2", "1"), ("4,2,2", "1")])
+def test_seeded_forms_match_bundle(amd, form, trim, monkeypatch):
     """Every instantiated form of the seeded grid kernel (ICP_GRID_SEEDED, read at each launch),
     the fp32-image forms included, with and without the rows trimmed to the seed's sphere
     (ICP_GRID_TRIM, trim_row), returns the bundle cascade's indices bit for bit over a run."""
     monkeypatch.setenv("ICP_GRID_SEEDED", form)
     monkeypatch.setenv("ICP_GRID_TRIM", trim)
-    monkeypatch.setenv("ICP_GRID_DRAIN", drain)
     m, p = amd.synthetic_pair(N, seed=42)
     a = run(amd, m, p, 16, amd.VARIANT_AUTO)
     monkeypatch.delenv("ICP_GRID_SEEDED")
     monkeypatch.delenv("ICP_GRID_TRIM")
-    monkeypatch.delenv("ICP_GRID_DRAIN")
     b = run(amd, m, p, 16, amd.VARIANT_BUNDLE)
     assert amd.FILTER_NAMES[a["stats"]["last_filter"]] == "grid"
     assert np.array_equal(a["dig"], b["dig"])
