@@ -1654,6 +1654,11 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     ctx->q_order_src = nullptr; // new contents: a new query order
     ctx->scene_slot = false;    // (in the caller's order)
     ctx->p32_stale = false;
+    // a shard against a model of at least twice its points (C5's 8-way shards: the model's cells
+    // are finer than the scene's spacing): icp_run's policy takes the bundle cascade for the first
+    // searches, so its images are built here rather than between two iterations of the run
+    if (ctx->bundle_pending && np_local > 0 && ctx->nm >= 2 * np_local && ctx->nn_variant == ICP_NN_VARIANT_AUTO)
+        TRY(ensure_bundle(ctx));
     return ICP_OK;
 }
 
