@@ -108,6 +108,11 @@ typedef struct icp_stats {
                                        the first barrier and ran the launch loop instead         */
     int last_filter; /* ICP_FILTER_* of the last NN search's O(N*M)-class level (-1: none since the
                         context was created or its stats reset)                                    */
+    long long bundle_builds;     /* builds of the bundle filter's images (set_model leaves them
+                                    pending; the first search that needs them builds them)         */
+    long long bundle_builds_in_run; /* ... of which between two iterations of an icp_run          */
+    long long run_bundle_searches;  /* icp_run searches that ran the bundle cascade                */
+    long long run_grid_searches;    /* icp_run searches that ran the exact grid search             */
 } icp_stats;
 /* icp_stats.last_filter: the search level that decided most queries */
 #define ICP_FILTER_VALU 0    /* fp32 direct-form filter on the vector ALUs */

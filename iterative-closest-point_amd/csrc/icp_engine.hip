@@ -766,17 +766,31 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     return ICP_OK;
 }
 
+// What icp_run's last enqueued transform wrote for the next search (transform_err_kernel, SeedArgs).
+// The next search may use each output only in the form it was written in: the bundle filter's
+// slot records exist in a global and a local pair-test form (local_r, icp_bundle_rec.h), and
+// seed16 holds either the f16 seed (mfma16_seed_value) or the local form's shift s0.
+struct SeedState {
+    bool seedd = false;      // b_seedd: each point's seed distance D64(p', y)
+    int seed16 = 0;          // seed16: 0 not written, 1 the f16 seeds, 2 the local shifts s0
+    bool records = false;    // b_qop / b_gop / b_gctr: the slot records and group bounds
+    double rec_local = -1.0; // the records' local_r (-1: the global form)
+};
+
 // Launches the complete NN search of the n queries in q against the resident model ->
 // ctx->idx, with no host synchronisation: every level is sized on the device.  Queue sizes:
 // amb_count [0] queue of the VALU certificate, [1] grid -> fp64 brute-force fallback,
 // [2] level-1 (MFMA) queue, [3] level-1 queries without a candidate.  ev0..ev1 brackets the
 // O(N*M) kernel.  seeded: ctx->idx holds a previous correspondence of each query (icp_run).
-// zero_counts = false: amb_count is already zero (icp_run: horn_step clears it)
+// zero_counts = false: amb_count is already zero (icp_run: horn_step clears it).  ws (nullable):
+// what icp_run's previous transform wrote (SeedState); each part is used only if its form is
+// the one this search runs, else rebuilt here.
 int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipEvent_t ev0, hipEvent_t ev1,
-                    bool zero_counts = true, bool seeds_ready = false, const int *stop = nullptr,
-                    bool slot_order = false, bool records_ready = false, bool grid_seeded = false,
-                    const double *seedd = nullptr)
+                    bool zero_counts = true, const SeedState *ws = nullptr, const int *stop = nullptr,
+                    bool slot_order = false, bool grid_seeded = false, const double *seedd = nullptr)
 {
+    const SeedState none;
+    const SeedState &w = ws ? *ws : none;
     TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
     ctx->kpos_valid = false;
     ctx->y_ready = false;
@@ -854,13 +868,15 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             LAUNCHCHK("nn_grid_search (first)");
             return ICP_OK;
         }
+        if (l1 == 3 && ctx->bundle_pending && ws) ctx->stats.bundle_builds_in_run += 1; // (icp_run, mid-run)
         if (l1 == 3) TRY(ensure_bundle(ctx)); // (built at their first use)
         const bool gseed = l1 >= 2 && !seeded && grid_seed && ctx->g_pts;
         if (gseed) {
             launch_nn_grid_seed((int)n, q.x, q.y, q.z, grid_view(ctx), (int)ctx->nm, ctx->idx, ctx->st);
             LAUNCHCHK("nn_grid_seed");
-            seeds_ready = false; // the seeds come from these candidates, below
         }
+        // (gseed: the seeds come from these candidates, below -- nothing the transform wrote)
+        const SeedState &wu = gseed ? none : w;
         const bool sd = (seeded || gseed) && l1 >= 2;
         const bool v2 = l1 == 3 && bundle_v2();
         ctx->stats.last_filter = l1 == 3 ? ICP_FILTER_BUNDLE : l1 == 2 ? ICP_FILTER_MFMA16 : ICP_FILTER_MFMA;
@@ -876,6 +892,15 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             TRY(grow(ctx, &ctx->kpos, &ctx->kpos_cap, n));
             kpos_out = ctx->kpos;
         }
+        // the transform's records serve only the form this search runs: the local pair test's
+        // with the current frames' R (b_rlmax, set by the build of the images), else the global
+        // one.  A run that started while the images were pending wrote no records before they
+        // were built, and a form written for other images is rebuilt by the prep.
+        const bool records_ready = v2 && wu.records && sd &&
+                                   (local ? wu.rec_local >= 0.0 && wu.rec_local == ctx->b_rlmax : wu.rec_local < 0.0);
+        // seed16 ready in this search's form: the shifts come with local records (else the prep
+        // writes them), the f16 seeds from a transform that wrote them
+        const bool seeds_ready = local ? records_ready && wu.seed16 == 2 : wu.seed16 == 1;
         if (sd && !seeds_ready) { // (icp_run: the previous iteration's transform wrote them)
             TRY(grow(ctx, &ctx->seed16, &ctx->seed16_cap, n));
             if (!local) // (local: the prep writes each query's shift there)
@@ -920,11 +945,11 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
                                       sizeof(unsigned long long) * kBundleCounterFields * ctx->b_counters_rows,
                                       ctx->st));
             }
-            // (seeds_ready: icp_run's previous transform wrote the seeds, and with them each
-            // point's seed distance, SeedArgs::seedd; records_ready: the records and group bounds
-            // themselves, SeedArgs::qop)
+            // (wu.seedd: icp_run's previous transform wrote each point's seed distance,
+            // SeedArgs::seedd, which the prep would otherwise gather; records_ready: the records
+            // and group bounds themselves, SeedArgs::qop)
             if (!records_ready) launch_bundle_prep(q.x, q.y, q.z, (int)n, order ? ctx->q_pos : nullptr, ctx->idx, ctx->m4,
-                               seeds_ready ? ctx->b_seedd : nullptr, ctx->c, ctx->scale16, sd ? ctx->seed16 : nullptr, nslots, ctx->b_qop,
+                               sd && wu.seedd && ctx->b_seedd ? ctx->b_seedd : nullptr, ctx->c, ctx->scale16, sd ? ctx->seed16 : nullptr, nslots, ctx->b_qop,
                                order ? ctx->b_qraw : nullptr, ctx->st, stop, order ? nullptr : ctx->b_gop,
                                order ? nullptr : ctx->b_gctr, local ? ctx->b_rlmax : -1.0);
             if (order && !records_ready) launch_bundle_groups(ctx->b_qop, nslots, ctx->b_gop, ctx->b_gctr, ctx->st, stop);
@@ -1154,9 +1179,10 @@ int check_ready(icp_ctx *ctx, bool need_scene)
 
 // The bundle filter's kd order, images, block frames and kd tables for the resident model (§3.6),
 // with kd_h (nullable) a host-built kd order (ICP_KD_HOST).  Synchronous (the frames' max R_B).
-static int build_bundle(icp_ctx *ctx, const int *kd_h)
+// nm: the model's point count -- passed, not read from ctx->nm, which set_model assigns only after
+// every image is built (ICP_KD_HOST builds these before that)
+static int build_bundle(icp_ctx *ctx, size_t nm, const int *kd_h)
 {
-    const size_t nm = ctx->nm;
     const int nb_pad = bundle_pad(nm);
     TRY(grow(ctx, &ctx->b_kd, &ctx->b_kd_cap, nm));
     if (kd_h) {
@@ -1196,13 +1222,14 @@ static int build_bundle(icp_ctx *ctx, const int *kd_h)
     ctx->b_rlmax = rl;
     ctx->nb_pad = nb_pad;
     ctx->bundle_pending = false;
+    ctx->stats.bundle_builds += 1;
     return ICP_OK;
 }
 
 // the bundle filter's images, built now if they are pending (the first search that needs them)
 int ensure_bundle(icp_ctx *ctx)
 {
-    return ctx->bundle_pending ? build_bundle(ctx, nullptr) : ICP_OK;
+    return ctx->bundle_pending ? build_bundle(ctx, ctx->nm, nullptr) : ICP_OK;
 }
 
 } // namespace
@@ -1547,7 +1574,7 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm)
     if (nm >= (size_t)kBundleMinModel) { // the bundle filter's kd images (icp_bundle.hip): at first use
         if (kd_host()) {
             kd_h = bundle_kd_order(m_xyz, nm); // (the host build needs the caller's array: now)
-            TRY(build_bundle(ctx, kd_h.data()));
+            TRY(build_bundle(ctx, nm, kd_h.data()));
         } else {
             ctx->bundle_pending = true;
         }
@@ -1656,8 +1683,14 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     ctx->p32_stale = false;
     // a shard against a model of at least twice its points (C5's 8-way shards: the model's cells
     // are finer than the scene's spacing): icp_run's policy takes the bundle cascade for the first
-    // searches, so its images are built here rather than between two iterations of the run
-    if (ctx->bundle_pending && np_local > 0 && ctx->nm >= 2 * np_local && ctx->nn_variant == ICP_NN_VARIANT_AUTO)
+    // searches, so its images are built here rather than between two iterations of the run (the
+    // lazy build between iterations gives the same results; ICP_EAGER_BUNDLE=0 leaves it to
+    // that).  Only for a scene the bundle filter would search (level1_kind == 3, the slot order)
+    const char *eager_env = getenv("ICP_EAGER_BUNDLE"); // (read per call: tests toggle it)
+    const bool eager = !(eager_env && eager_env[0] == '0');
+    if (eager && ctx->bundle_pending && np_local > 0 && ctx->nm >= 2 * np_local &&
+        ctx->nn_variant == ICP_NN_VARIANT_AUTO && ctx->nn_mode == ICP_NN_CERTIFIED && level1_kind(ctx, np_local) == 3 &&
+        want_slot_order(ctx, np_local))
         TRY(ensure_bundle(ctx));
     return ICP_OK;
 }
@@ -1859,7 +1892,7 @@ static int run_persistent(icp_ctx *ctx, int grid, size_t lds, bool mid, int max_
         }();
         if (!ctx->seeds_valid && prepass) {
             launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
-            TRY(nn_search_begin(ctx, P, n, false, nullptr, nullptr, false, false, &ctx->iter_state->done));
+            TRY(nn_search_begin(ctx, P, n, false, nullptr, nullptr, false, nullptr, &ctx->iter_state->done));
         }
         TRY(grow(ctx, &ctx->mid_q4, &ctx->mid_q4_cap, 4 * n));
         TRY(grow(ctx, &ctx->mid_res, &ctx->mid_res_cap, n));
@@ -2111,6 +2144,31 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         sa.far_d2 = sa_grid.far_d2 = 2.25 * h * h;
         sa_grid.seedd = sa.seedd; // (grid_seeded_search reads them: no gather of the seed point)
     }
+    // What the last enqueued transform wrote for the next search (nn_search_begin uses each part
+    // only in the form it was written in).  A carried-over run starts from the last run's seed
+    // distances (seedd_valid); everything else is rebuilt by the first search.
+    SeedState ws;
+    ws.seedd = carry;
+    // The transform before a bundle search writes that search's slot records (the prep's output,
+    // in order) once the images exist and a bundle search of this size has sized the buffers --
+    // decided per transform, in the form the next search will run: the local pair test's with the
+    // current frames' R, else the global one.  (It was decided once at the start of the run:
+    // after icp_set_model the images are pending, b_rlmax is -1, and a run whose policy turned to
+    // the bundle mid-run then wrote global-form records for a search that, its images built in
+    // between, ran the local form -- the C5 registration stall)
+    auto records_args = [&](SeedArgs &s) {
+        if (!transform_records || !ctx->scene_slot || !fuse_seeds || !s.seed16 || !s.seedd || ctx->bundle_pending ||
+            ctx->nb_pad <= 0 || level1_kind(ctx, n) != 3 || !bundle_v2())
+            return;
+        const size_t nslots = bundle2_slots(plan_nn_bundle2(n, ctx->nb_pad));
+        if (!ctx->b_qop || ctx->b_qop_cap < nslots * 64 || ctx->b_gop_cap < nslots || ctx->b_gctr_cap < nslots / 32)
+            return;
+        s.qop = ctx->b_qop;
+        s.gop = ctx->b_gop;
+        s.gctr = ctx->b_gctr;
+        s.nslots = (int)nslots;
+        s.local_r = ctx->b_rlmax >= 0.0 && bundle_local() ? ctx->b_rlmax : -1.0; // (as the search decides)
+    };
     launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
     // partials over several workgroups: the moments and / or the transform may fold their
     // partials in their own last workgroup (StepFold), and on one rank go on there to the Horn
@@ -2203,41 +2261,35 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         LAUNCHCHK("err_step");
         return ICP_OK;
     };
+    // A run that starts with the bundle images pending and nothing carried over has no far count
+    // until its first iteration completes: the host waits for it before enqueuing the second, so
+    // that the second search's path is decided on a count (a blind grid search right after the
+    // first alignment scans boxes as big as the first transform's moves)
+    const bool hold_first = grid_policy && !carry && ctx->bundle_pending;
     while (!stop && waited < max_iter) {
-        if (enqueued < max_iter && enqueued - waited <= kAhead + (lag ? 1 : 0)) {
+        if (enqueued < max_iter && enqueued - waited <= kAhead + (lag ? 1 : 0) &&
+            !(hold_first && enqueued == 1 && waited == 0)) {
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == timing_phase;
-            const bool grid_cur = grid_next; // (decided with the previous transform, or carried over)
-            // (nothing observed yet: the grid while the bundle images are still pending)
+            // the path of this search: on the last count the host has seen (the previous transform
+            // wrote for the path predicted when it was enqueued; a different decision here just
+            // rebuilds what this path reads, nn_search_begin), else as predicted (carried over,
+            // or the grid while the bundle images are still pending)
+            const bool grid_cur = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : grid_next);
             grid_next = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : ctx->bundle_pending);
             // (the search of an iteration queued behind the converged one returns at once)
             // (the seed distances the last transform wrote -- of this run, or of the last one when
             // carried over -- for a grid search)
-            const double *gseedd = (enqueued > 0 || (carry && grid_cur)) &&
-                                           (grid_cur || ctx->nn_variant == ICP_NN_VARIANT_GRID)
-                                       ? sa.seedd
-                                       : nullptr;
+            const double *gseedd =
+                ws.seedd && (grid_cur || ctx->nn_variant == ICP_NN_VARIANT_GRID) ? sa.seedd : nullptr;
             // (the second pass's grid: for four times the last queue seen, at least 256 queries)
             ctx->second_pass_items = grid_policy && q2_obs >= 0 ? std::max(256, 4 * q2_obs) : 0;
             TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
-                                timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false,
-                                fuse_seeds && enqueued > 0 && !grid_cur, &sd->done, ctx->scene_slot,
-                                sa.qop && enqueued > 0 && !grid_cur, grid_cur, gseedd)); // (run_init zeroed the counters)
-            if (enqueued == 0 && sa.seedd && ctx->scene_slot && transform_records) {
-                // a scene in slot order: from here on each transform writes the next search's
-                // slot records and group bounds in order (the first search sized the buffers;
-                // its prep wrote the padding slots, which no transform touches)
-                const size_t nslots = bundle2_slots(plan_nn_bundle2(n, ctx->nb_pad));
-                if (ctx->b_qop && ctx->b_qop_cap >= nslots * 64 && ctx->b_gop_cap >= nslots &&
-                    ctx->b_gctr_cap >= nslots / 32) {
-                    sa.qop = ctx->b_qop;
-                    sa.gop = ctx->b_gop;
-                    sa.gctr = ctx->b_gctr;
-                    sa.nslots = (int)nslots;
-                    sa.local_r = ctx->b_rlmax >= 0.0 && bundle_local() ? ctx->b_rlmax : -1.0; // (as the search decides)
-                }
-            }
+                                timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, &ws, &sd->done, ctx->scene_slot,
+                                grid_cur, gseedd)); // (run_init zeroed the counters)
+            if (ctx->stats.last_filter == ICP_FILTER_BUNDLE) ctx->stats.run_bundle_searches += 1;
+            else if (ctx->stats.last_filter == ICP_FILTER_GRID) ctx->stats.run_grid_searches += 1;
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
             TRY(cpu_rule_fixup(ctx, P, n, &sd->done)); // (ICP_NN_RULE_CPU_SQRT only: host near ties)
             ar_timed[slot] = false;
@@ -2256,6 +2308,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                             ctx->d_flags + 4 * sl, slot_ticket[sl], ctx->d_iter_mirror,
                                             ctx->d_trace, ctx->st);
                 LAUNCHCHK("iteration_tail_small");
+                ws = SeedState{}; // (it writes no seeds)
                 ++enqueued;
                 continue;
             }
@@ -2307,6 +2360,9 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 }
                 launch_iteration_tail_grid(ta, tail_blocks, ctx->st);
                 LAUNCHCHK("iteration_tail_grid");
+                ws = SeedState{}; // (its transform: the f16 seeds and the seed distances, no records)
+                ws.seed16 = sa.seed16 ? 1 : 0;
+                ws.seedd = sa.seedd != nullptr;
                 if (split_err) TRY(enqueue_err_step(enqueued));
                 tail_epoch += 2;
                 ++enqueued;
@@ -2350,7 +2406,13 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             // 4. Horn solve (gpu.cc:106-146) on the device
             if (!horn_fused) launch_horn_step(ctx->sums, N, ctx->c, enqueued > 0, ctx->amb_count, sd, ctx->st);
             // 5. apply + residual (gpu.cc:71-74): new_p <- sR new_p + t; e = sum ||Y - new_p||^2
-            const SeedArgs &sa_t = grid_next ? sa_grid : sa;
+            SeedArgs sa_t = grid_next ? sa_grid : sa;
+            if (!grid_next) records_args(sa_t); // (a bundle search next: its slot records, when they can be)
+            ws = SeedState{};
+            ws.seedd = sa_t.seedd != nullptr; // (every form writes the seed distances)
+            ws.seed16 = !sa_t.seed16 ? 0 : sa_t.qop && sa_t.local_r >= 0.0 ? 2 : 1;
+            ws.records = sa_t.qop != nullptr;
+            ws.rec_local = sa_t.qop ? sa_t.local_r : -1.0;
             StepFold ef;
             const bool err_fused = fused_steps && !sa_t.qop; // (the slot-record form keeps its own launch)
             if (err_fused && lag) { // (the fold only: the residual rides on the next all-reduce)
@@ -2439,8 +2501,9 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         ctx->seedd_valid = false;
         return kTailAborted;
     }
-    // (every transform of a policy run wrote the seed distances; the next run may start from them)
-    ctx->seedd_valid = grid_policy && sa.seedd != nullptr;
+    // (every transform of a policy run wrote the seed distances, whatever its form; the next run
+    // may start from them)
+    ctx->seedd_valid = grid_policy && ws.seedd;
     ctx->last_far = far_obs;
     ctx->last_q2 = q2_obs;
     ctx->second_pass_items = 0;

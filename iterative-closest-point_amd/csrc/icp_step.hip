@@ -125,11 +125,11 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
     double a[1] = {0.0};
     int far = 0; // (sa.far_acc: this thread's moved points beyond sqrt(far_d2) of their correspondence)
     if (QOP && sa.qop && write_p) {
-        // slot records (a scene in slot order): whole waves run to n rounded up to 64 (the
+        // slot records (a scene in slot order): whole waves run to nslots (a multiple of 512; the
         // stride is a multiple of 64), so that each 32-slot group's lanes are all present for
-        // its bound; the lanes past n build the padding's never-firing records
-        const int n64 = (n + 63) & ~63;
-        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n64; i += gridDim.x * kBlock) {
+        // its bound; the lanes past n build the padding's never-firing records -- every slot the
+        // filter reads, so no earlier prep's padding is relied on
+        for (int i = blockIdx.x * kBlock + threadIdx.x; i < sa.nslots; i += gridDim.x * kBlock) {
             BundleQuery r;
             if (i < n) {
                 double q0, q1, q2;
@@ -142,7 +142,11 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
                 if (p32)
                     p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
                 const double dx = q0 - y0, dy = q1 - y1, dz = q2 - y2;
-                far += ((dx * dx + dy * dy) + dz * dz > sa.far_d2) ? 1 : 0;
+                const double d2 = (dx * dx + dy * dy) + dz * dz;
+                far += d2 > sa.far_d2 ? 1 : 0;
+                // (the seed distance too, as the plain form writes it: a later grid search -- of
+                // this run, or of the next one carrying over -- reads it)
+                if (sa.seedd) sa.seedd[i] = d2;
                 double4 raw;
                 if (sa.local_r >= 0.0) { // (the local pair test: the shift is the finalize's seed)
                     float s0;

@@ -88,7 +88,9 @@ class Stats(C.Structure):
                 ("cert_min_margin", C.c_double), ("cert_audited", C.c_longlong),
                 ("persistent_runs", C.c_longlong), ("cpu_rule_ties", C.c_longlong),
                 ("cpu_rule_changed", C.c_longlong), ("persistent_fallbacks", C.c_longlong),
-                ("last_filter", C.c_int)]
+                ("last_filter", C.c_int), ("bundle_builds", C.c_longlong),
+                ("bundle_builds_in_run", C.c_longlong), ("run_bundle_searches", C.c_longlong),
+                ("run_grid_searches", C.c_longlong)]
 
 
 class BundleAudit(C.Structure):

@@ -31,7 +31,9 @@ def main():
     m, p = icp_amd.synthetic_pair(a.points, seed=42)
     b, c = icp_amd.shard_range(a.points, a.rank, a.world)
     with icp_amd.Context(0) as ctx:
-        r = bench.registration(ctx, m, p[b:b + c], a.points, a.iters, a.reps)
+        # (a shard alone is registered on its own sums: np_total = its size, as tools/shard_probe.py)
+        ctx.set_allow_unequal(True)
+        r = bench.registration(ctx, m, p[b:b + c], c, a.iters, a.reps)
     r.update({"points": a.points, "shard": [a.rank, a.world], "n_local": c, "tag": a.tag,
               "env": {k: v for k, v in os.environ.items() if k.startswith("ICP_")}})
     print(json.dumps(r), flush=True)

@@ -5,7 +5,10 @@ Rank 0 of a W-rank job holds ceil(N/W) scene points against the whole (replicate
 This runs exactly that shard through a context with a 1-rank RCCL communicator (so every
 per-iteration sum still goes through ncclAllReduce on the engine stream) and reports the
 per-iteration time.  The only thing missing against the real W-GPU run is the cross-GPU
-latency of the 3 small all-reduces per iteration (<= 88 B each, xGMI).
+latency of the one 18-double all-reduce per iteration (xGMI).  The shard is registered on its
+own (np_total = its own size, allow_unequal): its sums are a random sample's, so it follows
+the whole cloud's trajectory closely, where np_total = N with one shard's sums would centre it
+on an eighth of its centroid.
 
     python tools/shard_probe.py [--n 1048576] [--worlds 1 2 4 8] [--steps 20]
 """
@@ -38,8 +41,9 @@ def main():
         with icp_amd.Context(0, icp_amd.NN_CERTIFIED, rank=0, world_size=1, rccl_id=uid) as ctx:
             if a.variant == "grid":
                 ctx.set_nn_variant(icp_amd.VARIANT_GRID)
+            ctx.set_allow_unequal(True)
             ctx.set_model(m)
-            ctx.set_scene(p[b:b + c], np_total=a.n)
+            ctx.set_scene(p[b:b + c], np_total=c)
             if m.shape[0] >= 2 * c and a.variant != "grid":  # (the bundle images, as bench.py: untimed)
                 ctx.model_order(m.shape[0])
             ctx.run(a.warmup, -1.0)
