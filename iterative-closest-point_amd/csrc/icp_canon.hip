@@ -1,0 +1,276 @@
+// icp_canon.hip — an ICP iteration's sums in the canonical order (icp_canon.h) for a scene stored
+// in slot order: the one-pass moments (gpu.cc:98-104, :142), the transform + residual
+// (gpu.cc:71-74, compute.cu:315-346) and the fold that ends an iteration with the lagged error
+// step (gpu.cc:76-80) and the Horn step (gpu.cc:106-146).
+//
+// icp_run's loop over such a scene (run_loop, canon): iteration k's sums are its moments and the
+// residual of the transform that produced its scene (iteration k-1's), so iteration k ends with
+// ONE launch -- canon_fold_kernel: fold, error test of k-1, Horn solve of k -- instead of a moments
+// fold + Horn step and a residual fold + error step.  With several ranks the fold's 18 sums are
+// all-reduced before the error and Horn steps.  Compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include "icp_bundle_rec.h"
+#include "icp_canon.h"
+#include "icp_device.h"
+#include "icp_fold.h"
+#include "icp_kernels.h"
+#include "icp_mfma16.h"
+
+namespace icp {
+namespace {
+
+// Chunk sums of K columns over the workgroup's 256 leaves (thread t = leaf t), added to the row
+// accumulator held by thread k < K (acc).  Two barriers.
+template <int K>
+__device__ __forceinline__ void chunk_to_row(const double (&leaf)[K], double (*sh)[K], double &acc)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double w = wave_tree_63<1>(leaf[k]);
+        if (lane == 63) sh[wave][k] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        acc = acc + ((sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]));
+    }
+    __syncthreads();
+}
+
+// The one-pass moments of the points of chunks blockIdx.x, + gridDim.x, ... (row blockIdx.x, columns
+// 0..16): y from the search (YIN) or gathered (kpos ? m4kd[kpos] : m4[idx], and stored).  Two
+// chunks' loads are issued before their trees (the same leaves, the same order).
+template <bool YIN>
+__global__ __launch_bounds__(kBlock) void canon_moments_kernel(
+    const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
+    const double *__restrict__ py, const double *__restrict__ pz, int n, double *__restrict__ yx,
+    double *__restrict__ yy, double *__restrict__ yz, const IterState *__restrict__ st, double *__restrict__ rows,
+    const int *__restrict__ kpos, const double4 *__restrict__ m4kd)
+{
+    if (st->done) return; // a frozen (converged) ICP iteration: its sums are never used
+    __shared__ double sh[kBlock / 64][17];
+    const double cp[3] = {st->shift_p[0], st->shift_p[1], st->shift_p[2]};
+    const double cy[3] = {st->shift_y[0], st->shift_y[1], st->shift_y[2]};
+    const int nchunks = (n + kCanonChunk - 1) / kCanonChunk, R = gridDim.x;
+    double acc = 0.0;
+    constexpr int B = 2;
+    for (int c0 = blockIdx.x; c0 < nchunks; c0 += B * R) {
+        double4 y[B];
+        double q[B][3];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int c = c0 + u * R, i = c * kCanonChunk + threadIdx.x;
+            const bool in = c < nchunks && i < n;
+            if constexpr (YIN) {
+                y[u] = in ? make_double4(yx[i], yy[i], yz[i], 0.0) : make_double4(0.0, 0.0, 0.0, 0.0);
+            } else {
+                y[u] = in ? (kpos ? m4kd[kpos[i]] : m4[idx[i]]) : make_double4(0.0, 0.0, 0.0, 0.0);
+            }
+            q[u][0] = in ? px[i] : 0.0;
+            q[u][1] = in ? py[i] : 0.0;
+            q[u][2] = in ? pz[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+            const int c = c0 + u * R, i = c * kCanonChunk + threadIdx.x;
+            if (c >= nchunks) break; // (uniform)
+            double a[17];
+            if (i < n) {
+                if constexpr (!YIN) {
+                    yx[i] = y[u].x;
+                    yy[i] = y[u].y;
+                    yz[i] = y[u].z;
+                }
+                moment_leaves(q[u][0], q[u][1], q[u][2], y[u].x, y[u].y, y[u].z, cp, cy, a);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 17; ++k) a[k] = 0.0;
+            }
+            chunk_to_row<17>(a, sh, acc);
+        }
+    }
+    if (threadIdx.x < 17) rows[(size_t)blockIdx.x * kCanonCols + threadIdx.x] = acc;
+}
+
+// a workgroup's count into *acc: one atomic, and only when it is not zero
+__device__ __forceinline__ void canon_far_to_acc(int far, int *acc)
+{
+    __shared__ int s_far[kBlock / 64];
+    for (int o = 32; o >= 1; o >>= 1) far += __shfl_xor(far, o, 64);
+    if ((threadIdx.x & 63) == 0) s_far[threadIdx.x >> 6] = far;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += s_far[w];
+        if (tot) atomicAdd(acc, tot);
+    }
+}
+
+// p <- sR p + t (Eigen's order), the residual ||y - p'||^2 as the leaves of row column kSumErr,
+// and what the next search reads: the seed distance D64(p', y) (the residual's value), the f16
+// seed, the fp32 copy, the far count -- and with QOP the bundle filter's slot records for every
+// slot up to nslots (transform_err_kernel's forms, icp_step.hip).
+template <bool QOP>
+__global__ __launch_bounds__(kBlock) void canon_transform_kernel(
+    double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, const double *__restrict__ yx,
+    const double *__restrict__ yy, const double *__restrict__ yz, int n, const Xform *__restrict__ xfd,
+    const int *__restrict__ done, float4 *__restrict__ p32, double *__restrict__ rows, SeedArgs sa)
+{
+    __shared__ Xform sxf;
+    __shared__ int sdone;
+    __shared__ double sh[kBlock / 64][1];
+    if (threadIdx.x == 0) {
+        sdone = *done;
+        sxf = *xfd;
+    }
+    __syncthreads();
+    if (sdone) return;
+    const Xform xf = sxf;
+    const int nchunks = (n + kCanonChunk - 1) / kCanonChunk, R = gridDim.x;
+    // (QOP: every slot the filter reads, nslots a multiple of 512, in whole waves)
+    const int cmax = QOP ? (sa.nslots + kCanonChunk - 1) / kCanonChunk : nchunks;
+    double acc = 0.0;
+    int far = 0;
+    for (int c = blockIdx.x; c < cmax; c += R) {
+        const int i = c * kCanonChunk + threadIdx.x;
+        double leaf[1] = {0.0};
+        if (i < n) {
+            double q0, q1, q2;
+            transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
+            const double y0 = yx[i], y1 = yy[i], y2 = yz[i];
+            const double e = residual2(y0, y1, y2, q0, q1, q2); // (= the seed distance D64(p', y), bit for bit)
+            leaf[0] = 0.0 + e;
+            px[i] = q0;
+            py[i] = q1;
+            pz[i] = q2;
+            if (p32) p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
+            if (sa.seedd) sa.seedd[i] = e;
+            far += e > sa.far_d2 && sa.far_acc ? 1 : 0;
+            if constexpr (QOP) {
+                BundleQuery r;
+                double4 raw;
+                if (sa.local_r >= 0.0) { // (the local pair test: the shift is the finalize's seed)
+                    float s0;
+                    bundle_record(q0, q1, q2, i, e, 0u, sa.c[0], sa.c[1], sa.c[2], sa.scale, r, raw, sa.local_r, &s0);
+                    sa.seed16[i] = __float_as_uint(s0);
+                } else {
+                    const unsigned sd = mfma16_seed_value(q0, q1, q2, y0, y1, y2, sa.c[0], sa.c[1], sa.c[2], sa.scale);
+                    sa.seed16[i] = sd;
+                    bundle_record(q0, q1, q2, i, e, sd, sa.c[0], sa.c[1], sa.c[2], sa.scale, r, raw);
+                }
+                ((BundleQuery *)sa.qop)[i] = r;
+                bundle_group_store(r, i, sa.nslots, (half8_t *)sa.gop, sa.gctr);
+            } else if (sa.seed16) {
+                sa.seed16[i] = mfma16_seed_value(q0, q1, q2, y0, y1, y2, sa.c[0], sa.c[1], sa.c[2], sa.scale);
+            }
+        } else if constexpr (QOP) {
+            if (i < sa.nslots) {
+                BundleQuery r;
+                double4 raw;
+                bundle_never_record(r, raw);
+                ((BundleQuery *)sa.qop)[i] = r;
+                bundle_group_store(r, i, sa.nslots, (half8_t *)sa.gop, sa.gctr);
+            }
+        }
+        if (c < nchunks) chunk_to_row<1>(leaf, sh, acc); // (uniform)
+    }
+    if (threadIdx.x == 0) rows[(size_t)blockIdx.x * kCanonCols + kSumErr] = acc;
+    if (sa.far_acc) canon_far_to_acc(far, sa.far_acc);
+}
+
+// The fold of the R rows (columns [K0, K0 + K)): thread t adds rows t, t + 512, ... in order
+// (four rows' loads in flight), then the pairwise tree over the 512 threads (DPP within each
+// wave, then the 8 waves' sums pairwise).  MODE 0: -> sums[K0..]; MODE 1 (one rank, 18
+// columns): + the error step of the previous iteration and this iteration's Horn step; MODE 2
+// (one rank, the residual column): + the error step (the run's last iteration).
+constexpr int kFoldThreads = 512; // (the Horn solve on thread 0 fits 256 VGPRs without spills)
+template <int K0, int K, int MODE>
+__global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *__restrict__ rows, int R,
+                                                                  double *__restrict__ sums, CanonStep cs)
+{
+    __shared__ double sh[kFoldThreads / 64][K];
+    __shared__ double s_sum[kCanonCols];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.0;
+    constexpr int U = 4; // (R <= 2,048 rows: at most four a thread)
+    for (int r0 = threadIdx.x; r0 < R; r0 += U * kFoldThreads) {
+        double v[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + u * kFoldThreads;
+#pragma unroll
+            for (int k = 0; k < K; ++k) v[u][k] = r < R ? rows[(size_t)r * kCanonCols + K0 + k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (r0 + u * kFoldThreads < R)
+#pragma unroll
+                for (int k = 0; k < K; ++k) a[k] = a[k] + v[u][k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double w = wave_tree_63<1>(a[k]);
+        if (lane == 63) sh[wave][k] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        const int k = threadIdx.x;
+        double s[kFoldThreads / 64];
+#pragma unroll
+        for (int w = 0; w < kFoldThreads / 64; ++w) s[w] = sh[w][k];
+#pragma unroll
+        for (int span = 1; span < kFoldThreads / 64; span <<= 1)
+#pragma unroll
+            for (int w = 0; w < kFoldThreads / 64; w += 2 * span) s[w] = s[w] + s[w + span];
+        sums[K0 + k] = s[0];
+        s_sum[K0 + k] = s[0];
+    }
+    if constexpr (MODE == 0) return;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state, cs.h_trace);
+    if constexpr (MODE == 1) horn_step_body(s_sum, cs.N, cs.c[0], cs.c[1], cs.c[2], 1, cs.cnt, cs.s);
+}
+
+} // namespace
+
+void launch_canon_moments(const int *idx, const double4 *m4, const double *px, const double *py, const double *pz,
+                          int n, double *yx, double *yy, double *yz, const IterState *st_dev, double *rows,
+                          hipStream_t st, const int *kpos, const double4 *m4kd, bool y_ready)
+{
+    if (n <= 0) return;
+    const int R = canon_rows((size_t)n);
+    if (y_ready)
+        canon_moments_kernel<true><<<R, kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, rows, kpos, m4kd);
+    else
+        canon_moments_kernel<false><<<R, kBlock, 0, st>>>(idx, m4, px, py, pz, n, yx, yy, yz, st_dev, rows, kpos, m4kd);
+}
+
+void launch_canon_transform(double *px, double *py, double *pz, const double *yx, const double *yy, const double *yz,
+                            int n, const Xform *xf, const int *done, float4 *p32, double *rows, const SeedArgs &sa,
+                            hipStream_t st)
+{
+    if (n <= 0) return;
+    const int R = canon_rows((size_t)n);
+    if (sa.qop)
+        canon_transform_kernel<true><<<R, kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, done, p32, rows, sa);
+    else
+        canon_transform_kernel<false><<<R, kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, done, p32, rows, sa);
+}
+
+void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st)
+{
+    const int R = canon_rows((size_t)(n > 0 ? n : 1));
+    switch (mode) {
+    case 0: canon_fold_kernel<0, kCanonCols, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
+    case 1: canon_fold_kernel<0, kCanonCols, 1><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
+    case 2: canon_fold_kernel<kSumErr, 1, 2><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
+    default: canon_fold_kernel<kSumErr, 1, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
+    }
+}
+
+} // namespace icp

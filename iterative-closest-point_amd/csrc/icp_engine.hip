@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "icp_horn.h"
+#include "icp_canon.h"
 #include "icp_kernels.h"
 
 using namespace icp;
@@ -240,6 +241,9 @@ struct icp_ctx {
     double *partials = nullptr;
     double *err_part = nullptr; // (multi-rank icp_run: the transform's residual partials, run_loop)
     size_t err_part_cap = 0;
+    double *canon_rowbuf = nullptr; // (icp_run over a scene in slot order: the canonical rows, icp_canon.h)
+    size_t canon_rowbuf_cap = 0;
+    int *h_far = nullptr; // (pinned: a far count read back once, run_loop's hold_first)
     double *sums = nullptr;
     double *h_sums = nullptr; // pinned
     int *h_amb = nullptr;     // pinned
@@ -1428,12 +1432,13 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
                     (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame,
-                    (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos})
+                    (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos, (void *)ctx->canon_rowbuf})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
     if (ctx->h_iter) (void)hipHostFree(ctx->h_iter);
     if (ctx->h_flags) (void)hipHostFree(ctx->h_flags);
+    if (ctx->h_far) (void)hipHostFree(ctx->h_far);
     if (ctx->h_few) (void)hipHostFree(ctx->h_few);
     if (ctx->h_sig) (void)hipHostFree(ctx->h_sig);
     if (ctx->h_trace) (void)hipHostFree(ctx->h_trace);
@@ -2266,12 +2271,134 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // that the second search's path is decided on a count (a blind grid search right after the
     // first alignment scans boxes as big as the first transform's moves)
     const bool hold_first = grid_policy && !carry && ctx->bundle_pending;
+    // A scene in slot order (C4, C5, their shards): the canonical schedule (icp_canon.h).  The
+    // transform of iteration k - 1 is enqueued at the start of iteration k, right before its
+    // search, in the form that search reads; its residual and k's moments go to the canonical
+    // rows, and ONE fold launch ends iteration k with k - 1's error step and k's Horn step (with
+    // ranks: the fold, the all-reduce of the 18 sums, the error + Horn step) -- the error test
+    // runs one iteration late, as the multi-rank loop's always did, and the scene freezes at the
+    // same point.  Every search path adds to the same rows in the same order, so the NN variants'
+    // trajectories stay bitwise equal.  ICP_CANON=0: the round-4 schedule (A/B).
+    static const bool canon_env = [] {
+        const char *e = getenv("ICP_CANON");
+        return !(e && e[0] == '0');
+    }();
+    const bool canon = canon_env && ctx->scene_slot && n > 0;
+    if (canon) {
+        TRY(grow(ctx, &ctx->canon_rowbuf, &ctx->canon_rowbuf_cap, (size_t)canon_rows(n) * kCanonCols));
+        if (!ctx->h_far) HIPCHK(hipHostMalloc((void **)&ctx->h_far, sizeof(int), hipHostMallocDefault));
+    }
+    const bool lag_sched = lag || canon;
+    bool xf_pending = false; // (canon: the last Horn step's transform is still to be applied)
+    CanonStep cs;
+    cs.N = N;
+    cs.threshold = threshold;
+    cs.max_iter = max_iter;
+    cs.err_trace = ctx->err_trace_dev;
+    cs.s = sd;
+    cs.h_state = ctx->d_iter_mirror;
+    cs.h_trace = ctx->d_trace;
+    for (int a = 0; a < 3; ++a) cs.c[a] = ctx->c[a];
+    cs.cnt = ctx->amb_count;
+    // the canonical transform of the last Horn step's (s, R, t), in the form sa_t (its residual into
+    // the rows' kSumErr column, and what the next search reads)
+    auto canon_transform = [&](SeedArgs sa_t) -> int {
+        launch_canon_transform(P.x, P.y, P.z, Y.x, Y.y, Y.z, (int)n, &sd->xf, &sd->done, need_p32 ? P.f : nullptr,
+                               ctx->canon_rowbuf, sa_t, ctx->st);
+        LAUNCHCHK("canon_transform");
+        if (!need_p32) ctx->p32_stale = true;
+        ws = SeedState{};
+        ws.seedd = sa_t.seedd != nullptr;
+        ws.seed16 = !sa_t.seed16 ? 0 : sa_t.qop && sa_t.local_r >= 0.0 ? 2 : 1;
+        ws.records = sa_t.qop != nullptr;
+        ws.rec_local = sa_t.qop ? sa_t.local_r : -1.0;
+        xf_pending = false;
+        return ICP_OK;
+    };
+    // canon: the error step of iteration `it` (ticket of its slot) after the fold of the rows --
+    // with the Horn step of the current iteration (horn) or alone (the run's last residual)
+    auto canon_end = [&](int it, bool horn, int slot) -> int {
+        const int sl = it % kRing;
+        slot_ticket[sl] = ++ctx->flag_ticket;
+        cs.hflag = ctx->d_flags + 4 * sl;
+        cs.ticket = slot_ticket[sl];
+        if (!lag) {
+            launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, horn ? 1 : 2, cs, ctx->st);
+            LAUNCHCHK("canon_fold");
+            return ICP_OK;
+        }
+        launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, horn ? 0 : 3, cs, ctx->st);
+        LAUNCHCHK("canon_fold");
+        const bool tm = horn && slot >= 0 && ar_timed[slot];
+        if (tm) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 3], ctx->st));
+        TRY(horn ? allreduce(ctx, ctx->sums, kNumSums) : allreduce(ctx, ctx->sums + kSumErr, 1));
+        if (tm) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 4], ctx->st));
+        if (horn)
+            launch_err_horn_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, cs.hflag, cs.ticket,
+                                 ctx->d_iter_mirror, ctx->d_trace, ctx->c, 1, ctx->amb_count, ctx->st);
+        else
+            launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, cs.hflag, cs.ticket,
+                            ctx->d_iter_mirror, ctx->d_trace, ctx->st, nullptr, 0);
+        LAUNCHCHK("err_step");
+        return ICP_OK;
+    };
     while (!stop && waited < max_iter) {
-        if (enqueued < max_iter && enqueued - waited <= kAhead + (lag ? 1 : 0) &&
-            !(hold_first && enqueued == 1 && waited == 0)) {
+        if (enqueued < max_iter && enqueued - waited <= kAhead + (lag_sched ? 1 : 0) &&
+            !(!canon && hold_first && enqueued == 1 && waited == 0)) {
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == timing_phase;
+            if (canon) {
+                bool grid_c = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : grid_next);
+                grid_next = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : ctx->bundle_pending);
+                if (xf_pending && hold_first && enqueued == 1 && far_obs < 0) {
+                    // the images pending and no count yet: the first transform, then its far count,
+                    // before the second search's path is chosen (one synchronisation a run)
+                    TRY(canon_transform(sa_grid));
+                    HIPCHK(hipMemcpyAsync(ctx->h_far, &sd->far_acc, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+                    HIPCHK(hipStreamSynchronize(ctx->st));
+                    far_obs = *ctx->h_far;
+                    grid_c = far_obs <= far_thr;
+                }
+                if (xf_pending) { // the last Horn step's transform, in the form this search reads
+                    SeedArgs sa_t = grid_c ? sa_grid : sa;
+                    if (!grid_c) records_args(sa_t);
+                    TRY(canon_transform(sa_t));
+                }
+                const double *gs = ws.seedd && (grid_c || ctx->nn_variant == ICP_NN_VARIANT_GRID) ? sa.seedd : nullptr;
+                ctx->second_pass_items = grid_policy && q2_obs >= 0 ? std::max(256, 4 * q2_obs) : 0;
+                TRY(nn_search_begin(ctx, P, n, ctx->seeds_valid, timed ? ctx->iter_ev[5 * slot] : nullptr,
+                                    timed ? ctx->iter_ev[5 * slot + 1] : nullptr, false, &ws, &sd->done,
+                                    ctx->scene_slot, grid_c, gs));
+                if (ctx->stats.last_filter == ICP_FILTER_BUNDLE) ctx->stats.run_bundle_searches += 1;
+                else if (ctx->stats.last_filter == ICP_FILTER_GRID) ctx->stats.run_grid_searches += 1;
+                ctx->seeds_valid = true;
+                TRY(cpu_rule_fixup(ctx, P, n, &sd->done));
+                ar_timed[slot] = false;
+                if ((size_t)enqueued < ctx->digest_cap) {
+                    launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st,
+                                      digest_order);
+                    LAUNCHCHK("idx_digest");
+                }
+                if (enqueued == 0) { // the reference's two passes, then the (unshifted) Horn step
+                    TRY(moments_phase(ctx, n));
+                    launch_horn_step(ctx->sums, N, ctx->c, false, ctx->amb_count, sd, ctx->st);
+                    LAUNCHCHK("horn_step");
+                } else {
+                    launch_canon_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd, ctx->canon_rowbuf,
+                                         ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr, ctx->m4kd, ctx->y_ready);
+                    LAUNCHCHK("canon_moments");
+                    ar_timed[slot] = timed && lag;
+                    TRY(canon_end(enqueued - 1, true, slot));
+                }
+                xf_pending = true;
+                ++enqueued;
+                if (enqueued == max_iter) { // the last transform and its residual's error step
+                    TRY(canon_transform(grid_policy ? sa_grid : SeedArgs{}));
+                    TRY(canon_end(enqueued - 1, false, -1));
+                }
+                continue;
+            }
             // the path of this search: on the last count the host has seen (the previous transform
             // wrote for the path predicted when it was enqueued; a different decision here just
             // rebuilds what this path reads, nn_search_begin), else as predicted (carried over,

@@ -473,6 +473,33 @@ struct IterState {
                        // copied by the Horn step before it zeroes the counters (the host sizes
                        // the next second pass by it)
 };
+
+// ---- the canonical order of a slot-order scene's iteration sums (icp_canon.h / .hip) ------
+// The error step of the previous iteration and this iteration's Horn step (canon_fold_kernel)
+struct CanonStep {
+    double N = 0.0;
+    double threshold = 0.0;
+    int max_iter = 0;
+    double *err_trace = nullptr;
+    IterState *s = nullptr;
+    int *hflag = nullptr;
+    int ticket = 0;
+    IterState *h_state = nullptr;
+    double *h_trace = nullptr;
+    double c[3] = {0.0, 0.0, 0.0};
+    int *cnt = nullptr;
+};
+// rows: canon_rows(n) x 18 doubles.  Moments -> columns 0..16 (y from the search when y_ready,
+// else gathered through kpos / idx and stored); transform -> column kSumErr plus SeedArgs'
+// outputs; fold: mode 0 all 18 -> sums, 1 + error step + Horn step (one rank), 2 the residual
+// column + error step (the last iteration, one rank), 3 the residual column -> sums[kSumErr]
+void launch_canon_moments(const int *idx, const double4 *m4, const double *px, const double *py, const double *pz,
+                          int n, double *yx, double *yy, double *yz, const IterState *st_dev, double *rows,
+                          hipStream_t st, const int *kpos, const double4 *m4kd, bool y_ready);
+void launch_canon_transform(double *px, double *py, double *pz, const double *yx, const double *yy, const double *yz,
+                            int n, const Xform *xf, const int *done, float4 *p32, double *rows, const SeedArgs &sa,
+                            hipStream_t st);
+void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st);
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,
 // sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)
