@@ -156,6 +156,12 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm);
 /* Scene ("transform", p): this rank's np_local points of an np_total-point cloud.
  * Resets new_p = p (gpu.hh:47).  Single-GPU: np_local == np_total. */
 int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total);
+/* The same two calls for clouds already in device memory (AoS fp64, 3 x n col-major, on the
+ * context's device, e.g. the output of an earlier GPU stage): no PCIe copy -- the model's images
+ * and the scene's SoA copies are built from the caller's array on the context's stream.  The
+ * caller's array must stay valid and unmodified until the call returns. */
+int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm);
+int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total);
 /* Copy this rank's current new_p (gpu.hh:88) back to the host. */
 int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
 /* icp_set_model, unless the resident model already holds exactly these nm points, bit for bit

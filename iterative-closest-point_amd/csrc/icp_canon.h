@@ -9,15 +9,18 @@
 // trajectories of the NN variants stay bitwise equal to each other.
 //
 //   leaf      the point's term (0.0 past n);
-//   chunk c   256 consecutive points [256 c, 256 c + 256): the pairwise tree of its leaves,
-//             S[a, a + 2w) = S[a, a + w) + S[a + w, a + 2w) (fp addition commutes, so which
-//             lane holds which half does not matter -- only which two partial sums meet);
-//   row r     R = canon_rows(n) rows: row r = ((0 + S_r) + S_{r+R}) + S_{r+2R} + ... over the chunks
-//             c = r mod R, in increasing c;
+//   chunk c   32 consecutive points [32 c, 32 c + 32) (the fused grid kernel's wave task, and the
+//             bundle filter's 32-slot query group): the pairwise tree of its leaves,
+//             S[a, a + 2w) = S[a, a + w) + S[a + w, a + 2w) (fp addition commutes, so which lane
+//             holds which half does not matter -- only which two partial sums meet);
+//   strand s  S = canon_strands(n) strands: strand s = ((0 + S_s) + S_{s+S}) + S_{s+2S} + ... over
+//             the chunks c = s mod S, in increasing c (one wave's sequence of tasks);
+//   row r     R = ceil(S / 4) rows: row r = (strand 4r + strand 4r+1) + (strand 4r+2 + strand 4r+3)
+//             (a workgroup's four waves; a missing strand is 0.0);
 //   sum       canon_fold_kernel folds the R rows (the one implementation of that step).
+// The rows are stored by column (column k of row r at k R + r): the fold's loads coalesce.
 //
-// The pairwise trees run on DPP row shifts / broadcasts (wave_tree_63: the sum of a wave's 64
-// leaves lands in lane 63), with no LDS traffic below 64 leaves.  Compiled with
+// The pairwise trees run on DPP row shifts / broadcasts with no LDS traffic.  Compiled with
 // -ffp-contract=off.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -26,16 +29,17 @@
 
 namespace icp {
 
-constexpr int kCanonChunk = 256;     // points a chunk
-constexpr int kCanonRowsMax = 2048;  // rows the chunks are dealt to (the fold's input)
-constexpr int kCanonCols = 18;       // kSumP .. kSumSp (17 moments), kSumErr (the residual)
+constexpr int kCanonChunk = 32;         // points a chunk
+constexpr int kCanonStrandsMax = 8192;  // strands the chunks are dealt to (one wave each)
+constexpr int kCanonCols = 18;          // kSumP .. kSumSp (17 moments), kSumErr (the residual)
 
-inline int canon_chunks(size_t n) { return (int)((n + kCanonChunk - 1) / kCanonChunk); }
-inline int canon_rows(size_t n)
+__host__ __device__ inline int canon_chunks(size_t n) { return (int)((n + kCanonChunk - 1) / kCanonChunk); }
+__host__ __device__ inline int canon_strands(size_t n)
 {
     const int c = canon_chunks(n);
-    return c < 1 ? 1 : (c < kCanonRowsMax ? c : kCanonRowsMax);
+    return c < 1 ? 1 : (c < kCanonStrandsMax ? c : kCanonStrandsMax);
 }
+__host__ __device__ inline int canon_rows(size_t n) { return (canon_strands(n) + 3) / 4; }
 
 // v moved by one DPP pattern (two 32-bit halves; lanes the pattern does not write read 0)
 template <int CTRL, int ROW_MASK = 0xf>
@@ -47,31 +51,38 @@ __device__ __forceinline__ double dpp_f64(double v)
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-// The pairwise sum of leaves sitting in lanes L + k*S (k = 0 .. 64/S - 1, S = 1 or 4 with L = S - 1):
-// S = 1: all 64 lanes; S = 4: every fourth lane (a query's group of four lanes holds its leaf in
-// lane 4u + 3).  The result is in lane 63; other lanes hold partial sums.
-template <int S>
-__device__ __forceinline__ double wave_tree_63(double v)
+// Two 32-leaf chunks per wave, one leaf per lane: lane 31 <- the pairwise sum of lanes 0..31,
+// lane 63 <- that of lanes 32..63 (other lanes hold partial sums)
+__device__ __forceinline__ double wave_tree_halves(double v)
 {
-    static_assert(S == 1 || S == 4, "leaf stride");
-    if constexpr (S == 1) {
-        v = v + dpp_f64<0x111>(v); // row_shr:1  -> lane 2i+1: S[2i, 2i+2)
-        v = v + dpp_f64<0x112>(v); // row_shr:2  -> lane 4i+3
-    }
+    v = v + dpp_f64<0x111>(v);      // row_shr:1  -> lane 2i+1: S[2i, 2i+2)
+    v = v + dpp_f64<0x112>(v);      // row_shr:2  -> lane 4i+3
     v = v + dpp_f64<0x114>(v);      // row_shr:4  -> lane 8i+7
     v = v + dpp_f64<0x118>(v);      // row_shr:8  -> lane 16i+15: a row's sum
-    v = v + dpp_f64<0x142, 0xa>(v); // row_bcast:15 -> lanes 31, 63: two rows
-    v = v + dpp_f64<0x143, 0xc>(v); // row_bcast:31 -> lane 63: the wave
+    v = v + dpp_f64<0x142, 0xa>(v); // row_bcast:15 -> lane 31: rows 0 + 1, lane 63: rows 2 + 3
     return v;
 }
 
-__device__ __forceinline__ double lane63(double v)
+// One 32-leaf chunk per wave, the leaves in the odd lanes 2u+1 (a query's two lanes): lane 63 <-
+// the pairwise sum of the 32 leaves
+__device__ __forceinline__ double wave_tree_odd(double v)
+{
+    v = v + dpp_f64<0x112>(v);      // row_shr:2  -> lane 4i+3: leaves (2i, 2i+1)
+    v = v + dpp_f64<0x114>(v);      // row_shr:4  -> lane 8i+7
+    v = v + dpp_f64<0x118>(v);      // row_shr:8  -> lane 16i+15
+    v = v + dpp_f64<0x142, 0xa>(v); // row_bcast:15 -> lanes 31, 63
+    v = v + dpp_f64<0x143, 0xc>(v); // row_bcast:31 -> lane 63
+    return v;
+}
+
+__device__ __forceinline__ double lane_value(double v, int lane)
 {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), 63);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+
 
 // point i's 17 moment terms around the shifts (shifted_moment_terms' arithmetic, as leaves: each
 // term is 0.0 + x, the same as the accumulating form's first add)

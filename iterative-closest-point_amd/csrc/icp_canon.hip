@@ -20,28 +20,39 @@
 namespace icp {
 namespace {
 
-// Chunk sums of K columns over the workgroup's 256 leaves (thread t = leaf t), added to the row
-// accumulator held by thread k < K (acc).  Two barriers.
+// A workgroup's four strands (waves) -> its row: thread k < K of the workgroup writes
+// rows[k R + blockIdx.x] = (strand 0 + strand 1) + (strand 2 + strand 3) of column k
 template <int K>
-__device__ __forceinline__ void chunk_to_row(const double (&leaf)[K], double (*sh)[K], double &acc)
+__device__ __forceinline__ void strands_to_row(const double (&acc)[K], double *__restrict__ rows, int R)
 {
+    __shared__ double sh[kBlock / 64][K];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double w = wave_tree_63<1>(leaf[k]);
-        if (lane == 63) sh[wave][k] = w;
-    }
+        for (int k = 0; k < K; ++k) sh[wave][k] = acc[k];
     __syncthreads();
     if (threadIdx.x < K) {
         const int k = threadIdx.x;
-        acc = acc + ((sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]));
+        rows[(size_t)k * R + blockIdx.x] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
     }
-    __syncthreads();
 }
 
-// The one-pass moments of the points of chunks blockIdx.x, + gridDim.x, ... (row blockIdx.x, columns
-// 0..16): y from the search (YIN) or gathered (kpos ? m4kd[kpos] : m4[idx], and stored).  Two
-// chunks' loads are issued before their trees (the same leaves, the same order).
+// Two chunks' leaves (lanes 0..31: chunk c, lanes 32..63: chunk c + S) into the strand's
+// accumulators, in chunk order (the second only if it exists)
+template <int K>
+__device__ __forceinline__ void two_chunks_to_strand(const double (&leaf)[K], bool second, double (&acc)[K])
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const double w = wave_tree_halves(leaf[k]);
+        acc[k] = acc[k] + lane_value(w, 31);
+        if (second) acc[k] = acc[k] + lane_value(w, 63);
+    }
+}
+
+// The one-pass moments (columns 0..16): wave w of workgroup b is strand s = 4 b + w, its chunks
+// s, s + S, ... two at a time (a half-wave each), two such pairs' loads issued before their
+// trees; y from the search (YIN) or gathered (kpos ? m4kd[kpos] : m4[idx], and stored)
 template <bool YIN>
 __global__ __launch_bounds__(kBlock) void canon_moments_kernel(
     const int *__restrict__ idx, const double4 *__restrict__ m4, const double *__restrict__ px,
@@ -50,19 +61,21 @@ __global__ __launch_bounds__(kBlock) void canon_moments_kernel(
     const int *__restrict__ kpos, const double4 *__restrict__ m4kd)
 {
     if (st->done) return; // a frozen (converged) ICP iteration: its sums are never used
-    __shared__ double sh[kBlock / 64][17];
     const double cp[3] = {st->shift_p[0], st->shift_p[1], st->shift_p[2]};
     const double cy[3] = {st->shift_y[0], st->shift_y[1], st->shift_y[2]};
-    const int nchunks = (n + kCanonChunk - 1) / kCanonChunk, R = gridDim.x;
-    double acc = 0.0;
-    constexpr int B = 2;
-    for (int c0 = blockIdx.x; c0 < nchunks; c0 += B * R) {
+    const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
+    const int lane = threadIdx.x & 63, s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    double acc[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) acc[k] = 0.0;
+    constexpr int B = 2; // (pairs of chunks whose loads go out together)
+    for (int c0 = s; s < S && c0 < C; c0 += 2 * B * S) {
         double4 y[B];
         double q[B][3];
 #pragma unroll
         for (int u = 0; u < B; ++u) {
-            const int c = c0 + u * R, i = c * kCanonChunk + threadIdx.x;
-            const bool in = c < nchunks && i < n;
+            const int c = c0 + (2 * u + (lane >> 5)) * S, i = c * kCanonChunk + (lane & 31);
+            const bool in = c < C && i < n;
             if constexpr (YIN) {
                 y[u] = in ? make_double4(yx[i], yy[i], yz[i], 0.0) : make_double4(0.0, 0.0, 0.0, 0.0);
             } else {
@@ -74,10 +87,11 @@ __global__ __launch_bounds__(kBlock) void canon_moments_kernel(
         }
 #pragma unroll
         for (int u = 0; u < B; ++u) {
-            const int c = c0 + u * R, i = c * kCanonChunk + threadIdx.x;
-            if (c >= nchunks) break; // (uniform)
+            const int cl = c0 + 2 * u * S; // (the pair's first chunk)
+            if (cl >= C) break;            // (uniform)
+            const int c = cl + (lane >> 5) * S, i = c * kCanonChunk + (lane & 31);
             double a[17];
-            if (i < n) {
+            if (c < C && i < n) {
                 if constexpr (!YIN) {
                     yx[i] = y[u].x;
                     yy[i] = y[u].y;
@@ -88,10 +102,10 @@ __global__ __launch_bounds__(kBlock) void canon_moments_kernel(
 #pragma unroll
                 for (int k = 0; k < 17; ++k) a[k] = 0.0;
             }
-            chunk_to_row<17>(a, sh, acc);
+            two_chunks_to_strand<17>(a, cl + S < C, acc);
         }
     }
-    if (threadIdx.x < 17) rows[(size_t)blockIdx.x * kCanonCols + threadIdx.x] = acc;
+    strands_to_row<17>(acc, rows, R);
 }
 
 // a workgroup's count into *acc: one atomic, and only when it is not zero
@@ -108,10 +122,11 @@ __device__ __forceinline__ void canon_far_to_acc(int far, int *acc)
     }
 }
 
-// p <- sR p + t (Eigen's order), the residual ||y - p'||^2 as the leaves of row column kSumErr,
-// and what the next search reads: the seed distance D64(p', y) (the residual's value), the f16
-// seed, the fp32 copy, the far count -- and with QOP the bundle filter's slot records for every
-// slot up to nslots (transform_err_kernel's forms, icp_step.hip).
+// p <- sR p + t (Eigen's order), the residual ||y - p'||^2 as the leaves of column kSumErr, and
+// what the next search reads: the seed distance D64(p', y) (the residual's value), the f16 seed,
+// the fp32 copy, the far count -- and with QOP the bundle filter's slot records for every slot up
+// to nslots (transform_err_kernel's forms, icp_step.hip): a chunk is a 32-slot group, and the
+// chunks past the points' (padding groups) get never-firing records.  Strands as the moments'.
 template <bool QOP>
 __global__ __launch_bounds__(kBlock) void canon_transform_kernel(
     double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, const double *__restrict__ yx,
@@ -120,7 +135,6 @@ __global__ __launch_bounds__(kBlock) void canon_transform_kernel(
 {
     __shared__ Xform sxf;
     __shared__ int sdone;
-    __shared__ double sh[kBlock / 64][1];
     if (threadIdx.x == 0) {
         sdone = *done;
         sxf = *xfd;
@@ -128,15 +142,16 @@ __global__ __launch_bounds__(kBlock) void canon_transform_kernel(
     __syncthreads();
     if (sdone) return;
     const Xform xf = sxf;
-    const int nchunks = (n + kCanonChunk - 1) / kCanonChunk, R = gridDim.x;
-    // (QOP: every slot the filter reads, nslots a multiple of 512, in whole waves)
-    const int cmax = QOP ? (sa.nslots + kCanonChunk - 1) / kCanonChunk : nchunks;
-    double acc = 0.0;
+    const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
+    const int lane = threadIdx.x & 63, s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    // (QOP: every 32-slot group the filter reads; nslots is a multiple of 512)
+    const int Cmax = QOP ? sa.nslots / kCanonChunk : C;
+    double acc[1] = {0.0};
     int far = 0;
-    for (int c = blockIdx.x; c < cmax; c += R) {
-        const int i = c * kCanonChunk + threadIdx.x;
+    for (int cl = s; s < S && cl < Cmax; cl += 2 * S) {
+        const int c = cl + (lane >> 5) * S, i = c * kCanonChunk + (lane & 31);
         double leaf[1] = {0.0};
-        if (i < n) {
+        if (c < C && i < n) {
             double q0, q1, q2;
             transform_point(xf, px[i], py[i], pz[i], q0, q1, q2);
             const double y0 = yx[i], y1 = yy[i], y2 = yz[i];
@@ -165,18 +180,16 @@ __global__ __launch_bounds__(kBlock) void canon_transform_kernel(
             } else if (sa.seed16) {
                 sa.seed16[i] = mfma16_seed_value(q0, q1, q2, y0, y1, y2, sa.c[0], sa.c[1], sa.c[2], sa.scale);
             }
-        } else if constexpr (QOP) {
-            if (i < sa.nslots) {
-                BundleQuery r;
-                double4 raw;
-                bundle_never_record(r, raw);
-                ((BundleQuery *)sa.qop)[i] = r;
-                bundle_group_store(r, i, sa.nslots, (half8_t *)sa.gop, sa.gctr);
-            }
+        } else if constexpr (QOP) { // (every lane of the wave takes part in the group bounds)
+            BundleQuery r;
+            double4 raw;
+            bundle_never_record(r, raw);
+            if (c < Cmax) ((BundleQuery *)sa.qop)[i] = r;
+            bundle_group_store(r, c < Cmax ? i : sa.nslots, sa.nslots, (half8_t *)sa.gop, sa.gctr);
         }
-        if (c < nchunks) chunk_to_row<1>(leaf, sh, acc); // (uniform)
+        if (cl < C) two_chunks_to_strand<1>(leaf, cl + S < C, acc); // (uniform)
     }
-    if (threadIdx.x == 0) rows[(size_t)blockIdx.x * kCanonCols + kSumErr] = acc;
+    strands_to_row<1>(acc, rows + (size_t)kSumErr * R, R);
     if (sa.far_acc) canon_far_to_acc(far, sa.far_acc);
 }
 
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
         for (int u = 0; u < U; ++u) {
             const int r = r0 + u * kFoldThreads;
 #pragma unroll
-            for (int k = 0; k < K; ++k) v[u][k] = r < R ? rows[(size_t)r * kCanonCols + K0 + k] : 0.0;
+            for (int k = 0; k < K; ++k) v[u][k] = r < R ? rows[(size_t)(K0 + k) * R + r] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -213,8 +226,9 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const double w = wave_tree_63<1>(a[k]);
-        if (lane == 63) sh[wave][k] = w;
+        const double w = wave_tree_halves(a[k]);
+        const double two = lane_value(w, 31) + lane_value(w, 63); // (the wave's 64 lanes, pairwise)
+        if (lane == 0) sh[wave][k] = two;
     }
     __syncthreads();
     if (threadIdx.x < K) {

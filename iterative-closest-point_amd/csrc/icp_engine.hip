@@ -615,6 +615,19 @@ static bool grid_auto()
     return on;
 }
 
+// icp_run's grid iterations over a scene in slot order as ONE launch each (nn_grid_iter_kernel:
+// the transform, the seeded search with the task's boxes staged in LDS, the moments);
+// ICP_GRID_ITER=1 enables it (default off until it beats the separate transform, seeded search
+// and moments passes)
+static bool grid_iter_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_GRID_ITER");
+        return e && atoi(e) == 1;
+    }();
+    return on;
+}
+
 // the seeded grid search of a sparse scene in slot order, each XCD on a contiguous eighth of it
 // (launch_nn_grid_resolve_all); ICP_GRID_XCD=0: the plain block order, =2: every scene (A/B)
 static int grid_xcd()
@@ -1503,9 +1516,11 @@ static bool kd_host()
 // (icp_model.hip); the host reads back 13 doubles and, for models that fit the one-launch
 // loops (<= 64k points), builds their Morton image.  Nothing of the context changes before the
 // model has passed its checks.
-static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm)
+// aos_dev (nullable): the model's AoS copy in device memory (icp_set_model_device), else ctx->stage.
+// m_xyz: the host copy, for the host-side images (small models, ICP_KD_HOST, the CPU rule)
+static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const double *aos_dev = nullptr)
 {
-    const double *aos = ctx->stage;
+    const double *aos = aos_dev ? aos_dev : ctx->stage;
     if (!ctx->mstat_part) {
         HIPCHK(hipMalloc((void **)&ctx->mstat_part, sizeof(double) * model_stats_scratch_doubles()));
         HIPCHK(hipMalloc((void **)&ctx->mstat_out, sizeof(double) * 16));
@@ -1638,6 +1653,28 @@ int icp_set_model(icp_ctx *ctx, const double *m_xyz, size_t nm)
     return set_model_staged(ctx, m_xyz, nm);
 }
 
+// a host copy of the model is needed only for the host-side images: the one-launch loops' model
+// image (small models), the host kd order (ICP_KD_HOST) and the CPU rule's host fix-up
+static bool model_needs_host(const icp_ctx *ctx, size_t nm)
+{
+    return nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel) || kd_host() ||
+           ctx->nn_rule == ICP_NN_RULE_CPU_SQRT;
+}
+
+int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm)
+{
+    if (!ctx || !m_xyz_dev || nm == 0) return ICP_E_ARG;
+    if (nm > (size_t)0x7fffffff - kTile32) return fail(ctx, ICP_E_ARG, "model too large");
+    HIPCHK(hipSetDevice(ctx->device));
+    std::vector<double> host; // (only when a host-side image needs the points)
+    if (model_needs_host(ctx, nm)) {
+        host.resize(3 * nm);
+        HIPCHK(hipMemcpyAsync(host.data(), m_xyz_dev, sizeof(double) * 3 * nm, hipMemcpyDeviceToHost, ctx->st));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+    }
+    return set_model_staged(ctx, host.empty() ? nullptr : host.data(), nm, m_xyz_dev);
+}
+
 int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded)
 {
     if (!ctx || !m_xyz || nm == 0) return ICP_E_ARG;
@@ -1668,6 +1705,8 @@ int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded
     return ICP_OK;
 }
 
+static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total);
+
 int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total)
 {
     if (!ctx || (!p_xyz && np_local) || np_local > np_total) return ICP_E_ARG;
@@ -1679,6 +1718,28 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     // a small cloud went through the mapped staging buffer (host-copied: the caller's array is
     // free again), a large one through a pageable copy; either way the stream orders the rest
     if (3 * np_local > kMappedIo) HIPCHK(hipStreamSynchronize(ctx->st));
+    return set_scene_common(ctx, np_local, np_total);
+}
+
+int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total)
+{
+    if (!ctx || (!p_xyz_dev && np_local) || np_local > np_total) return ICP_E_ARG;
+    if (np_total > (size_t)0x7fffffff) return fail(ctx, ICP_E_ARG, "scene too large");
+    HIPCHK(hipSetDevice(ctx->device));
+    TRY(ensure_reduction_space(ctx));
+    TRY(grow_cloud(ctx, ctx->Y, np_local, false));
+    TRY(grow_cloud(ctx, ctx->scene, np_local, true));
+    if (np_local) { // (the caller's device array: converted on the stream, no copy)
+        launch_aos_to_soa(p_xyz_dev, np_local, ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->st);
+        launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, np_local, ctx->c[0], ctx->c[1], ctx->c[2],
+                        ctx->scene.f, ctx->st);
+        LAUNCHCHK("set_scene_device");
+    }
+    return set_scene_common(ctx, np_local, np_total);
+}
+
+static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total)
+{
     ctx->np_total = np_total;
     ctx->has_scene = true;
     ctx->seeds_valid = false;
@@ -2289,6 +2350,15 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         if (!ctx->h_far) HIPCHK(hipHostMalloc((void **)&ctx->h_far, sizeof(int), hipHostMallocDefault));
     }
     const bool lag_sched = lag || canon;
+    // ICP_ITER_DEBUG=1: nn_grid_iter_kernel's phase clocks and counts, summed over the run, to stderr
+    static const bool iter_debug = getenv("ICP_ITER_DEBUG") != nullptr;
+    unsigned long long *iter_dbg = nullptr;
+    if (iter_debug && canon) {
+        static unsigned long long *buf = nullptr;
+        if (!buf) HIPCHK(hipMalloc((void **)&buf, 16 * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(buf, 0, 16 * sizeof(unsigned long long), ctx->st));
+        iter_dbg = buf;
+    }
     bool xf_pending = false; // (canon: the last Horn step's transform is still to be applied)
     CanonStep cs;
     cs.N = N;
@@ -2359,6 +2429,42 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     HIPCHK(hipStreamSynchronize(ctx->st));
                     far_obs = *ctx->h_far;
                     grid_c = far_obs <= far_thr;
+                }
+                // the grid's iterations as ONE launch: the pending transform, the seeded search
+                // of every point and the moments (nn_grid_iter_kernel)
+                const bool k1 = grid_iter_on() && xf_pending && ctx->seeds_valid && enqueued > 0 &&
+                                ctx->nn_mode == ICP_NN_CERTIFIED && ctx->nn_rule == ICP_NN_RULE_SQUARED &&
+                                (grid_c || ctx->nn_variant == ICP_NN_VARIANT_GRID) && ctx->g_pts32;
+                if (k1) {
+                    if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
+                    launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd, need_p32 ? P.f : nullptr,
+                                        grid_view(ctx), kSeededBox, grid_budget(ctx), (int)ctx->nm, ctx->m4,
+                                        ctx->canon_rowbuf, grid_policy ? &sd->far_acc : nullptr, sa_grid.far_d2,
+                                        ctx->amb_count + 2, ctx->st, iter_dbg);
+                    LAUNCHCHK("nn_grid_iter");
+                    if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));
+                    if (!need_p32) ctx->p32_stale = true;
+                    ws = SeedState{}; // (no seed distances written: the next grid iteration computes its own)
+                    xf_pending = false;
+                    ctx->stats.last_filter = ICP_FILTER_GRID;
+                    ctx->stats.run_grid_searches += 1;
+                    ctx->kpos_valid = false;
+                    ctx->y_ready = true;
+                    ar_timed[slot] = false;
+                    if ((size_t)enqueued < ctx->digest_cap) {
+                        launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st,
+                                          digest_order);
+                        LAUNCHCHK("idx_digest");
+                    }
+                    ar_timed[slot] = timed && lag;
+                    TRY(canon_end(enqueued - 1, true, slot));
+                    xf_pending = true;
+                    ++enqueued;
+                    if (enqueued == max_iter) {
+                        TRY(canon_transform(grid_policy ? sa_grid : SeedArgs{}));
+                        TRY(canon_end(enqueued - 1, false, -1));
+                    }
+                    continue;
                 }
                 if (xf_pending) { // the last Horn step's transform, in the form this search reads
                     SeedArgs sa_t = grid_c ? sa_grid : sa;
@@ -2627,6 +2733,14 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         ctx->seeds_valid = seeds_at_start;
         ctx->seedd_valid = false;
         return kTailAborted;
+    }
+    if (iter_dbg) {
+        unsigned long long h[16];
+        HIPCHK(hipMemcpy(h, iter_dbg, sizeof(h), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[iter_debug] tasks %llu staged %llu pts %llu big %llu flushes %llu rows_over %llu pts_over %llu "
+                        "| wave-us A %.1f BC %.1f D %.1f E %.1f FG %.1f\n",
+                h[0], h[1], h[2], h[3], h[4], h[10], h[11], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01, h[8] * 0.01,
+                h[9] * 0.01);
     }
     // (every transform of a policy run wrote the seed distances, whatever its form; the next run
     // may start from them)

@@ -24,6 +24,8 @@
 #include <cstdlib>
 #include <string>
 
+#include "icp_canon.h"
+#include "icp_device.h"
 #include "icp_kernels.h"
 
 namespace icp {
@@ -767,6 +769,384 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
     }
 }
 
+
+// ---- the fused grid iteration (icp_run's grid searches over a scene in slot order) ----------
+//
+// ONE launch per ICP iteration for the policy's grid searches (run_loop, canon): the previous
+// iteration's transform p <- sR p + t (gpu.cc:71-74) with its residual ||y - p'||^2, which is
+// also each query's seed distance D64(p', m[idx]) bit for bit; the exact seeded search of
+// nn_grid_seeded32_kernel (compute.cu:94-150's rule: the fp64 first minimum); and this
+// iteration's one-pass moments (gpu.cc:98-104, :142) -- the 17 moments and the residual added in
+// the canonical order (icp_canon.h: a wave is a strand, a task of 32 consecutive queries a chunk).
+//
+// A task's boxes overlap (the queries are Morton neighbours: at C4 the union of 32 boxes holds
+// ~400 model points where the 32 boxes hold ~500 between them), so the wave stages the union
+// once: the x-runs of the union box's rows, read coalesced from the fp32 grid image into LDS
+// (kIterPts points), then each query (two lanes) tests the LDS points of the union rows that
+// cross its own box against seeded_bound32 and decides its candidates in fp64.  Scanning the
+// union row beyond the query's own x-cells only adds candidates the bound rejects: every point
+// at least as close as the seed lies in the query's box (the file header), hence in those rows.
+// A union over the row or point capacity takes the per-query walk of nn_grid_seeded32_kernel
+// from global memory; a query whose own box exceeds `box` cells (or has no finite seed) is
+// searched by the whole wave afterwards (its box up to `budget` cells, flattened, else every
+// model point), as the second pass of grid_seeded_search does.
+#ifndef ICP_ITER_KB
+#define ICP_ITER_KB 4 // (staged points a lane loads together: 122 VGPRs with KCAND 2, four waves a SIMD)
+#endif
+#ifndef ICP_ITER_KCAND
+#define ICP_ITER_KCAND 2 // (candidate records a lane loads together)
+#endif
+constexpr int kIterRows = 128, kIterPts = 512;
+__global__ __launch_bounds__(kBlock) void nn_grid_iter_kernel(
+    int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
+    double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
+    float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
+    double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, unsigned long long *__restrict__ dbg)
+{
+    // dbg (nullable, ICP_ITER_DEBUG): per-wave phase clocks (s_memrealtime, 100 MHz) and counts
+    unsigned long long dcnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tclk = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    auto lap = [&](int f) {
+        if (dbg) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            dcnt[f] += now - tclk;
+            tclk = now;
+        }
+    };
+    __shared__ float4 s_pts[kBlock / 64][kIterPts];
+    __shared__ int s_rbase[kBlock / 64][kIterRows + 1], s_rstart[kBlock / 64][kIterRows];
+    // (st is uniform: its fields are scalar loads into SGPRs -- an LDS copy would hold the
+    // transform's 15 doubles in VGPRs all kernel long)
+    if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
+    const Xform xf = st->xf;
+    const double cp[3] = {st->shift_p[0], st->shift_p[1], st->shift_p[2]};
+    const double cy[3] = {st->shift_y[0], st->shift_y[1], st->shift_y[2]};
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane >> 1, sub = lane & 1;
+    const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
+    const int s = blockIdx.x * 4 + wave;
+    float4 *const lp = s_pts[wave];
+    int *const rbase = s_rbase[wave], *const rstart = s_rstart[wave];
+    double acc = 0.0; // (lane k < 18: column k of this strand)
+    int far = 0, nbig = 0;
+    for (int c = s; s < S && c < C; c += S) {
+        const int t = c * kCanonChunk + u;
+        const bool active = t < n;
+        // A: the previous transform, its residual = the seed distance
+        double q[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
+        int h = -1;
+        if (active) {
+            const double p0 = px[t], p1 = py[t], p2 = pz[t];
+            y[0] = yx[t];
+            y[1] = yy[t];
+            y[2] = yz[t];
+            h = idx[t];
+            transform_point(xf, p0, p1, p2, q[0], q[1], q[2]);
+        }
+        const double e = active ? residual2(y[0], y[1], y[2], q[0], q[1], q[2]) : 0.0;
+        lap(5);
+        if (active && sub == 0) {
+            px[t] = q[0];
+            py[t] = q[1];
+            pz[t] = q[2];
+            if (p32) p32[t] = make_float4((float)(q[0] - xf.c[0]), (float)(q[1] - xf.c[1]), (float)(q[2] - xf.c[2]), 0.0f);
+            far += e > far_d2 ? 1 : 0;
+        }
+        // B: the query's complete box around its seed, the task's union of them
+        double best = e;
+        int bi = h, bk = -1, c0[3] = {0, 0, 0}, c1[3] = {-1, -1, -1};
+        const bool ok = active && h >= 0 && e == e && e < INFINITY && complete_box(q, e, gv, box, c0, c1);
+        int lo3[3], hi3[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo3[a] = ok ? c0[a] : 0x7fffffff;
+            hi3[a] = ok ? c1[a] : -1;
+        }
+#pragma unroll
+        for (int o = 2; o < 64; o <<= 1) // (the two lanes of a query agree: start at 2)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                lo3[a] = min(lo3[a], __shfl_xor(lo3[a], o, 64));
+                hi3[a] = max(hi3[a], __shfl_xor(hi3[a], o, 64));
+            }
+        const bool anyok = __ballot(ok) != 0ull;
+        const int ux = hi3[0] - lo3[0] + 1, uy = hi3[1] - lo3[1] + 1, uz = hi3[2] - lo3[2] + 1;
+        const int nrows = anyok ? uy * uz : 0;
+        bool staged = false;
+        int total = 0;
+        if (anyok && nrows <= kIterRows) {
+            // C: the union rows' runs (two rows a lane at most), their prefix, then the points
+            int len[2] = {0, 0};
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int r = lane + 64 * v;
+                if (r < nrows) {
+                    const int gy = lo3[1] + r % uy, gz = lo3[2] + r / uy;
+                    const int row = (gz * gv.g[1] + gy) * gv.g[0];
+                    const int a0 = gv.start[row + lo3[0]], a1 = gv.start[row + hi3[0] + 1];
+                    rstart[r] = a0;
+                    len[v] = a1 - a0;
+                }
+            }
+            int carry = 0;
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                int incl = len[v];
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int w = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += w;
+                }
+                const int r = lane + 64 * v;
+                if (r < nrows) rbase[r] = carry + incl - len[v];
+                carry += __shfl(incl, 63, 64);
+            }
+            total = carry;
+            if (lane == 0) rbase[nrows] = total;
+            if (total <= kIterPts) {
+                staged = true;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                constexpr int kB = ICP_ITER_KB; // (points a lane loads together)
+                for (int v0 = 0; v0 < (total + 63) / 64; v0 += kB) {
+                    float4 pv[kB];
+                    int kk[kB];
+#pragma unroll
+                    for (int v = 0; v < kB; ++v) {
+                        const int k = lane + 64 * (v0 + v);
+                        kk[v] = -1;
+                        if (k < total) { // the row of point k: the last r with rbase[r] <= k
+                            int r = 0;
+#pragma unroll
+                            for (int step = kIterRows / 2; step >= 1; step >>= 1)
+                                if (r + step < nrows && rbase[r + step] <= k) r += step;
+                            kk[v] = rstart[r] + (k - rbase[r]);
+                        }
+                    }
+#pragma unroll
+                    for (int v = 0; v < kB; ++v) pv[v] = gv.pts32[kk[v] >= 0 ? kk[v] : 0]; // (index 0: a load never used)
+#pragma unroll
+                    for (int v = 0; v < kB; ++v)
+                        if (kk[v] >= 0) lp[lane + 64 * (v0 + v)] = pv[v];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+        lap(6);
+        if (dbg) {
+            dcnt[0] += 1;
+            dcnt[1] += staged ? 1 : 0;
+            dcnt[2] += staged ? (unsigned long long)total : 0ull;
+            dcnt[10] += anyok && nrows > kIterRows ? 1 : 0;
+            dcnt[11] += anyok && nrows <= kIterRows && !staged ? 1 : 0;
+        }
+        // D: each query against the points of its rows (LDS when staged, else its own box from
+        // global memory), fp32 bound first; the candidates are decided in fp64 a few at a time with
+        // their record loads in flight together (the seed itself needs none: its index is known)
+        double wx = 0.0, wy = 0.0, wz = 0.0; // (the winner's coordinates, when a candidate won)
+        int wset = 0;
+        if (ok) {
+            const double o0 = q[0] - gv.c32[0], o1 = q[1] - gv.c32[1], o2 = q[2] - gv.c32[2];
+            const float f0 = (float)o0, f1 = (float)o1, f2 = (float)o2;
+            const double eq = std::ldexp(fmax(fabs(o0), fmax(fabs(o1), fabs(o2))), -23) + gv.em32;
+            const float T = seeded_bound32(best, eq);
+            const int ny = c1[1] - c0[1] + 1, nrq = ny * (c1[2] - c0[2] + 1);
+            constexpr int kCand = ICP_ITER_KCAND;
+            int cand[kCand], nc = 0;
+            auto flush = [&]() {
+                if (dbg) dcnt[4] += (unsigned long long)nc; // (per lane; summed over the wave below)
+                double4 w[kCand];
+#pragma unroll
+                for (int j = 0; j < kCand; ++j) w[j] = gv.pts[cand[j < nc ? j : 0]];
+#pragma unroll
+                for (int j = 0; j < kCand; ++j) {
+                    if (j >= nc) break;
+                    const int mi = (int)w[j].w;
+                    const double d = d64g(q[0], q[1], q[2], w[j].x, w[j].y, w[j].z);
+                    if (d < best || (d == best && (unsigned)mi < (unsigned)bi)) {
+                        best = d;
+                        bi = mi;
+                        bk = cand[j];
+                        wx = w[j].x;
+                        wy = w[j].y;
+                        wz = w[j].z;
+                        wset = 1;
+                    }
+                }
+                nc = 0;
+            };
+            auto test = [&](const float4 &m, int pos) {
+                const float dx = f0 - m.x, dy = f1 - m.y, dz = f2 - m.z;
+                if ((dx * dx + dy * dy) + dz * dz > T) return; // (strictly farther than best)
+                if (__float_as_int(m.w) == bi) {
+                    bk = pos; // (the current winner itself)
+                } else {
+                    cand[nc++] = pos;
+                    if (nc == kCand) flush();
+                }
+            };
+            if (staged) {
+                for (int rq = sub; rq < nrq; rq += 2) {
+                    const int gy = c0[1] + rq % ny, gz = c0[2] + rq / ny;
+                    const int r = (gz - lo3[2]) * uy + (gy - lo3[1]);
+                    const int k0 = rbase[r], k1 = rbase[r + 1], p0 = rstart[r] - k0;
+                    for (int k = k0; k < k1; ++k) test(lp[k], p0 + k);
+                }
+            } else {
+                for (int rq = sub; rq < nrq; rq += 2) {
+                    const int gy = c0[1] + rq % ny, gz = c0[2] + rq / ny;
+                    const int row = (gz * gv.g[1] + gy) * gv.g[0];
+                    const int a0 = gv.start[row + c0[0]], a1 = gv.start[row + c1[0] + 1];
+                    for (int k = a0; k < a1; k += 2) {
+                        const float4 m0 = gv.pts32[k];
+                        const float4 m1 = gv.pts32[k + 1 < a1 ? k + 1 : k];
+                        test(m0, k);
+                        if (k + 1 < a1) test(m1, k + 1);
+                    }
+                }
+            }
+            if (nc) flush();
+        }
+        lap(7);
+        { // the query's two lanes: the (D64, index) minimum, its position and coordinates
+            const double ob = __shfl_xor(best, 1, 64);
+            const int oi = __shfl_xor(bi, 1, 64), ok2 = __shfl_xor(bk, 1, 64), ows = __shfl_xor(wset, 1, 64);
+            const double ox = __shfl_xor(wx, 1, 64), oy = __shfl_xor(wy, 1, 64), oz = __shfl_xor(wz, 1, 64);
+            if (ob < best || (ob == best && (unsigned)oi < (unsigned)bi)) {
+                best = ob;
+                bi = oi;
+                bk = ok2;
+                wx = ox;
+                wy = oy;
+                wz = oz;
+                wset = ows;
+            } else if (ob == best && oi == bi) {
+                bk = max(bk, ok2);
+                if (!wset && ows) {
+                    wx = ox;
+                    wy = oy;
+                    wz = oz;
+                    wset = 1;
+                }
+            }
+        }
+        // E: the queries whose box exceeds `box` cells (or has no finite seed), one at a time by the
+        // whole wave: the box up to `budget` cells, else every model point
+        unsigned long long bigm = __ballot(active && !ok && sub == 0);
+        nbig += __popcll(bigm);
+        if (dbg) dcnt[3] += __popcll(bigm);
+        while (bigm) {
+            const int bl = __ffsll((long long)bigm) - 1;
+            bigm &= bigm - 1;
+            const double bq[3] = {__shfl(q[0], bl, 64), __shfl(q[1], bl, 64), __shfl(q[2], bl, 64)};
+            const double be = __shfl(e, bl, 64);
+            const int bh = __shfl(h, bl, 64);
+            double b2 = INFINITY;
+            int bj = -1;
+            int d0[3], d1[3];
+            if (bh >= 0 && be == be && be < INFINITY && complete_box(bq, be, gv, budget, d0, d1)) {
+                b2 = be;
+                bj = bh;
+                scan_box<64>(bq, d0, d1, gv, lane, b2, bj); // (rows a lane: fewer registers than the flat scan)
+            } else { // the exact fp64 scan of every point (a NaN query keeps index -1 -> 0)
+                for (int k = lane; k < nm; k += 64) {
+                    const double4 m = m4[k];
+                    lex_min(b2, bj, d64g(bq[0], bq[1], bq[2], m.x, m.y, m.z), k);
+                }
+            }
+            group_lex_min<64>(b2, bj);
+            if ((lane >> 1) == (bl >> 1)) {
+                best = b2;
+                bi = bj < 0 ? 0 : bj;
+                bk = -1;
+                wset = 0;
+            }
+        }
+        lap(8);
+        // F: the correspondence: the seed's coordinates are the previous y, a candidate's came with
+        // its record; only a query the whole wave took reads m4
+        if (active) {
+            if (!(ok && bi == h)) {
+                if (wset) {
+                    y[0] = wx;
+                    y[1] = wy;
+                    y[2] = wz;
+                } else {
+                    const double4 w = m4[bi];
+                    y[0] = w.x;
+                    y[1] = w.y;
+                    y[2] = w.z;
+                }
+            }
+            if (sub == 0) {
+                idx[t] = bi;
+                yx[t] = y[0];
+                yy[t] = y[1];
+                yz[t] = y[2];
+            }
+        }
+        // G: this chunk's 17 moments and the residual (leaves in the odd lanes), into the strand;
+        // one column at a time (moment_leaves' terms)
+        const double d[6] = {active ? q[0] - cp[0] : 0.0, active ? q[1] - cp[1] : 0.0, active ? q[2] - cp[2] : 0.0,
+                             active ? y[0] - cy[0] : 0.0, active ? y[1] - cy[1] : 0.0, active ? y[2] - cy[2] : 0.0};
+#pragma unroll
+        for (int k = 0; k < kCanonCols; ++k) {
+            double leaf;
+            if (k < 6) leaf = 0.0 + d[k];
+            else if (k < 15) leaf = 0.0 + d[(k - 6) / 3] * d[3 + (k - 6) % 3];
+            else if (k == 15) leaf = 0.0 + ((d[3] * d[3] + d[4] * d[4]) + d[5] * d[5]);
+            else if (k == 16) leaf = 0.0 + ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+            else leaf = active ? 0.0 + e : 0.0;
+            if (!active) leaf = 0.0;
+            const double v = lane_value(wave_tree_odd(leaf), 63);
+            if (lane == k) acc = acc + v;
+        }
+        lap(9);
+    }
+    if (dbg)
+        for (int o = 32; o >= 1; o >>= 1) dcnt[4] += __shfl_xor(dcnt[4], o, 64);
+    if (dbg && lane == 0)
+        for (int f = 0; f < 12; ++f)
+            if (dcnt[f]) atomicAdd(dbg + f, dcnt[f]);
+    // the workgroup's four strands -> its row (column k from lane k of each wave)
+    __shared__ double sh[kBlock / 64][kCanonCols];
+    if (lane < kCanonCols) sh[wave][lane] = acc;
+    __syncthreads();
+    if (threadIdx.x < kCanonCols) {
+        const int k = threadIdx.x;
+        rows[(size_t)k * R + blockIdx.x] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+    }
+    // the far count (the policy's) and the big boxes (the search statistics), one atomic each
+    __shared__ int s_cnt[2][kBlock / 64];
+    for (int o = 32; o >= 1; o >>= 1) far += __shfl_xor(far, o, 64);
+    if (lane == 0) {
+        s_cnt[0][wave] = far;
+        s_cnt[1][wave] = nbig;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += s_cnt[threadIdx.x][w];
+        int *dst = threadIdx.x == 0 ? far_acc : big_count;
+        if (tot && dst) atomicAdd(dst, tot);
+    }
+}
+
+} // namespace
+
+void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
+                         const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
+                         const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
+                         unsigned long long *dbg)
+{
+    if (n <= 0) return;
+    nn_grid_iter_kernel<<<canon_rows((size_t)n), kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
+                                                                   budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+}
+
+namespace {
 } // namespace
 
 GridParams grid_params(const double *m_xyz, size_t nm)

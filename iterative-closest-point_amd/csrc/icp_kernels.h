@@ -489,7 +489,7 @@ struct CanonStep {
     double c[3] = {0.0, 0.0, 0.0};
     int *cnt = nullptr;
 };
-// rows: canon_rows(n) x 18 doubles.  Moments -> columns 0..16 (y from the search when y_ready,
+// rows: canon_rows(n) x 18 doubles, by column (k R + r).  Moments -> columns 0..16 (y from the search when y_ready,
 // else gathered through kpos / idx and stored); transform -> column kSumErr plus SeedArgs'
 // outputs; fold: mode 0 all 18 -> sums, 1 + error step + Horn step (one rank), 2 the residual
 // column + error step (the last iteration, one rank), 3 the residual column -> sums[kSumErr]
@@ -500,6 +500,16 @@ void launch_canon_transform(double *px, double *py, double *pz, const double *yx
                             int n, const Xform *xf, const int *done, float4 *p32, double *rows, const SeedArgs &sa,
                             hipStream_t st);
 void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st);
+// the fused grid iteration (icp_grid.hip, nn_grid_iter_kernel): the previous transform (st->xf) of
+// the scene in slot order, the exact seeded grid search of every point (box: cells a query's own
+// box may have before the whole wave takes it; budget: cells before every model point), and the
+// moments + residual into the canonical rows; far_acc += the far count (far_d2), big_count += the
+// queries the whole wave took.  No-op once st->done.
+struct GridView;
+void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
+                         const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
+                         const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
+                         unsigned long long *dbg = nullptr); // (dbg: ICP_ITER_DEBUG's 12 counters)
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,
 // sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)

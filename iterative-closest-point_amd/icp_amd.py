@@ -58,6 +58,7 @@ EXPORTED = [
     "icp_ctx_create", "icp_ctx_create_dist", "icp_rccl_unique_id", "icp_ctx_create_sharded",
     "icp_ctx_destroy",
     "icp_last_error", "icp_strerror", "icp_device_count", "icp_set_model", "icp_set_scene",
+    "icp_set_model_device", "icp_set_scene_device",
     "icp_get_scene", "icp_set_allow_unequal", "icp_set_nn_variant", "icp_run", "icp_closest_matrix",
     "icp_compute_centroid", "icp_y_p_norm", "icp_err_compute", "icp_find_alignment",
     "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
@@ -130,6 +131,8 @@ def lib() -> C.CDLL:
     L.icp_strerror.restype = C.c_char_p
     L.icp_device_count.argtypes = [C.POINTER(C.c_int)]
     L.icp_set_model.argtypes = [vp, dp, sz]
+    L.icp_set_model_device.argtypes = [vp, vp, sz]
+    L.icp_set_scene_device.argtypes = [vp, vp, sz, sz]
     L.icp_set_scene.argtypes = [vp, dp, sz, sz]
     L.icp_get_scene.argtypes = [vp, dp]
     L.icp_set_allow_unequal.argtypes = [vp, C.c_int]
@@ -318,6 +321,17 @@ class Context:
     def set_model(self, m):
         m = _cloud(m)
         self._check(lib().icp_set_model(self._h, _dp(m), m.shape[0]))
+
+    def set_model_device(self, ptr: int, nm: int):
+        """icp_set_model_device: the model's AoS fp64 array already in device memory (a device
+        pointer, e.g. a torch tensor's data_ptr(), written by work ordered before this call)."""
+        self._check(lib().icp_set_model_device(self._h, C.c_void_p(ptr), nm))
+
+    def set_scene_device(self, ptr: int, np_local: int, np_total: int | None = None):
+        """icp_set_scene_device: the scene's AoS fp64 array already in device memory."""
+        self._check(lib().icp_set_scene_device(self._h, C.c_void_p(ptr), np_local,
+                                               np_local if np_total is None else np_total))
+        self._np_local = np_local
 
     def ensure_model(self, m) -> bool:
         """icp_ensure_model: upload unless the resident model has these exact contents."""
