@@ -171,6 +171,13 @@ int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
  * (compute_Y_w_opti, compute.cu:154-160, re-uploads per call).  *uploaded (nullable) = 1 if
  * the model changed. */
 int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded);
+/* Progress of icp_run (the reference prints "[ICP] iteration number i | error value = e" as each
+ * iteration ends, src/GPU/gpu.cc:65,77): fn(i, err_i, user) is called on the calling thread, in
+ * order, once per recorded iteration, while the run waits for the device (from the mapped error
+ * trace: no extra synchronisation); a one-launch registration reports when its launch ends.
+ * fn = NULL switches it off. */
+typedef void (*icp_progress_fn)(int iteration, double err, void *user);
+int icp_set_progress(icp_ctx *ctx, icp_progress_fn fn, void *user);
 /* Reference behaviour is to refuse np != nm (gpu.cc:54-57); 1 lifts that check. */
 int icp_set_allow_unequal(icp_ctx *ctx, int allow);
 /* ICP_NN_VARIANT_* (default AUTO). */

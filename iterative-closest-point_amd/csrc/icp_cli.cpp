@@ -91,13 +91,15 @@ int main(int argc, char **argv)
     }
     double *errs = (double *)std::calloc(max_iter > 0 ? (size_t)max_iter : 1, sizeof(double));
     icp_result res{};
+    // each iteration's line as it ends (gpu.cc:65,77), from the engine's progress callback
+    icp_set_progress(
+        ctx, [](int i, double e, void *) { std::fprintf(stderr, "[ICP] iteration number %d | error value = %g\n", i, e); },
+        nullptr);
     rc = icp_run(ctx, max_iter, threshold, errs, &res);
     if (rc != ICP_OK) {
         std::fprintf(stderr, "[error] %s: %s\n", icp_strerror(rc), icp_last_error(ctx));
         return 3;
     }
-    for (int i = 0; i < res.iterations; ++i) // gpu.cc:65,77
-        std::fprintf(stderr, "[ICP] iteration number %d | error value = %g\n", i, errs[i]);
     if ((rc = icp_get_scene(ctx, p)) != ICP_OK) {
         std::fprintf(stderr, "[error] %s: %s\n", icp_strerror(rc), icp_last_error(ctx));
         return 3;

@@ -148,6 +148,9 @@ struct icp_ctx {
     ncclComm_t comm = nullptr;
     icp_allreduce_fn host_reduce = nullptr; // alternative to RCCL (icp_ctx_create_sharded)
     void *host_reduce_user = nullptr;
+    icp_progress_fn progress_fn = nullptr; // (icp_set_progress: each recorded iteration's error, as it ends)
+    void *progress_user = nullptr;
+    int progress_next = 0; // (the next iteration of the current run to report)
 
     // model (replicated)
     DevCloud model;
@@ -617,13 +620,13 @@ static bool grid_auto()
 
 // icp_run's grid iterations over a scene in slot order as ONE launch each (nn_grid_iter_kernel:
 // the transform, the seeded search with the task's boxes staged in LDS, the moments);
-// ICP_GRID_ITER=1 enables it (default off until it beats the separate transform, seeded search
-// and moments passes)
+// ICP_GRID_ITER=0: the separate transform, seeded search and moments passes (A/B; measured at
+// C4 0.167 against 0.162 ms an iteration, the W = 8 shard 0.058 against 0.055, profiles/r05g)
 static bool grid_iter_on()
 {
     static const bool on = [] {
         const char *e = getenv("ICP_GRID_ITER");
-        return e && atoi(e) == 1;
+        return !(e && atoi(e) == 0);
     }();
     return on;
 }
@@ -1486,6 +1489,14 @@ int icp_set_run_mode(icp_ctx *ctx, int mode)
     return ICP_OK;
 }
 
+int icp_set_progress(icp_ctx *ctx, icp_progress_fn fn, void *user)
+{
+    if (!ctx) return ICP_E_ARG;
+    ctx->progress_fn = fn;
+    ctx->progress_user = user;
+    return ICP_OK;
+}
+
 int icp_set_allow_unequal(icp_ctx *ctx, int allow)
 {
     if (!ctx) return ICP_E_ARG;
@@ -1818,6 +1829,15 @@ static int wait_flag(icp_ctx *ctx, const int *flag, int ticket)
     }
 }
 
+// icp_set_progress: iterations [progress_next, upto) of the running icp_run, from the mapped
+// error trace (each entry written before its iteration's ticket was released)
+static void report_progress(icp_ctx *ctx, int upto)
+{
+    if (!ctx->progress_fn) return;
+    for (; ctx->progress_next < upto; ++ctx->progress_next)
+        ctx->progress_fn(ctx->progress_next, ctx->h_trace[ctx->progress_next], ctx->progress_user);
+}
+
 static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_result *res,
                       std::chrono::steady_clock::time_point wall0);
 
@@ -2120,6 +2140,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_trace, ctx->h_trace, 0));
     }
     std::memset(ctx->h_iter, 0, sizeof(IterState));
+    ctx->progress_next = 0;
     if (!ctx->h_flags) {
         HIPCHK(hipHostMalloc((void **)&ctx->h_flags, sizeof(int) * 4 * kRing,
                              hipHostMallocMapped | hipHostMallocCoherent));
@@ -2698,6 +2719,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             if (dbg) fprintf(stderr, "[policy] waited %d far %d thr %d next_grid %d\n", waited, far_obs, far_thr, (int)grid_next);
         }
         const int done = ctx->h_flags[4 * slot], iters = ctx->h_flags[4 * slot + 1];
+        report_progress(ctx, iters); // (the iterations recorded so far, as they end)
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;
             if (n && (waited - 1) % timing_stride == timing_phase) { // (an empty shard records no events)
@@ -2756,6 +2778,7 @@ static int finish_run(icp_ctx *ctx, double threshold, double *err_trace, icp_res
                       std::chrono::steady_clock::time_point wall0)
 {
     const IterState &hs = *ctx->h_iter; // mirrored by the last recorded err step
+    report_progress(ctx, hs.iter); // (the rest: a one-launch run reports here)
     icp_result r{};
     r.iterations = hs.iter;
     r.s = 1.0; // GPU::ICP ctor state (gpu.hh:53-55) when no iteration ran

@@ -797,6 +797,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
 #define ICP_ITER_KCAND 2 // (candidate records a lane loads together)
 #endif
 constexpr int kIterRows = 128, kIterPts = 512;
+template <bool STAGE>
 __global__ __launch_bounds__(kBlock) void nn_grid_iter_kernel(
     int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
@@ -813,8 +814,8 @@ __global__ __launch_bounds__(kBlock) void nn_grid_iter_kernel(
             tclk = now;
         }
     };
-    __shared__ float4 s_pts[kBlock / 64][kIterPts];
-    __shared__ int s_rbase[kBlock / 64][kIterRows + 1], s_rstart[kBlock / 64][kIterRows];
+    __shared__ float4 s_pts[kBlock / 64][STAGE ? kIterPts : 1];
+    __shared__ int s_rbase[kBlock / 64][STAGE ? kIterRows + 1 : 1], s_rstart[kBlock / 64][STAGE ? kIterRows : 1];
     // (st is uniform: its fields are scalar loads into SGPRs -- an LDS copy would hold the
     // transform's 15 doubles in VGPRs all kernel long)
     if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
@@ -861,19 +862,20 @@ __global__ __launch_bounds__(kBlock) void nn_grid_iter_kernel(
             lo3[a] = ok ? c0[a] : 0x7fffffff;
             hi3[a] = ok ? c1[a] : -1;
         }
+        if constexpr (STAGE)
 #pragma unroll
-        for (int o = 2; o < 64; o <<= 1) // (the two lanes of a query agree: start at 2)
+            for (int o = 2; o < 64; o <<= 1) // (the two lanes of a query agree: start at 2)
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                lo3[a] = min(lo3[a], __shfl_xor(lo3[a], o, 64));
-                hi3[a] = max(hi3[a], __shfl_xor(hi3[a], o, 64));
-            }
+                for (int a = 0; a < 3; ++a) {
+                    lo3[a] = min(lo3[a], __shfl_xor(lo3[a], o, 64));
+                    hi3[a] = max(hi3[a], __shfl_xor(hi3[a], o, 64));
+                }
         const bool anyok = __ballot(ok) != 0ull;
         const int ux = hi3[0] - lo3[0] + 1, uy = hi3[1] - lo3[1] + 1, uz = hi3[2] - lo3[2] + 1;
         const int nrows = anyok ? uy * uz : 0;
         bool staged = false;
         int total = 0;
-        if (anyok && nrows <= kIterRows) {
+        if (STAGE && anyok && nrows <= kIterRows) {
             // C: the union rows' runs (two rows a lane at most), their prefix, then the points
             int len[2] = {0, 0};
 #pragma unroll
@@ -994,16 +996,42 @@ __global__ __launch_bounds__(kBlock) void nn_grid_iter_kernel(
                     const int k0 = rbase[r], k1 = rbase[r + 1], p0 = rstart[r] - k0;
                     for (int k = k0; k < k1; ++k) test(lp[k], p0 + k);
                 }
-            } else {
-                for (int rq = sub; rq < nrq; rq += 2) {
-                    const int gy = c0[1] + rq % ny, gz = c0[2] + rq / ny;
-                    const int row = (gz * gv.g[1] + gy) * gv.g[0];
-                    const int a0 = gv.start[row + c0[0]], a1 = gv.start[row + c1[0] + 1];
-                    for (int k = a0; k < a1; k += 2) {
-                        const float4 m0 = gv.pts32[k];
-                        const float4 m1 = gv.pts32[k + 1 < a1 ? k + 1 : k];
-                        test(m0, k);
-                        if (k + 1 < a1) test(m1, k + 1);
+            } else { // nn_grid_seeded32_kernel's walk (2 lanes a query, 2 rows' bounds, 2 loads in flight)
+                constexpr int KR = 2, KU = 2;
+                for (int r0 = sub; r0 < nrq; r0 += KR * 2) {
+                    int k0[KR], pre[KR + 1];
+                    pre[0] = 0;
+#pragma unroll
+                    for (int v = 0; v < KR; ++v) {
+                        const int r = r0 + v * 2;
+                        int a0 = 0, a1 = 0;
+                        if (r < nrq) {
+                            const int gy = c0[1] + r % ny, gz = c0[2] + r / ny;
+                            const int row = (gz * gv.g[1] + gy) * gv.g[0];
+                            a0 = gv.start[row + c0[0]];
+                            a1 = gv.start[row + c1[0] + 1];
+                        }
+                        k0[v] = a0;
+                        pre[v + 1] = pre[v] + (a1 - a0);
+                    }
+                    const int tot = pre[KR];
+                    for (int f0 = 0; f0 < tot; f0 += KU) { // the lane's runs as one sequence
+                        int kk[KU];
+#pragma unroll
+                        for (int v = 0; v < KU; ++v) {
+                            const int f = f0 + v;
+                            int pp = k0[0] + f;
+#pragma unroll
+                            for (int w = 1; w < KR; ++w)
+                                if (f >= pre[w]) pp = k0[w] + (f - pre[w]);
+                            kk[v] = f < tot ? pp : -1;
+                        }
+                        float4 mm[KU];
+#pragma unroll
+                        for (int v = 0; v < KU; ++v) mm[v] = gv.pts32[kk[v] >= 0 ? kk[v] : 0];
+#pragma unroll
+                        for (int v = 0; v < KU; ++v)
+                            if (kk[v] >= 0) test(mm[v], kk[v]);
                     }
                 }
             }
@@ -1142,8 +1170,19 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
                          unsigned long long *dbg)
 {
     if (n <= 0) return;
-    nn_grid_iter_kernel<<<canon_rows((size_t)n), kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                                   budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+    // ICP_ITER_STAGE=1: the task's union of boxes staged in LDS (measured slower: the staging's two
+    // dependent round trips and the LDS-limited occupancy cost more than the gathers they save)
+    static const bool stage = [] {
+        const char *e = getenv("ICP_ITER_STAGE");
+        return e && atoi(e) == 1;
+    }();
+#define ITER(S)                                                                                                       \
+    nn_grid_iter_kernel<S><<<canon_rows((size_t)n), kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, \
+                                                                      box, budget, nm, m4, rows, far_acc, far_d2,       \
+                                                                      big_count, dbg)
+    if (stage) ITER(true);
+    else ITER(false);
+#undef ITER
 }
 
 namespace {

@@ -58,7 +58,7 @@ EXPORTED = [
     "icp_ctx_create", "icp_ctx_create_dist", "icp_rccl_unique_id", "icp_ctx_create_sharded",
     "icp_ctx_destroy",
     "icp_last_error", "icp_strerror", "icp_device_count", "icp_set_model", "icp_set_scene",
-    "icp_set_model_device", "icp_set_scene_device",
+    "icp_set_model_device", "icp_set_scene_device", "icp_set_progress",
     "icp_get_scene", "icp_set_allow_unequal", "icp_set_nn_variant", "icp_run", "icp_closest_matrix",
     "icp_compute_centroid", "icp_y_p_norm", "icp_err_compute", "icp_find_alignment",
     "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
@@ -104,6 +104,7 @@ FILTER_NAMES = {-1: None, 0: "valu", 1: "mfma", 2: "mfma16", 3: "bundle", 4: "gr
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_void_p)
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_int, C.c_double, C.c_void_p)
 
 _lib = None
 
@@ -132,6 +133,7 @@ def lib() -> C.CDLL:
     L.icp_device_count.argtypes = [C.POINTER(C.c_int)]
     L.icp_set_model.argtypes = [vp, dp, sz]
     L.icp_set_model_device.argtypes = [vp, vp, sz]
+    L.icp_set_progress.argtypes = [vp, PROGRESS_FN, vp]
     L.icp_set_scene_device.argtypes = [vp, vp, sz, sz]
     L.icp_set_scene.argtypes = [vp, dp, sz, sz]
     L.icp_get_scene.argtypes = [vp, dp]
@@ -332,6 +334,12 @@ class Context:
         self._check(lib().icp_set_scene_device(self._h, C.c_void_p(ptr), np_local,
                                                np_local if np_total is None else np_total))
         self._np_local = np_local
+
+    def set_progress(self, fn):
+        """icp_set_progress: fn(iteration, err) for each recorded iteration of icp_run, as it ends
+        (None switches it off).  The ctypes thunk is kept alive with the context."""
+        self._progress = PROGRESS_FN(lambda i, e, _u: fn(i, e)) if fn is not None else None
+        self._check(lib().icp_set_progress(self._h, self._progress if fn is not None else PROGRESS_FN(), None))
 
     def ensure_model(self, m) -> bool:
         """icp_ensure_model: upload unless the resident model has these exact contents."""

@@ -199,3 +199,28 @@ def test_kd_host_models_of_different_sizes(amd):
     r = subprocess.run([sys.executable, "-c", KD_HOST_SCRIPT, os.path.join(ROOT, "iterative-closest-point_amd"),
                         os.path.join(ROOT, "oracle")], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0 and "kd_host ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("case", ["slot_order", "one_launch"])
+def test_progress_callback_streams_each_iteration(amd, case):
+    """icp_set_progress (the reference prints each iteration's error as it ends, gpu.cc:65,77):
+    one call per recorded iteration, in order, with the trace's values -- on the launch loop
+    (a slot-order scene, its errors reported while the run waits) and on the one-launch path."""
+    if case == "slot_order":
+        m, p = amd.synthetic_pair(1 << 16, seed=9)
+        iters, thr = 7, -1.0
+    else:
+        import datasets
+        m = amd.load_matrix(datasets.path("cow_ref"))
+        p = amd.load_matrix(datasets.path("cow_tr1"))
+        iters, thr = 20, 1e-5
+    seen = []
+    with amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        ctx.set_progress(lambda i, e: seen.append((i, e)))
+        res, errs = ctx.run(iters, thr)
+        ctx.set_progress(None)
+        ctx.run(1, -1.0)  # (off: nothing more)
+    assert [i for i, _ in seen] == list(range(res.iterations))
+    assert np.array_equal(np.array([e for _, e in seen]), errs)
