@@ -2352,7 +2352,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // until its first iteration completes: the host waits for it before enqueuing the second, so
     // that the second search's path is decided on a count (a blind grid search right after the
     // first alignment scans boxes as big as the first transform's moves)
-    const bool hold_first = grid_policy && !carry && ctx->bundle_pending;
+    // (only a shard against a model of at least twice its points, whose first transform leaves more
+    // than n/32 points far -- C5's shards: 40,739 of 2^20 by a CPU model; a scene of
+    // the model's size goes straight on to the grid -- C4: 107 big boxes, searched in the fused
+    // kernel -- without the synchronisation)
+    const bool hold_first = grid_policy && !carry && ctx->bundle_pending && ctx->nm >= 2 * n;
     // A scene in slot order (C4, C5, their shards): the canonical schedule (icp_canon.h).  The
     // transform of iteration k - 1 is enqueued at the start of iteration k, right before its
     // search, in the form that search reads; its residual and k's moments go to the canonical

@@ -797,8 +797,11 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
 #define ICP_ITER_KCAND 2 // (candidate records a lane loads together)
 #endif
 constexpr int kIterRows = 128, kIterPts = 512;
+#ifndef ICP_ITER_WAVES
+#define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
+#endif
 template <bool STAGE>
-__global__ __launch_bounds__(kBlock) void nn_grid_iter_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER_WAVES))) void nn_grid_iter_kernel(
     int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
     float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
