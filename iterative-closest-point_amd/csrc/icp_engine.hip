@@ -200,6 +200,8 @@ struct icp_ctx {
     double4 *g_pts = nullptr;
     float4 *g_pts32 = nullptr; // (the fp32 image of g_pts: the seeded grid search's prefilter)
     size_t g_pts32_cap = 0;
+    int *g_rep = nullptr; // each empty cell's stand-in seed (launch_grid_rep): unseeded searches
+    size_t g_rep_cap = 0;
     size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
@@ -786,6 +788,30 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     return ICP_OK;
 }
 
+// An unseeded search of a scene in slot order takes the seeded grid pass from cell seeds
+// (launch_nn_grid_cell_seed: the first minimum over the query's own cell, or the empty cell's
+// stand-in) instead of the ring search (nn_grid_search_kernel: rings of cells until one holds a
+// point, then the complete box).  Both end in the exact first minimum over a complete box; the
+// seeded pass is the tuned one (its lanes, loads in flight, y written for the moments).
+// ICP_CELL_SEED=0: the ring search (A/B).
+static bool cell_seed_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("ICP_CELL_SEED");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+static int grid_unseeded_slot(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop, hipEvent_t ev1)
+{
+    TRY(grow(ctx, &ctx->b_seedd, &ctx->b_seedd_cap, n));
+    launch_nn_grid_cell_seed((int)n, q.x, q.y, q.z, grid_view(ctx), ctx->g_rep, ctx->m4, ctx->idx, ctx->b_seedd,
+                             ctx->st);
+    LAUNCHCHK("nn_grid_cell_seed");
+    return grid_seeded_search(ctx, q, n, stop, ctx->b_seedd, ev1);
+}
+
 // What icp_run's last enqueued transform wrote for the next search (transform_err_kernel, SeedArgs).
 // The next search may use each output only in the form it was written in: the bundle filter's
 // slot records exist in a global and a local pair-test form (local_r, icp_bundle_rec.h), and
@@ -849,6 +875,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
         TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
         TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
         if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
+        if (!seeded && slot_order && cell_seed_on()) return grid_unseeded_slot(ctx, q, n, stop, ev1);
         if (seeded) // (icp_run: the previous correspondence is each query's candidate; no ring search)
             launch_nn_grid_resolve_all((int)n, q.x, q.y, q.z, ctx->m4, grid_view(ctx), grid_budget(ctx), ctx->idx,
                                        ctx->amb_count + 1, ctx->fb_list, ctx->fb_T, ctx->st, stop, 0,
@@ -880,6 +907,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             TRY(grow(ctx, &ctx->fb_list, &ctx->fb_list_cap, n));
             TRY(grow(ctx, &ctx->fb_T, &ctx->fb_T_cap, n));
             if (ev0) HIPCHK(hipEventRecord(ev0, ctx->st));
+            if (cell_seed_on()) return grid_unseeded_slot(ctx, q, n, stop, ev1);
             launch_nn_grid_search((int)n, q.x, q.y, q.z, grid_view(ctx), grid_budget(ctx), ctx->idx, ctx->amb_count + 1,
                                   ctx->fb_list, ctx->fb_T, ctx->st);
             if (ev1) HIPCHK(hipEventRecord(ev1, ctx->st));
@@ -1435,7 +1463,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials, (void *)ctx->err_part,
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
-                    (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts, (void *)ctx->g_pts32,
+                    (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts, (void *)ctx->g_pts32, (void *)ctx->g_rep,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest, (void *)ctx->fold_ticket,
@@ -1593,6 +1621,8 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     TRY(grow(ctx, &ctx->g_pts32, &ctx->g_pts32_cap, nm));
     launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_cid, ctx->g_count,
                       ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->g_pts32, ctx->st);
+    TRY(grow(ctx, &ctx->g_rep, &ctx->g_rep_cap, (size_t)ncell));
+    launch_grid_rep(grid_view(ctx), ncell, ctx->g_rep, ctx->st);
     LAUNCHCHK("grid_build");
     for (int k = 0; k < 3; ++k) { // the model's box (the query orders: mid-size loop, bundle filter)
         ctx->m_lo[k] = lo[k];
@@ -1644,6 +1674,18 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     ctx->has_model = true;
     ctx->seeds_valid = false;
     ctx->seedd_valid = false;
+    // a scene in slot order (the last model's box) goes back to file order: icp_run sorts it by
+    // the new box from there, as after set_model then set_scene -- the same order, hence the same
+    // reductions, whichever call came first
+    if (ctx->has_scene && ctx->scene.n && ctx->scene_slot) {
+        DevCloud &P = ctx->scene;
+        TRY(grow_cloud(ctx, ctx->s_tmp, P.n, true));
+        launch_permute_cloud(ctx->s_order, (int)P.n, 1, P.x, P.y, P.z, nullptr, nullptr, ctx->s_tmp.x, ctx->s_tmp.y,
+                             ctx->s_tmp.z, nullptr, nullptr, ctx->st);
+        LAUNCHCHK("scene_to_file_order");
+        std::swap(ctx->scene, ctx->s_tmp);
+        ctx->scene_slot = false;
+    }
     // the scene's fp32 copy depends on c: refresh it
     if (ctx->has_scene && ctx->scene.n) {
         launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1],
@@ -1716,7 +1758,34 @@ int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded
     return ICP_OK;
 }
 
-static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total);
+static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total, bool slot);
+
+// The scene's resident copies from its AoS array in device memory (the caller's, or the staged
+// upload).  A scene icp_run keeps in slot order (want_slot_order, against the current model) is
+// sorted here and gathered straight from the AoS array into the SoA fp64 streams and the fp32
+// copy -- one 24-byte read a point, where the run's scene_to_slot_order moves the four SoA
+// streams at random (a cache line each: 76 us at C4, profiles/r05h); the order is the same
+// (stable sort of the same keys from file order).  Returns whether the scene is in slot order.
+static int scene_from_aos(icp_ctx *ctx, const double *aos, size_t n, bool *slot)
+{
+    *slot = false;
+    if (!n) return ICP_OK;
+    DevCloud &P = ctx->scene;
+    if (ctx->has_model && want_slot_order(ctx, n)) {
+        TRY(grow(ctx, &ctx->s_order, &ctx->s_order_cap, n));
+        const size_t bytes = query_order_scratch_bytes((int)n);
+        TRY(grow(ctx, &ctx->q_order_tmp, &ctx->q_order_tmp_cap, bytes));
+        if (launch_slot_order_aos(aos, (int)n, ctx->m_lo, ctx->m_hi, ctx->q_order_tmp, bytes, ctx->s_order, ctx->c,
+                                  P.x, P.y, P.z, P.f, ctx->st) != 0)
+            return fail(ctx, ICP_E_HIP, "scene order: radix sort failed");
+        LAUNCHCHK("scene_slot_order_aos");
+        *slot = true;
+        return ICP_OK;
+    }
+    launch_aos_to_soa_f32(aos, n, P.x, P.y, P.z, ctx->c, P.f, ctx->st);
+    LAUNCHCHK("scene_from_aos");
+    return ICP_OK;
+}
 
 int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_total)
 {
@@ -1725,11 +1794,18 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     HIPCHK(hipSetDevice(ctx->device));
     TRY(ensure_reduction_space(ctx));
     TRY(grow_cloud(ctx, ctx->Y, np_local, false));
-    TRY(upload_cloud(ctx, ctx->scene, p_xyz, np_local, true));
-    // a small cloud went through the mapped staging buffer (host-copied: the caller's array is
-    // free again), a large one through a pageable copy; either way the stream orders the rest
-    if (3 * np_local > kMappedIo) HIPCHK(hipStreamSynchronize(ctx->st));
-    return set_scene_common(ctx, np_local, np_total);
+    bool slot = false;
+    if (3 * np_local <= kMappedIo) { // small: through the mapped staging buffer (host-copied: the
+        // caller's array is free again when this returns)
+        TRY(upload_cloud(ctx, ctx->scene, p_xyz, np_local, true));
+    } else { // large: a pageable copy into the stage, then as icp_set_scene_device
+        TRY(grow_cloud(ctx, ctx->scene, np_local, true));
+        TRY(grow(ctx, &ctx->stage, &ctx->stage_cap, 3 * np_local));
+        HIPCHK(hipMemcpyAsync(ctx->stage, p_xyz, sizeof(double) * 3 * np_local, hipMemcpyHostToDevice, ctx->st));
+        TRY(scene_from_aos(ctx, ctx->stage, np_local, &slot));
+        HIPCHK(hipStreamSynchronize(ctx->st));
+    }
+    return set_scene_common(ctx, np_local, np_total, slot);
 }
 
 int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total)
@@ -1740,23 +1816,21 @@ int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local,
     TRY(ensure_reduction_space(ctx));
     TRY(grow_cloud(ctx, ctx->Y, np_local, false));
     TRY(grow_cloud(ctx, ctx->scene, np_local, true));
-    if (np_local) { // (the caller's device array: converted on the stream, no copy)
-        launch_aos_to_soa(p_xyz_dev, np_local, ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->st);
-        launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, np_local, ctx->c[0], ctx->c[1], ctx->c[2],
-                        ctx->scene.f, ctx->st);
-        LAUNCHCHK("set_scene_device");
-    }
-    return set_scene_common(ctx, np_local, np_total);
+    bool slot = false;
+    TRY(scene_from_aos(ctx, p_xyz_dev, np_local, &slot)); // (the caller's array: no copy)
+    // the caller's array is read on the context's stream: done before the call returns
+    if (np_local) HIPCHK(hipStreamSynchronize(ctx->st));
+    return set_scene_common(ctx, np_local, np_total, slot);
 }
 
-static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total)
+static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total, bool slot)
 {
     ctx->np_total = np_total;
     ctx->has_scene = true;
     ctx->seeds_valid = false;
     ctx->seedd_valid = false;
     ctx->q_order_src = nullptr; // new contents: a new query order
-    ctx->scene_slot = false;    // (in the caller's order)
+    ctx->scene_slot = slot;     // (else in the caller's order)
     ctx->p32_stale = false;
     // a shard against a model of at least twice its points (C5's 8-way shards: the model's cells
     // are finer than the scene's spacing): icp_run's policy takes the bundle cascade for the first

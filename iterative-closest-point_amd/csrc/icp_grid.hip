@@ -534,6 +534,77 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const doub
     }
 }
 
+// Each empty cell's stand-in seed (set_model, after the grid): the model point nearest the
+// cell's centre over the first ring of cells around it that holds any (rings up to 3), -1 if
+// none.  A cell that holds points needs none (rep = -1 too): nn_grid_cell_seed scans it.
+__global__ __launch_bounds__(kBlock) void grid_rep_kernel(GridView gv, int ncell, int *__restrict__ rep)
+{
+    const int id = blockIdx.x * kBlock + threadIdx.x;
+    if (id >= ncell) return;
+    int r_out = -1;
+    if (gv.start[id] == gv.start[id + 1]) {
+        const int cx = id % gv.g[0], cy = (id / gv.g[0]) % gv.g[1], cz = id / (gv.g[0] * gv.g[1]);
+        const double h = 1.0 / gv.inv_h;
+        const double ctr[3] = {gv.lo[0] + (cx + 0.5) * h, gv.lo[1] + (cy + 0.5) * h, gv.lo[2] + (cz + 0.5) * h};
+        double best = INFINITY;
+        for (int r = 1; r <= 3 && r_out < 0; ++r) {
+            for (int z = max(cz - r, 0); z <= min(cz + r, gv.g[2] - 1); ++z)
+                for (int y = max(cy - r, 0); y <= min(cy + r, gv.g[1] - 1); ++y) {
+                    const int row = (z * gv.g[1] + y) * gv.g[0];
+                    const int a = gv.start[row + max(cx - r, 0)], b = gv.start[row + min(cx + r, gv.g[0] - 1) + 1];
+                    for (int k = a; k < b; ++k) {
+                        const double4 m = gv.pts[k];
+                        const double d = d64g(ctr[0], ctr[1], ctr[2], m.x, m.y, m.z);
+                        const int mi = (int)m.w;
+                        if (d < best || (d == best && mi < r_out)) {
+                            best = d;
+                            r_out = mi;
+                        }
+                    }
+                }
+        }
+    }
+    rep[id] = r_out;
+}
+
+// An unseeded search's seeds, one lane per query: the (D64, index) first minimum over the points
+// of the query's own cell, or the cell's stand-in (grid_rep_kernel) when it is empty -- any model
+// point bounds a complete box; a near one keeps the box small.  seedd[t] = D64(q, m[idx[t]]) with
+// d64g on the same values the seeded scan reads, so the scan meets the seed with d == best.
+__global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const double *__restrict__ px,
+                                                                  const double *__restrict__ py,
+                                                                  const double *__restrict__ pz, GridView gv,
+                                                                  const int *__restrict__ rep,
+                                                                  const double4 *__restrict__ m4,
+                                                                  int *__restrict__ idx, double *__restrict__ seedd)
+{
+    const int t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= n) return;
+    const double q[3] = {px[t], py[t], pz[t]};
+    const int c = (cell1(q[2], gv.lo[2], gv.inv_h, gv.g[2]) * gv.g[1] + cell1(q[1], gv.lo[1], gv.inv_h, gv.g[1])) *
+                      gv.g[0] +
+                  cell1(q[0], gv.lo[0], gv.inv_h, gv.g[0]);
+    const int a = gv.start[c], b = gv.start[c + 1];
+    double best = INFINITY;
+    int bi = -1;
+    for (int k = a; k < b; ++k) {
+        const double4 m = gv.pts[k];
+        const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
+        const int mi = (int)m.w;
+        if (d < best || (d == best && mi < bi)) {
+            best = d;
+            bi = mi;
+        }
+    }
+    if (bi < 0) { // (an empty cell: its stand-in, else point 0)
+        bi = max(rep[c], 0);
+        const double4 m = m4[bi];
+        best = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
+    }
+    idx[t] = bi;
+    seedd[t] = best;
+}
+
 // (D64, index) first minimum that also carries the winner's position k in pts.  The seed enters
 // as (best, bi) with no position; the scan meets the seed point itself (it lies in its own box)
 // and then takes its position (the equal-index case), so a scanned winner always has one.
@@ -874,7 +945,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                     hi3[a] = max(hi3[a], __shfl_xor(hi3[a], o, 64));
                 }
         const bool anyok = __ballot(ok) != 0ull;
-        const int ux = hi3[0] - lo3[0] + 1, uy = hi3[1] - lo3[1] + 1, uz = hi3[2] - lo3[2] + 1;
+        const int uy = hi3[1] - lo3[1] + 1, uz = hi3[2] - lo3[2] + 1;
         const int nrows = anyok ? uy * uz : 0;
         bool staged = false;
         int total = 0;
@@ -1302,6 +1373,19 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
         else SEARCH(16, false);
     }
 #undef SEARCH
+}
+
+void launch_grid_rep(const GridView &gv, long long ncell, int *rep, hipStream_t st)
+{
+    if (ncell <= 0) return;
+    grid_rep_kernel<<<(int)((ncell + kBlock - 1) / kBlock), kBlock, 0, st>>>(gv, (int)ncell, rep);
+}
+
+void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv,
+                              const int *rep, const double4 *m4, int *idx, double *seedd, hipStream_t st)
+{
+    if (n <= 0) return;
+    nn_grid_cell_seed_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, px, py, pz, gv, rep, m4, idx, seedd);
 }
 
 void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,

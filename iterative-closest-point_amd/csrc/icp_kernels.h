@@ -248,6 +248,11 @@ size_t query_order_scratch_bytes(int n);
 int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
                        const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st,
                        int *pos = nullptr);
+// the same order of an AoS cloud (3 x n col-major) and, in that order, its SoA fp64 streams
+// x, y, z and centred fp32 copy f (point s = aos point order[s]); scratch as above
+int launch_slot_order_aos(const double *aos, int n, const double lo[3], const double hi[3], void *scratch,
+                          size_t bytes, int *order, const double c[3], double *x, double *y, double *z, float4 *f,
+                          hipStream_t st);
 // the resident scene into (inverse = 0: dst[s] = src[order[s]]) or out of (inverse = 1:
 // dst[order[s]] = src[s]) a query order; a stream (xyz, fp32 copy, indices) moves when both its
 // pointers are non-null
@@ -305,6 +310,13 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
 // index): seeds for an unseeded f16 brute-force search
 void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,
                          int nm, int *idx, hipStream_t st);
+// rep[ncell]: each empty cell's stand-in seed (the model point nearest its centre in the first
+// ring of cells that holds any, up to 3 rings; else -1), -1 for a cell with points
+void launch_grid_rep(const GridView &gv, long long ncell, int *rep, hipStream_t st);
+// an unseeded search's seeds: idx[t] = the first minimum over query t's own cell (or its
+// stand-in), seedd[t] = its D64 -- the input of the seeded grid pass
+void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv,
+                              const int *rep, const double4 *m4, int *idx, double *seedd, hipStream_t st);
 // inline_nm > 0 (a model of that many points): queries the grid cannot take are scanned
 // exactly in place (no fallback queue, no nn_resolve launch)
 // seeded grid variant: every query's previous correspondence (idx[t]) as the candidate, its

@@ -6,6 +6,7 @@
 // which queries share a batch; every result is the exact first minimum regardless.
 #include <hip/hip_runtime.h>
 #include <hipcub/device/device_radix_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "icp_kernels.h"
 
@@ -52,12 +53,8 @@ __global__ __launch_bounds__(kBlock) void order_pos_kernel(const int *__restrict
 constexpr int kOrderBits = 15;
 
 // 10 bits per axis (1024^3 cells) -> 30-bit Morton key
-__global__ __launch_bounds__(kBlock) void query_keys_kernel(const double *__restrict__ px, const double *__restrict__ py,
-                                                          const double *__restrict__ pz, int n, OrderBox bx,
-                                                          unsigned *__restrict__ key, int *__restrict__ val)
+__device__ __forceinline__ unsigned morton30(double x, double y, double z, const OrderBox &bx)
 {
-    const int q = blockIdx.x * kBlock + threadIdx.x;
-    if (q >= n) return;
     auto cell = [](double v, double l, double s) {
         const double t = (v - l) * s;
         return !(t > 0.0) ? 0u : t >= 1023.0 ? 1023u : (unsigned)t;
@@ -69,9 +66,47 @@ __global__ __launch_bounds__(kBlock) void query_keys_kernel(const double *__rest
         v = (v | (v << 2)) & 0x09249249u;
         return v;
     };
-    key[q] = spread(cell(px[q], bx.lo[0], bx.sc[0])) | (spread(cell(py[q], bx.lo[1], bx.sc[1])) << 1) |
-             (spread(cell(pz[q], bx.lo[2], bx.sc[2])) << 2);
+    return spread(cell(x, bx.lo[0], bx.sc[0])) | (spread(cell(y, bx.lo[1], bx.sc[1])) << 1) |
+           (spread(cell(z, bx.lo[2], bx.sc[2])) << 2);
+}
+
+__global__ __launch_bounds__(kBlock) void query_keys_kernel(const double *__restrict__ px, const double *__restrict__ py,
+                                                          const double *__restrict__ pz, int n, OrderBox bx,
+                                                          unsigned *__restrict__ key, int *__restrict__ val)
+{
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= n) return;
+    key[q] = morton30(px[q], py[q], pz[q], bx);
     val[q] = q;
+}
+
+// the same keys from an AoS cloud (3 x n col-major: point q at aos[3q .. 3q+2])
+__global__ __launch_bounds__(kBlock) void query_keys_aos_kernel(const double *__restrict__ aos, int n, OrderBox bx,
+                                                              unsigned *__restrict__ key, int *__restrict__ val)
+{
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= n) return;
+    const double *p = aos + 3 * (size_t)q;
+    key[q] = morton30(p[0], p[1], p[2], bx);
+    val[q] = q;
+}
+
+// The slot-ordered scene straight from the AoS cloud: point s of the SoA fp64 streams and of the
+// centred fp32 copy is aos point order[s] -- one 24-byte read a point (permute_cloud_kernel moves
+// the four SoA streams at random: a cache line each)
+__global__ __launch_bounds__(kBlock) void gather_aos_kernel(const int *__restrict__ order, int n,
+                                                          const double *__restrict__ aos, double cx, double cy,
+                                                          double cz, double *__restrict__ x, double *__restrict__ y,
+                                                          double *__restrict__ z, float4 *__restrict__ f)
+{
+    const int s = blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n) return;
+    const double *p = aos + 3 * (size_t)order[s];
+    const double a = p[0], b = p[1], c = p[2];
+    x[s] = a;
+    y[s] = b;
+    z[s] = c;
+    f[s] = make_float4((float)(a - cx), (float)(b - cy), (float)(c - cz), 0.0f);
 }
 
 constexpr int kQueryOrderBits = 30;
@@ -107,30 +142,72 @@ void launch_permute_cloud(const int *order, int n, int inverse, const double *sx
                                                                         dy, dz, df, didx);
 }
 
+// The query orders' sort: stable LSD radix sort of (key, index) pairs.  rocprim's default sends
+// n <= 2^20 -- a whole C4 scene -- to its merge sort (a block sort and 10 merge passes: 173 us for
+// 2^20 pairs, profiles/r05h); a merge-sort limit of 0 takes onesweep's digit passes at every size
+// above one block.  Both are stable: the same order either way.
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+
+static hipError_t sort_pairs(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
+                             int n, int bits, hipStream_t st)
+{
+    return rocprim::radix_sort_pairs<OnesweepSort>(temp, temp_bytes, k0, k1, v0, v1, (size_t)n, 0u, (unsigned)bits, st,
+                                                   false);
+}
+
+// the sort's temporary storage starts on a 256-byte boundary after the three n-int arrays
+// (onesweep's 64-bit look-back atomics fault on a 4-byte-aligned address: n odd)
+static size_t keys_bytes(int n, int arrays)
+{
+    return ((size_t)arrays * (size_t)n * sizeof(int) + 255) & ~(size_t)255;
+}
+
 size_t query_order_scratch_bytes(int n)
 {
     size_t temp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned *)nullptr, (unsigned *)nullptr,
-                                             (const int *)nullptr, (int *)nullptr, n, 0, kQueryOrderBits);
-    return 3 * (size_t)n * sizeof(int) + ((temp + 255) & ~(size_t)255);
+    (void)sort_pairs(nullptr, temp, nullptr, nullptr, nullptr, nullptr, n, kQueryOrderBits, nullptr);
+    return keys_bytes(n, 3) + ((temp + 255) & ~(size_t)255);
 }
 
-int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
-                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st, int *pos)
+static OrderBox query_box(const double lo[3], const double hi[3])
 {
     OrderBox bx;
     for (int k = 0; k < 3; ++k) {
         bx.lo[k] = lo[k];
         bx.sc[k] = hi[k] > lo[k] ? 1024.0 / (hi[k] - lo[k]) : 0.0;
     }
+    return bx;
+}
+
+int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
+                       const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st, int *pos)
+{
+    const OrderBox bx = query_box(lo, hi);
     unsigned *k0 = (unsigned *)scratch, *k1 = k0 + n;
     int *v0 = (int *)(k1 + n);
-    void *temp = v0 + n;
-    size_t temp_bytes = bytes - 3 * (size_t)n * sizeof(int);
+    void *temp = (char *)scratch + keys_bytes(n, 3);
+    size_t temp_bytes = bytes - keys_bytes(n, 3);
     query_keys_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(px, py, pz, n, bx, k0, v0);
-    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, order, n, 0, kQueryOrderBits, st) != hipSuccess)
-        return -1;
+    if (sort_pairs(temp, temp_bytes, k0, k1, v0, order, n, kQueryOrderBits, st) != hipSuccess) return -1;
     if (pos) order_pos_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(order, n, pos);
+    return 0;
+}
+
+int launch_slot_order_aos(const double *aos, int n, const double lo[3], const double hi[3], void *scratch,
+                          size_t bytes, int *order, const double c[3], double *x, double *y, double *z, float4 *f,
+                          hipStream_t st)
+{
+    if (n <= 0) return 0;
+    const OrderBox bx = query_box(lo, hi);
+    unsigned *k0 = (unsigned *)scratch, *k1 = k0 + n;
+    int *v0 = (int *)(k1 + n);
+    void *temp = (char *)scratch + keys_bytes(n, 3);
+    size_t temp_bytes = bytes - keys_bytes(n, 3);
+    const int g = (n + kBlock - 1) / kBlock;
+    query_keys_aos_kernel<<<g, kBlock, 0, st>>>(aos, n, bx, k0, v0);
+    if (sort_pairs(temp, temp_bytes, k0, k1, v0, order, n, kQueryOrderBits, st) != hipSuccess) return -1;
+    gather_aos_kernel<<<g, kBlock, 0, st>>>(order, n, aos, c[0], c[1], c[2], x, y, z, f);
     return 0;
 }
 
@@ -139,7 +216,7 @@ size_t mid_order_scratch_bytes(int n)
     size_t temp = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned *)nullptr, (unsigned *)nullptr,
                                              (const int *)nullptr, (int *)nullptr, n, 0, kOrderBits);
-    return 4 * (size_t)n * sizeof(int) + ((temp + 255) & ~(size_t)255);
+    return keys_bytes(n, 4) + ((temp + 255) & ~(size_t)255);
 }
 
 int launch_mid_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
@@ -152,8 +229,8 @@ int launch_mid_order(const double *px, const double *py, const double *pz, int n
     }
     unsigned *k0 = (unsigned *)scratch, *k1 = k0 + n;
     int *v0 = (int *)(k1 + n), *v1 = v0 + n;
-    void *temp = v1 + n;
-    size_t temp_bytes = bytes - 4 * (size_t)n * sizeof(int);
+    void *temp = (char *)scratch + keys_bytes(n, 4);
+    size_t temp_bytes = bytes - keys_bytes(n, 4);
     const int g = (n + kBlock - 1) / kBlock;
     order_keys_kernel<<<g, kBlock, 0, st>>>(px, py, pz, n, bx, k0, v0);
     if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, v1, n, 0, kOrderBits, st) != hipSuccess)
