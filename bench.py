@@ -51,6 +51,13 @@ import icp_amd  # noqa: E402
 import roofline as RF  # noqa: E402
 
 GRID_SEEDED_KERNEL = "nn_grid_seeded_kernel"  # (tools/roofline.py GRID_KERNELS: its algorithmic bytes)
+# the fused grid iteration (transform + seeded search + moments, one launch per seeded iteration:
+# icp_run's canonical schedule); ICP_GRID_ITER=0 runs the separate kernels
+GRID_ITER_KERNEL = "nn_grid_iter_kernel"
+
+
+def grid_kernel():
+    return GRID_SEEDED_KERNEL if os.environ.get("ICP_GRID_ITER") == "0" else GRID_ITER_KERNEL
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32 MFMA peak
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
@@ -237,22 +244,26 @@ def bundle_roofline(n_local, n_model, t_kernel, work, v1=False):
 
 
 def grid_roofline(n_local, n_model, avg_ms, traffic, traffic_src, explicit_variant):
-    """The seeded grid search's pass over every query (nn_grid_seeded_kernel: the dominant kernel
-    of an AUTO iteration once icp_run's policy takes the grid) against HBM.  Algorithmic bytes per
-    launch: per query its fp64 position (24 B), seed distance (8 B), index in and out (8 B) and
-    its correspondence's fp64 coordinates out (24 B); per model point its 32-byte grid record and
-    ~2 B of the cell table, each once."""
-    bq, bm = RF.GRID_KERNELS[GRID_SEEDED_KERNEL]
+    """The grid iteration's dominant kernel (nn_grid_iter_kernel: the pending transform, the seeded
+    search of every query and the moments' leaves in one launch; nn_grid_seeded_kernel with
+    ICP_GRID_ITER=0) against HBM.  Algorithmic bytes per launch (tools/roofline.py GRID_KERNELS):
+    fused -- per query its fp64 position in and out (48 B), previous and new correspondence (48 B),
+    index in and out (8 B) and the winner's 32-byte grid record; per model point its 16-byte fp32
+    grid record and ~2 B of the cell table, once.  Seeded alone -- 64 B per query, 34 B per model
+    point."""
+    kern = grid_kernel()
+    bq, bm = RF.GRID_KERNELS[kern]
     gbytes = bq * n_local + bm * n_model
     t = avg_ms * 1e-3
     ach = gbytes / t / 1e9 if t > 0 else 0.0
-    return {"bound": "hbm", "kernel": f"{GRID_SEEDED_KERNEL} (seeded, every query)",
+    what = ("fused grid iteration: transform + seeded search + moments, every query" if kern == GRID_ITER_KERNEL
+            else "seeded, every query")
+    return {"bound": "hbm", "kernel": f"{kern} ({what})",
             "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
             "traffic": traffic, "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src, "avg_launch_ms": avg_ms, "bytes_per_launch": gbytes,
-            "bytes_definition": f"algorithmic: {bq:.0f} B per query (fp64 xyz, seed distance, index in/out, "
-                                f"correspondence xyz out) + {bm:.0f} B per model point (32-byte grid record + "
-                                "cell table), once",
+            "bytes_definition": f"algorithmic: {bq:.0f} B per query + {bm:.0f} B per model point, once "
+                                "(tools/roofline.py GRID_KERNELS)",
             "path": "ICP_NN_VARIANT_GRID" if explicit_variant else
                     "AUTO: icp_run's policy (seeded iterations once the scene is near the model)",
             "note": "latency-bound gather: each query walks the grid rows of its box (dependent loads)"}
@@ -348,9 +359,9 @@ def grid_nn_rate(device, m, p, steps, warmup=3):
         st = ctx.stats()
     return {"iterations_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps,
             "nn_kernel_ms": st["nn_ms"] / max(st["nn_launches"], 1), "brute_force_fallbacks": st["grid_fallback"],
-            "final_err": float(errs[-1]), "kernel": f"{GRID_SEEDED_KERNEL} (seeded, every query)",
+            "final_err": float(errs[-1]), "kernel": grid_kernel(),
             "roofline": grid_roofline(p.shape[0], m.shape[0], st["nn_ms"] / max(st["nn_launches"], 1),
-                                      *pmc_traffic(GRID_SEEDED_KERNEL), True)}
+                                      *pmc_traffic(grid_kernel()), True)}
 
 
 def baseline_configs(device, reps=3):
@@ -633,7 +644,7 @@ def main():
         # timed iterations are seeded (warm-up leaves every query a correspondence): the seeded
         # resolve (launch_nn_grid_resolve_all) scans each query's complete candidate box; AUTO
         # takes it by icp_run's policy once the scene is near the model
-        kernel = GRID_SEEDED_KERNEL
+        kernel = grid_kernel()
     # the capture of this workload's kernels: C4 on one GPU, or rank 0's shard of the 8-way C5
     traffic_cfg = {(1 << 20, 1): "", (1 << 23, 8): "c5shard"}.get((args.n, world))
     traffic, traffic_src = pmc_traffic(kernel, traffic_cfg) if traffic_cfg is not None else (None, None)
@@ -734,7 +745,8 @@ def main():
                 rf = {"error": str(e)}
             if rf and "kernels" in rf:
                 keep = ("shifted_moments_kernel", "gather_moments_kernel", "centred_moments_kernel",
-                        "transform_err_kernel")
+                        "transform_err_kernel", "canon_moments_kernel", "canon_transform_kernel",
+                        "gather_aos_kernel")
                 out["streaming"] = {"source": f"profiles/{rf['tag']}_bench_kernel_stats.csv + "
                                               f"profiles/{rf['tag']}_pmc_traffic.json (tools/roofline.py)",
                                     "kernels": {k: v for k, v in rf["kernels"].items() if k in keep}}

@@ -196,13 +196,15 @@ struct icp_ctx {
     size_t amb_cap = 0;
     // exact grid resolver (icp_grid.hip): model grid + the queues around it
     GridParams grid{};
-    int *g_cid = nullptr, *g_count = nullptr, *g_start = nullptr, *g_bsum = nullptr, *g_fill = nullptr;
+    int *g_start = nullptr;
+    char *g_sort = nullptr; // the build's sort scratch (launch_grid_build)
+    size_t g_sort_cap = 0;
     double4 *g_pts = nullptr;
     float4 *g_pts32 = nullptr; // (the fp32 image of g_pts: the seeded grid search's prefilter)
     size_t g_pts32_cap = 0;
     int *g_rep = nullptr; // each empty cell's stand-in seed (launch_grid_rep): unseeded searches
     size_t g_rep_cap = 0;
-    size_t g_cid_cap = 0, g_count_cap = 0, g_start_cap = 0, g_bsum_cap = 0, g_fill_cap = 0, g_pts_cap = 0;
+    size_t g_start_cap = 0, g_pts_cap = 0;
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
     IterState *h_iter = nullptr;     // mapped host mirror of the last recorded iteration's state
@@ -1462,8 +1464,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->mms16, ctx->part2,
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials, (void *)ctx->err_part,
-                    (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_cid, (void *)ctx->g_count,
-                    (void *)ctx->g_start, (void *)ctx->g_bsum, (void *)ctx->g_fill, (void *)ctx->g_pts, (void *)ctx->g_pts32, (void *)ctx->g_rep,
+                    (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_sort,
+                    (void *)ctx->g_start, (void *)ctx->g_pts, (void *)ctx->g_pts32, (void *)ctx->g_rep,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest, (void *)ctx->fold_ticket,
@@ -1578,13 +1580,20 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
         lo[k] = ctx->h_mstat[3 + k];
         hi[k] = ctx->h_mstat[6 + k];
     }
-    // 2. the fp32 range around c (the certificate's rm) and the fp64 one (the f16 image's scale)
-    launch_model_range(aos, (int)nm, c, ctx->mstat_part, ctx->mstat_out, ctx->st);
-    LAUNCHCHK("model_range");
-    HIPCHK(hipMemcpyAsync(ctx->h_mstat, ctx->mstat_out, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
-    HIPCHK(hipStreamSynchronize(ctx->st));
-    if (ctx->h_mstat[2] != 0.0) return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
-    const double rm = ctx->h_mstat[0], rm64 = ctx->h_mstat[1];
+    // 2. the fp32 range around c (the certificate's rm: max |fl32(m - c)|) and the fp64 one (the
+    // f16 image's scale: max |m - c|), over every point and axis.  Both are monotone in each
+    // coordinate (one rounded subtraction, then a rounding to fp32), so their maxima are taken at
+    // the box's faces: lo and hi give exactly the values a pass over the points would (the pass
+    // and its synchronisation before round 5)
+    double rm = 0.0, rm64 = 0.0;
+    for (int k = 0; k < 3; ++k)
+        for (const double v : {lo[k], hi[k]}) {
+            const double d = v - c[k];
+            const float f = (float)d;
+            if (!std::isfinite(f)) return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
+            rm = std::max(rm, std::fabs((double)f));
+            rm64 = std::max(rm64, std::fabs(d));
+        }
     if (rm > 1e15) return fail(ctx, ICP_E_RANGE, "model coordinates exceed 1e15 around the centroid");
     ctx->has_model = false; // (until every image below is built)
     for (int k = 0; k < 3; ++k) ctx->c[k] = c[k];
@@ -1594,7 +1603,8 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     // [2^11, 2^12), the double4 rows, the grid
     const size_t nm_pad = (nm + kTile32 - 1) / kTile32 * kTile32;
     TRY(grow_cloud(ctx, ctx->model, nm, true));
-    launch_aos_to_soa(aos, nm, ctx->model.x, ctx->model.y, ctx->model.z, ctx->st);
+    TRY(grow(ctx, &ctx->m4, &ctx->m4_cap, nm));
+    launch_aos_to_soa4(aos, nm, ctx->model.x, ctx->model.y, ctx->model.z, ctx->m4, ctx->st);
     TRY(grow(ctx, &ctx->m32, &ctx->m32_cap, nm_pad));
     TRY(grow(ctx, &ctx->mperm, &ctx->mperm_cap, nm_pad));
     TRY(grow(ctx, &ctx->mm, &ctx->mm_cap, nm_pad));
@@ -1607,20 +1617,17 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, (int)nm_pad, ctx->c,
                           ctx->scale16, ctx->mimg16, ctx->mms16, ctx->st);
     LAUNCHCHK("build_mimage16");
-    TRY(grow(ctx, &ctx->m4, &ctx->m4_cap, nm));
-    launch_make_aos4(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->m4, ctx->st);
     // uniform grid over the fp64 model for the exact resolver (its box: step 1's)
     ctx->grid = grid_params_box(lo, hi, nm);
     const long long ncell = grid_cells(ctx->grid);
-    TRY(grow(ctx, &ctx->g_cid, &ctx->g_cid_cap, nm));
-    TRY(grow(ctx, &ctx->g_count, &ctx->g_count_cap, (size_t)ncell + 1));
     TRY(grow(ctx, &ctx->g_start, &ctx->g_start_cap, (size_t)ncell + 1));
-    TRY(grow(ctx, &ctx->g_bsum, &ctx->g_bsum_cap, grid_scan_blocks(ncell + 1)));
-    TRY(grow(ctx, &ctx->g_fill, &ctx->g_fill_cap, (size_t)ncell));
     TRY(grow(ctx, &ctx->g_pts, &ctx->g_pts_cap, nm));
     TRY(grow(ctx, &ctx->g_pts32, &ctx->g_pts32_cap, nm));
-    launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_cid, ctx->g_count,
-                      ctx->g_start, ctx->g_bsum, ctx->g_fill, ctx->g_pts, ctx->g_pts32, ctx->st);
+    const size_t gbytes = grid_build_scratch_bytes((int)nm, ncell);
+    TRY(grow(ctx, &ctx->g_sort, &ctx->g_sort_cap, gbytes));
+    if (launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_sort, gbytes,
+                          ctx->g_start, ctx->g_pts, ctx->g_pts32, ctx->st) != 0)
+        return fail(ctx, ICP_E_HIP, "grid build: radix sort failed");
     TRY(grow(ctx, &ctx->g_rep, &ctx->g_rep_cap, (size_t)ncell));
     launch_grid_rep(grid_view(ctx), ncell, ctx->g_rep, ctx->st);
     LAUNCHCHK("grid_build");

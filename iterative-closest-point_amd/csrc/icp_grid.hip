@@ -53,83 +53,51 @@ __device__ __forceinline__ int cell1(double x, double lo, double inv_h, int g)
     return cellt((x - lo) * inv_h, g);
 }
 
-__global__ __launch_bounds__(kBlock) void grid_count_kernel(
-    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
-    int nm, GridView gv, int *__restrict__ cid, int *__restrict__ count)
+// The grid build (launch_grid_build): every model point's cell id, a stable radix sort of
+// (cell, index) pairs, each cell's start by a binary search of the sorted ids, and the points
+// gathered in sorted order -- cells in id order, each cell's points in index order (the build
+// before round 5 placed them by atomics: ~100 us of device-scope atomics at C4, and an order that
+// changed from build to build).
+__global__ __launch_bounds__(kBlock) void grid_keys_kernel(const double *__restrict__ mx, const double *__restrict__ my,
+                                                         const double *__restrict__ mz, int nm, GridView gv,
+                                                         unsigned *__restrict__ key, int *__restrict__ val)
 {
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < nm; i += gridDim.x * kBlock) {
-        const int cx = cell1(mx[i], gv.lo[0], gv.inv_h, gv.g[0]);
-        const int cy = cell1(my[i], gv.lo[1], gv.inv_h, gv.g[1]);
-        const int cz = cell1(mz[i], gv.lo[2], gv.inv_h, gv.g[2]);
-        const int c = (cz * gv.g[1] + cy) * gv.g[0] + cx;
-        cid[i] = c;
-        atomicAdd(count + c, 1);
-    }
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nm) return;
+    const int cx = cell1(mx[i], gv.lo[0], gv.inv_h, gv.g[0]);
+    const int cy = cell1(my[i], gv.lo[1], gv.inv_h, gv.g[1]);
+    const int cz = cell1(mz[i], gv.lo[2], gv.inv_h, gv.g[2]);
+    key[i] = (unsigned)((cz * gv.g[1] + cy) * gv.g[0] + cx);
+    val[i] = i;
 }
 
-// exclusive scan, 4096 ints per block: local scan + block totals
-constexpr int kScanThreads = 1024, kScanPer = 4, kScanChunk = kScanThreads * kScanPer;
-
-__global__ __launch_bounds__(kScanThreads) void scan_local_kernel(const int *__restrict__ in, int n,
-                                                                  int *__restrict__ out,
-                                                                  int *__restrict__ bsum)
+// start[c] = the first sorted position whose cell id is >= c (c = 0 .. ncell: start[ncell] = nm)
+__global__ __launch_bounds__(kBlock) void grid_starts_kernel(const unsigned *__restrict__ skey, int nm, int ncell,
+                                                           int *__restrict__ start)
 {
-    __shared__ int sh[kScanThreads];
-    const int base = blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
-    int v[kScanPer], s = 0;
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        v[k] = base + k < n ? in[base + k] : 0;
-        s += v[k];
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    if (c > ncell) return;
+    int lo = 0, hi = nm;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (skey[mid] < (unsigned)c) lo = mid + 1;
+        else hi = mid;
     }
-    sh[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < kScanThreads; off <<= 1) { // Hillis-Steele inclusive scan
-        const int t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
-        __syncthreads();
-        sh[threadIdx.x] += t;
-        __syncthreads();
-    }
-    int run = sh[threadIdx.x] - s; // exclusive prefix of this thread within the block
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        if (base + k < n) out[base + k] = run;
-        run += v[k];
-    }
-    if (threadIdx.x == kScanThreads - 1) bsum[blockIdx.x] = sh[threadIdx.x];
+    start[c] = lo;
 }
 
-__global__ void scan_blocks_kernel(int *bsum, int nb) // one thread: nb <= a few thousand
+__global__ __launch_bounds__(kBlock) void grid_gather_kernel(const double *__restrict__ mx, const double *__restrict__ my,
+                                                           const double *__restrict__ mz, int nm,
+                                                           const int *__restrict__ sval, double4 *__restrict__ pts,
+                                                           float4 *__restrict__ pts32, double c0, double c1, double c2)
 {
-    int run = 0;
-    for (int b = 0; b < nb; ++b) {
-        const int t = bsum[b];
-        bsum[b] = run;
-        run += t;
-    }
-}
-
-__global__ __launch_bounds__(kScanThreads) void scan_add_kernel(int *__restrict__ out, int n,
-                                                                const int *__restrict__ bsum)
-{
-    const int add = bsum[blockIdx.x];
-    const int base = blockIdx.x * kScanChunk;
-    for (int k = threadIdx.x; k < kScanChunk && base + k < n; k += kScanThreads) out[base + k] += add;
-}
-
-__global__ __launch_bounds__(kBlock) void grid_scatter_kernel(
-    const double *__restrict__ mx, const double *__restrict__ my, const double *__restrict__ mz,
-    int nm, const int *__restrict__ cid, const int *__restrict__ start, int *__restrict__ fill,
-    double4 *__restrict__ pts, float4 *__restrict__ pts32, double c0, double c1, double c2)
-{
-    for (int i = blockIdx.x * kBlock + threadIdx.x; i < nm; i += gridDim.x * kBlock) {
-        const int c = cid[i];
-        const int pos = start[c] + atomicAdd(fill + c, 1); // order within a cell is irrelevant
-        const double x = mx[i], y = my[i], z = mz[i];
-        pts[pos] = make_double4(x, y, z, (double)i);
-        // (the fp32 image: offsets from the box centre, the index's bits in w)
-        if (pts32) pts32[pos] = make_float4((float)(x - c0), (float)(y - c1), (float)(z - c2), __int_as_float(i));
-    }
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nm) return;
+    const int i = sval[k];
+    const double x = mx[i], y = my[i], z = mz[i];
+    pts[k] = make_double4(x, y, z, (double)i);
+    // (the fp32 image: offsets from the box centre, the index's bits in w)
+    if (pts32) pts32[k] = make_float4((float)(x - c0), (float)(y - c1), (float)(z - c2), __int_as_float(i));
 }
 
 // Lexicographic (D64, index) minimum, i.e. the first minimum (compute.cu:137 tie rule).
@@ -868,6 +836,12 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
 #define ICP_ITER_KCAND 2 // (candidate records a lane loads together)
 #endif
 constexpr int kIterRows = 128, kIterPts = 512;
+#ifndef ICP_ITER_KR
+#define ICP_ITER_KR 2 // (the walk: rows whose bounds a lane reads together)
+#endif
+#ifndef ICP_ITER_KU
+#define ICP_ITER_KU 2 // (the walk: points a lane loads together)
+#endif
 #ifndef ICP_ITER_WAVES
 #define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
 #endif
@@ -1071,7 +1045,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                     for (int k = k0; k < k1; ++k) test(lp[k], p0 + k);
                 }
             } else { // nn_grid_seeded32_kernel's walk (2 lanes a query, 2 rows' bounds, 2 loads in flight)
-                constexpr int KR = 2, KU = 2;
+                constexpr int KR = ICP_ITER_KR, KU = ICP_ITER_KU;
                 for (int r0 = sub; r0 < nrq; r0 += KR * 2) {
                     int k0[KR], pre[KR + 1];
                     pre[0] = 0;
@@ -1325,11 +1299,24 @@ static bool grid_flat_scan(int g)
 
 long long grid_cells(const GridParams &p) { return (long long)p.g[0] * p.g[1] * p.g[2]; }
 
-size_t grid_scan_blocks(long long n) { return (size_t)((n + kScanChunk - 1) / kScanChunk); }
+static int cell_bits(long long ncell)
+{
+    int bits = 1;
+    while (bits < 32 && (1ll << bits) <= ncell) ++bits;
+    return bits;
+}
 
-void launch_grid_build(const double *mx, const double *my, const double *mz, int nm,
-                       const GridParams &p, int *cid, int *count, int *start, int *bsum, int *fill,
-                       double4 *pts, float4 *pts32, hipStream_t st)
+static size_t grid_keys_bytes(int nm) { return (4 * (size_t)nm * sizeof(int) + 255) & ~(size_t)255; }
+
+size_t grid_build_scratch_bytes(int nm, long long ncell)
+{
+    size_t temp = 0;
+    (void)sort_pairs_u32(nullptr, temp, nullptr, nullptr, nullptr, nullptr, nm, cell_bits(ncell), nullptr);
+    return grid_keys_bytes(nm) + ((temp + 255) & ~(size_t)255);
+}
+
+int launch_grid_build(const double *mx, const double *my, const double *mz, int nm, const GridParams &p, void *scratch,
+                      size_t bytes, int *start, double4 *pts, float4 *pts32, hipStream_t st)
 {
     const long long ncell = grid_cells(p);
     GridView gv{};
@@ -1338,17 +1325,17 @@ void launch_grid_build(const double *mx, const double *my, const double *mz, int
         gv.lo[a] = p.lo[a];
     }
     gv.inv_h = p.inv_h;
-    const int blocks = std::max(1, std::min((nm + kBlock - 1) / kBlock, 4096));
-    (void)hipMemsetAsync(count, 0, sizeof(int) * (ncell + 1), st);
-    (void)hipMemsetAsync(fill, 0, sizeof(int) * ncell, st);
-    grid_count_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, gv, cid, count);
-    const int n = (int)(ncell + 1);
-    const int nb = (int)grid_scan_blocks(n);
-    scan_local_kernel<<<nb, kScanThreads, 0, st>>>(count, n, start, bsum);
-    scan_blocks_kernel<<<1, 1, 0, st>>>(bsum, nb);
-    scan_add_kernel<<<nb, kScanThreads, 0, st>>>(start, n, bsum);
-    grid_scatter_kernel<<<blocks, kBlock, 0, st>>>(mx, my, mz, nm, cid, start, fill, pts, pts32, p.c32[0], p.c32[1],
-                                                   p.c32[2]);
+    unsigned *k0 = (unsigned *)scratch, *k1 = k0 + nm;
+    int *v0 = (int *)(k1 + nm), *v1 = v0 + nm;
+    size_t temp_bytes = bytes - grid_keys_bytes(nm);
+    const int g = (nm + kBlock - 1) / kBlock;
+    grid_keys_kernel<<<g, kBlock, 0, st>>>(mx, my, mz, nm, gv, k0, v0);
+    if (sort_pairs_u32((char *)scratch + grid_keys_bytes(nm), temp_bytes, k0, k1, v0, v1, nm, cell_bits(ncell), st) !=
+        hipSuccess)
+        return -1;
+    grid_starts_kernel<<<(int)((ncell + kBlock) / kBlock), kBlock, 0, st>>>(k1, nm, (int)ncell, start);
+    grid_gather_kernel<<<g, kBlock, 0, st>>>(mx, my, mz, nm, v1, pts, pts32, p.c32[0], p.c32[1], p.c32[2]);
+    return 0;
 }
 
 void launch_nn_grid_search(int np, const double *px, const double *py, const double *pz, const GridView &gv,

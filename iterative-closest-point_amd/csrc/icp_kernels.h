@@ -96,6 +96,8 @@ void launch_aos_to_soa(const double *aos, size_t n, double *x, double *y, double
                        hipStream_t st);
 void launch_soa_to_aos(const double *x, const double *y, const double *z, size_t n, double *aos,
                        hipStream_t st);
+// SoA fp64 + the double4 rows (x, y, z, 0) at once
+void launch_aos_to_soa4(const double *aos, size_t n, double *x, double *y, double *z, double4 *m4, hipStream_t st);
 // both at once: SoA fp64 + the centred fp32 copy
 void launch_aos_to_soa_f32(const double *aos, size_t n, double *x, double *y, double *z, const double c[3],
                            float4 *f, hipStream_t st);
@@ -245,6 +247,10 @@ void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bim
 // 1024^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
 // = k); scratch: query_order_scratch_bytes(n)
 size_t query_order_scratch_bytes(int n);
+// stable LSD radix sort of (key, value) pairs on the low `bits` key bits (rocprim onesweep at
+// every size): temp == nullptr -> temp_bytes = the storage it needs
+hipError_t sort_pairs_u32(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
+                          int n, int bits, hipStream_t st);
 int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],
                        const double hi[3], void *scratch, size_t bytes, int *order, hipStream_t st,
                        int *pos = nullptr);
@@ -297,11 +303,11 @@ struct GridView {
 GridParams grid_params(const double *m_xyz, size_t nm); // host: bounding box, ~2 points/cell
 GridParams grid_params_box(const double lo[3], const double hi[3], size_t nm); // (from the model's box)
 long long grid_cells(const GridParams &p);
-size_t grid_scan_blocks(long long n);
-// cid[nm], count/start[ncells + 1], bsum[grid_scan_blocks(ncells + 1)], fill[ncells], pts[nm]
-void launch_grid_build(const double *mx, const double *my, const double *mz, int nm,
-                       const GridParams &p, int *cid, int *count, int *start, int *bsum, int *fill,
-                       double4 *pts, float4 *pts32, hipStream_t st); // (pts32 nullable)
+// the model grid: start[ncells + 1], pts[nm], pts32[nm] (nullable); scratch of
+// grid_build_scratch_bytes(nm, ncells).  Returns 0, or -1 when the sort fails to launch.
+size_t grid_build_scratch_bytes(int nm, long long ncell);
+int launch_grid_build(const double *mx, const double *my, const double *mz, int nm, const GridParams &p, void *scratch,
+                      size_t bytes, int *start, double4 *pts, float4 *pts32, hipStream_t st);
 // For queued query list[t] (t < *count_ptr) with candidate hint[t]: exact fp64 first minimum
 // over the grid box that must contain every point at least as close as the candidate ->
 // idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its window T_in[t]
@@ -674,12 +680,10 @@ void launch_reduce_pair(const double *part17, const double *part1, int nblocks, 
 void launch_reduce(const double *partials, int nblocks, int K, double *out, hipStream_t st);
 
 // ---- the model's preparation on the device (icp_model.hip) ------------------------------------
-// out[10] = (sum x, sum y, sum z, lo xyz, hi xyz, non-finite coordinates) of n AoS points; out[3] =
-// (max |(float)(m - c)| over the fp32 values, max |m - c|, non-finite fp32 values): fixed-order
-// two-stage reductions; scratch: model_stats_scratch_doubles()
+// out[10] = (sum x, sum y, sum z, lo xyz, hi xyz, non-finite coordinates) of n AoS points:
+// fixed-order two-stage reductions; scratch: model_stats_scratch_doubles()
 size_t model_stats_scratch_doubles();
 void launch_model_stats(const double *aos, int n, double *scratch, double *out, hipStream_t st);
-void launch_model_range(const double *aos, int n, const double c[3], double *scratch, double *out, hipStream_t st);
 // m32 (centred fp32, nm_pad rows, padding = far points), mperm (the f32 MFMA operand order), mm
 void launch_model_f32_images(const double *aos, int nm, int nm_pad, const double c[3], float4 *m32, float *mperm,
                              float *mm, hipStream_t st);

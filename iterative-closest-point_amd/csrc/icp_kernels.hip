@@ -120,6 +120,19 @@ __global__ __launch_bounds__(kBlock) void aos_to_soa_f32_kernel(const double *__
     }
 }
 
+// the model's SoA fp64 streams and its double4 rows (m4) from the AoS array, one read of it
+__global__ __launch_bounds__(kBlock) void aos_to_soa4_kernel(const double *__restrict__ aos, size_t n, double *x,
+                                                           double *y, double *z, double4 *m4)
+{
+    for (size_t i = blockIdx.x * (size_t)kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) {
+        const double a = aos[3 * i], b = aos[3 * i + 1], c = aos[3 * i + 2];
+        x[i] = a;
+        y[i] = b;
+        z[i] = c;
+        m4[i] = make_double4(a, b, c, 0.0);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(const double *__restrict__ x,
                                                             const double *__restrict__ y,
                                                             const double *__restrict__ z,
@@ -1896,6 +1909,12 @@ void launch_aos_to_soa(const double *aos, size_t n, double *x, double *y, double
 {
     if (!n) return;
     aos_to_soa_kernel<<<grid_for(n), kBlock, 0, st>>>(aos, n, x, y, z);
+}
+
+void launch_aos_to_soa4(const double *aos, size_t n, double *x, double *y, double *z, double4 *m4, hipStream_t st)
+{
+    if (!n) return;
+    aos_to_soa4_kernel<<<grid_for(n), kBlock, 0, st>>>(aos, n, x, y, z, m4);
 }
 
 void launch_soa_to_aos(const double *x, const double *y, const double *z, size_t n, double *aos,

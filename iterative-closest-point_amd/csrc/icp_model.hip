@@ -91,39 +91,6 @@ __global__ __launch_bounds__(kBlock) void model_stats_kernel(const double *__res
 }
 
 // Stage 1 of the range pass around c: (max |(float)(m - c)|, max |m - c|, non-finite fp32 values)
-__global__ __launch_bounds__(kBlock) void model_range_kernel(const double *__restrict__ aos, int n, double cx,
-                                                             double cy, double cz, double *__restrict__ part)
-{
-    double r32 = 0.0, r64 = 0.0, bad = 0.0;
-    const double c[3] = {cx, cy, cz};
-    for (int j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock)
-        for (int a = 0; a < 3; ++a) {
-            const double d = aos[3 * (size_t)j + a] - c[a];
-            const float f = (float)d;
-            if (!isfinite(f)) bad += 1.0;
-            else r32 = fmax(r32, fabs((double)f));
-            r64 = fmax(r64, fabs(d));
-        }
-    __shared__ double sh[kBlock / 64][3];
-    for (int off = 32; off > 0; off >>= 1) {
-        r32 = fmax(r32, __shfl_down(r32, off, 64));
-        r64 = fmax(r64, __shfl_down(r64, off, 64));
-        bad += __shfl_down(bad, off, 64);
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) {
-        sh[wave][0] = r32;
-        sh[wave][1] = r64;
-        sh[wave][2] = bad;
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        const int k = threadIdx.x;
-        double v = sh[0][k];
-        for (int w = 1; w < kBlock / 64; ++w) v = k < 2 ? fmax(v, sh[w][k]) : v + sh[w][k];
-        part[blockIdx.x * 3 + k] = v;
-    }
-}
 
 // Stage 2: one workgroup folds G rows of K (kinds: 0 sum, 1 min, 2 max) in a fixed order.
 template <int K>
@@ -470,12 +437,6 @@ void launch_model_stats(const double *aos, int n, double *scratch, double *out, 
 {
     model_stats_kernel<<<kStatBlocks, kBlock, 0, st>>>(aos, n, scratch);
     stats_fold_kernel<10><<<1, kBlock, 0, st>>>(scratch, kStatBlocks, out);
-}
-
-void launch_model_range(const double *aos, int n, const double c[3], double *scratch, double *out, hipStream_t st)
-{
-    model_range_kernel<<<kStatBlocks, kBlock, 0, st>>>(aos, n, c[0], c[1], c[2], scratch);
-    stats_fold_kernel<3><<<1, kBlock, 0, st>>>(scratch, kStatBlocks, out);
 }
 
 void launch_model_f32_images(const double *aos, int nm, int nm_pad, const double c[3], float4 *m32, float *mperm,

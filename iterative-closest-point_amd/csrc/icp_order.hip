@@ -149,11 +149,17 @@ void launch_permute_cloud(const int *order, int n, int inverse, const double *sx
 using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                 rocprim::default_config, 0>;
 
-static hipError_t sort_pairs(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
-                             int n, int bits, hipStream_t st)
+hipError_t sort_pairs_u32(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
+                          int n, int bits, hipStream_t st)
 {
     return rocprim::radix_sort_pairs<OnesweepSort>(temp, temp_bytes, k0, k1, v0, v1, (size_t)n, 0u, (unsigned)bits, st,
                                                    false);
+}
+
+static hipError_t sort_pairs(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
+                             int n, int bits, hipStream_t st)
+{
+    return sort_pairs_u32(temp, temp_bytes, k0, k1, v0, v1, n, bits, st);
 }
 
 // the sort's temporary storage starts on a 256-byte boundary after the three n-int arrays

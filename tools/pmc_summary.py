@@ -45,6 +45,8 @@ def short(name):
         return f"{base}<{qg}>"
     if base.startswith("nn_mfma16") and ("<true" in tmpl or "true>" in tmpl or "Lb1E" in full):
         return base + "<seeded>"
+    if base == "canon_fold_kernel" and tmpl:  # <K0, K, mode>: the iteration's fold / the first moments' folds
+        return base + tmpl.replace(" ", "")
     if base == "nn_grid_resolve_kernel" and tmpl:  # lanes per query: 4 (every query), 16 / 64 (queues)
         return f"{base}<{tmpl.strip('<>').split(',')[0].strip()}>"
     return base

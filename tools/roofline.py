@@ -26,6 +26,13 @@ Algorithmic bytes per scene point (fp64 SoA clouds):
 From profiles/r04x on (every C4 search the seeded grid search, which writes Y; no bundle record):
   shifted_moments_kernel: p 24 + Y 24 = 48 (the search wrote Y: no index, no gather)
   transform_err_kernel: p 24 + Y 24 + write p 24 + the next search's seed distance 8 = 80
+Round 5 (the canonical schedule: one fused grid iteration per seeded iteration):
+  canon_moments_kernel (the first iteration's moments; the search wrote Y): p 24 + Y 24 = 48
+  canon_transform_kernel (the run's last transform): p 24 + Y 24 + write p 24 + seed distance 8 = 80
+  gather_aos_kernel (set_scene into slot order): order 4 + AoS point 24 + write p 24 + fp32 copy 16 = 68
+  nn_grid_iter_kernel (GRID_KERNELS): per query p in/out 48 + previous Y 24 + Y out 24 + index
+    in/out 8 + the winner's 32-byte grid record = 136; per model point its fp32 grid record 16 +
+    cell table 2 = 18
 """
 from __future__ import annotations
 
@@ -44,7 +51,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense ~2.5 PF
 NN_KERNELS = ("nn_mfma16r_kernel<8>", "nn_mfma16r_kernel<4>", "nn_mfma16_kernel", "nn_mfma16_kernel<seeded>")
 BYTES_PER_POINT = {"shifted_moments_kernel": 84, "gather_moments_kernel": 84, "centred_moments_kernel": 48,
-                   "transform_err_kernel": 140}
+                   "transform_err_kernel": 140, "canon_moments_kernel": 48, "canon_transform_kernel": 80,
+                   "gather_aos_kernel": 68}
 
 
 def bytes_per_point(kernel, tag):
@@ -131,8 +139,9 @@ C3_ITERATIONS = 50
 # kernel (round 4: fp64 query 24 B + seed distance 8 + index in 4 / out 4 + correspondence out 24;
 # 32-byte grid record + cell table 2) or, in captures before it, the generic resolver's all-mode
 # (query 24 + index in/out; 32-byte record) -- its JSON keyed without the template argument
-GRID_KERNELS = {"nn_grid_seeded_kernel": (64.0, 34.0), "nn_grid_resolve_kernel<4>": (28.0, 32.0)}
-GRID_KERNEL = "nn_grid_seeded_kernel"
+GRID_KERNELS = {"nn_grid_iter_kernel": (136.0, 18.0), "nn_grid_seeded_kernel": (64.0, 34.0),
+                "nn_grid_resolve_kernel<4>": (28.0, 32.0)}
+GRID_KERNEL = "nn_grid_iter_kernel"
 
 
 def grid_kernel_keys(times, pmc):
