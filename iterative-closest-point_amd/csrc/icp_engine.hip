@@ -158,6 +158,7 @@ struct icp_ctx {
     float4 *mperm = nullptr; // same, (mm, x, y, z) permuted for the MFMA operands
     float *mm = nullptr;     // |m~|^2 rounded to fp32 (the MFMA's k = 0 operand)
     char *mimg16 = nullptr;  // f16 split image for the 32x32x16 f16 MFMA (1 KiB / 32 points)
+    bool mimg16_pending = false; // (built at the first search that reads it: ensure_mimage16)
     float *mms16 = nullptr;  // |b_s|^2 (scaled) per model point, fp32
     double scale16 = 1.0;    // power of two: max |b_s| in [2^11, 2^12)
     size_t nm = 0, nm_pad = 0, m32_cap = 0, mperm_cap = 0, mm_cap = 0, mimg16_cap = 0, mms16_cap = 0;
@@ -790,6 +791,21 @@ static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const i
     return ICP_OK;
 }
 
+// The f16 split image and its norms (the f16 filter's operands, the f16 / bundle finalize's
+// certificate) at the first search that reads them: a registration the grid serves from its
+// first search never builds them (13 us at C4, profiles/r05h)
+static int ensure_mimage16(icp_ctx *ctx)
+{
+    if (!ctx->mimg16_pending) return ICP_OK;
+    TRY(grow(ctx, &ctx->mimg16, &ctx->mimg16_cap, ctx->nm_pad * 32));
+    TRY(grow(ctx, &ctx->mms16, &ctx->mms16_cap, ctx->nm_pad));
+    launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)ctx->nm, (int)ctx->nm_pad, ctx->c,
+                          ctx->scale16, ctx->mimg16, ctx->mms16, ctx->st);
+    LAUNCHCHK("build_mimage16");
+    ctx->mimg16_pending = false;
+    return ICP_OK;
+}
+
 // An unseeded search of a scene in slot order takes the seeded grid pass from cell seeds
 // (launch_nn_grid_cell_seed: the first minimum over the query's own cell, or the empty cell's
 // stand-in) instead of the ring search (nn_grid_search_kernel: rings of cells until one holds a
@@ -918,6 +934,7 @@ int nn_search_begin(icp_ctx *ctx, const DevCloud &q, size_t n, bool seeded, hipE
             LAUNCHCHK("nn_grid_search (first)");
             return ICP_OK;
         }
+        if (l1 >= 2) TRY(ensure_mimage16(ctx));
         if (l1 == 3 && ctx->bundle_pending && ws) ctx->stats.bundle_builds_in_run += 1; // (icp_run, mid-run)
         if (l1 == 3) TRY(ensure_bundle(ctx)); // (built at their first use)
         const bool gseed = l1 >= 2 && !seeded && grid_seed && ctx->g_pts;
@@ -1612,11 +1629,7 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     LAUNCHCHK("model_f32_images");
     ctx->scale16 = rm64 > 0.0 ? std::ldexp(1.0, (int)std::floor(std::log2(4096.0 / rm64))) : 1.0;
     while (rm64 * ctx->scale16 >= 4096.0) ctx->scale16 *= 0.5;
-    TRY(grow(ctx, &ctx->mimg16, &ctx->mimg16_cap, nm_pad * 32));
-    TRY(grow(ctx, &ctx->mms16, &ctx->mms16_cap, nm_pad));
-    launch_build_mimage16(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, (int)nm_pad, ctx->c,
-                          ctx->scale16, ctx->mimg16, ctx->mms16, ctx->st);
-    LAUNCHCHK("build_mimage16");
+    ctx->mimg16_pending = true; // (the f16 image: at the first f16 / bundle search, ensure_mimage16)
     // uniform grid over the fp64 model for the exact resolver (its box: step 1's)
     ctx->grid = grid_params_box(lo, hi, nm);
     const long long ncell = grid_cells(ctx->grid);

@@ -836,6 +836,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
 #define ICP_ITER_KCAND 2 // (candidate records a lane loads together)
 #endif
 constexpr int kIterRows = 128, kIterPts = 512;
+#ifndef ICP_ITER_PREFETCH
+#define ICP_ITER_PREFETCH 1 // (the next task's point, correspondence and index loaded during this one)
+#endif
 #ifndef ICP_ITER_KR
 #define ICP_ITER_KR 2 // (the walk: rows whose bounds a lane reads together)
 #endif
@@ -877,20 +880,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     int *const rbase = s_rbase[wave], *const rstart = s_rstart[wave];
     double acc = 0.0; // (lane k < 18: column k of this strand)
     int far = 0, nbig = 0;
+    // the task's point, correspondence and index (ICP_ITER_PREFETCH: the next task's are loaded
+    // while this one walks its rows -- their round trip overlaps the walk's first loads)
+    double fp[3] = {0.0, 0.0, 0.0}, fy[3] = {0.0, 0.0, 0.0};
+    int fh = -1;
+    auto fetch = [&](int cc) {
+        const int tt = cc * kCanonChunk + u;
+        if (tt < n) {
+            fp[0] = px[tt];
+            fp[1] = py[tt];
+            fp[2] = pz[tt];
+            fy[0] = yx[tt];
+            fy[1] = yy[tt];
+            fy[2] = yz[tt];
+            fh = idx[tt];
+        }
+    };
+    if (ICP_ITER_PREFETCH && s < S) fetch(s);
     for (int c = s; s < S && c < C; c += S) {
         const int t = c * kCanonChunk + u;
         const bool active = t < n;
         // A: the previous transform, its residual = the seed distance
         double q[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
         int h = -1;
+        if (!ICP_ITER_PREFETCH) fetch(c);
         if (active) {
-            const double p0 = px[t], p1 = py[t], p2 = pz[t];
-            y[0] = yx[t];
-            y[1] = yy[t];
-            y[2] = yz[t];
-            h = idx[t];
+            const double p0 = fp[0], p1 = fp[1], p2 = fp[2];
+            y[0] = fy[0];
+            y[1] = fy[1];
+            y[2] = fy[2];
+            h = fh;
             transform_point(xf, p0, p1, p2, q[0], q[1], q[2]);
         }
+        if (ICP_ITER_PREFETCH && c + S < C) fetch(c + S);
         const double e = active ? residual2(y[0], y[1], y[2], q[0], q[1], q[2]) : 0.0;
         lap(5);
         if (active && sub == 0) {

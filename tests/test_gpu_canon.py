@@ -1,0 +1,85 @@
+"""The canonical schedule and the fused grid iteration (icp_canon.h, icp_canon.hip,
+icp_grid.hip nn_grid_iter_kernel, icp_engine.hip run_loop).
+
+The loop is src/GPU/gpu.cc:52-83: per iteration the exact NN of every point, the alignment
+(gpu.cc:95-151) and the transform with its residual.  Every path that produces an iteration's
+sums writes the same canonical rows (32-point chunk trees, strands, rows, one fold), so:
+
+  * the fused kernel (transform + seeded search + moments in one launch, the default) and the
+    separate kernels of the same schedule (ICP_GRID_ITER=0) give the same trajectory bit for bit:
+    errors, per-iteration index digests, final scene and transform -- on a whole scene and on a
+    sparse shard (a W = 8 rank's share against the whole model);
+  * the round-4 schedule (ICP_CANON=0: per-path reduction orders) finds the same correspondences
+    in every iteration (digests equal) and errors equal to rounding (rtol 1e-12).
+
+Each setting runs in its own process (the switches are read once per process).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import icp_amd
+out = {}
+iters = 12
+for name, n, frac in (("whole", 1 << 17, 1), ("shard", 1 << 19, 8)):
+    m, p = icp_amd.synthetic_pair(n, seed=31, angle_deg=6.0)
+    b, c = icp_amd.shard_range(n, 0, frac)
+    scene = np.ascontiguousarray(p[b:b + c])
+    with icp_amd.Context(0) as ctx:
+        ctx.set_allow_unequal(True)
+        ctx.set_model(m)
+        ctx.set_scene(scene, np_total=c)
+        ctx.set_index_digest(iters)
+        res, errs = ctx.run(iters, -1.0)
+        out[name + "_errs"] = errs
+        out[name + "_dig"] = ctx.index_digest(iters)
+        out[name + "_scene"] = ctx.get_scene()
+        out[name + "_xf"] = np.concatenate([[res.s], np.array(res.R[:]), np.array(res.t[:])])
+        out[name + "_grid"] = np.array([ctx.stats()["run_grid_searches"]])
+np.savez(sys.argv[2], **out)
+print("canon ok")
+"""
+
+
+def run_setting(tmp_path, name, env):
+    out = str(tmp_path / f"canon_{name}.npz")
+    r = subprocess.run([sys.executable, "-c", SCRIPT, os.path.join(ROOT, "iterative-closest-point_amd"), out],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, **env))
+    assert r.returncode == 0 and "canon ok" in r.stdout, r.stdout + r.stderr
+    return dict(np.load(out))
+
+
+@pytest.fixture(scope="module")
+def settings(icp_lib, tmp_path_factory):
+    if icp_lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    tmp = tmp_path_factory.mktemp("canon")
+    return {"fused": run_setting(tmp, "fused", {}),
+            "separate": run_setting(tmp, "separate", {"ICP_GRID_ITER": "0"}),
+            "round4": run_setting(tmp, "round4", {"ICP_CANON": "0"})}
+
+
+@pytest.mark.parametrize("case", ["whole", "shard"])
+def test_fused_equals_separate_bitwise(settings, case):
+    a, b = settings["fused"], settings["separate"]
+    assert a[case + "_grid"][0] >= 8  # (the grid's seeded iterations ran: the fused kernel's path)
+    for k in ("errs", "dig", "scene", "xf"):
+        assert np.array_equal(a[f"{case}_{k}"], b[f"{case}_{k}"]), k
+
+
+@pytest.mark.parametrize("case", ["whole", "shard"])
+def test_canonical_matches_round4_schedule(settings, case):
+    a, b = settings["fused"], settings["round4"]
+    assert np.array_equal(a[case + "_dig"], b[case + "_dig"])
+    np.testing.assert_allclose(a[case + "_errs"], b[case + "_errs"], rtol=1e-12)
+    np.testing.assert_allclose(a[case + "_scene"], b[case + "_scene"], rtol=0, atol=1e-12)
