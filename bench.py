@@ -442,23 +442,36 @@ def csv_io(m):
             "load_mb_per_s": size / tl / 1e6, "roundtrip_rows": int(back.shape[0])}
 
 
-def registration(ctx, m, p_local, n_total, iters=30, reps=3):
+def registration(ctx, m, p_local, n_total, iters=30, reps=3, device=None):
     """SURVEY §8d's clock: a whole registration from model upload through the last iteration's
     err -- icp_set_model (host AoS in, every device image built), icp_set_scene, the first
     (unseeded) iteration and the seeded ones.  Each rep re-uploads both clouds (set_model always
     rebuilds), on the caller's context (one-time hipInit / RCCL init excluded, as §8d says).
     The first iteration is timed by a separate run(1) after a fresh set_scene; the seeded ones
-    are the rest of the 30-iteration run."""
+    are the rest of the 30-iteration run.  device = (model tensor, scene tensor): the same phases
+    from device-resident clouds (icp_set_model_device / icp_set_scene_device: the headline's step)."""
+    def set_model():
+        if device is None:
+            ctx.set_model(m)
+        else:
+            ctx.set_model_device(device[0].data_ptr(), m.shape[0])
+
+    def set_scene():
+        if device is None:
+            ctx.set_scene(p_local, np_total=n_total)
+        else:
+            ctx.set_scene_device(device[1].data_ptr(), p_local.shape[0], n_total)
+
     rows = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        ctx.set_model(m)
+        set_model()
         t1 = time.perf_counter()
-        ctx.set_scene(p_local, np_total=n_total)
+        set_scene()
         t2 = time.perf_counter()
         res, _ = ctx.run(iters, -1.0)
         t3 = time.perf_counter()
-        ctx.set_scene(p_local, np_total=n_total)
+        set_scene()
         t4 = time.perf_counter()
         ctx.run(1, -1.0)
         t5 = time.perf_counter()
@@ -619,6 +632,8 @@ def main():
     # all-reduces), untimed by the headline
     progress("timed iterations done")
     reg = registration(ctx, m, p[b:b + c], args.n, iters=REGISTRATION_ITERS) if args.registration else None
+    # the headline step's phases (device-resident clouds), untimed by the headline
+    reg_dev = registration(ctx, m, p[b:b + c], args.n, iters=REGISTRATION_ITERS, device=(dm, dps))
     progress("registration timed")
     host_reduce = world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1"
     its = args.steps * REGISTRATION_ITERS
@@ -717,6 +732,10 @@ def main():
             "fp64_resolved_per_iter": st["ambiguous"] / max(st["iterations"], 1),
             "final_err": float(errs[-1]) if errs.size else None,
         }
+        out["step_phases"] = dict(reg_dev)
+        out["step_phases"]["note"] = ("the headline step's phases from device-resident clouds (median of 3 "
+                                      "registrations after the timed region): set_model_device, set_scene_device, "
+                                      "first (unseeded) iteration, seeded iterations")
         if reg is not None:  # (host arrays in: the PCIe copy of both clouds included)
             regs = [r for r in per_rank if r.get("registration_ms")]
             out["registration"] = dict(reg)

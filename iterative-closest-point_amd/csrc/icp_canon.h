@@ -75,6 +75,18 @@ __device__ __forceinline__ double wave_tree_odd(double v)
     return v;
 }
 
+// Half a chunk per wave, the 16 leaves in lanes 4u+3 (a query's four lanes): lane 63 <- the
+// pairwise sum of the 16 leaves, S[0, 16) or S[16, 32) of the chunk, whose two waves then join
+// them as the 32-leaf tree's last step does
+__device__ __forceinline__ double wave_tree_quad(double v)
+{
+    v = v + dpp_f64<0x114>(v);      // row_shr:4  -> lane 8i+7: leaves (2i, 2i+1)
+    v = v + dpp_f64<0x118>(v);      // row_shr:8  -> lane 16i+15
+    v = v + dpp_f64<0x142, 0xa>(v); // row_bcast:15 -> lanes 31, 63
+    v = v + dpp_f64<0x143, 0xc>(v); // row_bcast:31 -> lane 63
+    return v;
+}
+
 __device__ __forceinline__ double lane_value(double v, int lane)
 {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);

@@ -836,6 +836,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
 #define ICP_ITER_KCAND 2 // (candidate records a lane loads together)
 #endif
 constexpr int kIterRows = 128, kIterPts = 512;
+// the four-lane form: every strand one chunk (C <= kCanonStrandsMax), so the chunk's two waves
+// join their halves once, after the task
+constexpr int kIterWideMax = kCanonStrandsMax * kCanonChunk;
 #ifndef ICP_ITER_PREFETCH
 #define ICP_ITER_PREFETCH 1 // (the next task's point, correspondence and index loaded during this one)
 #endif
@@ -848,8 +851,11 @@ constexpr int kIterRows = 128, kIterPts = 512;
 #ifndef ICP_ITER_WAVES
 #define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
 #endif
-template <bool STAGE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER_WAVES))) void nn_grid_iter_kernel(
+// G lanes a query (2, or 4 for shards of at most kIterWideMax points: two waves a chunk, a chunk
+// a strand -- twice the waves for a scene too small to fill the chip with one wave a chunk);
+// a workgroup is the four strands of one row (G / 2 waves each)
+template <bool STAGE, int G>
+__global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(ICP_ITER_WAVES))) void nn_grid_iter_kernel(
     int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
     float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
@@ -865,17 +871,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             tclk = now;
         }
     };
-    __shared__ float4 s_pts[kBlock / 64][STAGE ? kIterPts : 1];
-    __shared__ int s_rbase[kBlock / 64][STAGE ? kIterRows + 1 : 1], s_rstart[kBlock / 64][STAGE ? kIterRows : 1];
+    static_assert(G == 2 || (G == 4 && !STAGE), "lanes a query: 2 (staged or not) or 4 (not staged)");
+    constexpr int H = G / 2;          // waves a chunk
+    constexpr int QW = 64 / G;        // queries a wave
+    constexpr int NW = kBlock / 64 * H; // waves a workgroup
+    __shared__ float4 s_pts[NW][STAGE ? kIterPts : 1];
+    __shared__ int s_rbase[NW][STAGE ? kIterRows + 1 : 1], s_rstart[NW][STAGE ? kIterRows : 1];
     // (st is uniform: its fields are scalar loads into SGPRs -- an LDS copy would hold the
     // transform's 15 doubles in VGPRs all kernel long)
     if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
     const Xform xf = st->xf;
     const double cp[3] = {st->shift_p[0], st->shift_p[1], st->shift_p[2]};
     const double cy[3] = {st->shift_y[0], st->shift_y[1], st->shift_y[2]};
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane >> 1, sub = lane & 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane / G, sub = lane % G;
+    const int half = wave % H; // (G = 4: which 16 queries of the chunk)
     const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
-    const int s = blockIdx.x * 4 + wave;
+    const int s = blockIdx.x * 4 + wave / H;
     float4 *const lp = s_pts[wave];
     int *const rbase = s_rbase[wave], *const rstart = s_rstart[wave];
     double acc = 0.0; // (lane k < 18: column k of this strand)
@@ -885,7 +896,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     double fp[3] = {0.0, 0.0, 0.0}, fy[3] = {0.0, 0.0, 0.0};
     int fh = -1;
     auto fetch = [&](int cc) {
-        const int tt = cc * kCanonChunk + u;
+        const int tt = cc * kCanonChunk + half * QW + u;
         if (tt < n) {
             fp[0] = px[tt];
             fp[1] = py[tt];
@@ -898,7 +909,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     };
     if (ICP_ITER_PREFETCH && s < S) fetch(s);
     for (int c = s; s < S && c < C; c += S) {
-        const int t = c * kCanonChunk + u;
+        const int t = c * kCanonChunk + half * QW + u;
         const bool active = t < n;
         // A: the previous transform, its residual = the seed distance
         double q[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
@@ -1068,7 +1079,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                 }
             } else { // nn_grid_seeded32_kernel's walk (2 lanes a query, 2 rows' bounds, 2 loads in flight)
                 constexpr int KR = ICP_ITER_KR, KU = ICP_ITER_KU;
-                for (int r0 = sub; r0 < nrq; r0 += KR * 2) {
+                for (int r0 = sub; r0 < nrq; r0 += KR * G) {
                     int k0[KR], pre[KR + 1];
                     pre[0] = 0;
 #pragma unroll
@@ -1108,10 +1119,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             if (nc) flush();
         }
         lap(7);
-        { // the query's two lanes: the (D64, index) minimum, its position and coordinates
-            const double ob = __shfl_xor(best, 1, 64);
-            const int oi = __shfl_xor(bi, 1, 64), ok2 = __shfl_xor(bk, 1, 64), ows = __shfl_xor(wset, 1, 64);
-            const double ox = __shfl_xor(wx, 1, 64), oy = __shfl_xor(wy, 1, 64), oz = __shfl_xor(wz, 1, 64);
+        // the query's G lanes: the (D64, index) minimum, its position and coordinates
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+            const double ob = __shfl_xor(best, o, 64);
+            const int oi = __shfl_xor(bi, o, 64), ok2 = __shfl_xor(bk, o, 64), ows = __shfl_xor(wset, o, 64);
+            const double ox = __shfl_xor(wx, o, 64), oy = __shfl_xor(wy, o, 64), oz = __shfl_xor(wz, o, 64);
             if (ob < best || (ob == best && (unsigned)oi < (unsigned)bi)) {
                 best = ob;
                 bi = oi;
@@ -1155,7 +1168,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                 }
             }
             group_lex_min<64>(b2, bj);
-            if ((lane >> 1) == (bl >> 1)) {
+            if (lane / G == bl / G) {
                 best = b2;
                 bi = bj < 0 ? 0 : bj;
                 bk = -1;
@@ -1198,8 +1211,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             else if (k == 16) leaf = 0.0 + ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
             else leaf = active ? 0.0 + e : 0.0;
             if (!active) leaf = 0.0;
-            const double v = lane_value(wave_tree_odd(leaf), 63);
-            if (lane == k) acc = acc + v;
+            if constexpr (G == 2) {
+                const double v = lane_value(wave_tree_odd(leaf), 63);
+                if (lane == k) acc = acc + v;
+            } else { // (a strand is one chunk: this wave's half of it, joined below)
+                const double v = lane_value(wave_tree_quad(leaf), 63);
+                if (lane == k) acc = v;
+            }
         }
         lap(9);
     }
@@ -1209,15 +1227,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         for (int f = 0; f < 12; ++f)
             if (dcnt[f]) atomicAdd(dbg + f, dcnt[f]);
     // the workgroup's four strands -> its row (column k from lane k of each wave)
-    __shared__ double sh[kBlock / 64][kCanonCols];
+    __shared__ double sh[NW][kCanonCols];
     if (lane < kCanonCols) sh[wave][lane] = acc;
     __syncthreads();
     if (threadIdx.x < kCanonCols) {
         const int k = threadIdx.x;
-        rows[(size_t)k * R + blockIdx.x] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+        double v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) // (G = 4: the chunk's halves, then the strand's 0.0 + chunk)
+            v[j] = H == 1 ? sh[j][k] : 0.0 + (sh[H * j][k] + sh[H * j + H - 1][k]);
+        rows[(size_t)k * R + blockIdx.x] = (v[0] + v[1]) + (v[2] + v[3]);
     }
     // the far count (the policy's) and the big boxes (the search statistics), one atomic each
-    __shared__ int s_cnt[2][kBlock / 64];
+    __shared__ int s_cnt[2][NW];
     for (int o = 32; o >= 1; o >>= 1) far += __shfl_xor(far, o, 64);
     if (lane == 0) {
         s_cnt[0][wave] = far;
@@ -1226,7 +1248,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     __syncthreads();
     if (threadIdx.x < 2) {
         int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += s_cnt[threadIdx.x][w];
+        for (int w = 0; w < NW; ++w) tot += s_cnt[threadIdx.x][w];
         int *dst = threadIdx.x == 0 ? far_acc : big_count;
         if (tot && dst) atomicAdd(dst, tot);
     }
@@ -1246,13 +1268,21 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         const char *e = getenv("ICP_ITER_STAGE");
         return e && atoi(e) == 1;
     }();
-#define ITER(S)                                                                                                       \
-    nn_grid_iter_kernel<S><<<canon_rows((size_t)n), kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, \
-                                                                      box, budget, nm, m4, rows, far_acc, far_d2,       \
-                                                                      big_count, dbg)
-    if (stage) ITER(true);
-    else ITER(false);
-#undef ITER
+    // a shard of at most kIterWideMax points: four lanes a query (ICP_ITER_WIDE=0: two)
+    static const bool wide_on = [] {
+        const char *e = getenv("ICP_ITER_WIDE");
+        return !(e && atoi(e) == 0);
+    }();
+    const int R = canon_rows((size_t)n);
+    if (!stage && wide_on && n <= kIterWideMax)
+        nn_grid_iter_kernel<false, 4><<<R, 2 * kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
+                                                                 budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+    else if (stage)
+        nn_grid_iter_kernel<true, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
+                                                            budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+    else
+        nn_grid_iter_kernel<false, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
+                                                             budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
 }
 
 namespace {

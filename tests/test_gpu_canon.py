@@ -7,8 +7,11 @@ sums writes the same canonical rows (32-point chunk trees, strands, rows, one fo
 
   * the fused kernel (transform + seeded search + moments in one launch, the default) and the
     separate kernels of the same schedule (ICP_GRID_ITER=0) give the same trajectory bit for bit:
-    errors, per-iteration index digests, final scene and transform -- on a whole scene and on a
-    sparse shard (a W = 8 rank's share against the whole model);
+    errors, per-iteration index digests, final scene and transform -- on a whole scene, on a
+    sparse shard (a W = 8 rank's share against the whole model) and on a scene of two chunks a
+    strand (2^19); so do the fused kernel's four-lane form (scenes of at most 2^18 points: two
+    waves a chunk, the chunk's halves joined as the 32-leaf tree's last step) and its two-lane
+    form (ICP_ITER_WIDE=0);
   * the round-4 schedule (ICP_CANON=0: per-path reduction orders) finds the same correspondences
     in every iteration (digests equal) and errors equal to rounding (rtol 1e-12).
 
@@ -31,7 +34,7 @@ sys.path.insert(0, sys.argv[1])
 import icp_amd
 out = {}
 iters = 12
-for name, n, frac in (("whole", 1 << 17, 1), ("shard", 1 << 19, 8)):
+for name, n, frac in (("whole", 1 << 17, 1), ("shard", 1 << 19, 8), ("big", 1 << 19, 1)):
     m, p = icp_amd.synthetic_pair(n, seed=31, angle_deg=6.0)
     b, c = icp_amd.shard_range(n, 0, frac)
     scene = np.ascontiguousarray(p[b:b + c])
@@ -65,19 +68,21 @@ def settings(icp_lib, tmp_path_factory):
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
     tmp = tmp_path_factory.mktemp("canon")
     return {"fused": run_setting(tmp, "fused", {}),
+            "narrow": run_setting(tmp, "narrow", {"ICP_ITER_WIDE": "0"}),
             "separate": run_setting(tmp, "separate", {"ICP_GRID_ITER": "0"}),
             "round4": run_setting(tmp, "round4", {"ICP_CANON": "0"})}
 
 
-@pytest.mark.parametrize("case", ["whole", "shard"])
-def test_fused_equals_separate_bitwise(settings, case):
-    a, b = settings["fused"], settings["separate"]
+@pytest.mark.parametrize("other", ["separate", "narrow"])
+@pytest.mark.parametrize("case", ["whole", "shard", "big"])
+def test_fused_equals_separate_bitwise(settings, case, other):
+    a, b = settings["fused"], settings[other]
     assert a[case + "_grid"][0] >= 8  # (the grid's seeded iterations ran: the fused kernel's path)
     for k in ("errs", "dig", "scene", "xf"):
         assert np.array_equal(a[f"{case}_{k}"], b[f"{case}_{k}"]), k
 
 
-@pytest.mark.parametrize("case", ["whole", "shard"])
+@pytest.mark.parametrize("case", ["whole", "shard", "big"])
 def test_canonical_matches_round4_schedule(settings, case):
     a, b = settings["fused"], settings["round4"]
     assert np.array_equal(a[case + "_dig"], b[case + "_dig"])
