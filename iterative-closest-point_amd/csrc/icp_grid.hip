@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                     pre[0] = 0;
 #pragma unroll
                     for (int v = 0; v < KR; ++v) {
-                        const int r = r0 + v * 2;
+                        const int r = r0 + v * G;
                         int a0 = 0, a1 = 0;
                         if (r < nrq) {
                             const int gy = c0[1] + r % ny, gz = c0[2] + r / ny;
@@ -1268,10 +1268,12 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         const char *e = getenv("ICP_ITER_STAGE");
         return e && atoi(e) == 1;
     }();
-    // a shard of at most kIterWideMax points: four lanes a query (ICP_ITER_WIDE=0: two)
+    // ICP_ITER_WIDE=1: four lanes a query for a shard of at most kIterWideMax points (measured:
+    // W = 4 shard 0.078 against 0.068 ms an iteration, W = 8 0.049 against 0.051 -- not kept,
+    // profiles/r05l/wide_ab.log)
     static const bool wide_on = [] {
         const char *e = getenv("ICP_ITER_WIDE");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) == 1;
     }();
     const int R = canon_rows((size_t)n);
     if (!stage && wide_on && n <= kIterWideMax)

@@ -9,9 +9,9 @@ sums writes the same canonical rows (32-point chunk trees, strands, rows, one fo
     separate kernels of the same schedule (ICP_GRID_ITER=0) give the same trajectory bit for bit:
     errors, per-iteration index digests, final scene and transform -- on a whole scene, on a
     sparse shard (a W = 8 rank's share against the whole model) and on a scene of two chunks a
-    strand (2^19); so do the fused kernel's four-lane form (scenes of at most 2^18 points: two
-    waves a chunk, the chunk's halves joined as the 32-leaf tree's last step) and its two-lane
-    form (ICP_ITER_WIDE=0);
+    strand (2^19); so does the fused kernel's opt-in four-lane form (ICP_ITER_WIDE=1, scenes of
+    at most 2^18 points: two waves a chunk, the chunk's halves joined as the 32-leaf tree's last
+    step);
   * the round-4 schedule (ICP_CANON=0: per-path reduction orders) finds the same correspondences
     in every iteration (digests equal) and errors equal to rounding (rtol 1e-12).
 
@@ -68,12 +68,12 @@ def settings(icp_lib, tmp_path_factory):
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
     tmp = tmp_path_factory.mktemp("canon")
     return {"fused": run_setting(tmp, "fused", {}),
-            "narrow": run_setting(tmp, "narrow", {"ICP_ITER_WIDE": "0"}),
+            "wide": run_setting(tmp, "wide", {"ICP_ITER_WIDE": "1"}),
             "separate": run_setting(tmp, "separate", {"ICP_GRID_ITER": "0"}),
             "round4": run_setting(tmp, "round4", {"ICP_CANON": "0"})}
 
 
-@pytest.mark.parametrize("other", ["separate", "narrow"])
+@pytest.mark.parametrize("other", ["separate", "wide"])
 @pytest.mark.parametrize("case", ["whole", "shard", "big"])
 def test_fused_equals_separate_bitwise(settings, case, other):
     a, b = settings["fused"], settings[other]
