@@ -203,8 +203,6 @@ struct icp_ctx {
     double4 *g_pts = nullptr;
     float4 *g_pts32 = nullptr; // (the fp32 image of g_pts: the seeded grid search's prefilter)
     size_t g_pts32_cap = 0;
-    int *g_rep = nullptr; // each empty cell's stand-in seed (launch_grid_rep): unseeded searches
-    size_t g_rep_cap = 0;
     size_t g_start_cap = 0, g_pts_cap = 0;
     IterState *iter_state = nullptr; // device-resident loop state (icp_iter.hip)
     size_t iter_state_cap = 0;
@@ -351,6 +349,9 @@ struct icp_ctx {
     // moments + Horn step, [1] the transform + error step; zero between launches
     unsigned *fold_ticket = nullptr;
     bool scene_slot = false;
+    // scene_revert: the scene is in the slot order of a model since replaced -- icp_run puts it
+    // back into file order (and sorts it by the new model's box) unless a new scene comes first
+    bool scene_revert = false;
     bool p32_stale = false; // the scene's fp32 copy was not kept by the last icp_run (its path never read it)
     int *s_order = nullptr;
     size_t s_order_cap = 0;
@@ -692,6 +693,25 @@ static bool want_slot_order(const icp_ctx *ctx, size_t n)
            (double)n * (double)ctx->nm >= 2147483648.0;
 }
 
+// A pending scene_revert (set_model while the scene was in slot order): the scene back into
+// file order, its fp32 copy around the new model's c
+static int scene_revert_now(icp_ctx *ctx)
+{
+    if (!ctx->scene_revert) return ICP_OK;
+    DevCloud &P = ctx->scene;
+    TRY(grow_cloud(ctx, ctx->s_tmp, P.n, true));
+    launch_permute_cloud(ctx->s_order, (int)P.n, 1, P.x, P.y, P.z, nullptr, nullptr, ctx->s_tmp.x, ctx->s_tmp.y,
+                         ctx->s_tmp.z, nullptr, nullptr, ctx->st);
+    std::swap(ctx->scene, ctx->s_tmp);
+    launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1], ctx->c[2],
+                    ctx->scene.f, ctx->st);
+    LAUNCHCHK("scene_to_file_order");
+    ctx->scene_slot = false;
+    ctx->scene_revert = false;
+    ctx->p32_stale = false;
+    return ICP_OK;
+}
+
 // The resident scene (and its correspondences while seeds_valid) into slot order, once per
 // uploaded scene: gathered into the second buffer, which then becomes the scene.
 static int scene_to_slot_order(icp_ctx *ctx)
@@ -824,8 +844,7 @@ static bool cell_seed_on()
 static int grid_unseeded_slot(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop, hipEvent_t ev1)
 {
     TRY(grow(ctx, &ctx->b_seedd, &ctx->b_seedd_cap, n));
-    launch_nn_grid_cell_seed((int)n, q.x, q.y, q.z, grid_view(ctx), ctx->g_rep, ctx->m4, ctx->idx, ctx->b_seedd,
-                             ctx->st);
+    launch_nn_grid_cell_seed((int)n, q.x, q.y, q.z, grid_view(ctx), (int)ctx->nm, ctx->idx, ctx->b_seedd, ctx->st);
     LAUNCHCHK("nn_grid_cell_seed");
     return grid_seeded_search(ctx, q, n, stop, ctx->b_seedd, ev1);
 }
@@ -1482,7 +1501,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->amb1, (void *)ctx->idx, ctx->part, (void *)ctx->amb_count,
                     (void *)ctx->amb_list, (void *)ctx->amb_T, (void *)ctx->partials, (void *)ctx->err_part,
                     (void *)ctx->sums, (void *)ctx->stage, (void *)ctx->g_sort,
-                    (void *)ctx->g_start, (void *)ctx->g_pts, (void *)ctx->g_pts32, (void *)ctx->g_rep,
+                    (void *)ctx->g_start, (void *)ctx->g_pts, (void *)ctx->g_pts32,
                     (void *)ctx->amb1_hint, (void *)ctx->amb_hint, (void *)ctx->fb_list,
                     (void *)ctx->fb_T, (void *)ctx->seed16, (void *)ctx->m4,
                     (void *)ctx->iter_state, (void *)ctx->err_trace_dev, (void *)ctx->digest, (void *)ctx->fold_ticket,
@@ -1638,11 +1657,9 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     TRY(grow(ctx, &ctx->g_pts32, &ctx->g_pts32_cap, nm));
     const size_t gbytes = grid_build_scratch_bytes((int)nm, ncell);
     TRY(grow(ctx, &ctx->g_sort, &ctx->g_sort_cap, gbytes));
-    if (launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, (int)nm, ctx->grid, ctx->g_sort, gbytes,
+    if (launch_grid_build(ctx->model.x, ctx->model.y, ctx->model.z, ctx->m4, (int)nm, ctx->grid, ctx->g_sort, gbytes,
                           ctx->g_start, ctx->g_pts, ctx->g_pts32, ctx->st) != 0)
         return fail(ctx, ICP_E_HIP, "grid build: radix sort failed");
-    TRY(grow(ctx, &ctx->g_rep, &ctx->g_rep_cap, (size_t)ncell));
-    launch_grid_rep(grid_view(ctx), ncell, ctx->g_rep, ctx->st);
     LAUNCHCHK("grid_build");
     for (int k = 0; k < 3; ++k) { // the model's box (the query orders: mid-size loop, bundle filter)
         ctx->m_lo[k] = lo[k];
@@ -1694,20 +1711,13 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     ctx->has_model = true;
     ctx->seeds_valid = false;
     ctx->seedd_valid = false;
-    // a scene in slot order (the last model's box) goes back to file order: icp_run sorts it by
-    // the new box from there, as after set_model then set_scene -- the same order, hence the same
-    // reductions, whichever call came first
-    if (ctx->has_scene && ctx->scene.n && ctx->scene_slot) {
-        DevCloud &P = ctx->scene;
-        TRY(grow_cloud(ctx, ctx->s_tmp, P.n, true));
-        launch_permute_cloud(ctx->s_order, (int)P.n, 1, P.x, P.y, P.z, nullptr, nullptr, ctx->s_tmp.x, ctx->s_tmp.y,
-                             ctx->s_tmp.z, nullptr, nullptr, ctx->st);
-        LAUNCHCHK("scene_to_file_order");
-        std::swap(ctx->scene, ctx->s_tmp);
-        ctx->scene_slot = false;
-    }
-    // the scene's fp32 copy depends on c: refresh it
-    if (ctx->has_scene && ctx->scene.n) {
+    // a scene in slot order (the last model's box) goes back to file order before the next run
+    // sorts it by the new box (scene_revert_now), as after set_model then set_scene -- the same
+    // order, hence the same reductions, whichever call came first.  Not here: a set_scene that
+    // replaces it (every registration of the bench) would make the permutation wasted work
+    if (ctx->has_scene && ctx->scene.n && ctx->scene_slot) ctx->scene_revert = true;
+    // the scene's fp32 copy depends on c: refresh it (a pending revert refreshes it then)
+    if (ctx->has_scene && ctx->scene.n && !ctx->scene_revert) {
         launch_make_f32(ctx->scene.x, ctx->scene.y, ctx->scene.z, ctx->scene.n, ctx->c[0], ctx->c[1],
                         ctx->c[2], ctx->scene.f, ctx->st);
         LAUNCHCHK("make_f32");
@@ -1851,6 +1861,7 @@ static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total, bool
     ctx->seedd_valid = false;
     ctx->q_order_src = nullptr; // new contents: a new query order
     ctx->scene_slot = slot;     // (else in the caller's order)
+    ctx->scene_revert = false;
     ctx->p32_stale = false;
     // a shard against a model of at least twice its points (C5's 8-way shards: the model's cells
     // are finer than the scene's spacing): icp_run's policy takes the bundle cascade for the first
@@ -2211,6 +2222,7 @@ int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp
 static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res, bool no_tail)
 {
     TRY(check_ready(ctx, true));
+    TRY(scene_revert_now(ctx));
     // alignement_check (gpu.cc:54-62)
     if (ctx->np_total != ctx->nm && !ctx->allow_unequal)
         return fail(ctx, ICP_E_SIZE_MISMATCH, "Point sets need to have the same number of points.");

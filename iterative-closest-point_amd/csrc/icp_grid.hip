@@ -86,15 +86,15 @@ __global__ __launch_bounds__(kBlock) void grid_starts_kernel(const unsigned *__r
     start[c] = lo;
 }
 
-__global__ __launch_bounds__(kBlock) void grid_gather_kernel(const double *__restrict__ mx, const double *__restrict__ my,
-                                                           const double *__restrict__ mz, int nm,
+__global__ __launch_bounds__(kBlock) void grid_gather_kernel(const double4 *__restrict__ m4, int nm,
                                                            const int *__restrict__ sval, double4 *__restrict__ pts,
                                                            float4 *__restrict__ pts32, double c0, double c1, double c2)
 {
     const int k = blockIdx.x * kBlock + threadIdx.x;
     if (k >= nm) return;
     const int i = sval[k];
-    const double x = mx[i], y = my[i], z = mz[i];
+    const double4 m = m4[i]; // (one 32-byte record: the SoA streams would cost a line each)
+    const double x = m.x, y = m.y, z = m.z;
     pts[k] = make_double4(x, y, z, (double)i);
     // (the fp32 image: offsets from the box centre, the index's bits in w)
     if (pts32) pts32[k] = make_float4((float)(x - c0), (float)(y - c1), (float)(z - c2), __int_as_float(i));
@@ -502,48 +502,15 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const doub
     }
 }
 
-// Each empty cell's stand-in seed (set_model, after the grid): the model point nearest the
-// cell's centre over the first ring of cells around it that holds any (rings up to 3), -1 if
-// none.  A cell that holds points needs none (rep = -1 too): nn_grid_cell_seed scans it.
-__global__ __launch_bounds__(kBlock) void grid_rep_kernel(GridView gv, int ncell, int *__restrict__ rep)
-{
-    const int id = blockIdx.x * kBlock + threadIdx.x;
-    if (id >= ncell) return;
-    int r_out = -1;
-    if (gv.start[id] == gv.start[id + 1]) {
-        const int cx = id % gv.g[0], cy = (id / gv.g[0]) % gv.g[1], cz = id / (gv.g[0] * gv.g[1]);
-        const double h = 1.0 / gv.inv_h;
-        const double ctr[3] = {gv.lo[0] + (cx + 0.5) * h, gv.lo[1] + (cy + 0.5) * h, gv.lo[2] + (cz + 0.5) * h};
-        double best = INFINITY;
-        for (int r = 1; r <= 3 && r_out < 0; ++r) {
-            for (int z = max(cz - r, 0); z <= min(cz + r, gv.g[2] - 1); ++z)
-                for (int y = max(cy - r, 0); y <= min(cy + r, gv.g[1] - 1); ++y) {
-                    const int row = (z * gv.g[1] + y) * gv.g[0];
-                    const int a = gv.start[row + max(cx - r, 0)], b = gv.start[row + min(cx + r, gv.g[0] - 1) + 1];
-                    for (int k = a; k < b; ++k) {
-                        const double4 m = gv.pts[k];
-                        const double d = d64g(ctr[0], ctr[1], ctr[2], m.x, m.y, m.z);
-                        const int mi = (int)m.w;
-                        if (d < best || (d == best && mi < r_out)) {
-                            best = d;
-                            r_out = mi;
-                        }
-                    }
-                }
-        }
-    }
-    rep[id] = r_out;
-}
-
 // An unseeded search's seeds, one lane per query: the (D64, index) first minimum over the points
-// of the query's own cell, or the cell's stand-in (grid_rep_kernel) when it is empty -- any model
-// point bounds a complete box; a near one keeps the box small.  seedd[t] = D64(q, m[idx[t]]) with
-// d64g on the same values the seeded scan reads, so the scan meets the seed with d == best.
+// of the query's own cell; for an empty cell, over the two points the cell sits between in the
+// grid's order (the last of the previous non-empty cell, the first of the next: usually its
+// x-neighbours) -- any model point bounds a complete box; a near one keeps the box small.
+// seedd[t] = D64(q, m[idx[t]]) with d64g on the same values the seeded scan reads, so the scan
+// meets the seed with d == best.
 __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const double *__restrict__ px,
                                                                   const double *__restrict__ py,
-                                                                  const double *__restrict__ pz, GridView gv,
-                                                                  const int *__restrict__ rep,
-                                                                  const double4 *__restrict__ m4,
+                                                                  const double *__restrict__ pz, GridView gv, int nm,
                                                                   int *__restrict__ idx, double *__restrict__ seedd)
 {
     const int t = blockIdx.x * kBlock + threadIdx.x;
@@ -552,7 +519,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const 
     const int c = (cell1(q[2], gv.lo[2], gv.inv_h, gv.g[2]) * gv.g[1] + cell1(q[1], gv.lo[1], gv.inv_h, gv.g[1])) *
                       gv.g[0] +
                   cell1(q[0], gv.lo[0], gv.inv_h, gv.g[0]);
-    const int a = gv.start[c], b = gv.start[c + 1];
+    const int a0 = gv.start[c], b0 = gv.start[c + 1];
+    // (empty: the neighbours in the grid's order; nm >= 1, so at least one exists)
+    const int a = a0 < b0 ? a0 : max(a0 - 1, 0), b = a0 < b0 ? b0 : min(a0 + 1, nm);
     double best = INFINITY;
     int bi = -1;
     for (int k = a; k < b; ++k) {
@@ -564,11 +533,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const 
             bi = mi;
         }
     }
-    if (bi < 0) { // (an empty cell: its stand-in, else point 0)
-        bi = max(rep[c], 0);
-        const double4 m = m4[bi];
-        best = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
-    }
+    if (bi < 0) bi = (int)gv.pts[a].w; // (a NaN query: no comparison held -- any valid seed)
     idx[t] = bi;
     seedd[t] = best;
 }
@@ -1369,8 +1334,9 @@ size_t grid_build_scratch_bytes(int nm, long long ncell)
     return grid_keys_bytes(nm) + ((temp + 255) & ~(size_t)255);
 }
 
-int launch_grid_build(const double *mx, const double *my, const double *mz, int nm, const GridParams &p, void *scratch,
-                      size_t bytes, int *start, double4 *pts, float4 *pts32, hipStream_t st)
+int launch_grid_build(const double *mx, const double *my, const double *mz, const double4 *m4, int nm,
+                      const GridParams &p, void *scratch, size_t bytes, int *start, double4 *pts, float4 *pts32,
+                      hipStream_t st)
 {
     const long long ncell = grid_cells(p);
     GridView gv{};
@@ -1388,7 +1354,7 @@ int launch_grid_build(const double *mx, const double *my, const double *mz, int 
         hipSuccess)
         return -1;
     grid_starts_kernel<<<(int)((ncell + kBlock) / kBlock), kBlock, 0, st>>>(k1, nm, (int)ncell, start);
-    grid_gather_kernel<<<g, kBlock, 0, st>>>(mx, my, mz, nm, v1, pts, pts32, p.c32[0], p.c32[1], p.c32[2]);
+    grid_gather_kernel<<<g, kBlock, 0, st>>>(m4, nm, v1, pts, pts32, p.c32[0], p.c32[1], p.c32[2]);
     return 0;
 }
 
@@ -1416,17 +1382,11 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 #undef SEARCH
 }
 
-void launch_grid_rep(const GridView &gv, long long ncell, int *rep, hipStream_t st)
-{
-    if (ncell <= 0) return;
-    grid_rep_kernel<<<(int)((ncell + kBlock - 1) / kBlock), kBlock, 0, st>>>(gv, (int)ncell, rep);
-}
-
-void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv,
-                              const int *rep, const double4 *m4, int *idx, double *seedd, hipStream_t st)
+void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv, int nm,
+                              int *idx, double *seedd, hipStream_t st)
 {
     if (n <= 0) return;
-    nn_grid_cell_seed_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, px, py, pz, gv, rep, m4, idx, seedd);
+    nn_grid_cell_seed_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, px, py, pz, gv, nm, idx, seedd);
 }
 
 void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,

@@ -306,8 +306,9 @@ long long grid_cells(const GridParams &p);
 // the model grid: start[ncells + 1], pts[nm], pts32[nm] (nullable); scratch of
 // grid_build_scratch_bytes(nm, ncells).  Returns 0, or -1 when the sort fails to launch.
 size_t grid_build_scratch_bytes(int nm, long long ncell);
-int launch_grid_build(const double *mx, const double *my, const double *mz, int nm, const GridParams &p, void *scratch,
-                      size_t bytes, int *start, double4 *pts, float4 *pts32, hipStream_t st);
+int launch_grid_build(const double *mx, const double *my, const double *mz, const double4 *m4, int nm,
+                      const GridParams &p, void *scratch, size_t bytes, int *start, double4 *pts, float4 *pts32,
+                      hipStream_t st); // (m4: the model's double4 rows, gathered into pts)
 // For queued query list[t] (t < *count_ptr) with candidate hint[t]: exact fp64 first minimum
 // over the grid box that must contain every point at least as close as the candidate ->
 // idx; hint < 0 or a box over `budget` cells -> appended to fb_list with its window T_in[t]
@@ -316,13 +317,11 @@ int launch_grid_build(const double *mx, const double *my, const double *mz, int 
 // index): seeds for an unseeded f16 brute-force search
 void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,
                          int nm, int *idx, hipStream_t st);
-// rep[ncell]: each empty cell's stand-in seed (the model point nearest its centre in the first
-// ring of cells that holds any, up to 3 rings; else -1), -1 for a cell with points
-void launch_grid_rep(const GridView &gv, long long ncell, int *rep, hipStream_t st);
-// an unseeded search's seeds: idx[t] = the first minimum over query t's own cell (or its
-// stand-in), seedd[t] = its D64 -- the input of the seeded grid pass
-void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv,
-                              const int *rep, const double4 *m4, int *idx, double *seedd, hipStream_t st);
+// an unseeded search's seeds: idx[t] = the first minimum over query t's own cell (an empty
+// cell: over its two neighbours in the grid's order), seedd[t] = its D64 -- the input of the
+// seeded grid pass
+void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv, int nm,
+                              int *idx, double *seedd, hipStream_t st);
 // inline_nm > 0 (a model of that many points): queries the grid cannot take are scanned
 // exactly in place (no fallback queue, no nn_resolve launch)
 // seeded grid variant: every query's previous correspondence (idx[t]) as the candidate, its
