@@ -807,6 +807,10 @@ constexpr int kIterWideMax = kCanonStrandsMax * kCanonChunk;
 #ifndef ICP_ITER_PREFETCH
 #define ICP_ITER_PREFETCH 1 // (the next task's point, correspondence and index loaded during this one)
 #endif
+#ifndef ICP_ITER_LDS_TREE
+#define ICP_ITER_LDS_TREE 1 // (the chunk trees through LDS, one column a lane; 0: DPP trees)
+#endif
+constexpr int kLeafStride = 33; // (doubles a column of the leaf tile: lane k's reads fall in distinct banks)
 #ifndef ICP_ITER_KR
 #define ICP_ITER_KR 2 // (the walk: rows whose bounds a lane reads together)
 #endif
@@ -841,6 +845,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
     constexpr int QW = 64 / G;        // queries a wave
     constexpr int NW = kBlock / 64 * H; // waves a workgroup
     __shared__ float4 s_pts[NW][STAGE ? kIterPts : 1];
+    __shared__ double s_leaf[NW][G == 2 && ICP_ITER_LDS_TREE ? kCanonCols * kLeafStride : 1];
     __shared__ int s_rbase[NW][STAGE ? kIterRows + 1 : 1], s_rstart[NW][STAGE ? kIterRows : 1];
     // (st is uniform: its fields are scalar loads into SGPRs -- an LDS copy would hold the
     // transform's 15 doubles in VGPRs all kernel long)
@@ -1167,6 +1172,40 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
         // one column at a time (moment_leaves' terms)
         const double d[6] = {active ? q[0] - cp[0] : 0.0, active ? q[1] - cp[1] : 0.0, active ? q[2] - cp[2] : 0.0,
                              active ? y[0] - cy[0] : 0.0, active ? y[1] - cy[1] : 0.0, active ? y[2] - cy[2] : 0.0};
+        if constexpr (G == 2 && ICP_ITER_LDS_TREE) {
+            // the 18 x 32 leaves through LDS: lane k < 18 folds column k by the chunk's pairwise
+            // tree in registers (31 adds; the DPP trees take 18 x 5 steps of two moves and an add)
+            double *const lf = s_leaf[wave];
+#pragma unroll
+            for (int k = 0; k < kCanonCols; ++k) {
+                double leaf;
+                if (k < 6) leaf = 0.0 + d[k];
+                else if (k < 15) leaf = 0.0 + d[(k - 6) / 3] * d[3 + (k - 6) % 3];
+                else if (k == 15) leaf = 0.0 + ((d[3] * d[3] + d[4] * d[4]) + d[5] * d[5]);
+                else if (k == 16) leaf = 0.0 + ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+                else leaf = active ? 0.0 + e : 0.0;
+                if (!active) leaf = 0.0;
+                if (sub == 0) lf[k * kLeafStride + u] = leaf;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < kCanonCols) {
+                const double *col = lf + lane * kLeafStride;
+                double part[4];
+#pragma unroll
+                for (int g8 = 0; g8 < 4; ++g8) {
+                    double v[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = col[8 * g8 + j];
+                    part[g8] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+                }
+                acc = acc + ((part[0] + part[1]) + (part[2] + part[3]));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else
 #pragma unroll
         for (int k = 0; k < kCanonCols; ++k) {
             double leaf;
