@@ -807,6 +807,9 @@ constexpr int kIterWideMax = kCanonStrandsMax * kCanonChunk;
 #ifndef ICP_ITER_PREFETCH
 #define ICP_ITER_PREFETCH 1 // (the next task's point, correspondence and index loaded during this one)
 #endif
+#ifndef ICP_ITER_RELOAD
+#define ICP_ITER_RELOAD 0 // (1: the transform and shifts re-read from st at every task)
+#endif
 #ifndef ICP_ITER_LDS_TREE
 #define ICP_ITER_LDS_TREE 1 // (the chunk trees through LDS, one column a lane; 0: DPP trees)
 #endif
@@ -850,9 +853,14 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
     // (st is uniform: its fields are scalar loads into SGPRs -- an LDS copy would hold the
     // transform's 15 doubles in VGPRs all kernel long)
     if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
-    const Xform xf = st->xf;
-    const double cp[3] = {st->shift_p[0], st->shift_p[1], st->shift_p[2]};
-    const double cy[3] = {st->shift_y[0], st->shift_y[1], st->shift_y[2]};
+    // (ICP_ITER_RELOAD=1: the transform and the shifts re-read from st at each task -- scalar
+    // loads where values held across the task spill to VGPR lanes, a v_readlane at every use;
+    // measured slower, 0.153 against 0.148 ms a C4 iteration, profiles/r05r)
+    auto fresh = [&]() {
+        const IterState *p = st;
+        if (ICP_ITER_RELOAD) __asm__ volatile("" : "+s"(p)); // (no hoisting: the loads stay inside the task)
+        return p;
+    };
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane / G, sub = lane % G;
     const int half = wave % H; // (G = 4: which 16 queries of the chunk)
     const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
@@ -891,7 +899,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
             y[1] = fy[1];
             y[2] = fy[2];
             h = fh;
-            transform_point(xf, p0, p1, p2, q[0], q[1], q[2]);
+            transform_point(fresh()->xf, p0, p1, p2, q[0], q[1], q[2]);
         }
         if (ICP_ITER_PREFETCH && c + S < C) fetch(c + S);
         const double e = active ? residual2(y[0], y[1], y[2], q[0], q[1], q[2]) : 0.0;
@@ -900,7 +908,11 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
             px[t] = q[0];
             py[t] = q[1];
             pz[t] = q[2];
-            if (p32) p32[t] = make_float4((float)(q[0] - xf.c[0]), (float)(q[1] - xf.c[1]), (float)(q[2] - xf.c[2]), 0.0f);
+            if (p32) {
+                const IterState *sp = fresh();
+                p32[t] = make_float4((float)(q[0] - sp->xf.c[0]), (float)(q[1] - sp->xf.c[1]), (float)(q[2] - sp->xf.c[2]),
+                                     0.0f);
+            }
             far += e > far_d2 ? 1 : 0;
         }
         // B: the query's complete box around its seed, the task's union of them
@@ -1049,6 +1061,9 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                 }
             } else { // nn_grid_seeded32_kernel's walk (2 lanes a query, 2 rows' bounds, 2 loads in flight)
                 constexpr int KR = ICP_ITER_KR, KU = ICP_ITER_KU;
+                // (r / ny by an fp32 reciprocal: r < 2^12 and ny <= 125 keep (r + 0.5) / ny at least
+                // 0.004 from an integer, far beyond fp32's error -- no integer division in the loop)
+                const float inv_ny = 1.0f / (float)ny;
                 for (int r0 = sub; r0 < nrq; r0 += KR * G) {
                     int k0[KR], pre[KR + 1];
                     pre[0] = 0;
@@ -1057,7 +1072,8 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                         const int r = r0 + v * G;
                         int a0 = 0, a1 = 0;
                         if (r < nrq) {
-                            const int gy = c0[1] + r % ny, gz = c0[2] + r / ny;
+                            const int rz = (int)(((float)r + 0.5f) * inv_ny), ry = r - rz * ny;
+                            const int gy = c0[1] + ry, gz = c0[2] + rz;
                             const int row = (gz * gv.g[1] + gy) * gv.g[0];
                             a0 = gv.start[row + c0[0]];
                             a1 = gv.start[row + c1[0] + 1];
@@ -1170,6 +1186,9 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
         }
         // G: this chunk's 17 moments and the residual (leaves in the odd lanes), into the strand;
         // one column at a time (moment_leaves' terms)
+        const IterState *sh_ = fresh();
+        const double cp[3] = {sh_->shift_p[0], sh_->shift_p[1], sh_->shift_p[2]};
+        const double cy[3] = {sh_->shift_y[0], sh_->shift_y[1], sh_->shift_y[2]};
         const double d[6] = {active ? q[0] - cp[0] : 0.0, active ? q[1] - cp[1] : 0.0, active ? q[2] - cp[2] : 0.0,
                              active ? y[0] - cy[0] : 0.0, active ? y[1] - cy[1] : 0.0, active ? y[2] - cy[2] : 0.0};
         if constexpr (G == 2 && ICP_ITER_LDS_TREE) {
