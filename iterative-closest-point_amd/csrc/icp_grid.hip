@@ -807,6 +807,10 @@ constexpr int kIterWideMax = kCanonStrandsMax * kCanonChunk;
 #ifndef ICP_ITER_PREFETCH
 #define ICP_ITER_PREFETCH 1 // (the next task's point, correspondence and index loaded during this one)
 #endif
+#ifndef ICP_ITER_DBG
+#define ICP_ITER_DBG 0 // (1: the phase clocks and counters ICP_ITER_DEBUG reads -- 12 VGPRs of counters)
+#endif
+constexpr bool kIterDbg = ICP_ITER_DBG != 0;
 #ifndef ICP_ITER_RELOAD
 #define ICP_ITER_RELOAD 0 // (1: the transform and shifts re-read from st at every task)
 #endif
@@ -835,9 +839,9 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
 {
     // dbg (nullable, ICP_ITER_DEBUG): per-wave phase clocks (s_memrealtime, 100 MHz) and counts
     unsigned long long dcnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tclk = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long tclk = kIterDbg && dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     auto lap = [&](int f) {
-        if (dbg) {
+        if (kIterDbg && dbg) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             dcnt[f] += now - tclk;
             tclk = now;
@@ -1000,7 +1004,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
             }
         }
         lap(6);
-        if (dbg) {
+        if (kIterDbg && dbg) {
             dcnt[0] += 1;
             dcnt[1] += staged ? 1 : 0;
             dcnt[2] += staged ? (unsigned long long)total : 0ull;
@@ -1021,7 +1025,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
             constexpr int kCand = ICP_ITER_KCAND;
             int cand[kCand], nc = 0;
             auto flush = [&]() {
-                if (dbg) dcnt[4] += (unsigned long long)nc; // (per lane; summed over the wave below)
+                if (kIterDbg && dbg) dcnt[4] += (unsigned long long)nc; // (per lane; summed over the wave below)
                 double4 w[kCand];
 #pragma unroll
                 for (int j = 0; j < kCand; ++j) w[j] = gv.pts[cand[j < nc ? j : 0]];
@@ -1133,7 +1137,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
         // whole wave: the box up to `budget` cells, else every model point
         unsigned long long bigm = __ballot(active && !ok && sub == 0);
         nbig += __popcll(bigm);
-        if (dbg) dcnt[3] += __popcll(bigm);
+        if (kIterDbg && dbg) dcnt[3] += __popcll(bigm);
         while (bigm) {
             const int bl = __ffsll((long long)bigm) - 1;
             bigm &= bigm - 1;
@@ -1244,9 +1248,9 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
         }
         lap(9);
     }
-    if (dbg)
+    if (kIterDbg && dbg)
         for (int o = 32; o >= 1; o >>= 1) dcnt[4] += __shfl_xor(dcnt[4], o, 64);
-    if (dbg && lane == 0)
+    if (kIterDbg && dbg && lane == 0)
         for (int f = 0; f < 12; ++f)
             if (dcnt[f]) atomicAdd(dbg + f, dcnt[f]);
     // the workgroup's four strands -> its row (column k from lane k of each wave)
@@ -1342,10 +1346,17 @@ GridParams grid_params_box(const double lo[3], const double hi[3], size_t nm)
         p.inv_h = 1.0;
         return p;
     }
-    // ~2 model points per cell of the bounding box (flat axes count as 1e-3 of the largest)
+    // ~2 model points per cell of the bounding box (flat axes count as 1e-3 of the largest);
+    // ICP_GRID_PPC: another density (A/B: 1 point a cell ran the C4 iteration 3% faster and the
+    // W = 8 shard's 6% slower, 0.5 both slower -- profiles/r05s/ppc_ab.log)
+    static const double ppc = [] {
+        const char *e = getenv("ICP_GRID_PPC");
+        const double v = e ? atof(e) : 0.0;
+        return v > 0.0 ? v : 2.0;
+    }();
     double vol = 1.0;
     for (int a = 0; a < 3; ++a) vol *= std::max(ext[a], emax * 1e-3);
-    double h = std::cbrt(vol * 2.0 / (double)std::max<size_t>(nm, 1));
+    double h = std::cbrt(vol * ppc / (double)std::max<size_t>(nm, 1));
     auto dims = [&](double hh, int g[3]) {
         long long tot = 1;
         for (int a = 0; a < 3; ++a) {
