@@ -14,6 +14,7 @@
 #include "icp_canon.h"
 #include "icp_device.h"
 #include "icp_fold.h"
+#include "icp_gridbox.h"
 #include "icp_kernels.h"
 #include "icp_mfma16.h"
 
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void canon_transform_kernel(
             pz[i] = q2;
             if (p32) p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
             if (sa.seedd) sa.seedd[i] = e;
-            far += e > sa.far_d2 && sa.far_acc ? 1 : 0;
+            far += sa.far_acc && seed_far(sa, q0, q1, q2, e) ? 1 : 0;
             if constexpr (QOP) {
                 BundleQuery r;
                 double4 raw;

@@ -1863,13 +1863,15 @@ static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total, bool
     ctx->scene_slot = slot;     // (else in the caller's order)
     ctx->scene_revert = false;
     ctx->p32_stale = false;
-    // a shard against a model of at least twice its points (C5's 8-way shards: the model's cells
-    // are finer than the scene's spacing): icp_run's policy takes the bundle cascade for the first
-    // searches, so its images are built here rather than between two iterations of the run (the
-    // lazy build between iterations gives the same results; ICP_EAGER_BUNDLE=0 leaves it to
-    // that).  Only for a scene the bundle filter would search (level1_kind == 3, the slot order)
+    // ICP_EAGER_BUNDLE=1: a shard against a model of at least twice its points (C5's 8-way shards)
+    // gets the bundle images here instead of at their first use.  Round 4 built them here always:
+    // its far rule sent a C5 shard's first searches to the bundle cascade.  With the box rule
+    // (run_loop: the queries whose clamped box the grid walk cannot take) the same shard stays on
+    // the grid (0.9% of its points against the n/32 threshold), and a scene that does need the
+    // cascade builds the images between two iterations (the same results, tests/test_gpu_lazy_bundle.py).
+    // Only for a scene the bundle filter would search (level1_kind == 3, the slot order)
     const char *eager_env = getenv("ICP_EAGER_BUNDLE"); // (read per call: tests toggle it)
-    const bool eager = !(eager_env && eager_env[0] == '0');
+    const bool eager = eager_env && eager_env[0] == '1';
     if (eager && ctx->bundle_pending && np_local > 0 && ctx->nm >= 2 * np_local &&
         ctx->nn_variant == ICP_NN_VARIANT_AUTO && ctx->nn_mode == ICP_NN_CERTIFIED && level1_kind(ctx, np_local) == 3 &&
         want_slot_order(ctx, np_local))
@@ -2331,10 +2333,24 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     int q2_obs = carry ? ctx->last_q2 : -1;   // queued2 of the last iteration the host has seen
     bool grid_next = carry && far_obs >= 0 && far_obs <= far_thr; // the path of the next search
     SeedArgs sa_grid;       // a transform before a grid search: its seed distances only
+    // The far count's rule: a moved point whose complete box around its seed distance, clamped to
+    // the grid, exceeds kSeededBox cells -- the queries the seeded grid search could not take in
+    // its walk.  Round 4 counted points farther than 1.5 cells from their correspondence, which
+    // also counted the points outside the model's box whose clamped box is small: a C5 shard (3.9%
+    // of its points outside, 0.9% with a big box) then built the bundle images for its first
+    // iterations (15 ms of a 31 ms registration).  ICP_GRID_FAR=dist: the distance rule (A/B).
+    static const bool far_dist = [] {
+        const char *e = getenv("ICP_GRID_FAR");
+        return e && std::string(e) == "dist";
+    }();
     if (grid_policy) {
         const double h = 1.0 / ctx->grid.inv_h;
         sa.far_acc = sa_grid.far_acc = &ctx->iter_state->far_acc;
         sa.far_d2 = sa_grid.far_d2 = 2.25 * h * h;
+        if (!far_dist) {
+            sa.far_gv = sa_grid.far_gv = grid_view(ctx);
+            sa.far_box = sa_grid.far_box = kSeededBox;
+        }
         sa_grid.seedd = sa.seedd; // (grid_seeded_search reads them: no gather of the seed point)
     }
     // What the last enqueued transform wrote for the next search (nn_search_begin uses each part
@@ -2570,7 +2586,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
                     launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd, need_p32 ? P.f : nullptr,
                                         grid_view(ctx), kSeededBox, grid_budget(ctx), (int)ctx->nm, ctx->m4,
-                                        ctx->canon_rowbuf, grid_policy ? &sd->far_acc : nullptr, sa_grid.far_d2,
+                                        ctx->canon_rowbuf, grid_policy ? &sd->far_acc : nullptr,
+                                        sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2,
                                         ctx->amb_count + 2, ctx->st, iter_dbg);
                     LAUNCHCHK("nn_grid_iter");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));

@@ -26,6 +26,7 @@
 
 #include "icp_canon.h"
 #include "icp_device.h"
+#include "icp_gridbox.h"
 #include "icp_kernels.h"
 
 namespace icp {
@@ -40,18 +41,6 @@ __device__ __forceinline__ double d64g(double px, double py, double pz, double m
     return (dx * dx + dy * dy) + dz * dz; // cpu.cc:17-19 order, no FMA (-ffp-contract=off)
 }
 
-// the cell of a coordinate t in cell units (t = (x - lo) inv_h), clamped to [0, g - 1]: monotone in t
-__device__ __forceinline__ int cellt(double t, int g)
-{
-    if (!(t > 0.0)) return 0;
-    if (t >= (double)(g - 1)) return g - 1;
-    return (int)t;
-}
-
-__device__ __forceinline__ int cell1(double x, double lo, double inv_h, int g)
-{
-    return cellt((x - lo) * inv_h, g);
-}
 
 // The grid build (launch_grid_build): every model point's cell id, a stable radix sort of
 // (cell, index) pairs, each cell's start by a binary search of the sorted ids, and the points
@@ -243,21 +232,6 @@ template <int G = kGroup> __device__ __forceinline__ void group_lex_min(double &
     }
 }
 
-// the cell box that must hold every m with D64(q, m) <= r2 (see the header); false if over budget
-__device__ __forceinline__ bool complete_box(const double q[3], double r2, const GridView &gv, int budget,
-                                             int c0[3], int c1[3])
-{
-    const double R = sqrt(r2);
-    long long cells = 1;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const double s = (fabs(q[a]) + R) * 0x1.0p-44;
-        c0[a] = cell1(q[a] - (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
-        c1[a] = cell1(q[a] + (R + s), gv.lo[a], gv.inv_h, gv.g[a]);
-        cells *= (long long)(c1[a] - c0[a] + 1);
-    }
-    return cells <= budget;
-}
 
 // The box's rows trimmed to the sphere (round 4): the x-cells of row (cy, cz) that can hold a
 // point m with D64(q, m) <= best, narrowed from [x0, x1] (false: the row holds none).  fp32 in
@@ -917,12 +891,13 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                 p32[t] = make_float4((float)(q[0] - sp->xf.c[0]), (float)(q[1] - sp->xf.c[1]), (float)(q[2] - sp->xf.c[2]),
                                      0.0f);
             }
-            far += e > far_d2 ? 1 : 0;
+            if (far_d2 >= 0.0) far += e > far_d2 ? 1 : 0; // (far_d2 < 0: the box rule, below)
         }
         // B: the query's complete box around its seed, the task's union of them
         double best = e;
         int bi = h, bk = -1, c0[3] = {0, 0, 0}, c1[3] = {-1, -1, -1};
         const bool ok = active && h >= 0 && e == e && e < INFINITY && complete_box(q, e, gv, box, c0, c1);
+        if (far_d2 < 0.0 && active && sub == 0 && !ok) ++far; // (a box over `box` cells: SeedArgs::far_box's rule)
         int lo3[3], hi3[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {

@@ -464,6 +464,12 @@ struct SeedArgs {
     // next seeded grid search's queries with a big box (icp_run's search policy)
     int *far_acc = nullptr;
     double far_d2 = 0.0;
+    // far_box > 0: "far" is instead a query whose complete box around its seed distance (on
+    // far_gv, clamped to the grid) exceeds far_box cells -- the queries the next seeded grid
+    // search could not take in its walk (a point outside the model's box, whose box the grid
+    // clamps, is far only if even the clamped box is big)
+    GridView far_gv{};
+    int far_box = 0;
 };
 // same, the transform read from device memory (the device Horn solve); a no-op once *done
 void launch_transform_err_dev(double *px, double *py, double *pz, const double *yx, const double *yy,

@@ -9,6 +9,7 @@
 #include "icp_bundle_rec.h"
 #include "icp_device.h"
 #include "icp_fold.h"
+#include "icp_gridbox.h"
 #include "icp_kernels.h"
 #include "icp_mfma16.h"
 
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
                     p32[i] = make_float4((float)(q0 - xf.c[0]), (float)(q1 - xf.c[1]), (float)(q2 - xf.c[2]), 0.0f);
                 const double dx = q0 - y0, dy = q1 - y1, dz = q2 - y2;
                 const double d2 = (dx * dx + dy * dy) + dz * dz;
-                far += d2 > sa.far_d2 ? 1 : 0;
+                far += sa.far_acc && seed_far(sa, q0, q1, q2, d2) ? 1 : 0;
                 // (the seed distance too, as the plain form writes it: a later grid search -- of
                 // this run, or of the next one carrying over -- reads it)
                 if (sa.seedd) sa.seedd[i] = d2;
@@ -209,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void transform_err_kernel(
                     const double dx = q0 - y0[u], dy = q1 - y1[u], dz = q2 - y2[u];
                     const double d2 = (dx * dx + dy * dy) + dz * dz;
                     if (sa.seedd) sa.seedd[i] = d2;
-                    far += d2 > sa.far_d2 ? 1 : 0;
+                    far += sa.far_acc && seed_far(sa, q0, q1, q2, d2) ? 1 : 0;
                 }
             }
         }

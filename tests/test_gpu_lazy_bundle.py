@@ -7,9 +7,9 @@ first minimum whichever path runs it (the bundle cascade or the grid), so a regi
 follow the same trajectory bit for bit however the images come to be built and whichever
 transform form preceded each search.  Cases:
 
-  * C5 sizes (a 2^20-point shard against the 2^23-point model, BASELINE configs[4]) with the
-    eager build of icp_set_scene switched off (ICP_EAGER_BUNDLE=0): the policy turns to the
-    bundle cascade mid-run and builds the images between two iterations.  Twice on one context
+  * C5 sizes (a 2^20-point shard against the 2^23-point model, BASELINE configs[4]) rotated 30°
+    with the images left to their first use (ICP_EAGER_BUNDLE=0, the default since round 5): the
+    policy turns to the bundle cascade mid-run and builds the images between two iterations.  Twice on one context
     with icp_set_model in between -- the second registration is the one the round-4 stall hit
     (its transforms wrote global-form slot records for a search that, its images built in
     between, ran the local form) -- against a fresh context with the eager build, bit for bit,
@@ -66,7 +66,7 @@ def assert_same(a, b):
 
 def test_c5_shard_mid_run_bundle_build(amd, oracle, monkeypatch):
     n = 1 << 23
-    m, p = amd.synthetic_pair(n, seed=42, angle_deg=10.0)
+    m, p = amd.synthetic_pair(n, seed=42, angle_deg=30.0)  # (far enough that the policy turns to the bundle)
     b, c = amd.shard_range(n, 0, 8)
     shard = np.ascontiguousarray(p[b:b + c])
     iters = 12
