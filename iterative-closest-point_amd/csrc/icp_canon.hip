@@ -10,6 +10,8 @@
 // all-reduced before the error and Horn steps.  Compiled with -ffp-contract=off.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "icp_bundle_rec.h"
 #include "icp_canon.h"
 #include "icp_device.h"
@@ -251,6 +253,63 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
     if constexpr (MODE == 1) horn_step_body(s_sum, cs.N, cs.c[0], cs.c[1], cs.c[2], 1, cs.cnt, cs.s);
 }
 
+
+// The same fold, one column a workgroup (18 workgroups: the rows' 295 KB read by 18 CUs instead
+// of one): workgroup k computes column k exactly as canon_fold_kernel does (thread t's rows in
+// order, the wave trees, the 8 waves' pairwise tree: the same bits).  MODE 1: the last workgroup
+// to finish (an agent-scope ticket, release before and acquire after) runs the error step and
+// the Horn step on the 18 sums.  MODE 0: the sums only (several ranks: the all-reduce follows).
+template <int MODE>
+__global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const double *__restrict__ rows, int R,
+                                                                       double *__restrict__ sums, CanonStep cs)
+{
+    __shared__ double sh[kFoldThreads / 64];
+    __shared__ double s_sum[kCanonCols];
+    __shared__ int s_last;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, k = blockIdx.x;
+    const double *col = rows + (size_t)k * R;
+    double a = 0.0;
+    constexpr int U = 4;
+    for (int r0 = threadIdx.x; r0 < R; r0 += U * kFoldThreads) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + u * kFoldThreads;
+            v[u] = r < R ? col[r] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (r0 + u * kFoldThreads < R) a = a + v[u];
+    }
+    const double w = wave_tree_halves(a);
+    const double two = lane_value(w, 31) + lane_value(w, 63);
+    if (lane == 0) sh[wave] = two;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t[kFoldThreads / 64];
+#pragma unroll
+        for (int i = 0; i < kFoldThreads / 64; ++i) t[i] = sh[i];
+#pragma unroll
+        for (int span = 1; span < kFoldThreads / 64; span <<= 1)
+#pragma unroll
+            for (int i = 0; i < kFoldThreads / 64; i += 2 * span) t[i] = t[i] + t[i + span];
+        __hip_atomic_store(sums + k, t[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (MODE == 1) {
+            __atomic_thread_fence(__ATOMIC_RELEASE); // (this column before the ticket)
+            s_last = __hip_atomic_fetch_add(cs.fold_ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                     kCanonCols - 1;
+        }
+    }
+    if constexpr (MODE == 0) return;
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE); // (every column's sum)
+    for (int i = 0; i < kCanonCols; ++i) s_sum[i] = __hip_atomic_load(sums + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *cs.fold_ticket = 0; // (the next iteration's ticket: stream order puts the next fold after this kernel)
+    err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state, cs.h_trace);
+    horn_step_body(s_sum, cs.N, cs.c[0], cs.c[1], cs.c[2], 1, cs.cnt, cs.s);
+}
+
 } // namespace
 
 void launch_canon_moments(const int *idx, const double4 *m4, const double *px, const double *py, const double *pz,
@@ -280,6 +339,16 @@ void launch_canon_transform(double *px, double *py, double *pz, const double *yx
 void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st)
 {
     const int R = canon_rows((size_t)(n > 0 ? n : 1));
+    // (ICP_FOLD_ONE=1: the 18 columns in one workgroup, A/B)
+    static const bool one = [] {
+        const char *e = getenv("ICP_FOLD_ONE");
+        return e && atoi(e) == 1;
+    }();
+    if (!one && cs.fold_ticket && (mode == 0 || mode == 1)) {
+        if (mode == 0) canon_fold_cols_kernel<0><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
+        else canon_fold_cols_kernel<1><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
+        return;
+    }
     switch (mode) {
     case 0: canon_fold_kernel<0, kCanonCols, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
     case 1: canon_fold_kernel<0, kCanonCols, 1><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;

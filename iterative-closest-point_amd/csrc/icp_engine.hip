@@ -248,6 +248,7 @@ struct icp_ctx {
     double *err_part = nullptr; // (multi-rank icp_run: the transform's residual partials, run_loop)
     size_t err_part_cap = 0;
     double *canon_rowbuf = nullptr; // (icp_run over a scene in slot order: the canonical rows, icp_canon.h)
+    int *canon_ticket = nullptr;    // (the fold's workgroup ticket, CanonStep::fold_ticket)
     size_t canon_rowbuf_cap = 0;
     int *h_far = nullptr; // (pinned: a far count read back once, run_loop's hold_first)
     double *sums = nullptr;
@@ -1514,7 +1515,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->cr_count, (void *)ctx->cr_fix, (void *)ctx->tail_part, (void *)ctx->tail_sync,
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
                     (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame,
-                    (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos, (void *)ctx->canon_rowbuf})
+                    (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos, (void *)ctx->canon_rowbuf,
+                    (void *)ctx->canon_ticket})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -2517,6 +2519,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     cs.h_trace = ctx->d_trace;
     for (int a = 0; a < 3; ++a) cs.c[a] = ctx->c[a];
     cs.cnt = ctx->amb_count;
+    if (!ctx->canon_ticket) {
+        HIPCHK(hipMalloc((void **)&ctx->canon_ticket, sizeof(int)));
+        HIPCHK(hipMemsetAsync(ctx->canon_ticket, 0, sizeof(int), ctx->st));
+    }
+    cs.fold_ticket = ctx->canon_ticket;
     // the canonical transform of the last Horn step's (s, R, t), in the form sa_t (its residual into
     // the rows' kSumErr column, and what the next search reads)
     auto canon_transform = [&](SeedArgs sa_t) -> int {

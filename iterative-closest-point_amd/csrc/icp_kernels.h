@@ -511,6 +511,7 @@ struct CanonStep {
     double *h_trace = nullptr;
     double c[3] = {0.0, 0.0, 0.0};
     int *cnt = nullptr;
+    int *fold_ticket = nullptr; // (zeroed device int: the one-column-a-workgroup fold's ticket)
 };
 // rows: canon_rows(n) x 18 doubles, by column (k R + r).  Moments -> columns 0..16 (y from the search when y_ready,
 // else gathered through kpos / idx and stored); transform -> column kSumErr plus SeedArgs'
