@@ -244,7 +244,7 @@ void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bim
                        hipStream_t st, const int *stop = nullptr, unsigned long long *counters = nullptr,
                        const float4 *bframe = nullptr); // (bframe: the local pair test, pimg = its image);
 // order[k] = the query processed k-th: the queries sorted by the Morton code of their cell in a
-// 1024^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
+// 256^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
 // = k); scratch: query_order_scratch_bytes(n)
 size_t query_order_scratch_bytes(int n);
 // stable LSD radix sort of (key, value) pairs on the low `bits` key bits (rocprim onesweep at

@@ -1,4 +1,4 @@
-// icp_order.hip — query orders: the bundle filter's (launch_query_order, a 30-bit Morton
+// icp_order.hip — query orders: the bundle filter's (launch_query_order, a 24-bit Morton
 // order over the model's box) and the mid-size one-launch loop's search order (icp_iter.hip,
 // icp_persistent_mid_kernel): the scene's queries sorted by the Morton cell of a 32^3 grid over
 // the model's box that holds them, stably (file order within a cell), so that the four queries
@@ -52,14 +52,16 @@ __global__ __launch_bounds__(kBlock) void order_pos_kernel(const int *__restrict
 
 constexpr int kOrderBits = 15;
 
-// 10 bits per axis (1024^3 cells) -> 30-bit Morton key
-__device__ __forceinline__ unsigned morton30(double x, double y, double z, const OrderBox &bx)
+// 8 bits per axis (256^3 cells over the model's box) -> 24-bit Morton key: three onesweep passes of
+// 8-bit digits where 30 bits took four (each ~26 us at 2^20 pairs with its two state resets,
+// profiles/r05m); a cell is a third of the grid's, ~0.06 points (ties in file order: stable)
+__device__ __forceinline__ unsigned morton24(double x, double y, double z, const OrderBox &bx)
 {
     auto cell = [](double v, double l, double s) {
         const double t = (v - l) * s;
-        return !(t > 0.0) ? 0u : t >= 1023.0 ? 1023u : (unsigned)t;
+        return !(t > 0.0) ? 0u : t >= 255.0 ? 255u : (unsigned)t;
     };
-    auto spread = [](unsigned v) { // 10 bits -> every third bit
+    auto spread = [](unsigned v) { // (up to 10 bits) -> every third bit
         v = (v | (v << 16)) & 0x030000ffu;
         v = (v | (v << 8)) & 0x0300f00fu;
         v = (v | (v << 4)) & 0x030c30c3u;
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void query_keys_kernel(const double *__rest
 {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= n) return;
-    key[q] = morton30(px[q], py[q], pz[q], bx);
+    key[q] = morton24(px[q], py[q], pz[q], bx);
     val[q] = q;
 }
 
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void query_keys_aos_kernel(const double *__
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= n) return;
     const double *p = aos + 3 * (size_t)q;
-    key[q] = morton30(p[0], p[1], p[2], bx);
+    key[q] = morton24(p[0], p[1], p[2], bx);
     val[q] = q;
 }
 
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void gather_aos_kernel(const int *__restric
     f[s] = make_float4((float)(a - cx), (float)(b - cy), (float)(c - cz), 0.0f);
 }
 
-constexpr int kQueryOrderBits = 30;
+constexpr int kQueryOrderBits = 24;
 
 // dst[s] = src[order[s]] (into the slot order) or dst[order[s]] = src[s] (back to file order);
 // each of the xyz / fp32 / index streams is moved when both its pointers are non-null
@@ -181,7 +183,7 @@ static OrderBox query_box(const double lo[3], const double hi[3])
     OrderBox bx;
     for (int k = 0; k < 3; ++k) {
         bx.lo[k] = lo[k];
-        bx.sc[k] = hi[k] > lo[k] ? 1024.0 / (hi[k] - lo[k]) : 0.0;
+        bx.sc[k] = hi[k] > lo[k] ? 256.0 / (hi[k] - lo[k]) : 0.0;
     }
     return bx;
 }
