@@ -249,8 +249,10 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
     if constexpr (MODE == 0) return;
     __syncthreads();
     if (threadIdx.x != 0) return;
-    err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state, cs.h_trace);
-    if constexpr (MODE == 1) horn_step_body(s_sum, cs.N, cs.c[0], cs.c[1], cs.c[2], 1, cs.cnt, cs.s);
+    if constexpr (MODE != 4)
+        err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state,
+                      cs.h_trace);
+    if constexpr (MODE == 1 || MODE == 4) horn_step_body(s_sum, cs.N, cs.c[0], cs.c[1], cs.c[2], 1, cs.cnt, cs.s);
 }
 
 
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const dou
 #pragma unroll
             for (int i = 0; i < kFoldThreads / 64; i += 2 * span) t[i] = t[i] + t[i + span];
         __hip_atomic_store(sums + k, t[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if constexpr (MODE == 1) {
+        if constexpr (MODE != 0) {
             __atomic_thread_fence(__ATOMIC_RELEASE); // (this column before the ticket)
             s_last = __hip_atomic_fetch_add(cs.fold_ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
                      kCanonCols - 1;
@@ -306,7 +308,9 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const dou
     __atomic_thread_fence(__ATOMIC_ACQUIRE); // (every column's sum)
     for (int i = 0; i < kCanonCols; ++i) s_sum[i] = __hip_atomic_load(sums + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *cs.fold_ticket = 0; // (the next iteration's ticket: stream order puts the next fold after this kernel)
-    err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state, cs.h_trace);
+    if constexpr (MODE == 1)
+        err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state,
+                      cs.h_trace);
     horn_step_body(s_sum, cs.N, cs.c[0], cs.c[1], cs.c[2], 1, cs.cnt, cs.s);
 }
 
@@ -344,14 +348,16 @@ void launch_canon_fold(const double *rows, int n, double *sums, int mode, const 
         const char *e = getenv("ICP_FOLD_ONE");
         return e && atoi(e) == 1;
     }();
-    if (!one && cs.fold_ticket && (mode == 0 || mode == 1)) {
+    if (!one && cs.fold_ticket && (mode == 0 || mode == 1 || mode == 4)) {
         if (mode == 0) canon_fold_cols_kernel<0><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
-        else canon_fold_cols_kernel<1><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
+        else if (mode == 1) canon_fold_cols_kernel<1><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
+        else canon_fold_cols_kernel<4><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
         return;
     }
     switch (mode) {
     case 0: canon_fold_kernel<0, kCanonCols, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
     case 1: canon_fold_kernel<0, kCanonCols, 1><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
+    case 4: canon_fold_kernel<0, kCanonCols, 4><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
     case 2: canon_fold_kernel<kSumErr, 1, 2><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
     default: canon_fold_kernel<kSumErr, 1, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
     }

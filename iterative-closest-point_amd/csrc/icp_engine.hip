@@ -2380,7 +2380,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         s.nslots = (int)nslots;
         s.local_r = ctx->b_rlmax >= 0.0 && bundle_local() ? ctx->b_rlmax : -1.0; // (as the search decides)
     };
-    launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st);
+    launch_run_init(ctx->iter_state, ctx->amb_count, ctx->st, ctx->c);
     // partials over several workgroups: the moments and / or the transform may fold their
     // partials in their own last workgroup (StepFold), and on one rank go on there to the Horn
     // step / the error step -- one launch fewer each, bit-identical.  ICP_FUSED_STEPS = bit 0:
@@ -2566,6 +2566,22 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         LAUNCHCHK("err_step");
         return ICP_OK;
     };
+    // canon: a run's first iteration ends in the Horn step alone -- its moments in one pass
+    // around the shifts run_init set (c), no error step before it (round 4: the reference's two
+    // passes and an unshifted Horn step, four more launches)
+    auto canon_first = [&]() -> int {
+        if (!lag) {
+            launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, 4, cs, ctx->st);
+            LAUNCHCHK("canon_fold");
+            return ICP_OK;
+        }
+        launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, 0, cs, ctx->st);
+        LAUNCHCHK("canon_fold");
+        TRY(allreduce(ctx, ctx->sums, kNumSums));
+        launch_horn_step(ctx->sums, N, ctx->c, true, ctx->amb_count, sd, ctx->st);
+        LAUNCHCHK("horn_step");
+        return ICP_OK;
+    };
     while (!stop && waited < max_iter) {
         if (enqueued < max_iter && enqueued - waited <= kAhead + (lag_sched ? 1 : 0) &&
             !(!canon && hold_first && enqueued == 1 && waited == 0)) {
@@ -2583,6 +2599,56 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     HIPCHK(hipStreamSynchronize(ctx->st));
                     far_obs = *ctx->h_far;
                     grid_c = far_obs <= far_thr;
+                }
+                // a fresh run's first iteration on the grid as ONE launch too: cell seeds (their
+                // coordinates as the correspondences), then the fused kernel with no pending
+                // transform -- the search nn_search_begin would run (its unseeded grid path) and the
+                // one-pass moments, into the same rows
+                // (ICP_FIRST_K1=1; measured slower: the cell seeds' big boxes, 0.4% of the queries, are
+                // each the whole owning wave's serial work there, where the seeded pass queues them for
+                // a second pass of one wave each -- first iteration 0.53 against 0.37 ms, profiles/r05ab)
+                static const bool first_k1 = [] {
+                    const char *e = getenv("ICP_FIRST_K1");
+                    return e && atoi(e) == 1;
+                }();
+                const bool k1_first =
+                    first_k1 && grid_iter_on() && enqueued == 0 && !xf_pending && !ctx->seeds_valid && cell_seed_on() &&
+                    ctx->nn_mode == ICP_NN_CERTIFIED && ctx->nn_rule == ICP_NN_RULE_SQUARED && ctx->g_pts32 &&
+                    (ctx->nn_variant == ICP_NN_VARIANT_GRID ||
+                     (ctx->nn_variant == ICP_NN_VARIANT_AUTO && ctx->bundle_pending && level1_kind(ctx, n) == 3));
+                if (k1_first) {
+                    TRY(grow(ctx, &ctx->idx, &ctx->idx_cap, n));
+                    launch_nn_grid_cell_seed((int)n, P.x, P.y, P.z, grid_view(ctx), (int)ctx->nm, ctx->idx, nullptr,
+                                             ctx->st, Y.x, Y.y, Y.z);
+                    LAUNCHCHK("nn_grid_cell_seed");
+                    if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
+                    launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd, need_p32 ? P.f : nullptr,
+                                        grid_view(ctx), kSeededBox, grid_budget(ctx), (int)ctx->nm, ctx->m4,
+                                        ctx->canon_rowbuf, grid_policy ? &sd->far_acc : nullptr,
+                                        sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2, ctx->st,
+                                        iter_dbg, 0);
+                    LAUNCHCHK("nn_grid_iter (first)");
+                    if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));
+                    ws = SeedState{};
+                    ctx->seeds_valid = true;
+                    ctx->stats.last_filter = ICP_FILTER_GRID;
+                    ctx->stats.run_grid_searches += 1;
+                    ctx->kpos_valid = false;
+                    ctx->y_ready = true;
+                    ar_timed[slot] = false;
+                    if ((size_t)enqueued < ctx->digest_cap) {
+                        launch_idx_digest(ctx->idx, (int)n, &sd->done, ctx->digest + 3 * (size_t)enqueued, ctx->st,
+                                          digest_order);
+                        LAUNCHCHK("idx_digest");
+                    }
+                    TRY(canon_first());
+                    xf_pending = true;
+                    ++enqueued;
+                    if (enqueued == max_iter) {
+                        TRY(canon_transform(grid_policy ? sa_grid : SeedArgs{}));
+                        TRY(canon_end(enqueued - 1, false, -1));
+                    }
+                    continue;
                 }
                 // the grid's iterations as ONE launch: the pending transform, the seeded search
                 // of every point and the moments (nn_grid_iter_kernel)
@@ -2641,10 +2707,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                       digest_order);
                     LAUNCHCHK("idx_digest");
                 }
-                if (enqueued == 0) { // the reference's two passes, then the (unshifted) Horn step
-                    TRY(moments_phase(ctx, n));
-                    launch_horn_step(ctx->sums, N, ctx->c, false, ctx->amb_count, sd, ctx->st);
-                    LAUNCHCHK("horn_step");
+                if (enqueued == 0) { // the first moments in one pass around c, then the Horn step
+                    launch_canon_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd, ctx->canon_rowbuf,
+                                         ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr, ctx->m4kd, ctx->y_ready);
+                    LAUNCHCHK("canon_moments");
+                    TRY(canon_first());
                 } else {
                     launch_canon_moments(ctx->idx, ctx->m4, P.x, P.y, P.z, (int)n, Y.x, Y.y, Y.z, sd, ctx->canon_rowbuf,
                                          ctx->st, ctx->kpos_valid ? ctx->kpos : nullptr, ctx->m4kd, ctx->y_ready);

@@ -485,7 +485,9 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seed_kernel(int np, const doub
 __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const double *__restrict__ px,
                                                                   const double *__restrict__ py,
                                                                   const double *__restrict__ pz, GridView gv, int nm,
-                                                                  int *__restrict__ idx, double *__restrict__ seedd)
+                                                                  int *__restrict__ idx, double *__restrict__ seedd,
+                                                                  double *__restrict__ yx, double *__restrict__ yy,
+                                                                  double *__restrict__ yz)
 {
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= n) return;
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const 
     // (empty: the neighbours in the grid's order; nm >= 1, so at least one exists)
     const int a = a0 < b0 ? a0 : max(a0 - 1, 0), b = a0 < b0 ? b0 : min(a0 + 1, nm);
     double best = INFINITY;
-    int bi = -1;
+    int bi = -1, bk = a;
     for (int k = a; k < b; ++k) {
         const double4 m = gv.pts[k];
         const double d = d64g(q[0], q[1], q[2], m.x, m.y, m.z);
@@ -505,11 +507,18 @@ __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const 
         if (d < best || (d == best && mi < bi)) {
             best = d;
             bi = mi;
+            bk = k;
         }
     }
     if (bi < 0) bi = (int)gv.pts[a].w; // (a NaN query: no comparison held -- any valid seed)
     idx[t] = bi;
-    seedd[t] = best;
+    if (yx) { // (the seed's coordinates: the fused kernel's seed is y)
+        const double4 w = gv.pts[bk];
+        yx[t] = w.x;
+        yy[t] = w.y;
+        yz[t] = w.z;
+    }
+    if (seedd) seedd[t] = best;
 }
 
 // (D64, index) first minimum that also carries the winner's position k in pts.  The seed enters
@@ -809,7 +818,8 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
     int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
     float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
-    double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, unsigned long long *__restrict__ dbg)
+    double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, unsigned long long *__restrict__ dbg,
+    int xform)
 {
     // dbg (nullable, ICP_ITER_DEBUG): per-wave phase clocks (s_memrealtime, 100 MHz) and counts
     unsigned long long dcnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -877,12 +887,18 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
             y[1] = fy[1];
             y[2] = fy[2];
             h = fh;
-            transform_point(fresh()->xf, p0, p1, p2, q[0], q[1], q[2]);
+            if (xform) {
+                transform_point(fresh()->xf, p0, p1, p2, q[0], q[1], q[2]);
+            } else { // (a run's first iteration: no pending transform, the point as it is)
+                q[0] = p0;
+                q[1] = p1;
+                q[2] = p2;
+            }
         }
         if (ICP_ITER_PREFETCH && c + S < C) fetch(c + S);
         const double e = active ? residual2(y[0], y[1], y[2], q[0], q[1], q[2]) : 0.0;
         lap(5);
-        if (active && sub == 0) {
+        if (active && sub == 0 && xform) {
             px[t] = q[0];
             py[t] = q[1];
             pz[t] = q[2];
@@ -1261,7 +1277,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
 void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
                          const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
                          const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
-                         unsigned long long *dbg)
+                         unsigned long long *dbg, int xform)
 {
     if (n <= 0) return;
     // ICP_ITER_STAGE=1: the task's union of boxes staged in LDS (measured slower: the staging's two
@@ -1280,13 +1296,13 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
     const int R = canon_rows((size_t)n);
     if (!stage && wide_on && n <= kIterWideMax)
         nn_grid_iter_kernel<false, 4><<<R, 2 * kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                                 budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+                                                                 budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform);
     else if (stage)
         nn_grid_iter_kernel<true, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                            budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+                                                            budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform);
     else
         nn_grid_iter_kernel<false, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                             budget, nm, m4, rows, far_acc, far_d2, big_count, dbg);
+                                                             budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform);
 }
 
 namespace {
@@ -1427,10 +1443,11 @@ void launch_nn_grid_search(int np, const double *px, const double *py, const dou
 }
 
 void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv, int nm,
-                              int *idx, double *seedd, hipStream_t st)
+                              int *idx, double *seedd, hipStream_t st, double *yx, double *yy, double *yz)
 {
     if (n <= 0) return;
-    nn_grid_cell_seed_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, px, py, pz, gv, nm, idx, seedd);
+    nn_grid_cell_seed_kernel<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(n, px, py, pz, gv, nm, idx, seedd, yx, yy,
+                                                                          yz);
 }
 
 void launch_nn_grid_seed(int np, const double *px, const double *py, const double *pz, const GridView &gv,

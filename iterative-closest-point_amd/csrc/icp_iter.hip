@@ -1743,16 +1743,24 @@ void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, 
 }
 
 // a run's device state and NN queue counters to zero (one launch instead of two memsets)
-__global__ void run_init_kernel(IterState *__restrict__ s, int *__restrict__ cnt)
+// (the first iteration's shifts: c, the model's centring point -- icp_run's canonical schedule
+// sums its first moments in one pass around them, §3.7; the two-pass paths ignore them)
+__global__ void run_init_kernel(IterState *__restrict__ s, int *__restrict__ cnt, double c0, double c1, double c2)
 {
     constexpr int kWords = (int)(sizeof(IterState) / sizeof(int));
     for (int k = threadIdx.x; k < kWords; k += blockDim.x) ((int *)s)[k] = 0;
     if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s->shift_p[0] = s->shift_y[0] = c0;
+        s->shift_p[1] = s->shift_y[1] = c1;
+        s->shift_p[2] = s->shift_y[2] = c2;
+    }
 }
 
-void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st)
+void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st, const double *c)
 {
-    run_init_kernel<<<1, 64, 0, st>>>(st_dev, amb_count);
+    run_init_kernel<<<1, 64, 0, st>>>(st_dev, amb_count, c ? c[0] : 0.0, c ? c[1] : 0.0, c ? c[2] : 0.0);
 }
 
 } // namespace icp

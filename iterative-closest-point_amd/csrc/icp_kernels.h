@@ -321,7 +321,8 @@ void launch_nn_grid_seed(int np, const double *px, const double *py, const doubl
 // cell: over its two neighbours in the grid's order), seedd[t] = its D64 -- the input of the
 // seeded grid pass
 void launch_nn_grid_cell_seed(int n, const double *px, const double *py, const double *pz, const GridView &gv, int nm,
-                              int *idx, double *seedd, hipStream_t st);
+                              int *idx, double *seedd, hipStream_t st, double *yx = nullptr, double *yy = nullptr,
+                              double *yz = nullptr); // (y nullable: the seed's coordinates, for the fused kernel)
 // inline_nm > 0 (a model of that many points): queries the grid cannot take are scanned
 // exactly in place (no fallback queue, no nn_resolve launch)
 // seeded grid variant: every query's previous correspondence (idx[t]) as the candidate, its
@@ -516,7 +517,8 @@ struct CanonStep {
 // rows: canon_rows(n) x 18 doubles, by column (k R + r).  Moments -> columns 0..16 (y from the search when y_ready,
 // else gathered through kpos / idx and stored); transform -> column kSumErr plus SeedArgs'
 // outputs; fold: mode 0 all 18 -> sums, 1 + error step + Horn step (one rank), 2 the residual
-// column + error step (the last iteration, one rank), 3 the residual column -> sums[kSumErr]
+// column + error step (the last iteration, one rank), 3 the residual column -> sums[kSumErr],
+// 4 all 18 + the Horn step alone (a run's first iteration, one rank)
 void launch_canon_moments(const int *idx, const double4 *m4, const double *px, const double *py, const double *pz,
                           int n, double *yx, double *yy, double *yz, const IterState *st_dev, double *rows,
                           hipStream_t st, const int *kpos, const double4 *m4kd, bool y_ready);
@@ -533,7 +535,8 @@ struct GridView;
 void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
                          const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
                          const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
-                         unsigned long long *dbg = nullptr); // (dbg: ICP_ITER_DEBUG's 12 counters)
+                         unsigned long long *dbg = nullptr, // (dbg: ICP_ITER_DEBUG's 12 counters)
+                         int xform = 1); // (0: no pending transform -- a run's first iteration, seeds in idx / y)
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,
 // sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)
@@ -672,7 +675,7 @@ void launch_small_err(const double *y_aos, double *p_aos, int n, const Xform &xf
                       hipStream_t st);
 void launch_small_alignment(const double *p_aos, const double *y_aos, int n, double *out, hipStream_t st);
 // zero a run's IterState and the NN queue counters (amb_count[0..3])
-void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st);
+void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st, const double *c = nullptr);
 
 // exact NN of nq (few) queries, one workgroup each: q_aos (3 x nq) in, idx and y = m[idx]
 // (3 x nq) out -- all three may be mapped host memory
