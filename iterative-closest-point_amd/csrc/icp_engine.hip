@@ -350,6 +350,7 @@ struct icp_ctx {
     // moments + Horn step, [1] the transform + error step; zero between launches
     unsigned *fold_ticket = nullptr;
     bool scene_slot = false;
+    unsigned runs = 0; // (icp_run calls: the timing sample's phase)
     // scene_revert: the scene is in the slot order of a model since replaced -- icp_run puts it
     // back into file order (and sorts it by the new model's box) unless a new scene comes first
     bool scene_revert = false;
@@ -2454,8 +2455,12 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         return e ? std::max(1, atoi(e)) : 0;
     }();
     const int timing_stride = forced_stride ? forced_stride : 8;
-    // iteration 0 of a run is not sampled (its search may be unseeded): 1, 9, 17, ...
-    const int timing_phase = timing_stride > 1 ? 1 : 0;
+    // the sampled iterations rotate from run to run (run r: those = r mod the stride), so that over
+    // a stride's worth of registrations every iteration index is timed once -- the mean of the timed
+    // launches is then the mean of all of them, as a kernel trace of the same runs gives it (a fixed
+    // phase sampled iterations 1, 9, 17, 25 only, the slower early ones among them); iteration 0
+    // (its search unseeded) is never sampled
+    const int timing_phase = timing_stride > 1 ? (int)(ctx->runs++ % (unsigned)timing_stride) : 0;
     // (partials: the residual's unreduced rows, folded in the same launch)
     // (horn: this iteration's Horn step in the same single-thread launch, right after it)
     auto enqueue_err_step = [&](int it, const double *partials = nullptr, bool horn = false) -> int {
@@ -2587,7 +2592,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
             !(!canon && hold_first && enqueued == 1 && waited == 0)) {
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
-            const bool timed = enqueued % timing_stride == timing_phase;
+            const bool timed = enqueued % timing_stride == timing_phase && (enqueued > 0 || timing_stride == 1);
             if (canon) {
                 bool grid_c = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : grid_next);
                 grid_next = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : ctx->bundle_pending);
@@ -2923,7 +2928,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         report_progress(ctx, iters); // (the iterations recorded so far, as they end)
         if (iters > recorded) { // this iteration counted: its NN kernel time (if timed)
             float ms = 0.f;
-            if (n && (waited - 1) % timing_stride == timing_phase) { // (an empty shard records no events)
+            if (n && (waited - 1) % timing_stride == timing_phase && (waited - 1 > 0 || timing_stride == 1)) {
+                // (an empty shard records no events)
                 if (hipEventElapsedTime(&ms, ctx->iter_ev[5 * slot], ctx->iter_ev[5 * slot + 1]) == hipSuccess) {
                     ctx->stats.nn_ms += ms;
                     ctx->stats.nn_launches += 1;
