@@ -807,6 +807,9 @@ constexpr int kLeafStride = 33; // (doubles a column of the leaf tile: lane k's 
 #ifndef ICP_ITER_KU
 #define ICP_ITER_KU 2 // (the walk: points a lane loads together)
 #endif
+#ifndef ICP_ITER_PRUNE
+#define ICP_ITER_PRUNE 1 // (the walk: rows beyond the seed sphere skipped, each row's x-run cut to its chord)
+#endif
 #ifndef ICP_ITER_WAVES
 #define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
 #endif
@@ -1059,6 +1062,25 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                 // (r / ny by an fp32 reciprocal: r < 2^12 and ny <= 125 keep (r + 0.5) / ny at least
                 // 0.004 from an integer, far beyond fp32's error -- no integer division in the loop)
                 const float inv_ny = 1.0f / (float)ny;
+#if ICP_ITER_PRUNE
+                // The seed sphere in cell units, relative to the box's first cell: a point m of row
+                // (gy, gz) with D64(q, m) <= e has true |m - q| <= sqrt(e) (1 + 2^-50) and true cell
+                // coordinates within 2^-50 (1 + |t|) of its cell; tr, q's coordinates (fp32), lie
+                // within 2^-23 (1 + |tr|) of the true ones.  rc's room (2^-18 relative, 2^-20 (1 +
+                // sum |tr|) absolute) covers those errors, so dy^2 + dz^2 + dx^2 <= rc^2 with dy, dz
+                // the row's computed gaps to tr, and the relative room alone exceeds the fp32
+                // rounding of rem = rc^2 - dy^2 - dz^2 (3 2^-24 rc^2): rem >= dx^2 as computed.  The
+                // row is skipped when rem < 0, else its x-run is cut to the cells within xw =
+                // sqrt(rem) (1 + 2^-20) + 2^-20 (1 + |tr_x|) of tr_x (the root's and the bounds'
+                // roundings)
+                float tr[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) tr[a] = (float)((q[a] - gv.lo[a]) * gv.inv_h - (double)c0[a]);
+                const float rcf = (float)(sqrt(e) * gv.inv_h * (1.0 + 0x1.0p-18) +
+                                          0x1.0p-20 * (1.0 + fabs((double)tr[0]) + fabs((double)tr[1]) + fabs((double)tr[2])));
+                const float rc2 = rcf * rcf, xroom = 0x1.0p-20f * (1.0f + fabsf(tr[0]));
+                const float xspan = (float)(c1[0] - c0[0] + 1);
+#endif
                 for (int r0 = sub; r0 < nrq; r0 += KR * G) {
                     int k0[KR], pre[KR + 1];
                     pre[0] = 0;
@@ -1070,8 +1092,23 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                             const int rz = (int)(((float)r + 0.5f) * inv_ny), ry = r - rz * ny;
                             const int gy = c0[1] + ry, gz = c0[2] + rz;
                             const int row = (gz * gv.g[1] + gy) * gv.g[0];
-                            a0 = gv.start[row + c0[0]];
-                            a1 = gv.start[row + c1[0] + 1];
+                            int x0 = c0[0], x1 = c1[0];
+#if ICP_ITER_PRUNE
+                            const float dy = fmaxf(0.0f, fmaxf((float)ry - tr[1], tr[1] - (float)(ry + 1)));
+                            const float dz = fmaxf(0.0f, fmaxf((float)rz - tr[2], tr[2] - (float)(rz + 1)));
+                            const float rem = rc2 - dy * dy - dz * dz;
+                            if (rem < 0.0f) {
+                                x1 = x0 - 1; // (the row lies beyond the sphere)
+                            } else {
+                                const float xw = sqrtf(rem) * (1.0f + 0x1.0p-20f) + xroom;
+                                x0 = max(x0, c0[0] + (int)floorf(fmaxf(tr[0] - xw, -1.0f)));
+                                x1 = min(x1, c0[0] + (int)floorf(fminf(tr[0] + xw, xspan)));
+                            }
+#endif
+                            if (x0 <= x1) {
+                                a0 = gv.start[row + x0];
+                                a1 = gv.start[row + x1 + 1];
+                            }
                         }
                         k0[v] = a0;
                         pre[v + 1] = pre[v] + (a1 - a0);
