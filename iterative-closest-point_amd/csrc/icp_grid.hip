@@ -810,9 +810,27 @@ constexpr int kLeafStride = 33; // (doubles a column of the leaf tile: lane k's 
 #ifndef ICP_ITER_PRUNE
 #define ICP_ITER_PRUNE 1 // (the walk: rows beyond the seed sphere skipped, each row's x-run cut to its chord)
 #endif
+#ifndef ICP_ITER_BAL
+#define ICP_ITER_BAL 1 // (the walk: a round's rows of a query's two lanes dealt point by point to both)
+#endif
 #ifndef ICP_ITER_WAVES
 #define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
 #endif
+// Block b of nb -> row, so that an XCD's blocks (b = k, k + 8, ...: k = b % 8) take runs of L
+// consecutive rows: XCD k's i th block takes row (8 (i / L) + k) L + i % L, a bijection of the
+// first 8 L floor(nb / 8 L) blocks; the rest keep their own index.  L < 0: one run per XCD,
+// [k q + min(k, e), (k + 1) q + min(k + 1, e)) (q = nb / 8, e = nb % 8); L = 0: the identity.
+__device__ __forceinline__ int xcd_row(int b, int nb, int L)
+{
+    const int k = b & 7, i = b >> 3;
+    if (L < 0) {
+        const int q = nb >> 3, e = nb & 7;
+        return k * q + min(k, e) + i;
+    }
+    if (L == 0 || b >= nb / (8 * L) * (8 * L)) return b;
+    return ((i / L) * 8 + k) * L + i % L;
+}
+
 // G lanes a query (2, or 4 for shards of at most kIterWideMax points: two waves a chunk, a chunk
 // a strand -- twice the waves for a scene too small to fill the chip with one wave a chunk);
 // a workgroup is the four strands of one row (G / 2 waves each)
@@ -822,7 +840,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
     float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
     double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, unsigned long long *__restrict__ dbg,
-    int xform)
+    int xform, int xcd_l)
 {
     // dbg (nullable, ICP_ITER_DEBUG): per-wave phase clocks (s_memrealtime, 100 MHz) and counts
     unsigned long long dcnt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -855,7 +873,12 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane / G, sub = lane % G;
     const int half = wave % H; // (G = 4: which 16 queries of the chunk)
     const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
-    const int s = blockIdx.x * 4 + wave / H;
+    // the workgroup's row: blocks b and b + 8 share an XCD (its L2), so consecutive rows go to one
+    // XCD -- its strands' chunks are four contiguous eighths of the Morton-ordered scene, whose
+    // model neighbourhoods its L2 then holds (ICP_ITER_XCD; the row, not the block, fixes the
+    // arithmetic: the same bits either way)
+    const int wr = xcd_row((int)blockIdx.x, R, xcd_l);
+    const int s = wr * 4 + wave / H;
     float4 *const lp = s_pts[wave];
     int *const rbase = s_rbase[wave], *const rstart = s_rstart[wave];
     double acc = 0.0; // (lane k < 18: column k of this strand)
@@ -1081,12 +1104,16 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                 const float rc2 = rcf * rcf, xroom = 0x1.0p-20f * (1.0f + fabsf(tr[0]));
                 const float xspan = (float)(c1[0] - c0[0] + 1);
 #endif
-                for (int r0 = sub; r0 < nrq; r0 += KR * G) {
+                // (ICP_ITER_BAL, G = 2: the pair's 2 KR rows of a round are one sequence, dealt point by
+                // point to its two lanes -- each lane ceil(T / 2) points where the rows' owner had its
+                // own rows' count; the loop counts are the same on both lanes)
+                constexpr bool kBal = ICP_ITER_BAL && G == 2;
+                for (int r0 = kBal ? 0 : sub; r0 < nrq; r0 += KR * G) {
                     int k0[KR], pre[KR + 1];
                     pre[0] = 0;
 #pragma unroll
                     for (int v = 0; v < KR; ++v) {
-                        const int r = r0 + v * G;
+                        const int r = r0 + v * G + (kBal ? sub : 0);
                         int a0 = 0, a1 = 0;
                         if (r < nrq) {
                             const int rz = (int)(((float)r + 0.5f) * inv_ny), ry = r - rz * ny;
@@ -1112,6 +1139,41 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                         }
                         k0[v] = a0;
                         pre[v + 1] = pre[v] + (a1 - a0);
+                    }
+                    if constexpr (kBal) {
+                        // the pair's sequence: own row v at 2 v + sub, the other lane's at 2 v + 1 - sub
+                        int K[2 * KR], P[2 * KR + 1];
+                        P[0] = 0;
+#pragma unroll
+                        for (int v = 0; v < KR; ++v) {
+                            const int len = pre[v + 1] - pre[v];
+                            const int ok0 = __builtin_amdgcn_update_dpp(0, k0[v], 0xB1, 0xf, 0xf, true);
+                            const int ol = __builtin_amdgcn_update_dpp(0, len, 0xB1, 0xf, 0xf, true);
+                            K[2 * v] = sub ? ok0 : k0[v];
+                            K[2 * v + 1] = sub ? k0[v] : ok0;
+                            P[2 * v + 1] = P[2 * v] + (sub ? ol : len);
+                            P[2 * v + 2] = P[2 * v + 1] + (sub ? len : ol);
+                        }
+                        const int T = P[2 * KR];
+                        for (int f0 = 0; f0 < T; f0 += G * KU) {
+                            int kk[KU];
+#pragma unroll
+                            for (int v = 0; v < KU; ++v) {
+                                const int f = f0 + sub + G * v;
+                                int pp = K[0] + f;
+#pragma unroll
+                                for (int w = 1; w < 2 * KR; ++w)
+                                    if (f >= P[w]) pp = K[w] + (f - P[w]);
+                                kk[v] = f < T ? pp : -1;
+                            }
+                            float4 mm[KU];
+#pragma unroll
+                            for (int v = 0; v < KU; ++v) mm[v] = gv.pts32[kk[v] >= 0 ? kk[v] : 0];
+#pragma unroll
+                            for (int v = 0; v < KU; ++v)
+                                if (kk[v] >= 0) test(mm[v], kk[v]);
+                        }
+                        continue;
                     }
                     const int tot = pre[KR];
                     for (int f0 = 0; f0 < tot; f0 += KU) { // the lane's runs as one sequence
@@ -1291,7 +1353,7 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
         for (int j = 0; j < 4; ++j) // (G = 4: the chunk's halves, then the strand's 0.0 + chunk)
             v[j] = H == 1 ? sh[j][k] : 0.0 + (sh[H * j][k] + sh[H * j + H - 1][k]);
-        rows[(size_t)k * R + blockIdx.x] = (v[0] + v[1]) + (v[2] + v[3]);
+        rows[(size_t)k * R + wr] = (v[0] + v[1]) + (v[2] + v[3]);
     }
     // the far count (the policy's) and the big boxes (the search statistics), one atomic each
     __shared__ int s_cnt[2][NW];
@@ -1331,15 +1393,24 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         return e && atoi(e) == 1;
     }();
     const int R = canon_rows((size_t)n);
+    // Runs of rows an XCD takes (xcd_row): 32 when a strand walks several chunks (C4: 6,888 it/s
+    // against 6,520 for one run an XCD and 6,660 for rows dealt round-robin), one run an XCD when a
+    // strand is one chunk (the W = 8 shard: 0.048 against 0.050 ms an iteration for runs of 32 and
+    // 0.053 round-robin; profiles/r05ak).  ICP_ITER_XCD_L overrides (-1 one run, 0 round-robin).
+    static const int xcd_env = [] {
+        const char *e = getenv("ICP_ITER_XCD_L");
+        return e ? atoi(e) : -2;
+    }();
+    const int xcd_l = xcd_env != -2 ? xcd_env : (canon_chunks((size_t)n) > canon_strands((size_t)n) ? 32 : -1);
     if (!stage && wide_on && n <= kIterWideMax)
         nn_grid_iter_kernel<false, 4><<<R, 2 * kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                                 budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform);
+                                                                 budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform, xcd_l);
     else if (stage)
         nn_grid_iter_kernel<true, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                            budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform);
+                                                            budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform, xcd_l);
     else
         nn_grid_iter_kernel<false, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
-                                                             budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform);
+                                                             budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform, xcd_l);
 }
 
 namespace {
