@@ -550,6 +550,21 @@ template <int G> __device__ __forceinline__ void group_lex_min_pos(double &best,
     }
 }
 
+// Block b of nb -> row, so that an XCD's blocks (b = k, k + 8, ...: k = b % 8) take runs of L
+// consecutive rows: XCD k's i th block takes row (8 (i / L) + k) L + i % L, a bijection of the
+// first 8 L floor(nb / 8 L) blocks; the rest keep their own index.  L < 0: one run per XCD,
+// [k q + min(k, e), (k + 1) q + min(k + 1, e)) (q = nb / 8, e = nb % 8); L = 0: the identity.
+__device__ __forceinline__ int xcd_row(int b, int nb, int L)
+{
+    const int k = b & 7, i = b >> 3;
+    if (L < 0) {
+        const int q = nb >> 3, e = nb & 7;
+        return k * q + min(k, e) + i;
+    }
+    if (L == 0 || b >= nb / (8 * L) * (8 * L)) return b;
+    return ((i / L) * 8 + k) * L + i % L;
+}
+
 // The seeded search of every query of a scene in slot order (icp_run's grid iterations,
 // grid_seeded_search): each query's box comes from its seed distance seedd[t] -- the last
 // transform's D64(q, m[idx[t]]), the same arithmetic on the same values, so the seed point is met
@@ -568,8 +583,7 @@ __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
     const int groups = gridDim.x * (kBlock / G);
-    const int bx = xcd_remap && (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
-                                                     : blockIdx.x;
+    const int bx = xcd_row((int)blockIdx.x, (int)gridDim.x, xcd_remap);
     for (int t = (bx * kBlock + threadIdx.x) / G; t < n; t += groups) {
         const int h = idx[t];
         const double q[3] = {px[t], py[t], pz[t]};
@@ -668,8 +682,7 @@ __global__ __launch_bounds__(kBlock) void nn_grid_seeded32_kernel(
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
     const int groups = gridDim.x * (kBlock / G);
-    const int bx = xcd_remap && (gridDim.x & 7) == 0 ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
-                                                     : blockIdx.x;
+    const int bx = xcd_row((int)blockIdx.x, (int)gridDim.x, xcd_remap);
     for (int t = (bx * kBlock + threadIdx.x) / G; t < n; t += groups) {
         const int h = idx[t];
         const double q[3] = {px[t], py[t], pz[t]};
@@ -816,21 +829,6 @@ constexpr int kLeafStride = 33; // (doubles a column of the leaf tile: lane k's 
 #ifndef ICP_ITER_WAVES
 #define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
 #endif
-// Block b of nb -> row, so that an XCD's blocks (b = k, k + 8, ...: k = b % 8) take runs of L
-// consecutive rows: XCD k's i th block takes row (8 (i / L) + k) L + i % L, a bijection of the
-// first 8 L floor(nb / 8 L) blocks; the rest keep their own index.  L < 0: one run per XCD,
-// [k q + min(k, e), (k + 1) q + min(k + 1, e)) (q = nb / 8, e = nb % 8); L = 0: the identity.
-__device__ __forceinline__ int xcd_row(int b, int nb, int L)
-{
-    const int k = b & 7, i = b >> 3;
-    if (L < 0) {
-        const int q = nb >> 3, e = nb & 7;
-        return k * q + min(k, e) + i;
-    }
-    if (L == 0 || b >= nb / (8 * L) * (8 * L)) return b;
-    return ((i / L) * 8 + k) * L + i % L;
-}
-
 // G lanes a query (2, or 4 for shards of at most kIterWideMax points: two waves a chunk, a chunk
 // a strand -- twice the waves for a scene too small to fill the chip with one wave a chunk);
 // a workgroup is the four strands of one row (G / 2 waves each)
@@ -1666,6 +1664,13 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     // is denser than the scene -- each query's chain of dependent loads is then the time
     // (C4 W = 8: 31.2 against 45.3 us, W = 2: 67.1 against 82.4; C5's shard: 208 against 240)
     const int form = forced >= 0 ? forced : (n >= (1 << 19) && nm_hint < 2 * (long long)n) ? 0 : 1;
+    // the XCD mapping (xcd_row): one run an XCD for a sparse shard (xcd_remap), else runs of 32
+    // blocks (C4 W = 1's first iteration; ICP_SEEDED_XCD_L overrides)
+    static const int xcd_env = [] {
+        const char *e = getenv("ICP_SEEDED_XCD_L");
+        return e ? atoi(e) : -2;
+    }();
+    const int xcd_l = xcd_env != -2 ? xcd_env : xcd_remap ? -1 : 32;
     const int f = form >= 4 && form != 9 && !gv.pts32 ? 0 : form; // (no fp32 image: the fp64 scan)
     const int per_block = kBlock / forms[f].g;
     int blocks = std::max(1, std::min((n + per_block - 1) / per_block, 16384));
@@ -1674,11 +1679,14 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
     // ~14% fewer cells at C4, but measured no faster there (109.7 against 109.9 us) and slower at
     // the W = 8 shard (37.0 against 33.4 us: its ALU sits in each query's dependent chain), so the
     // whole box stays the default (profiles/r04z/trim)
+    // Round 5: the first iteration's pass over cell seeds (boxes of ~14 cells) runs 0.318 against
+    // 0.351 ms with it at C4 (profiles/r05al), so the whole-scene form trims by default
+    // (ICP_GRID_TRIM=0/1 overrides)
     const char *te = getenv("ICP_GRID_TRIM");
-    const int trim = te && std::string(te) == "1" ? 1 : 0;
+    const int trim = te ? (std::string(te) == "1" ? 1 : 0) : (f == 0 ? 1 : 0);
 #define SEEDED(K, ...)                                                                                       \
     K<__VA_ARGS__><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz, far_count, \
-                                              far_list, far_hint, stop, xcd_remap ? 1 : 0, trim)
+                                              far_list, far_hint, stop, xcd_l, trim)
     switch (f) {
     case 1: SEEDED(nn_grid_seeded_kernel, 4, 2, 2, 1); break;
     case 2: SEEDED(nn_grid_seeded_kernel, 4, 2, 4, 1); break;
