@@ -826,6 +826,9 @@ constexpr int kLeafStride = 33; // (doubles a column of the leaf tile: lane k's 
 #ifndef ICP_ITER_BAL
 #define ICP_ITER_BAL 1 // (the walk: a round's rows of a query's two lanes dealt point by point to both)
 #endif
+#ifndef ICP_ITER_FLUSH_MASK
+#define ICP_ITER_FLUSH_MASK 1 // (the candidates' fp64 records: only the lanes that hold one load it)
+#endif
 #ifndef ICP_ITER_WAVES
 #define ICP_ITER_WAVES 1 // (waves per SIMD the fused kernel is compiled for: 1 = the compiler's choice)
 #endif
@@ -1043,7 +1046,8 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
                 if (kIterDbg && dbg) dcnt[4] += (unsigned long long)nc; // (per lane; summed over the wave below)
                 double4 w[kCand];
 #pragma unroll
-                for (int j = 0; j < kCand; ++j) w[j] = gv.pts[cand[j < nc ? j : 0]];
+                for (int j = 0; j < kCand; ++j)
+                    if (!ICP_ITER_FLUSH_MASK || j < nc) w[j] = gv.pts[cand[j < nc ? j : 0]]; // (masked: only the lanes holding j + 1 candidates load record j)
 #pragma unroll
                 for (int j = 0; j < kCand; ++j) {
                     if (j >= nc) break;
