@@ -30,7 +30,7 @@
 namespace icp {
 
 constexpr int kCanonChunk = 32;         // points a chunk
-constexpr int kCanonStrandsMax = 8192;  // strands the chunks are dealt to (one wave each)
+constexpr int kCanonStrandsMax = 16384; // strands the chunks are dealt to (one wave each; 8192 before r05ap: 7,013 against 7,445 it/s at C4, profiles/r05ap)
 constexpr int kCanonCols = 18;          // kSumP .. kSumSp (17 moments), kSumErr (the residual)
 
 __host__ __device__ inline int canon_chunks(size_t n) { return (int)((n + kCanonChunk - 1) / kCanonChunk); }

@@ -9,8 +9,8 @@ sums writes the same canonical rows (32-point chunk trees, strands, rows, one fo
     separate kernels of the same schedule (ICP_GRID_ITER=0) give the same trajectory bit for bit:
     errors, per-iteration index digests, final scene and transform -- on a whole scene, on a
     sparse shard (a W = 8 rank's share against the whole model) and on a scene of two chunks a
-    strand (2^19); so does the fused kernel's opt-in four-lane form (ICP_ITER_WIDE=1, scenes of
-    at most 2^18 points: two waves a chunk, the chunk's halves joined as the 32-leaf tree's last
+    strand (2^20); so does the fused kernel's opt-in four-lane form (ICP_ITER_WIDE=1, scenes of
+    at most 2^19 points: two waves a chunk, the chunk's halves joined as the 32-leaf tree's last
     step);
   * the round-4 schedule (ICP_CANON=0: per-path reduction orders) finds the same correspondences
     in every iteration (digests equal) and errors equal to rounding (rtol 1e-12).
@@ -34,7 +34,7 @@ sys.path.insert(0, sys.argv[1])
 import icp_amd
 out = {}
 iters = 12
-for name, n, frac in (("whole", 1 << 17, 1), ("shard", 1 << 19, 8), ("big", 1 << 19, 1)):
+for name, n, frac in (("whole", 1 << 17, 1), ("shard", 1 << 19, 8), ("big", 1 << 20, 1)):
     m, p = icp_amd.synthetic_pair(n, seed=31, angle_deg=6.0)
     b, c = icp_amd.shard_range(n, 0, frac)
     scene = np.ascontiguousarray(p[b:b + c])
