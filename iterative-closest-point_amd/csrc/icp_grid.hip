@@ -89,6 +89,10 @@ __global__ __launch_bounds__(kBlock) void grid_gather_kernel(const double4 *__re
     if (pts32) pts32[k] = make_float4((float)(x - c0), (float)(y - c1), (float)(z - c2), __int_as_float(i));
 }
 
+#ifndef ICP_CELL_SEED_RUN
+#define ICP_CELL_SEED_RUN 1 // (the cell seed: nearest point of the cell's x-run of three cells, 0: of the cell)
+#endif
+
 // Lexicographic (D64, index) minimum, i.e. the first minimum (compute.cu:137 tie rule).
 __device__ __forceinline__ void lex_min(double &best, int &bi, double d, int mi)
 {
@@ -492,10 +496,15 @@ __global__ __launch_bounds__(kBlock) void nn_grid_cell_seed_kernel(int n, const 
     const int t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= n) return;
     const double q[3] = {px[t], py[t], pz[t]};
-    const int c = (cell1(q[2], gv.lo[2], gv.inv_h, gv.g[2]) * gv.g[1] + cell1(q[1], gv.lo[1], gv.inv_h, gv.g[1])) *
-                      gv.g[0] +
-                  cell1(q[0], gv.lo[0], gv.inv_h, gv.g[0]);
-    const int a0 = gv.start[c], b0 = gv.start[c + 1];
+    const int cx = cell1(q[0], gv.lo[0], gv.inv_h, gv.g[0]);
+    const int row = (cell1(q[2], gv.lo[2], gv.inv_h, gv.g[2]) * gv.g[1] + cell1(q[1], gv.lo[1], gv.inv_h, gv.g[1])) * gv.g[0];
+#if ICP_CELL_SEED_RUN
+    // the cell and its two x-neighbours (one contiguous run of the grid order: ~6 points, a seed
+    // nearer than the cell's own ~2 give, so the first search's boxes are smaller)
+    const int a0 = gv.start[row + max(cx - 1, 0)], b0 = gv.start[row + min(cx + 1, gv.g[0] - 1) + 1];
+#else
+    const int a0 = gv.start[row + cx], b0 = gv.start[row + cx + 1];
+#endif
     // (empty: the neighbours in the grid's order; nm >= 1, so at least one exists)
     const int a = a0 < b0 ? a0 : max(a0 - 1, 0), b = a0 < b0 ? b0 : min(a0 + 1, nm);
     double best = INFINITY;
