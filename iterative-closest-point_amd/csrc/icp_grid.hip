@@ -1404,15 +1404,16 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         return e && atoi(e) == 1;
     }();
     const int R = canon_rows((size_t)n);
-    // Runs of rows an XCD takes (xcd_row): 32 when a strand walks several chunks (C4: 6,888 it/s
-    // against 6,520 for one run an XCD and 6,660 for rows dealt round-robin), one run an XCD when a
-    // strand is one chunk (the W = 8 shard: 0.048 against 0.050 ms an iteration for runs of 32 and
-    // 0.053 round-robin; profiles/r05ak).  ICP_ITER_XCD_L overrides (-1 one run, 0 round-robin).
+    // Runs of rows an XCD takes (xcd_row): 32 from 8,192 chunks up (C4: 6,888 it/s against 6,520
+    // for one run an XCD and 6,660 for rows dealt round-robin, profiles/r05ak; the W = 2 / 4 shards
+    // 0.085 / 0.061 against 0.100 / 0.064 ms an iteration, r05as), one run an XCD below (the W = 8
+    // shard: 0.048 against 0.050 ms for runs of 32 and 0.053 round-robin).  ICP_ITER_XCD_L
+    // overrides (-1 one run, 0 round-robin).
     static const int xcd_env = [] {
         const char *e = getenv("ICP_ITER_XCD_L");
         return e ? atoi(e) : -2;
     }();
-    const int xcd_l = xcd_env != -2 ? xcd_env : (canon_chunks((size_t)n) > canon_strands((size_t)n) ? 32 : -1);
+    const int xcd_l = xcd_env != -2 ? xcd_env : (canon_chunks((size_t)n) >= 8192 ? 32 : -1);
     if (!stage && wide_on && n <= kIterWideMax)
         nn_grid_iter_kernel<false, 4><<<R, 2 * kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
                                                                  budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform, xcd_l);
