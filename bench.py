@@ -442,6 +442,12 @@ def csv_io(m):
             "load_mb_per_s": size / tl / 1e6, "roundtrip_rows": int(back.shape[0])}
 
 
+def torch_stream(t):
+    """The HIP stream handle of torch's current stream on tensor t's device."""
+    import torch
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
 def registration(ctx, m, p_local, n_total, iters=30, reps=3, device=None):
     """SURVEY §8d's clock: a whole registration from model upload through the last iteration's
     err -- icp_set_model (host AoS in, every device image built), icp_set_scene, the first
@@ -454,13 +460,13 @@ def registration(ctx, m, p_local, n_total, iters=30, reps=3, device=None):
         if device is None:
             ctx.set_model(m)
         else:
-            ctx.set_model_device(device[0].data_ptr(), m.shape[0])
+            ctx.set_model_device(device[0].data_ptr(), m.shape[0], stream=torch_stream(device[0]))
 
     def set_scene():
         if device is None:
             ctx.set_scene(p_local, np_total=n_total)
         else:
-            ctx.set_scene_device(device[1].data_ptr(), p_local.shape[0], n_total)
+            ctx.set_scene_device(device[1].data_ptr(), p_local.shape[0], n_total, stream=torch_stream(device[1]))
 
     rows = []
     for _ in range(reps):
@@ -581,9 +587,13 @@ def main():
     dps = torch.from_numpy(np.ascontiguousarray(p[b:b + c])).to(dev)
     torch.cuda.synchronize(local)
 
+    # (the clouds were written on torch's current stream: the engine's stream waits for it,
+    # icp_set_*_device_stream, without a device synchronisation)
+    sm = torch_stream(dm)
+
     def registration_step():
-        ctx.set_model_device(dm.data_ptr(), m.shape[0])
-        ctx.set_scene_device(dps.data_ptr(), c, args.n)
+        ctx.set_model_device(dm.data_ptr(), m.shape[0], stream=sm)
+        ctx.set_scene_device(dps.data_ptr(), c, args.n, stream=sm)
         return ctx.run(REGISTRATION_ITERS, -1.0)
 
     progress("model and scene resident")

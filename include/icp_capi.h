@@ -113,6 +113,9 @@ typedef struct icp_stats {
     long long bundle_builds_in_run; /* ... of which between two iterations of an icp_run          */
     long long run_bundle_searches;  /* icp_run searches that ran the bundle cascade                */
     long long run_grid_searches;    /* icp_run searches that ran the exact grid search             */
+    long long run_certified; /* queries of icp_run's fused grid iterations that kept their
+                                correspondence by the exclusion certificate, without a walk    */
+    long long run_walked;    /* ... and those that walked their box (or were taken by a wave)  */
 } icp_stats;
 /* icp_stats.last_filter: the search level that decided most queries */
 #define ICP_FILTER_VALU 0    /* fp32 direct-form filter on the vector ALUs */
@@ -159,9 +162,16 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
 /* The same two calls for clouds already in device memory (AoS fp64, 3 x n col-major, on the
  * context's device, e.g. the output of an earlier GPU stage): no PCIe copy -- the model's images
  * and the scene's SoA copies are built from the caller's array on the context's stream.  The
- * caller's array must stay valid and unmodified until the call returns. */
+ * array is read after all work enqueued before the call on ANY stream of the device (the call
+ * synchronises the device first), and must stay valid and unmodified until the call returns. */
 int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm);
 int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total);
+/* ... reading the array after the work enqueued so far on `producer` only (a hipStream_t of the
+ * context's device; NULL = the legacy default stream): the context's stream waits for an event
+ * recorded there, with no device synchronisation.  Work on other streams is not waited for. */
+int icp_set_model_device_stream(icp_ctx *ctx, const double *m_xyz_dev, size_t nm, void *producer);
+int icp_set_scene_device_stream(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total,
+                                void *producer);
 /* Copy this rank's current new_p (gpu.hh:88) back to the host. */
 int icp_get_scene(icp_ctx *ctx, double *p_xyz_out);
 /* icp_set_model, unless the resident model already holds exactly these nm points, bit for bit

@@ -320,6 +320,13 @@ struct icp_ctx {
     int *b_glist = nullptr;                   // v2: fired-block list overflow
     double *b_seedd = nullptr;                // v2: per point, D64 to its seed (icp_run's transform)
     size_t b_seedd_cap = 0;
+    // the fused grid iteration's exclusion certificate (CertArgs): per point in slot order the
+    // bound and the pair; counts = (certified, walked) summed over the run (device)
+    hipEvent_t order_ev = nullptr; // icp_set_*_device_stream: the producer stream's point to wait for
+    float *cert_r = nullptr;
+    int2 *cert_pos = nullptr;
+    size_t cert_r_cap = 0, cert_pos_cap = 0;
+    unsigned long long *cert_counts = nullptr;
     char *tail_backup = nullptr;              // icp_run with the fused tail: the starting scene / idx
     size_t tail_backup_cap = 0;
     double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
@@ -1517,7 +1524,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
                     (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame,
                     (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos, (void *)ctx->canon_rowbuf,
-                    (void *)ctx->canon_ticket})
+                    (void *)ctx->canon_ticket, (void *)ctx->cert_r, (void *)ctx->cert_pos, (void *)ctx->cert_counts})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -1529,6 +1536,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->h_trace) (void)hipHostFree(ctx->h_trace);
     if (ctx->h_io) (void)hipHostFree(ctx->h_io);
     for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
+    if (ctx->order_ev) (void)hipEventDestroy(ctx->order_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -1747,11 +1755,28 @@ static bool model_needs_host(const icp_ctx *ctx, size_t nm)
            ctx->nn_rule == ICP_NN_RULE_CPU_SQRT;
 }
 
-int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm)
+// The caller's device array is read on the context's stream (non-blocking: nothing orders it after
+// other streams' work by itself).  producer: the stream whose work so far wrote the array -- the
+// context's stream waits for it (an event, no host synchronisation); nullptr (icp_set_*_device):
+// every stream of the device, by a device synchronisation.
+static int order_after_producer(icp_ctx *ctx, void *producer, bool any_stream)
+{
+    if (any_stream) {
+        HIPCHK(hipDeviceSynchronize());
+        return ICP_OK;
+    }
+    if (!ctx->order_ev) HIPCHK(hipEventCreateWithFlags(&ctx->order_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->order_ev, (hipStream_t)producer));
+    HIPCHK(hipStreamWaitEvent(ctx->st, ctx->order_ev, 0));
+    return ICP_OK;
+}
+
+static int set_model_device_impl(icp_ctx *ctx, const double *m_xyz_dev, size_t nm, void *producer, bool any_stream)
 {
     if (!ctx || !m_xyz_dev || nm == 0) return ICP_E_ARG;
     if (nm > (size_t)0x7fffffff - kTile32) return fail(ctx, ICP_E_ARG, "model too large");
     HIPCHK(hipSetDevice(ctx->device));
+    TRY(order_after_producer(ctx, producer, any_stream));
     std::vector<double> host; // (only when a host-side image needs the points)
     if (model_needs_host(ctx, nm)) {
         host.resize(3 * nm);
@@ -1759,6 +1784,16 @@ int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm)
         HIPCHK(hipStreamSynchronize(ctx->st));
     }
     return set_model_staged(ctx, host.empty() ? nullptr : host.data(), nm, m_xyz_dev);
+}
+
+int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm)
+{
+    return set_model_device_impl(ctx, m_xyz_dev, nm, nullptr, true);
+}
+
+int icp_set_model_device_stream(icp_ctx *ctx, const double *m_xyz_dev, size_t nm, void *producer)
+{
+    return set_model_device_impl(ctx, m_xyz_dev, nm, producer, false);
 }
 
 int icp_ensure_model(icp_ctx *ctx, const double *m_xyz, size_t nm, int *uploaded)
@@ -1841,11 +1876,13 @@ int icp_set_scene(icp_ctx *ctx, const double *p_xyz, size_t np_local, size_t np_
     return set_scene_common(ctx, np_local, np_total, slot);
 }
 
-int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total)
+static int set_scene_device_impl(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total,
+                                 void *producer, bool any_stream)
 {
     if (!ctx || (!p_xyz_dev && np_local) || np_local > np_total) return ICP_E_ARG;
     if (np_total > (size_t)0x7fffffff) return fail(ctx, ICP_E_ARG, "scene too large");
     HIPCHK(hipSetDevice(ctx->device));
+    if (np_local) TRY(order_after_producer(ctx, producer, any_stream));
     TRY(ensure_reduction_space(ctx));
     TRY(grow_cloud(ctx, ctx->Y, np_local, false));
     TRY(grow_cloud(ctx, ctx->scene, np_local, true));
@@ -1854,6 +1891,17 @@ int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local,
     // the caller's array is read on the context's stream: done before the call returns
     if (np_local) HIPCHK(hipStreamSynchronize(ctx->st));
     return set_scene_common(ctx, np_local, np_total, slot);
+}
+
+int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total)
+{
+    return set_scene_device_impl(ctx, p_xyz_dev, np_local, np_total, nullptr, true);
+}
+
+int icp_set_scene_device_stream(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total,
+                                void *producer)
+{
+    return set_scene_device_impl(ctx, p_xyz_dev, np_local, np_total, producer, false);
 }
 
 static int set_scene_common(icp_ctx *ctx, size_t np_local, size_t np_total, bool slot)
@@ -2504,6 +2552,36 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         if (!ctx->h_far) HIPCHK(hipHostMalloc((void **)&ctx->h_far, sizeof(int), hipHostMallocDefault));
     }
     const bool lag_sched = lag || canon;
+    // The fused grid iteration's exclusion certificate (icp_grid.hip): the state one fused
+    // iteration writes is read by the next one of this run only (cert_prev); any other search
+    // leaves it stale.  ICP_CERT=0: every query walks (A/B); ICP_CERT_TWO=0: the one-point form;
+    // ICP_CERT_SKIN: the walk's extra radius in grid cells (default 0.25).
+    static const bool cert_env = [] {
+        const char *e = getenv("ICP_CERT");
+        return !(e && e[0] == '0');
+    }();
+    static const int cert_two = [] {
+        const char *e = getenv("ICP_CERT_TWO");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    static const double cert_skin = [] {
+        const char *e = getenv("ICP_CERT_SKIN");
+        const double v = e ? atof(e) : 0.25;
+        return v >= 0.0 && v <= 4.0 ? v : 0.25;
+    }();
+    CertArgs cert;
+    bool cert_prev = false;
+    if (canon && cert_env && grid_iter_on() && ctx->g_pts32) {
+        TRY(grow(ctx, &ctx->cert_r, &ctx->cert_r_cap, n));
+        TRY(grow(ctx, &ctx->cert_pos, &ctx->cert_pos_cap, n));
+        if (!ctx->cert_counts) HIPCHK(hipMalloc((void **)&ctx->cert_counts, 2 * sizeof(unsigned long long)));
+        HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * sizeof(unsigned long long), ctx->st));
+        cert.r = ctx->cert_r;
+        cert.pos = ctx->cert_pos;
+        cert.two = cert_two;
+        cert.skin = cert_skin / ctx->grid.inv_h;
+        cert.counts = ctx->cert_counts;
+    }
     // ICP_ITER_DEBUG=1: nn_grid_iter_kernel's phase clocks and counts, summed over the run, to stderr
     static const bool iter_debug = getenv("ICP_ITER_DEBUG") != nullptr;
     unsigned long long *iter_dbg = nullptr;
@@ -2627,11 +2705,13 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                              ctx->st, Y.x, Y.y, Y.z);
                     LAUNCHCHK("nn_grid_cell_seed");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
-                    launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd, need_p32 ? P.f : nullptr,
-                                        grid_view(ctx), kSeededBox, grid_budget(ctx), (int)ctx->nm, ctx->m4,
-                                        ctx->canon_rowbuf, grid_policy ? &sd->far_acc : nullptr,
-                                        sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2, ctx->st,
-                                        iter_dbg, 0);
+                    cert.valid = 0;
+                    cert_prev = launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd,
+                                                    need_p32 ? P.f : nullptr, grid_view(ctx), kSeededBox,
+                                                    grid_budget(ctx), (int)ctx->nm, ctx->m4, ctx->canon_rowbuf,
+                                                    grid_policy ? &sd->far_acc : nullptr,
+                                                    sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2,
+                                                    ctx->st, iter_dbg, 0, cert);
                     LAUNCHCHK("nn_grid_iter (first)");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));
                     ws = SeedState{};
@@ -2662,11 +2742,13 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                 (grid_c || ctx->nn_variant == ICP_NN_VARIANT_GRID) && ctx->g_pts32;
                 if (k1) {
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
-                    launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd, need_p32 ? P.f : nullptr,
-                                        grid_view(ctx), kSeededBox, grid_budget(ctx), (int)ctx->nm, ctx->m4,
-                                        ctx->canon_rowbuf, grid_policy ? &sd->far_acc : nullptr,
-                                        sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2,
-                                        ctx->amb_count + 2, ctx->st, iter_dbg);
+                    cert.valid = cert_prev ? 1 : 0;
+                    cert_prev = launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd,
+                                                    need_p32 ? P.f : nullptr, grid_view(ctx), kSeededBox,
+                                                    grid_budget(ctx), (int)ctx->nm, ctx->m4, ctx->canon_rowbuf,
+                                                    grid_policy ? &sd->far_acc : nullptr,
+                                                    sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2,
+                                                    ctx->st, iter_dbg, 1, cert);
                     LAUNCHCHK("nn_grid_iter");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));
                     if (!need_p32) ctx->p32_stale = true;
@@ -2692,6 +2774,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     }
                     continue;
                 }
+                cert_prev = false; // (any other search: the certificate's state is stale)
                 if (xf_pending) { // the last Horn step's transform, in the form this search reads
                     SeedArgs sa_t = grid_c ? sa_grid : sa;
                     if (!grid_c) records_args(sa_t);
@@ -2973,6 +3056,12 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }
     // (every transform of a policy run wrote the seed distances, whatever its form; the next run
     // may start from them)
+    if (cert.counts) {
+        unsigned long long cc[2] = {0ull, 0ull};
+        HIPCHK(hipMemcpy(cc, ctx->cert_counts, sizeof(cc), hipMemcpyDeviceToHost));
+        ctx->stats.run_certified += (long long)cc[0];
+        ctx->stats.run_walked += (long long)cc[1];
+    }
     ctx->seedd_valid = grid_policy && ws.seedd;
     ctx->last_far = far_obs;
     ctx->last_q2 = q2_obs;

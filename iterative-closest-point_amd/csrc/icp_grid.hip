@@ -1382,14 +1382,518 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
+// ---- the fused grid iteration with the exclusion certificate (round 6) ------------------------
+//
+// nn_grid_iter_kernel's iteration (the pending transform, the exact seeded search of every query,
+// the moments and the residual into the canonical rows) in three phases per wave task (a chunk
+// of 32 queries, as there):
+//
+//   A  (two lanes a query) the transform, the residual (the seed distance), the policy's far
+//      count, p' written; the exclusion certificate (below) settles the query, or it is a walker:
+//      its state (p', seed, seed distance) goes to an LDS slot;
+//   D  (the walkers, packed) the task's walkers get G = 64 / 2^k lanes each (2^k >= their count):
+//      a task with 5..8 walkers walks each over 8 lanes, so a wave's walk takes as many load
+//      rounds as its busiest walker's rows / G, where the two-lane kernel took its busiest query's
+//      rows / 2 whatever the rest (the walk itself is that kernel's: a row's x-run cut to the seed
+//      sphere's chord, fp32 screen, candidates in fp64); the winner, its coordinates and the next
+//      certificate go back (idx / y / state in HBM, y in the slot); a box over `box` cells is the
+//      whole wave's, one query at a time, as before;
+//   G  (a lane a query) the 18 leaves into the LDS tile, lane k folds column k by the chunk tree
+//      (icp_canon.h).
+//
+// The exclusion certificate.  Per query the state (CertArgs) is a bound r and a pair pos = (the
+// correspondence, a second point) in grid positions: every model point outside the pair lies at
+// least r from the query's position when r was set.  The query moved by mot since (|p' - p|,
+// rounded up), so every such point is now at least Rc = r - mot away (the triangle inequality).
+// The nearer of the pair in the exact (D64, index) order is then the first minimum if its
+// distance is below Rc: every other D64 is above Rc^2 (1 - 3u) > that of the pair's winner (D64
+// is within a few ulps of the true square; the test keeps 2^-40 of room).  A walk sets the next
+// state: the pair (winner, the nearest other point it saw) and r = min(the radius it scanned, the
+// bound from the second-nearest other it saw).  The walk scans the seed sphere plus a skin
+// (ca.skin) so that a query that keeps its correspondence has room to move before it walks again.
+// Exactness is the walk's (every point as close as the seed is scanned and decided in fp64); the
+// bounds are pinned by tests/test_iter_prune.py.  Measured at C4: 75% of a registration's queries
+// certified (profiles/r06a/cert_probe.log), a CPU model of the trajectory agrees
+// (tools/cert_model.py).
+constexpr int kIter2Slot = 8; // doubles a query's hand-off slot: p' (3), seed distance, seed coordinates (3), (seed, h)
+constexpr int kIter2Tile = kCanonCols * kLeafStride; // doubles a chunk's leaf tile
+static_assert(32 * kIter2Slot + 32 / 2 <= kIter2Tile, "the hand-off slots and the walker list alias the tiles");
+
+#ifndef ICP_ITER2_WAVES
+#define ICP_ITER2_WAVES 4 // (waves a SIMD nn_grid_iter2_kernel is compiled for)
+#endif
+// CH chunks a task (1: a chunk, two lanes a query in phases A and G; 2: chunks c and c + S of the
+// strand together, a lane a query -- the walkers of 64 queries packed, one task a wave at C4)
+template <int KR, int KU, int CH>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER2_WAVES))) void nn_grid_iter2_kernel(
+    int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
+    double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
+    float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
+    double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, int xform, int xcd_l, CertArgs ca)
+{
+    static_assert(CH == 1 || CH == 2, "one or two chunks a task");
+    constexpr int NW = kBlock / 64, QL = 2 / CH; // (lanes a query in phases A and G)
+    __shared__ double s_tile[NW][CH * kIter2Tile];
+    if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane / QL, sub = lane % QL;
+    const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
+    const int wr = xcd_row((int)blockIdx.x, R, xcd_l); // (as nn_grid_iter_kernel: runs of rows an XCD)
+    const int s = wr * 4 + wave;
+    double *const tile = s_tile[wave];
+    double *const slots = tile;                            // (phases A-D) 32 CH slots of kIter2Slot doubles
+    int *const wl = (int *)(tile + 32 * CH * kIter2Slot);  // (phase D) the task's walkers, in query order
+    const bool cert_on = ca.r != nullptr, cert_in = cert_on && ca.valid != 0;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    double acc = 0.0; // (lane k < 18: column k of this strand)
+    int far = 0, nbig = 0, ncert = 0, nwalk = 0;
+    auto slot_t = [&](int c, int uu) { return (c + (uu >> 5) * S) * kCanonChunk + (uu & 31); }; // (query uu's point)
+    for (int c = s; s < S && c < C; c += CH * S) {
+        const int t = slot_t(c, u);
+        const bool active = c + (u >> 5) * S < C && t < n;
+        // ---- A: the previous transform, its residual = the seed distance, the certificate
+        double q[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
+        int h = -1;
+        float cr = -1.0f;
+        int2 cps = make_int2(-1, -1);
+        double mot = 0.0;
+        if (active) {
+            const double p0 = px[t], p1 = py[t], p2 = pz[t];
+            y[0] = yx[t];
+            y[1] = yy[t];
+            y[2] = yz[t];
+            h = idx[t];
+            if (cert_in) {
+                cr = ca.r[t];
+                cps = ca.pos[t];
+            }
+            if (xform) {
+                transform_point(st->xf, p0, p1, p2, q[0], q[1], q[2]);
+                if (cert_in) mot = sqrt(residual2(p0, p1, p2, q[0], q[1], q[2]));
+            } else { // (a run's first iteration: no pending transform, the point as it is)
+                q[0] = p0;
+                q[1] = p1;
+                q[2] = p2;
+            }
+        }
+        const double e = active ? residual2(y[0], y[1], y[2], q[0], q[1], q[2]) : 0.0;
+        if (active && sub == 0 && xform) {
+            px[t] = q[0];
+            py[t] = q[1];
+            pz[t] = q[2];
+            if (p32)
+                p32[t] = make_float4((float)(q[0] - st->xf.c[0]), (float)(q[1] - st->xf.c[1]), (float)(q[2] - st->xf.c[2]),
+                                     0.0f);
+        }
+        if (active && sub == 0) { // the policy's far count (SeedArgs::far_box's rule, or the distance rule)
+            if (far_d2 >= 0.0) {
+                if (xform) far += e > far_d2 ? 1 : 0;
+            } else {
+                int b0[3], b1[3];
+                far += h >= 0 && e == e && e < INFINITY && complete_box(q, e, gv, box, b0, b1) ? 0 : 1;
+            }
+        }
+        double best = e; // (the pair's winner: the correspondence, or the second point)
+        int bi = h;
+        double w[3] = {y[0], y[1], y[2]};
+        bool certd = false;
+        if (cert_in && active && h >= 0 && cr > 0.0f) {
+            // (the subtraction's own rounding: 2^-53 of cr at most, covered by the last term)
+            const double Rc = ((double)cr - mot * (1.0 + 0x1.0p-40)) - (double)cr * 0x1.0p-48;
+            if (ca.two && cps.y >= 0) {
+                const double4 r2 = gv.pts[cps.y];
+                const double d2 = d64g(q[0], q[1], q[2], r2.x, r2.y, r2.z);
+                const int mi2 = (int)r2.w;
+                if (d2 < best || (d2 == best && (unsigned)mi2 < (unsigned)bi)) {
+                    best = d2;
+                    bi = mi2;
+                    w[0] = r2.x;
+                    w[1] = r2.y;
+                    w[2] = r2.z;
+                }
+            }
+            certd = best == best && sqrt(best) * (1.0 + 0x1.0p-40) < Rc;
+            if (certd && sub == 0) {
+                ca.r[t] = __double2float_rd(Rc);
+                if (bi != h) { // (the second point won: the pair swaps)
+                    ca.pos[t] = make_int2(cps.y, cps.x);
+                    idx[t] = bi;
+                    yx[t] = w[0];
+                    yy[t] = w[1];
+                    yz[t] = w[2];
+                }
+            }
+        }
+        // the hand-off: a walker's state, or a settled query's correspondence
+        double *const sl = slots + u * kIter2Slot;
+        const bool walker = active && !certd;
+        if (walker && sub == 0) {
+            sl[0] = q[0];
+            sl[1] = q[1];
+            sl[2] = q[2];
+            sl[3] = best;
+            ((int *)(sl + 7))[0] = bi;
+            ((int *)(sl + 7))[1] = h;
+        }
+        if (active && sub == 0) {
+            sl[4] = w[0];
+            sl[5] = w[1];
+            sl[6] = w[2];
+        }
+        const unsigned long long wm = __ballot(walker && sub == 0);
+        ncert += certd && sub == 0 ? 1 : 0;
+        nwalk += walker && sub == 0 ? 1 : 0;
+        const int nW = __popcll(wm);
+        if (walker && sub == 0) wl[__popcll(wm & ((1ull << lane) - 1ull))] = u;
+        wave_sync();
+        // ---- D: the walkers, at most 32 at a time, G = 64 / 2^k lanes each
+        for (int b0 = 0; b0 < nW; b0 += 32) {
+            const int nb = min(32, nW - b0);
+            const int lg = nb > 16 ? 1 : nb > 8 ? 2 : nb > 4 ? 3 : nb > 2 ? 4 : nb > 1 ? 5 : 6;
+            const int G = 1 << lg, wi = lane >> lg, ws = lane & (G - 1);
+            const bool wact = wi < nb;
+            const int wu = wl[b0 + (wact ? wi : 0)];
+            const double *const ws_sl = slots + wu * kIter2Slot;
+            // (the walker's registers: its point, the winner's D64 / index / grid position; the seed's
+            // coordinates, the correspondence's index and the walk's radius stay in the slot)
+            double wq[3], wb = INFINITY;
+            int wbi = -1;
+            wq[0] = ws_sl[0];
+            wq[1] = ws_sl[1];
+            wq[2] = ws_sl[2];
+            if (wact) {
+                wb = ws_sl[3];
+                wbi = ((const int *)(ws_sl + 7))[0];
+            }
+            // the walk's squared radius: the seed distance, plus the skin the next bound needs
+            // (without the skin when that box is over `box`)
+            int c0[3] = {0, 0, 0}, c1[3] = {-1, -1, -1};
+            double ew = wb;
+            bool ok = false;
+            if (wact && wbi >= 0 && wb == wb && wb < INFINITY) {
+                if (cert_on) {
+                    const double rs = sqrt(wb) + ca.skin;
+                    ew = rs * rs;
+                    ok = complete_box(wq, ew, gv, box, c0, c1);
+                    if (!ok) ew = wb;
+                }
+                if (!ok) ok = complete_box(wq, ew, gv, box, c0, c1);
+            }
+            if (wact && ws == 0) slots[wu * kIter2Slot + 3] = ew; // (read back for the next bound)
+            int bk = -1;      // (the winner's grid position, when this lane scanned it)
+            float a1 = INFINITY, a2 = INFINITY; // (the certificate: the two smallest others, a1 at k1)
+            int k1 = -1;
+            auto other = [&](float v, int k) {
+                if (v < a2) {
+                    if (v < a1) {
+                        a2 = a1;
+                        a1 = v;
+                        k1 = k;
+                    } else {
+                        a2 = v;
+                    }
+                }
+            };
+            auto eq_of = [&]() { // (the per-axis fp32 coordinate error bound of the screen)
+                const double o0 = wq[0] - gv.c32[0], o1 = wq[1] - gv.c32[1], o2 = wq[2] - gv.c32[2];
+                return std::ldexp(fmax(fabs(o0), fmax(fabs(o1), fabs(o2))), -23) + gv.em32;
+            };
+            if (ok) {
+                const float f0 = (float)(wq[0] - gv.c32[0]), f1 = (float)(wq[1] - gv.c32[1]), f2 = (float)(wq[2] - gv.c32[2]);
+                const double eq = eq_of();
+                const float T = seeded_bound32(wb, eq);
+                const int ny = c1[1] - c0[1] + 1, nrq = ny * (c1[2] - c0[2] + 1);
+                constexpr int kCand = ICP_ITER_KCAND;
+                int cand[kCand], nc = 0;
+                auto flush = [&]() {
+                    double4 r[kCand];
+#pragma unroll
+                    for (int j = 0; j < kCand; ++j)
+                        if (j < nc) r[j] = gv.pts[cand[j]];
+#pragma unroll
+                    for (int j = 0; j < kCand; ++j) {
+                        if (j >= nc) break;
+                        const int mi = (int)r[j].w;
+                        const double d = d64g(wq[0], wq[1], wq[2], r[j].x, r[j].y, r[j].z);
+                        if (d < wb || (d == wb && (unsigned)mi < (unsigned)wbi)) {
+                            if (cert_on && bk >= 0) other(__double2float_rd(wb), bk); // (the displaced winner)
+                            wb = d;
+                            wbi = mi;
+                            bk = cand[j];
+                        } else if (cert_on) {
+                            other(__double2float_rd(d), cand[j]);
+                        }
+                    }
+                    nc = 0;
+                };
+                auto test = [&](const float4 &m, int pos) {
+                    const float dx = f0 - m.x, dy = f1 - m.y, dz = f2 - m.z;
+                    const float d32 = (dx * dx + dy * dy) + dz * dz;
+                    if (d32 > T) { // (strictly farther than the seed)
+                        if (cert_on) other(d32, pos);
+                        return;
+                    }
+                    if (__float_as_int(m.w) == wbi) {
+                        bk = pos; // (the current winner itself)
+                    } else {
+                        cand[nc++] = pos;
+                        if (nc == kCand) flush();
+                    }
+                };
+                // the sphere prune (nn_grid_iter_kernel's, radius sqrt(ew); tests/test_iter_prune.py)
+                const float inv_ny = 1.0f / (float)ny;
+                float tr[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) tr[a] = (float)((wq[a] - gv.lo[a]) * gv.inv_h - (double)c0[a]);
+                const float rcf = (float)(sqrt(ew) * gv.inv_h * (1.0 + 0x1.0p-18) +
+                                          0x1.0p-20 * (1.0 + fabs((double)tr[0]) + fabs((double)tr[1]) + fabs((double)tr[2])));
+                const float rc2 = rcf * rcf, xroom = 0x1.0p-20f * (1.0f + fabsf(tr[0]));
+                const float xspan = (float)(c1[0] - c0[0] + 1);
+                auto row_run = [&](int r, int &a0, int &a1r) {
+                    a0 = 0;
+                    a1r = 0;
+                    if (r >= nrq) return;
+                    const int rz = (int)(((float)r + 0.5f) * inv_ny), ry = r - rz * ny;
+                    const int row = ((c0[2] + rz) * gv.g[1] + c0[1] + ry) * gv.g[0];
+                    int x0 = c0[0], x1 = c1[0];
+                    const float dy = fmaxf(0.0f, fmaxf((float)ry - tr[1], tr[1] - (float)(ry + 1)));
+                    const float dz = fmaxf(0.0f, fmaxf((float)rz - tr[2], tr[2] - (float)(rz + 1)));
+                    const float rem = rc2 - dy * dy - dz * dz;
+                    if (rem < 0.0f) return; // (the row lies beyond the sphere)
+                    const float xw = sqrtf(rem) * (1.0f + 0x1.0p-20f) + xroom;
+                    x0 = max(x0, c0[0] + (int)floorf(fmaxf(tr[0] - xw, -1.0f)));
+                    x1 = min(x1, c0[0] + (int)floorf(fminf(tr[0] + xw, xspan)));
+                    if (x0 <= x1) {
+                        a0 = gv.start[row + x0];
+                        a1r = gv.start[row + x1 + 1];
+                    }
+                };
+                { // (each lane its own rows, r = ws, ws + G, ...; the two-lane kernel's point-by-point
+                  // deal of a pair's rows measured +0.3% there, profiles/r05am)
+                    for (int r0 = ws; r0 < nrq; r0 += KR * G) {
+                        int k0[KR], pre[KR + 1];
+                        pre[0] = 0;
+#pragma unroll
+                        for (int v = 0; v < KR; ++v) {
+                            int a0, a1r;
+                            row_run(r0 + v * G, a0, a1r);
+                            k0[v] = a0;
+                            pre[v + 1] = pre[v] + (a1r - a0);
+                        }
+                        const int tot = pre[KR];
+                        for (int f0 = 0; f0 < tot; f0 += KU) {
+                            int kk[KU];
+#pragma unroll
+                            for (int v = 0; v < KU; ++v) {
+                                const int f = f0 + v;
+                                int pp = k0[0] + f;
+#pragma unroll
+                                for (int x = 1; x < KR; ++x)
+                                    if (f >= pre[x]) pp = k0[x] + (f - pre[x]);
+                                kk[v] = f < tot ? pp : -1;
+                            }
+                            float4 mm[KU];
+#pragma unroll
+                            for (int v = 0; v < KU; ++v) mm[v] = gv.pts32[kk[v] >= 0 ? kk[v] : 0];
+#pragma unroll
+                            for (int v = 0; v < KU; ++v)
+                                if (kk[v] >= 0) test(mm[v], kk[v]);
+                        }
+                    }
+                }
+                if (nc) flush();
+            }
+            // the walker's G lanes: the (D64, index) minimum, its position and coordinates; with the
+            // certificate also the others (the two lists, and the sub-group winner that loses a merge
+            // -- one with no position here was scanned by a lane of another sub-group, which holds it)
+            for (int o = 1; o < G; o <<= 1) {
+                const double ob = __shfl_xor(wb, o, 64);
+                const int oi = __shfl_xor(wbi, o, 64), ok2 = __shfl_xor(bk, o, 64);
+                const bool theirs = ob < wb || (ob == wb && (unsigned)oi < (unsigned)wbi);
+                if (cert_on) {
+                    const float oa1 = __shfl_xor(a1, o, 64), oa2 = __shfl_xor(a2, o, 64);
+                    const int ok1 = __shfl_xor(k1, o, 64);
+                    if (a1 <= oa1) {
+                        a2 = fminf(a2, oa1);
+                    } else {
+                        a2 = fminf(oa2, a1);
+                        a1 = oa1;
+                        k1 = ok1;
+                    }
+                    if (oi != wbi) {
+                        const int lk = theirs ? bk : ok2;
+                        if (lk >= 0) other(__double2float_rd(theirs ? wb : ob), lk);
+                    }
+                }
+                if (theirs) {
+                    wb = ob;
+                    wbi = oi;
+                    bk = ok2;
+                } else if (ob == wb && oi == wbi) {
+                    bk = max(bk, ok2);
+                }
+            }
+            // a walker whose box exceeds `box` cells (or has no finite seed): the whole wave, one at
+            // a time -- the box up to `budget` cells, else every model point
+            unsigned long long bigm = __ballot(wact && ws == 0 && !ok);
+            nbig += __popcll(bigm);
+            bool whole = false;
+            while (bigm) {
+                const int bl = __ffsll((long long)bigm) - 1;
+                bigm &= bigm - 1;
+                const double bq[3] = {__shfl(wq[0], bl, 64), __shfl(wq[1], bl, 64), __shfl(wq[2], bl, 64)};
+                const double be = __shfl(wb, bl, 64);
+                const int bh = __shfl(wbi, bl, 64);
+                double b2 = INFINITY;
+                int bj = -1;
+                int d0[3], d1[3];
+                if (bh >= 0 && be == be && be < INFINITY && complete_box(bq, be, gv, budget, d0, d1)) {
+                    b2 = be;
+                    bj = bh;
+                    scan_box<64>(bq, d0, d1, gv, lane, b2, bj);
+                } else { // the exact fp64 scan of every point (a NaN query keeps index -1 -> 0)
+                    for (int k = lane; k < nm; k += 64) {
+                        const double4 m = m4[k];
+                        lex_min(b2, bj, d64g(bq[0], bq[1], bq[2], m.x, m.y, m.z), k);
+                    }
+                }
+                group_lex_min<64>(b2, bj);
+                if ((lane >> lg) == (bl >> lg)) {
+                    wb = b2;
+                    wbi = bj < 0 ? 0 : bj;
+                    whole = true;
+                }
+            }
+            // the walker's outputs: idx / y when changed, the next certificate, y for phase G
+            if (wact && ws == 0) {
+                double *const rs_sl = slots + wu * kIter2Slot;
+                const int seed = ((const int *)(rs_sl + 7))[0], wh = ((const int *)(rs_sl + 7))[1];
+                const int wt = slot_t(c, wu);
+                if (wbi != seed) { // (a new winner: its coordinates from its record; y in the slot)
+                    const double4 m = whole ? m4[wbi] : gv.pts[bk];
+                    rs_sl[4] = m.x;
+                    rs_sl[5] = m.y;
+                    rs_sl[6] = m.z;
+                }
+                if (wbi != wh) {
+                    idx[wt] = wbi;
+                    yx[wt] = rs_sl[4];
+                    yy[wt] = rs_sl[5];
+                    yz[wt] = rs_sl[6];
+                }
+                // the bound of the walk: the smaller of the radius it scanned (every point outside has
+                // D64 > ew, so a true distance above sqrt(ew) (1 - 2^-52)) and the bound of its
+                // smallest other outside the pair (two: a2, the second point being k1; one: a1).  A
+                // list value is a computed d32 (or a D64 rounded down, a larger lower bound): by
+                // seeded_bound32's analysis sqrt(d32) <= (|v| + sqrt(3) eq) (1 + 2^-24)^2.5, so the
+                // true distance |v| >= sqrt(d32) (1 - 2^-20) - sqrt(3) eq (1 + 2^-20).  A query the
+                // wave took whole gets no bound.
+                if (cert_on) {
+                    float rout = -1.0f;
+                    int2 pout = make_int2(-1, -1);
+                    if (ok && !whole && bk >= 0) {
+                        double rb = sqrt(rs_sl[3]) * (1.0 - 0x1.0p-40); // (rs_sl[3]: the walk's ew)
+                        const float as = ca.two ? a2 : a1;
+                        if (as < INFINITY)
+                            rb = fmin(rb, sqrt((double)as) * (1.0 - 0x1.0p-20) - 1.7320508075688774 * eq_of() * (1.0 + 0x1.0p-20));
+                        rout = rb > 0.0 ? __double2float_rd(rb) : -1.0f;
+                        pout = make_int2(bk, ca.two ? k1 : -1);
+                    }
+                    ca.r[wt] = rout;
+                    ca.pos[wt] = pout;
+                }
+            }
+            wave_sync();
+        }
+        // ---- G: this task's 18 leaves a query into the chunk tile, then the chunk tree
+        if (active) {
+            y[0] = sl[4];
+            y[1] = sl[5];
+            y[2] = sl[6];
+        }
+        wave_sync(); // (the tile aliases the slots)
+        const double cp[3] = {st->shift_p[0], st->shift_p[1], st->shift_p[2]};
+        const double cy[3] = {st->shift_y[0], st->shift_y[1], st->shift_y[2]};
+        const double d[6] = {active ? q[0] - cp[0] : 0.0, active ? q[1] - cp[1] : 0.0, active ? q[2] - cp[2] : 0.0,
+                             active ? y[0] - cy[0] : 0.0, active ? y[1] - cy[1] : 0.0, active ? y[2] - cy[2] : 0.0};
+        double *const lf = tile + (u >> 5) * kIter2Tile;
+#pragma unroll
+        for (int k = 0; k < kCanonCols; ++k) {
+            double leaf;
+            if (k < 6) leaf = 0.0 + d[k];
+            else if (k < 15) leaf = 0.0 + d[(k - 6) / 3] * d[3 + (k - 6) % 3];
+            else if (k == 15) leaf = 0.0 + ((d[3] * d[3] + d[4] * d[4]) + d[5] * d[5]);
+            else if (k == 16) leaf = 0.0 + ((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+            else leaf = active ? 0.0 + e : 0.0;
+            if (!active) leaf = 0.0;
+            if (sub == 0) lf[k * kLeafStride + (u & 31)] = leaf;
+        }
+        wave_sync();
+        double tv = 0.0;
+        if ((lane & 31) < kCanonCols && (CH == 2 || lane < 32)) { // lane k: column k (CH 2: lane 32 + k, chunk c + S's)
+            const double *col = tile + (lane >> 5) * kIter2Tile + (lane & 31) * kLeafStride;
+            double part[4];
+#pragma unroll
+            for (int g8 = 0; g8 < 4; ++g8) {
+                double v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = col[8 * g8 + j];
+                part[g8] = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+            }
+            tv = (part[0] + part[1]) + (part[2] + part[3]);
+        }
+        const double tb = CH == 2 ? __shfl(tv, (lane & 31) + 32, 64) : 0.0;
+        if (lane < kCanonCols) {
+            acc = acc + tv;
+            if (CH == 2 && c + S < C) acc = acc + tb;
+        }
+        wave_sync(); // (the next task's slots alias the tiles)
+    }
+    // the workgroup's four strands -> its row (column k from lane k of each wave)
+    __shared__ double sh[NW][kCanonCols];
+    if (lane < kCanonCols) sh[wave][lane] = acc;
+    __syncthreads();
+    if (threadIdx.x < kCanonCols) {
+        const int k = threadIdx.x;
+        rows[(size_t)k * R + wr] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+    }
+    // the far count (the policy's), the big boxes and the certificate's counts: one atomic each
+    __shared__ int s_cnt[4][NW];
+    for (int o = 32; o >= 1; o >>= 1) {
+        far += __shfl_xor(far, o, 64);
+        ncert += __shfl_xor(ncert, o, 64);
+        nwalk += __shfl_xor(nwalk, o, 64);
+    }
+    if (lane == 0) {
+        s_cnt[0][wave] = far;
+        s_cnt[1][wave] = nbig;
+        s_cnt[2][wave] = ncert;
+        s_cnt[3][wave] = nwalk;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        int tot = 0;
+        for (int w = 0; w < NW; ++w) tot += s_cnt[threadIdx.x][w];
+        if (threadIdx.x < 2) {
+            int *dst = threadIdx.x == 0 ? far_acc : big_count;
+            if (tot && dst) atomicAdd(dst, tot);
+        } else if (tot && ca.counts) {
+            atomicAdd(ca.counts + (threadIdx.x - 2), (unsigned long long)tot);
+        }
+    }
+}
+
 } // namespace
 
-void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
+bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
                          const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
                          const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
-                         unsigned long long *dbg, int xform)
+                         unsigned long long *dbg, int xform, const CertArgs &ca)
 {
-    if (n <= 0) return;
+    if (n <= 0) return false;
     // ICP_ITER_STAGE=1: the task's union of boxes staged in LDS (measured slower: the staging's two
     // dependent round trips and the LDS-limited occupancy cost more than the gathers they save)
     static const bool stage = [] {
@@ -1414,6 +1918,28 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         return e ? atoi(e) : -2;
     }();
     const int xcd_l = xcd_env != -2 ? xcd_env : (canon_chunks((size_t)n) >= 8192 ? 32 : -1);
+    // ICP_ITER_V2=0: the two-lane kernel of round 5 (every query walks; A/B) -- also the form of
+    // ICP_ITER_STAGE, ICP_ITER_WIDE and ICP_ITER_DEBUG
+    static const bool v2 = [] {
+        const char *e = getenv("ICP_ITER_V2");
+        return !(e && e[0] == '0');
+    }();
+    if (v2 && !stage && !(wide_on && n <= kIterWideMax) && !dbg) {
+        // ICP_ITER2_CH: chunks a task (2: the walkers of two chunks packed together; 1: a chunk)
+        static const int ch = [] {
+            const char *e = getenv("ICP_ITER2_CH");
+            return e && atoi(e) == 1 ? 1 : 2;
+        }();
+        if (ch == 2)
+            nn_grid_iter2_kernel<ICP_ITER_KR, ICP_ITER_KU, 2><<<R, kBlock, 0, st>>>(
+                n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
+                xform, xcd_l, ca);
+        else
+            nn_grid_iter2_kernel<ICP_ITER_KR, ICP_ITER_KU, 1><<<R, kBlock, 0, st>>>(
+                n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
+                xform, xcd_l, ca);
+        return ca.r != nullptr;
+    }
     if (!stage && wide_on && n <= kIterWideMax)
         nn_grid_iter_kernel<false, 4><<<R, 2 * kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
                                                                  budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform, xcd_l);
@@ -1423,6 +1949,7 @@ void launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
     else
         nn_grid_iter_kernel<false, 2><<<R, kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,
                                                              budget, nm, m4, rows, far_acc, far_d2, big_count, dbg, xform, xcd_l);
+    return false;
 }
 
 namespace {

@@ -58,7 +58,8 @@ EXPORTED = [
     "icp_ctx_create", "icp_ctx_create_dist", "icp_rccl_unique_id", "icp_ctx_create_sharded",
     "icp_ctx_destroy",
     "icp_last_error", "icp_strerror", "icp_device_count", "icp_set_model", "icp_set_scene",
-    "icp_set_model_device", "icp_set_scene_device", "icp_set_progress",
+    "icp_set_model_device", "icp_set_scene_device", "icp_set_model_device_stream",
+    "icp_set_scene_device_stream", "icp_set_progress",
     "icp_get_scene", "icp_set_allow_unequal", "icp_set_nn_variant", "icp_run", "icp_closest_matrix",
     "icp_compute_centroid", "icp_y_p_norm", "icp_err_compute", "icp_find_alignment",
     "icp_horn_solve", "icp_max_element_index", "icp_shard_range", "icp_synthetic_pair",
@@ -91,7 +92,8 @@ class Stats(C.Structure):
                 ("cpu_rule_changed", C.c_longlong), ("persistent_fallbacks", C.c_longlong),
                 ("last_filter", C.c_int), ("bundle_builds", C.c_longlong),
                 ("bundle_builds_in_run", C.c_longlong), ("run_bundle_searches", C.c_longlong),
-                ("run_grid_searches", C.c_longlong)]
+                ("run_grid_searches", C.c_longlong), ("run_certified", C.c_longlong),
+                ("run_walked", C.c_longlong)]
 
 
 class BundleAudit(C.Structure):
@@ -135,6 +137,9 @@ def lib() -> C.CDLL:
     L.icp_set_model_device.argtypes = [vp, vp, sz]
     L.icp_set_progress.argtypes = [vp, PROGRESS_FN, vp]
     L.icp_set_scene_device.argtypes = [vp, vp, sz, sz]
+    if hasattr(L, "icp_set_model_device_stream"):  # (an A/B library of an earlier round may lack them)
+        L.icp_set_model_device_stream.argtypes = [vp, vp, sz, vp]
+        L.icp_set_scene_device_stream.argtypes = [vp, vp, sz, sz, vp]
     L.icp_set_scene.argtypes = [vp, dp, sz, sz]
     L.icp_get_scene.argtypes = [vp, dp]
     L.icp_set_allow_unequal.argtypes = [vp, C.c_int]
@@ -324,15 +329,26 @@ class Context:
         m = _cloud(m)
         self._check(lib().icp_set_model(self._h, _dp(m), m.shape[0]))
 
-    def set_model_device(self, ptr: int, nm: int):
+    def set_model_device(self, ptr: int, nm: int, stream=None):
         """icp_set_model_device: the model's AoS fp64 array already in device memory (a device
-        pointer, e.g. a torch tensor's data_ptr(), written by work ordered before this call)."""
-        self._check(lib().icp_set_model_device(self._h, C.c_void_p(ptr), nm))
+        pointer, e.g. a torch tensor's data_ptr()).  stream None: read after all work enqueued so
+        far on the device (a device synchronisation); else a HIP stream handle (e.g.
+        torch.cuda.current_stream().cuda_stream): read after the work enqueued on that stream
+        (icp_set_model_device_stream, no host synchronisation)."""
+        if stream is None or not hasattr(lib(), "icp_set_model_device_stream"):
+            self._check(lib().icp_set_model_device(self._h, C.c_void_p(ptr), nm))
+        else:
+            self._check(lib().icp_set_model_device_stream(self._h, C.c_void_p(ptr), nm, C.c_void_p(stream)))
 
-    def set_scene_device(self, ptr: int, np_local: int, np_total: int | None = None):
-        """icp_set_scene_device: the scene's AoS fp64 array already in device memory."""
-        self._check(lib().icp_set_scene_device(self._h, C.c_void_p(ptr), np_local,
-                                               np_local if np_total is None else np_total))
+    def set_scene_device(self, ptr: int, np_local: int, np_total: int | None = None, stream=None):
+        """icp_set_scene_device: the scene's AoS fp64 array already in device memory (stream: as
+        set_model_device)."""
+        npt = np_local if np_total is None else np_total
+        if stream is None or not hasattr(lib(), "icp_set_scene_device_stream"):
+            self._check(lib().icp_set_scene_device(self._h, C.c_void_p(ptr), np_local, npt))
+        else:
+            self._check(lib().icp_set_scene_device_stream(self._h, C.c_void_p(ptr), np_local, npt,
+                                                          C.c_void_p(stream)))
         self._np_local = np_local
 
     def set_progress(self, fn):

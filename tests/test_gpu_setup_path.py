@@ -66,6 +66,39 @@ def test_scene_device_matches_host_upload(amd):
     assert_same(a, b)
 
 
+@pytest.mark.parametrize("form", ["any_stream", "producer_stream"])
+def test_device_arrays_written_on_another_stream(amd, form):
+    """The device-array setters read the caller's array after the work that writes it, with no
+    manual synchronisation: the clouds are zeros until a copy queued on a side stream
+    behind a ~10 ms spin fills them.  icp_set_*_device orders after every stream (device
+    synchronisation); icp_set_*_device_stream after the given producer stream."""
+    n = 1 << 16
+    m, p = amd.synthetic_pair(n, seed=21)
+    with amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        a = trajectory(ctx)
+    dm = torch.zeros((n, 3), dtype=torch.float64, device="cuda:0")
+    dp = torch.zeros((n, 3), dtype=torch.float64, device="cuda:0")
+    hm = torch.from_numpy(m).pin_memory()
+    hp = torch.from_numpy(p).pin_memory()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)  # (cycles: the copies land well after the calls are made)
+        dm.copy_(hm, non_blocking=True)
+        dp.copy_(hp, non_blocking=True)
+    with amd.Context(0) as ctx:
+        if form == "any_stream":
+            ctx.set_model_device(dm.data_ptr(), n)
+            ctx.set_scene_device(dp.data_ptr(), n)
+        else:
+            ctx.set_model_device(dm.data_ptr(), n, stream=side.cuda_stream)
+            ctx.set_scene_device(dp.data_ptr(), n, stream=side.cuda_stream)
+        b = trajectory(ctx)
+    assert_same(a, b)
+
+
 def test_scene_before_model_matches_after(amd):
     n = 1 << 16
     m0, _ = amd.synthetic_pair(n, seed=3)
