@@ -116,6 +116,9 @@ typedef struct icp_stats {
     long long run_certified; /* queries of icp_run's fused grid iterations that kept their
                                 correspondence by the exclusion certificate, without a walk    */
     long long run_walked;    /* ... and those that walked their box (or were taken by a wave)  */
+    unsigned long long run_path_bits; /* the last icp_run: bit k set when iteration k's search was the
+                                         exact grid search (k < 64); the rest ran the bundle cascade or
+                                         another filter.  The same on every rank of a job.           */
 } icp_stats;
 /* icp_stats.last_filter: the search level that decided most queries */
 #define ICP_FILTER_VALU 0    /* fp32 direct-form filter on the vector ALUs */

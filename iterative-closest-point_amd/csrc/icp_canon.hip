@@ -246,6 +246,8 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
         sums[K0 + k] = s[0];
         s_sum[K0 + k] = s[0];
     }
+    if (MODE == 0 && K0 == 0 && K == kCanonCols && threadIdx.x == 0) // (several ranks: the far count rides on the all-reduce)
+        sums[kSumFar] = (double)__hip_atomic_load(&cs.s->far_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (MODE == 0) return;
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -296,6 +298,8 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const dou
 #pragma unroll
             for (int i = 0; i < kFoldThreads / 64; i += 2 * span) t[i] = t[i] + t[i + span];
         __hip_atomic_store(sums + k, t[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (MODE == 0 && k == 0) // (several ranks: the far count rides on the all-reduce)
+            sums[kSumFar] = (double)__hip_atomic_load(&cs.s->far_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (MODE != 0) {
             __atomic_thread_fence(__ATOMIC_RELEASE); // (this column before the ticket)
             s_last = __hip_atomic_fetch_add(cs.fold_ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -323,9 +324,8 @@ struct icp_ctx {
     // the fused grid iteration's exclusion certificate (CertArgs): per point in slot order the
     // bound and the pair; counts = (certified, walked) summed over the run (device)
     hipEvent_t order_ev = nullptr; // icp_set_*_device_stream: the producer stream's point to wait for
-    float *cert_r = nullptr;
-    int2 *cert_pos = nullptr;
-    size_t cert_r_cap = 0, cert_pos_cap = 0;
+    int4 *cert_state = nullptr;
+    size_t cert_state_cap = 0;
     unsigned long long *cert_counts = nullptr;
     char *tail_backup = nullptr;              // icp_run with the fused tail: the starting scene / idx
     size_t tail_backup_cap = 0;
@@ -1263,6 +1263,19 @@ int allreduce(icp_ctx *ctx, double *buf, size_t count)
     return ICP_OK;
 }
 
+// an int summed over the ranks (several ranks: through the all-reduce; one: as it is), synchronous
+static int global_count(icp_ctx *ctx, int *v)
+{
+    if (!ctx->comm && ctx->world <= 1) return ICP_OK;
+    double x = (double)*v;
+    HIPCHK(hipMemcpyAsync(ctx->sums + kSumFar + 1, &x, sizeof(double), hipMemcpyHostToDevice, ctx->st));
+    TRY(allreduce(ctx, ctx->sums + kSumFar + 1, 1));
+    HIPCHK(hipMemcpyAsync(&x, ctx->sums + kSumFar + 1, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    *v = (int)x;
+    return ICP_OK;
+}
+
 int check_ready(icp_ctx *ctx, bool need_scene)
 {
     if (!ctx) return ICP_E_ARG;
@@ -1524,7 +1537,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
                     (void *)ctx->mid_q4, (void *)ctx->mid_res, (void *)ctx->mid_perm, (void *)ctx->mid_cnt,
                     (void *)ctx->s_order, (void *)ctx->s_tmp_idx, (void *)ctx->b_pimg_l, (void *)ctx->b_frame,
                     (void *)ctx->m4kd, (void *)ctx->kd_of, (void *)ctx->kpos, (void *)ctx->canon_rowbuf,
-                    (void *)ctx->canon_ticket, (void *)ctx->cert_r, (void *)ctx->cert_pos, (void *)ctx->cert_counts})
+                    (void *)ctx->canon_ticket, (void *)ctx->cert_state, (void *)ctx->cert_counts})
         if (p) (void)hipFree(p);
     if (ctx->h_sums) (void)hipHostFree(ctx->h_sums);
     if (ctx->h_amb) (void)hipHostFree(ctx->h_amb);
@@ -2534,6 +2547,18 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // the model's size goes straight on to the grid -- C4: 107 big boxes, searched in the fused
     // kernel -- without the synchronisation)
     const bool hold_first = grid_policy && !carry && ctx->bundle_pending && ctx->nm >= 2 * n;
+    // the canonical schedule's path rule (below): fold_far[j] = the far count mirrored with
+    // iteration j's (lagged) error step -- transform j's, counted by iteration j + 1's search kernel
+    // (all ranks'); hold_far = transform 0's, read by hold_first
+    std::vector<int> fold_far((size_t)std::max(max_iter, 1), -1);
+    int hold_far = -1;
+    // ICP_TEST_ENQUEUE_DELAY_US: the host sleeps this long before each enqueue attempt (tests: the
+    // path sequence must not depend on how far the host runs ahead)
+    const int enqueue_delay_us = [] {
+        const char *e = getenv("ICP_TEST_ENQUEUE_DELAY_US");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    ctx->stats.run_path_bits = 0;
     // A scene in slot order (C4, C5, their shards): the canonical schedule (icp_canon.h).  The
     // transform of iteration k - 1 is enqueued at the start of iteration k, right before its
     // search, in the form that search reads; its residual and k's moments go to the canonical
@@ -2569,21 +2594,25 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         const double v = e ? atof(e) : 0.25;
         return v >= 0.0 && v <= 4.0 ? v : 0.25;
     }();
+    static const double cert_skin1 = [] { // ICP_CERT_SKIN1: the skin of a launch with no state to read (A/B)
+        const char *e = getenv("ICP_CERT_SKIN1");
+        const double v = e ? atof(e) : -1.0;
+        return v >= 0.0 && v <= 4.0 ? v : cert_skin;
+    }();
     CertArgs cert;
     bool cert_prev = false;
     if (canon && cert_env && grid_iter_on() && ctx->g_pts32) {
-        TRY(grow(ctx, &ctx->cert_r, &ctx->cert_r_cap, n));
-        TRY(grow(ctx, &ctx->cert_pos, &ctx->cert_pos_cap, n));
+        TRY(grow(ctx, &ctx->cert_state, &ctx->cert_state_cap, n));
         if (!ctx->cert_counts) HIPCHK(hipMalloc((void **)&ctx->cert_counts, 2 * sizeof(unsigned long long)));
         HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * sizeof(unsigned long long), ctx->st));
-        cert.r = ctx->cert_r;
-        cert.pos = ctx->cert_pos;
+        cert.state = ctx->cert_state;
         cert.two = cert_two;
         cert.skin = cert_skin / ctx->grid.inv_h;
         cert.counts = ctx->cert_counts;
     }
     // ICP_ITER_DEBUG=1: nn_grid_iter_kernel's phase clocks and counts, summed over the run, to stderr
     static const bool iter_debug = getenv("ICP_ITER_DEBUG") != nullptr;
+    static const bool iter_debug_each = iter_debug && atoi(getenv("ICP_ITER_DEBUG")) == 2;
     unsigned long long *iter_dbg = nullptr;
     if (iter_debug && canon) {
         static unsigned long long *buf = nullptr;
@@ -2638,11 +2667,15 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         LAUNCHCHK("canon_fold");
         const bool tm = horn && slot >= 0 && ar_timed[slot];
         if (tm) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 3], ctx->st));
-        TRY(horn ? allreduce(ctx, ctx->sums, kNumSums) : allreduce(ctx, ctx->sums + kSumErr, 1));
+        // (the policy's runs: the far count rides along as a 19th sum, so every rank decides on the
+        // same global count -- run_loop's path rule)
+        TRY(horn ? allreduce(ctx, ctx->sums, grid_policy ? kNumSums + 1 : kNumSums)
+                 : allreduce(ctx, ctx->sums + kSumErr, 1));
         if (tm) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 4], ctx->st));
         if (horn)
             launch_err_horn_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, cs.hflag, cs.ticket,
-                                 ctx->d_iter_mirror, ctx->d_trace, ctx->c, 1, ctx->amb_count, ctx->st);
+                                 ctx->d_iter_mirror, ctx->d_trace, ctx->c, 1, ctx->amb_count, ctx->st,
+                                 grid_policy ? 1 : 0);
         else
             launch_err_step(ctx->sums, N, threshold, max_iter, ctx->err_trace_dev, sd, cs.hflag, cs.ticket,
                             ctx->d_iter_mirror, ctx->d_trace, ctx->st, nullptr, 0);
@@ -2666,22 +2699,33 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         return ICP_OK;
     };
     while (!stop && waited < max_iter) {
+        if (enqueue_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(enqueue_delay_us));
         if (enqueued < max_iter && enqueued - waited <= kAhead + (lag_sched ? 1 : 0) &&
-            !(!canon && hold_first && enqueued == 1 && waited == 0)) {
+            !(!canon && hold_first && enqueued == 1 && waited == 0) &&
+            !(canon && grid_policy && enqueued >= 3 && waited < enqueued - 2)) { // (fold_far[enqueued - 3] known)
             const int slot = enqueued % kRing;
             // 1. correspondences: compute_Y_w_opti(m, new_p, Y)  (gpu.cc:69)
             const bool timed = enqueued % timing_stride == timing_phase && (enqueued > 0 || timing_stride == 1);
             if (canon) {
-                bool grid_c = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : grid_next);
-                grid_next = grid_policy && (far_obs >= 0 ? far_obs <= far_thr : ctx->bundle_pending);
-                if (xf_pending && hold_first && enqueued == 1 && far_obs < 0) {
-                    // the images pending and no count yet: the first transform, then its far count,
-                    // before the second search's path is chosen (one synchronisation a run)
+                // The path of search k: on the far count of transform k - 3 (counted by iteration
+                // k - 2's search kernel, mirrored with iteration k - 3's lagged error step; all
+                // ranks' on several: kSumFar), which the host has waited for before enqueuing k
+                // (below: iteration k - 1 may still run meanwhile) -- the same count whatever the
+                // host's lead over the device, and on every rank.  Before that count exists:
+                // transform 0's count when hold_first read it, else the count the last run ended
+                // with (carry), else the grid while the bundle images are pending.
+                const int far_dec = enqueued >= 3 ? fold_far[enqueued - 3] : hold_far >= 0 ? hold_far : carry ? ctx->last_far : -1;
+                bool grid_c = grid_policy && (far_dec >= 0 ? far_dec <= far_thr : enqueued == 0 ? grid_next : ctx->bundle_pending);
+                if (xf_pending && hold_first && enqueued == 1 && far_dec < 0) {
+                    // the images pending and no count yet: the first transform, then its far count
+                    // (all ranks'), before the second search's path is chosen (one synchronisation a run)
                     TRY(canon_transform(sa_grid));
                     HIPCHK(hipMemcpyAsync(ctx->h_far, &sd->far_acc, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
                     HIPCHK(hipStreamSynchronize(ctx->st));
-                    far_obs = *ctx->h_far;
-                    grid_c = far_obs <= far_thr;
+                    hold_far = *ctx->h_far;
+                    if (lag) TRY(global_count(ctx, &hold_far));
+                    far_obs = hold_far;
+                    grid_c = hold_far <= far_thr;
                 }
                 // a fresh run's first iteration on the grid as ONE launch too: cell seeds (their
                 // coordinates as the correspondences), then the fused kernel with no pending
@@ -2706,6 +2750,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     LAUNCHCHK("nn_grid_cell_seed");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
                     cert.valid = 0;
+                    cert.skin = cert_skin1 / ctx->grid.inv_h;
                     cert_prev = launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd,
                                                     need_p32 ? P.f : nullptr, grid_view(ctx), kSeededBox,
                                                     grid_budget(ctx), (int)ctx->nm, ctx->m4, ctx->canon_rowbuf,
@@ -2718,6 +2763,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     ctx->seeds_valid = true;
                     ctx->stats.last_filter = ICP_FILTER_GRID;
                     ctx->stats.run_grid_searches += 1;
+                    if (enqueued < 64) ctx->stats.run_path_bits |= 1ull << enqueued;
                     ctx->kpos_valid = false;
                     ctx->y_ready = true;
                     ar_timed[slot] = false;
@@ -2743,12 +2789,21 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 if (k1) {
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot], ctx->st));
                     cert.valid = cert_prev ? 1 : 0;
+                    cert.skin = (cert_prev ? cert_skin : cert_skin1) / ctx->grid.inv_h;
                     cert_prev = launch_nn_grid_iter((int)n, P.x, P.y, P.z, Y.x, Y.y, Y.z, ctx->idx, sd,
                                                     need_p32 ? P.f : nullptr, grid_view(ctx), kSeededBox,
                                                     grid_budget(ctx), (int)ctx->nm, ctx->m4, ctx->canon_rowbuf,
                                                     grid_policy ? &sd->far_acc : nullptr,
                                                     sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2,
                                                     ctx->st, iter_dbg, 1, cert);
+                    if (iter_dbg && iter_debug_each) { // (ICP_ITER_DEBUG=2: each launch's counts, synchronising)
+                        unsigned long long h[16];
+                        HIPCHK(hipStreamSynchronize(ctx->st));
+                        HIPCHK(hipMemcpy(h, iter_dbg, sizeof(h), hipMemcpyDeviceToHost));
+                        fprintf(stderr, "[iter2_debug] it %d tasks %llu walkers %llu batches %llu pair %llu | wave-us A %.1f D %.1f G %.1f\n",
+                                enqueued, h[0], h[1], h[2], h[3], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01);
+                        HIPCHK(hipMemset(iter_dbg, 0, sizeof(h)));
+                    }
                     LAUNCHCHK("nn_grid_iter");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));
                     if (!need_p32) ctx->p32_stale = true;
@@ -2756,6 +2811,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                     xf_pending = false;
                     ctx->stats.last_filter = ICP_FILTER_GRID;
                     ctx->stats.run_grid_searches += 1;
+                    if (enqueued < 64) ctx->stats.run_path_bits |= 1ull << enqueued;
                     ctx->kpos_valid = false;
                     ctx->y_ready = true;
                     ar_timed[slot] = false;
@@ -2787,6 +2843,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                     ctx->scene_slot, grid_c, gs));
                 if (ctx->stats.last_filter == ICP_FILTER_BUNDLE) ctx->stats.run_bundle_searches += 1;
                 else if (ctx->stats.last_filter == ICP_FILTER_GRID) ctx->stats.run_grid_searches += 1;
+                if (ctx->stats.last_filter == ICP_FILTER_GRID && enqueued < 64) ctx->stats.run_path_bits |= 1ull << enqueued;
                 ctx->seeds_valid = true;
                 TRY(cpu_rule_fixup(ctx, P, n, &sd->done));
                 ar_timed[slot] = false;
@@ -2833,6 +2890,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                 grid_cur, gseedd)); // (run_init zeroed the counters)
             if (ctx->stats.last_filter == ICP_FILTER_BUNDLE) ctx->stats.run_bundle_searches += 1;
             else if (ctx->stats.last_filter == ICP_FILTER_GRID) ctx->stats.run_grid_searches += 1;
+            if (ctx->stats.last_filter == ICP_FILTER_GRID && enqueued < 64) ctx->stats.run_path_bits |= 1ull << enqueued;
             ctx->seeds_valid = true; // idx pairs every point of the resident scene
             TRY(cpu_rule_fixup(ctx, P, n, &sd->done)); // (ICP_NN_RULE_CPU_SQRT only: host near ties)
             ar_timed[slot] = false;
@@ -3003,6 +3061,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         ++waited;
         if (grid_policy) { // (mirrored by the error step of that iteration)
             far_obs = ctx->h_iter->far_acc;
+            if (waited - 1 < (int)fold_far.size()) fold_far[waited - 1] = far_obs;
             q2_obs = ctx->h_iter->queued2;
             static const bool dbg = getenv("ICP_DEBUG_POLICY") != nullptr;
             if (dbg) fprintf(stderr, "[policy] waited %d far %d thr %d next_grid %d\n", waited, far_obs, far_thr, (int)grid_next);
@@ -3053,6 +3112,9 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                         "| wave-us A %.1f BC %.1f D %.1f E %.1f FG %.1f\n",
                 h[0], h[1], h[2], h[3], h[4], h[10], h[11], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01, h[8] * 0.01,
                 h[9] * 0.01);
+        fprintf(stderr, "[iter2_debug] (nn_grid_iter2_kernel, an ICP_ITER2_DBG build) tasks %llu walkers %llu batches %llu "
+                        "pair tests %llu | wave-us A %.1f D %.1f G %.1f\n",
+                h[0], h[1], h[2], h[3], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01);
     }
     // (every transform of a policy run wrote the seed distances, whatever its form; the next run
     // may start from them)

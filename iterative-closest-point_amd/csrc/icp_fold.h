@@ -71,7 +71,7 @@ __device__ __forceinline__ void horn_step_body(const double *__restrict__ sums, 
 
 __device__ __forceinline__ void err_step_body(const double *__restrict__ sums, double N, double threshold, int max_iter,
                               double *__restrict__ err_trace, IterState *__restrict__ s, int *hflag, int ticket,
-                              IterState *h_state, double *h_trace, bool far_coherent = false)
+                              IterState *h_state, double *h_trace, bool far_coherent = false, int far_global = -1)
 {
     if (!s->done) {
         const double e = sums[kSumErr];
@@ -86,6 +86,7 @@ __device__ __forceinline__ void err_step_body(const double *__restrict__ sums, d
         // (far_coherent: s is global and this launch's workgroups added to s->far_acc -- a fused
         // transform -- so its count is read at agent scope; s may be an LDS copy otherwise)
         if (far_coherent) h_state->far_acc = __hip_atomic_load(&s->far_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (far_global >= 0) h_state->far_acc = far_global; // (all ranks' count: sums[kSumFar] after the all-reduce)
     }
     // (done, iter) to the host (mapped memory), then the ticket the host spins on
     __hip_atomic_store(hflag, s->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1415,10 +1415,19 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
 // bounds are pinned by tests/test_iter_prune.py.  Measured at C4: 75% of a registration's queries
 // certified (profiles/r06a/cert_probe.log), a CPU model of the trajectory agrees
 // (tools/cert_model.py).
+constexpr int kNoBound = (int)0xbf800000u; // (-1.0f: no bound)
 constexpr int kIter2Slot = 8; // doubles a query's hand-off slot: p' (3), seed distance, seed coordinates (3), (seed, h)
 constexpr int kIter2Tile = kCanonCols * kLeafStride; // doubles a chunk's leaf tile
 static_assert(32 * kIter2Slot + 32 / 2 <= kIter2Tile, "the hand-off slots and the walker list alias the tiles");
 
+#ifndef ICP_ITER2_DBG
+#define ICP_ITER2_DBG 0 // (1: per-wave phase clocks into ICP_ITER_DEBUG's buffer -- a diagnostic build)
+#endif
+#ifndef ICP_ITER2_F64
+#define ICP_ITER2_F64 0 // (0: nn_grid_iter_kernel's fp32 screen + candidates in fp64; 1: every point's fp64
+                        //  record decided at once -- no screen, no candidate round trip: 7,300 against
+                        //  8,038 it/s, profiles/r06/r06j_ab.txt)
+#endif
 #ifndef ICP_ITER2_WAVES
 #define ICP_ITER2_WAVES 4 // (waves a SIMD nn_grid_iter2_kernel is compiled for)
 #endif
@@ -1429,9 +1438,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
     float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
-    double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, int xform, int xcd_l, CertArgs ca)
+    double *__restrict__ rows, int *far_acc, double far_d2, int *big_count, int xform, int xcd_l, CertArgs ca,
+    unsigned long long *__restrict__ dbg)
 {
     static_assert(CH == 1 || CH == 2, "one or two chunks a task");
+    // (ICP_ITER2_DBG: dcnt = tasks, walkers, walk batches, pair tests, -, clocks A, D, G (100 MHz))
+    constexpr bool kDbg = ICP_ITER2_DBG != 0;
+    unsigned long long dcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tclk = 0;
+    auto lap = [&](int f) {
+        if (kDbg && dbg) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (f >= 0) dcnt[f] += now - tclk;
+            tclk = now;
+        }
+    };
     constexpr int NW = kBlock / 64, QL = 2 / CH; // (lanes a query in phases A and G)
     __shared__ double s_tile[NW][CH * kIter2Tile];
     if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
@@ -1442,7 +1463,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     double *const tile = s_tile[wave];
     double *const slots = tile;                            // (phases A-D) 32 CH slots of kIter2Slot doubles
     int *const wl = (int *)(tile + 32 * CH * kIter2Slot);  // (phase D) the task's walkers, in query order
-    const bool cert_on = ca.r != nullptr, cert_in = cert_on && ca.valid != 0;
+    const bool cert_on = ca.state != nullptr, cert_in = cert_on && ca.valid != 0;
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1454,11 +1475,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     for (int c = s; s < S && c < C; c += CH * S) {
         const int t = slot_t(c, u);
         const bool active = c + (u >> 5) * S < C && t < n;
+        lap(-1);
+        if (kDbg) dcnt[0] += 1;
         // ---- A: the previous transform, its residual = the seed distance, the certificate
         double q[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
         int h = -1;
-        float cr = -1.0f;
-        int2 cps = make_int2(-1, -1);
+        int4 cs4 = make_int4(kNoBound, kNoBound, -1, -1); // (the certificate's state: R1, R3 bits, the pair)
         double mot = 0.0;
         if (active) {
             const double p0 = px[t], p1 = py[t], p2 = pz[t];
@@ -1466,13 +1488,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             y[1] = yy[t];
             y[2] = yz[t];
             h = idx[t];
-            if (cert_in) {
-                cr = ca.r[t];
-                cps = ca.pos[t];
-            }
+            if (cert_in) cs4 = ca.state[t];
             if (xform) {
                 transform_point(st->xf, p0, p1, p2, q[0], q[1], q[2]);
-                if (cert_in) mot = sqrt(residual2(p0, p1, p2, q[0], q[1], q[2]));
+                // (the motion rounded up: the square up to fp32, its fp32 root one ulp low at most)
+                if (cert_in)
+                    mot = (double)(sqrtf(__double2float_ru(residual2(p0, p1, p2, q[0], q[1], q[2]))) * (1.0f + 0x1.0p-21f));
             } else { // (a run's first iteration: no pending transform, the point as it is)
                 q[0] = p0;
                 q[1] = p1;
@@ -1500,30 +1521,53 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         int bi = h;
         double w[3] = {y[0], y[1], y[2]};
         bool certd = false;
-        if (cert_in && active && h >= 0 && cr > 0.0f) {
-            // (the subtraction's own rounding: 2^-53 of cr at most, covered by the last term)
-            const double Rc = ((double)cr - mot * (1.0 + 0x1.0p-40)) - (double)cr * 0x1.0p-48;
-            if (ca.two && cps.y >= 0) {
-                const double4 r2 = gv.pts[cps.y];
+        const float R1 = __int_as_float(cs4.x), R3 = __int_as_float(cs4.y);
+        if (cert_in && active && h >= 0 && (R1 > 0.0f || R3 > 0.0f)) {
+            // both bounds lowered by the motion (the subtraction's rounding, 2^-53 of R at most, is
+            // covered by the last term); "d < R" as d (1 + 2^-38) < fl(R^2) (1 - 2^-50), no root
+            const double R1c = ((double)R1 - mot) - (double)R1 * 0x1.0p-48;
+            const double R3c = ((double)R3 - mot) - (double)R3 * 0x1.0p-48;
+            auto inside = [](double d2, double r) { return r > 0.0 && d2 * (1.0 + 0x1.0p-38) < r * r * (1.0 - 0x1.0p-50); };
+            double R1n = R1c;
+            int2 pn = make_int2(cs4.z, cs4.w);
+            certd = inside(e, R1c); // (one point: every other is beyond R1)
+            if (kDbg && !certd && ca.two && cs4.w >= 0 && R3c > 0.0) dcnt[3] += 1;
+            if (!certd && ca.two && cs4.w >= 0 && R3c > 0.0) {
+                // the pair: the second point's record, the exact (D64, index) order of the two, every
+                // other point beyond R3
+                const double4 r2 = gv.pts[cs4.w];
                 const double d2 = d64g(q[0], q[1], q[2], r2.x, r2.y, r2.z);
                 const int mi2 = (int)r2.w;
-                if (d2 < best || (d2 == best && (unsigned)mi2 < (unsigned)bi)) {
-                    best = d2;
-                    bi = mi2;
-                    w[0] = r2.x;
-                    w[1] = r2.y;
-                    w[2] = r2.z;
+                const bool swap = d2 < e || (d2 == e && (unsigned)mi2 < (unsigned)h);
+                const double db = swap ? d2 : e;
+                if (inside(db, R3c)) {
+                    certd = true;
+                    // the next one-point bound: the pair's loser at its own distance (D64 >= |v|^2 (1 - 3u))
+                    const double lb = fmin(R3c, sqrt(swap ? e : d2) * (1.0 - 0x1.0p-40));
+                    if (swap) {
+                        best = d2;
+                        bi = mi2;
+                        w[0] = r2.x;
+                        w[1] = r2.y;
+                        w[2] = r2.z;
+                        R1n = lb;
+                        pn = make_int2(cs4.w, cs4.z);
+                    } else {
+                        R1n = fmax(R1c, lb);
+                    }
                 }
             }
-            certd = best == best && sqrt(best) * (1.0 + 0x1.0p-40) < Rc;
             if (certd && sub == 0) {
-                ca.r[t] = __double2float_rd(Rc);
-                if (bi != h) { // (the second point won: the pair swaps)
-                    ca.pos[t] = make_int2(cps.y, cps.x);
+                const int4 ns = make_int4(__float_as_int(R1n > 0.0 ? __double2float_rd(R1n) : -1.0f),
+                                          __float_as_int(R3c > 0.0 ? __double2float_rd(R3c) : -1.0f), pn.x, pn.y);
+                if (bi != h) {
+                    ca.state[t] = ns;
                     idx[t] = bi;
                     yx[t] = w[0];
                     yy[t] = w[1];
                     yz[t] = w[2];
+                } else {
+                    *(int2 *)&ca.state[t] = make_int2(ns.x, ns.y); // (the pair as it was)
                 }
             }
         }
@@ -1549,8 +1593,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         const int nW = __popcll(wm);
         if (walker && sub == 0) wl[__popcll(wm & ((1ull << lane) - 1ull))] = u;
         wave_sync();
+        lap(5);
+        if (kDbg) dcnt[1] += nW;
         // ---- D: the walkers, at most 32 at a time, G = 64 / 2^k lanes each
         for (int b0 = 0; b0 < nW; b0 += 32) {
+            if (kDbg) dcnt[2] += 1;
             const int nb = min(32, nW - b0);
             const int lg = nb > 16 ? 1 : nb > 8 ? 2 : nb > 4 ? 3 : nb > 2 ? 4 : nb > 1 ? 5 : 6;
             const int G = 1 << lg, wi = lane >> lg, ws = lane & (G - 1);
@@ -1586,16 +1633,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             int bk = -1;      // (the winner's grid position, when this lane scanned it)
             float a1 = INFINITY, a2 = INFINITY; // (the certificate: the two smallest others, a1 at k1)
             int k1 = -1;
-            auto other = [&](float v, int k) {
-                if (v < a2) {
-                    if (v < a1) {
-                        a2 = a1;
-                        a1 = v;
-                        k1 = k;
-                    } else {
-                        a2 = v;
-                    }
-                }
+            auto other = [&](float v, int k) { // (branch-free: med3(a1, v, a2) is the new second, a1 <= a2)
+                const bool lt = v < a1;
+                a2 = __builtin_amdgcn_fmed3f(a1, v, a2);
+                a1 = lt ? v : a1;
+                k1 = lt ? k : k1;
             };
             auto eq_of = [&]() { // (the per-axis fp32 coordinate error bound of the screen)
                 const double o0 = wq[0] - gv.c32[0], o1 = wq[1] - gv.c32[1], o2 = wq[2] - gv.c32[2];
@@ -1629,18 +1671,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                     }
                     nc = 0;
                 };
-                auto test = [&](const float4 &m, int pos) {
-                    const float dx = f0 - m.x, dy = f1 - m.y, dz = f2 - m.z;
-                    const float d32 = (dx * dx + dy * dy) + dz * dz;
-                    if (d32 > T) { // (strictly farther than the seed)
-                        if (cert_on) other(d32, pos);
-                        return;
+                // a round's points, branch-free: d32 > T (strictly farther than the seed) -> an other;
+                // the current winner itself -> its position; the rest are candidates, decided in fp64
+                // (a wave-uniform branch: rare after the first iterations)
+                auto test = [&](const float4 (&m)[KU], const int (&kk)[KU]) {
+                    bool cnd[KU];
+                    bool anyc = false;
+#pragma unroll
+                    for (int v = 0; v < KU; ++v) {
+                        const float dx = f0 - m[v].x, dy = f1 - m[v].y, dz = f2 - m[v].z;
+                        const float d32 = (dx * dx + dy * dy) + dz * dz;
+                        const bool val = kk[v] >= 0, fr = d32 > T;
+                        if (cert_on) other(val && fr ? d32 : INFINITY, kk[v]);
+                        const bool self = val && !fr && __float_as_int(m[v].w) == wbi;
+                        bk = self ? kk[v] : bk;
+                        cnd[v] = val && !fr && !self;
+                        anyc = anyc || cnd[v];
                     }
-                    if (__float_as_int(m.w) == wbi) {
-                        bk = pos; // (the current winner itself)
-                    } else {
-                        cand[nc++] = pos;
-                        if (nc == kCand) flush();
+                    if (__ballot(anyc)) {
+#pragma unroll
+                        for (int v = 0; v < KU; ++v)
+                            if (cnd[v]) {
+                                cand[nc++] = kk[v];
+                                if (nc == kCand) flush();
+                            }
                     }
                 };
                 // the sphere prune (nn_grid_iter_kernel's, radius sqrt(ew); tests/test_iter_prune.py)
@@ -1663,7 +1717,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                     const float dz = fmaxf(0.0f, fmaxf((float)rz - tr[2], tr[2] - (float)(rz + 1)));
                     const float rem = rc2 - dy * dy - dz * dz;
                     if (rem < 0.0f) return; // (the row lies beyond the sphere)
-                    const float xw = sqrtf(rem) * (1.0f + 0x1.0p-20f) + xroom;
+                    // (v_sqrt_f32 within an ulp or two: the 2^-20 room covers it; the CPU restatement
+                    // takes the root two ulps low)
+                    const float xw = __builtin_amdgcn_sqrtf(rem) * (1.0f + 0x1.0p-20f) + xroom;
                     x0 = max(x0, c0[0] + (int)floorf(fmaxf(tr[0] - xw, -1.0f)));
                     x1 = min(x1, c0[0] + (int)floorf(fminf(tr[0] + xw, xspan)));
                     if (x0 <= x1) {
@@ -1695,16 +1751,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                                     if (f >= pre[x]) pp = k0[x] + (f - pre[x]);
                                 kk[v] = f < tot ? pp : -1;
                             }
-                            float4 mm[KU];
+                            if constexpr (ICP_ITER2_F64) {
+                                // a round's points from their fp64 records, each decided in the exact
+                                // (D64, index) order at once; the current winner itself records its
+                                // position; the displaced winner (when this lane scanned it) or the point
+                                // goes to the others as its D64 rounded down (fl32(D64) (1 - 2^-23) <=
+                                // D64: a lower bound on its true square)
+                                double4 mm[KU];
 #pragma unroll
-                            for (int v = 0; v < KU; ++v) mm[v] = gv.pts32[kk[v] >= 0 ? kk[v] : 0];
+                                for (int v = 0; v < KU; ++v) mm[v] = gv.pts[kk[v] >= 0 ? kk[v] : 0];
 #pragma unroll
-                            for (int v = 0; v < KU; ++v)
-                                if (kk[v] >= 0) test(mm[v], kk[v]);
+                                for (int v = 0; v < KU; ++v) {
+                                    const double d = d64g(wq[0], wq[1], wq[2], mm[v].x, mm[v].y, mm[v].z);
+                                    const int mi = (int)mm[v].w, kv = kk[v];
+                                    const bool val = kv >= 0, self = val && mi == wbi;
+                                    const bool win = val && !self && (d < wb || (d == wb && (unsigned)mi < (unsigned)wbi));
+                                    if (cert_on) {
+                                        const float ov = win ? (bk >= 0 ? (float)wb * 0x1.fffffcp-1f : INFINITY)
+                                                             : (val && !self ? (float)d * 0x1.fffffcp-1f : INFINITY);
+                                        other(ov, win ? bk : kv);
+                                    }
+                                    wb = win ? d : wb;
+                                    wbi = win ? mi : wbi;
+                                    bk = win || self ? kv : bk;
+                                }
+                            } else {
+                                float4 mm[KU];
+#pragma unroll
+                                for (int v = 0; v < KU; ++v) mm[v] = gv.pts32[kk[v] >= 0 ? kk[v] : 0];
+                                test(mm, kk);
+                            }
                         }
                     }
                 }
-                if (nc) flush();
+                if constexpr (!ICP_ITER2_F64)
+                    if (nc) flush();
             }
             // the walker's G lanes: the (D64, index) minimum, its position and coordinates; with the
             // certificate also the others (the two lists, and the sub-group winner that loses a merge
@@ -1725,7 +1806,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                     }
                     if (oi != wbi) {
                         const int lk = theirs ? bk : ok2;
-                        if (lk >= 0) other(__double2float_rd(theirs ? wb : ob), lk);
+                        if (lk >= 0) other((float)(theirs ? wb : ob) * 0x1.fffffcp-1f, lk); // (rounded down)
                     }
                 }
                 if (theirs) {
@@ -1792,22 +1873,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                 // true distance |v| >= sqrt(d32) (1 - 2^-20) - sqrt(3) eq (1 + 2^-20).  A query the
                 // wave took whole gets no bound.
                 if (cert_on) {
-                    float rout = -1.0f;
-                    int2 pout = make_int2(-1, -1);
+                    int4 ns = make_int4(kNoBound, kNoBound, -1, -1);
                     if (ok && !whole && bk >= 0) {
-                        double rb = sqrt(rs_sl[3]) * (1.0 - 0x1.0p-40); // (rs_sl[3]: the walk's ew)
-                        const float as = ca.two ? a2 : a1;
-                        if (as < INFINITY)
-                            rb = fmin(rb, sqrt((double)as) * (1.0 - 0x1.0p-20) - 1.7320508075688774 * eq_of() * (1.0 + 0x1.0p-20));
-                        rout = rb > 0.0 ? __double2float_rd(rb) : -1.0f;
-                        pout = make_int2(bk, ca.two ? k1 : -1);
+                        const double u0 = sqrt(rs_sl[3]) * (1.0 - 0x1.0p-40); // (rs_sl[3]: the walk's ew)
+                        // (a list value's bound, the scan radius beyond the lists: a D64 rounded down gives
+                        // |v| >= sqrt(a) (1 - 2^-52); an fp32 d32 needs the screen's error, -sqrt(3) eq)
+                        const double ec = ICP_ITER2_F64 ? 0.0 : 1.7320508075688774 * eq_of() * (1.0 + 0x1.0p-20);
+                        auto lower = [&](float a) {
+                            return a < INFINITY ? fmin(u0, sqrt((double)a) * (1.0 - 0x1.0p-20) - ec) : u0;
+                        };
+                        const double r1 = lower(a1), r3 = ca.two ? lower(a2) : -1.0;
+                        ns = make_int4(__float_as_int(r1 > 0.0 ? __double2float_rd(r1) : -1.0f),
+                                       __float_as_int(r3 > 0.0 ? __double2float_rd(r3) : -1.0f), bk, ca.two ? k1 : -1);
                     }
-                    ca.r[wt] = rout;
-                    ca.pos[wt] = pout;
+                    ca.state[wt] = ns;
                 }
             }
             wave_sync();
         }
+        lap(6);
         // ---- G: this task's 18 leaves a query into the chunk tile, then the chunk tree
         if (active) {
             y[0] = sl[4];
@@ -1851,7 +1935,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             if (CH == 2 && c + S < C) acc = acc + tb;
         }
         wave_sync(); // (the next task's slots alias the tiles)
+        lap(7);
     }
+    if (kDbg && dbg && lane == 0)
+        for (int f = 0; f < 8; ++f)
+            if (dcnt[f]) atomicAdd(dbg + f, dcnt[f]);
     // the workgroup's four strands -> its row (column k from lane k of each wave)
     __shared__ double sh[NW][kCanonCols];
     if (lane < kCanonCols) sh[wave][lane] = acc;
@@ -1924,7 +2012,7 @@ bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         const char *e = getenv("ICP_ITER_V2");
         return !(e && e[0] == '0');
     }();
-    if (v2 && !stage && !(wide_on && n <= kIterWideMax) && !dbg) {
+    if (v2 && !stage && !(wide_on && n <= kIterWideMax) && (!dbg || ICP_ITER2_DBG)) {
         // ICP_ITER2_CH: chunks a task (2: the walkers of two chunks packed together; 1: a chunk)
         static const int ch = [] {
             const char *e = getenv("ICP_ITER2_CH");
@@ -1933,12 +2021,12 @@ bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
         if (ch == 2)
             nn_grid_iter2_kernel<ICP_ITER_KR, ICP_ITER_KU, 2><<<R, kBlock, 0, st>>>(
                 n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
-                xform, xcd_l, ca);
+                xform, xcd_l, ca, dbg);
         else
             nn_grid_iter2_kernel<ICP_ITER_KR, ICP_ITER_KU, 1><<<R, kBlock, 0, st>>>(
                 n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
-                xform, xcd_l, ca);
-        return ca.r != nullptr;
+                xform, xcd_l, ca, dbg);
+        return ca.state != nullptr;
     }
     if (!stage && wide_on && n <= kIterWideMax)
         nn_grid_iter_kernel<false, 4><<<R, 2 * kBlock, 0, st>>>(n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box,

@@ -37,5 +37,8 @@ constexpr int kRedMaxK = 17;        // max sums per workgroup of a streaming red
 //  [17]    e = sum ||y - (sR p + t)||^2
 constexpr int kSumP = 0, kSumY = 3, kSumS = 6, kSumDcaps = 15, kSumSp = 16, kSumErr = 17,
               kNumSums = 18;
+// [18] the search policy's far count of the iteration's transform (icp_run's canonical schedule on
+// several ranks: all-reduced with the 18 sums, so that every rank takes the same path)
+constexpr int kSumFar = 18;
 
 } // namespace icp

@@ -74,10 +74,11 @@ __global__ __launch_bounds__(64) void err_horn_step_kernel(double *__restrict__ 
                                                            int max_iter, double *__restrict__ err_trace,
                                                            IterState *__restrict__ s, int *hflag, int ticket,
                                                            IterState *h_state, double *h_trace, double c0, double c1,
-                                                           double c2, int shifted, int *__restrict__ cnt)
+                                                           double c2, int shifted, int *__restrict__ cnt, int far_sum)
 {
     if (threadIdx.x != 0) return;
-    err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace);
+    err_step_body(sums, N, threshold, max_iter, err_trace, s, hflag, ticket, h_state, h_trace, false,
+                  far_sum ? (int)sums[kSumFar] : -1);
     horn_step_body(sums, N, c0, c1, c2, shifted, cnt, s);
 }
 
@@ -1725,10 +1726,10 @@ void launch_err_step(double *sums, double n_total, double threshold, int max_ite
 
 void launch_err_horn_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                           IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
-                          const double c[3], int shifted, int *amb_count, hipStream_t st)
+                          const double c[3], int shifted, int *amb_count, hipStream_t st, int far_sum)
 {
     err_horn_step_kernel<<<1, 64, 0, st>>>(sums, n_total, threshold, max_iter, err_trace, st_dev, hflag_dev, ticket,
-                                           h_state_dev, h_trace_dev, c[0], c[1], c[2], shifted, amb_count);
+                                           h_state_dev, h_trace_dev, c[0], c[1], c[2], shifted, amb_count, far_sum);
 }
 
 void launch_iteration_tail_small(const int *idx, const double4 *m4, double *px, double *py, double *pz, int n,

@@ -533,29 +533,29 @@ void launch_canon_fold(const double *rows, int n, double *sums, int mode, const 
 // queries the whole wave took.  No-op once st->done.
 struct GridView;
 // The exclusion certificate of the fused grid iteration (icp_grid.hip, "The exclusion
-// certificate"): per query in slot order, r = a lower bound on the distance from the query to
-// every model point other than the pair pos = (correspondence, second point) -- grid positions,
-// -1 for none -- or r < 0 for no bound.  Each iteration lowers r by the query's motion; a query
-// whose nearer point of the pair lies inside r keeps that point without a walk.  valid: r / pos
-// hold the state the previous fused iteration of this run wrote (else every query walks and the
-// state is written fresh); two = 0: the one-point form (the correspondence alone, pos.y = -1);
-// skin: the radius a walk scans beyond its seed distance (model units); counts (nullable):
-// += (queries certified, queries walked).
+// certificate"): per query in slot order, state = (R1, R3 as float bits, the pair's grid
+// positions): R1 a lower bound on the distance from the query to every model point other than
+// its correspondence (pair.x), R3 to every point outside the pair (the correspondence and a second
+// point pair.y); -1.0f: no bound, -1: no point.  Each iteration lowers both by the query's motion;
+// a query whose correspondence lies inside R1, or the nearer of its pair inside R3, keeps that
+// point without a walk.  valid: the state is the one the previous fused iteration of this run
+// wrote (else every query walks and the state is written fresh); two = 0: the one-point form
+// (R3 and pair.y unused); skin: the radius a walk scans beyond its seed distance (model units);
+// counts (nullable): += (queries certified, queries walked).
 struct CertArgs {
-    float *r = nullptr;
-    int2 *pos = nullptr;
+    int4 *state = nullptr;
     int valid = 0;
     int two = 1;
     double skin = 0.0;
     unsigned long long *counts = nullptr;
 };
-// Returns true when the launch wrote the certificate state (ca.r non-null and the two-lane form).
+// Returns true when the launch wrote the certificate state (ca.state non-null, the certificate form).
 bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
                          const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
                          const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
                          unsigned long long *dbg = nullptr, // (dbg: ICP_ITER_DEBUG's 12 counters)
                          int xform = 1, // (0: no pending transform -- a run's first iteration, seeds in idx / y)
-                         const CertArgs &ca = CertArgs{}); // (ca.r null: no certificate, every query walks)
+                         const CertArgs &ca = CertArgs{}); // (ca.state null: no certificate, every query walks)
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,
 // sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)
@@ -580,7 +580,8 @@ void launch_horn_step(const double *sums, double n_total, const double c[3], int
 // launch_err_step (no partials) then launch_horn_step, in one single-thread launch
 void launch_err_horn_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                           IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
-                          const double c[3], int shifted, int *amb_count, hipStream_t st);
+                          const double c[3], int shifted, int *amb_count, hipStream_t st,
+                          int far_sum = 0); // (far_sum: mirror sums[kSumFar] as the far count, all ranks')
 void launch_err_step(double *sums, double n_total, double threshold, int max_iter, double *err_trace,
                      IterState *st_dev, int *hflag_dev, int ticket, IterState *h_state_dev, double *h_trace_dev,
                      hipStream_t st, const double *partials = nullptr, int nblocks = 0);

@@ -93,7 +93,7 @@ class Stats(C.Structure):
                 ("last_filter", C.c_int), ("bundle_builds", C.c_longlong),
                 ("bundle_builds_in_run", C.c_longlong), ("run_bundle_searches", C.c_longlong),
                 ("run_grid_searches", C.c_longlong), ("run_certified", C.c_longlong),
-                ("run_walked", C.c_longlong)]
+                ("run_walked", C.c_longlong), ("run_path_bits", C.c_ulonglong)]
 
 
 class BundleAudit(C.Structure):

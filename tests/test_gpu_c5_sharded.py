@@ -62,21 +62,23 @@ STRETCH = 10
 
 
 def run_protocol(ctx):
-    errs, digs, snaps, idxs = [], [], [], []
+    errs, digs, snaps, idxs, paths = [], [], [], [], []
     res = None
     for _ in range(ITERS // STRETCH):
         ctx.set_index_digest(STRETCH - 1)
         _, e = ctx.run(STRETCH - 1, -1.0)
+        paths.append(ctx.stats()["run_path_bits"])
         errs.append(e)
         digs.append(ctx.index_digest(STRETCH - 1))
         snaps.append(ctx.get_scene())
         ctx.set_index_digest(1)
         res, e = ctx.run(1, -1.0)  # this search ran on the snapshot
+        paths.append(ctx.stats()["run_path_bits"])
         errs.append(e)
         digs.append(ctx.index_digest(1))
         idxs.append(ctx.get_indices())
     return dict(err=np.concatenate(errs), res=res, dig=np.concatenate(digs), snaps=snaps, idxs=idxs,
-                final=ctx.get_scene(), stats=ctx.stats())
+                final=ctx.get_scene(), stats=ctx.stats(), paths=paths)
 
 
 @pytest.fixture(scope="module")
@@ -126,6 +128,39 @@ def test_c5_ranks_bitwise_identical(c5):
         assert np.array_equal(o["err"], r0["err"])
         assert o["res"].s == r0["res"].s
         assert list(o["res"].R) == list(r0["res"].R) and list(o["res"].t) == list(r0["res"].t)
+
+
+def test_c5_ranks_take_the_same_paths(c5):
+    """Every rank takes the same search path (grid or bundle cascade) at every iteration: the path
+    of iteration k is decided on the all-ranks far count of transform k - 3 (kSumFar rides on the
+    per-iteration all-reduce), not on each rank's own count of whatever iteration its host saw."""
+    _, _, _, _, ranks = c5
+    for o in ranks[1:]:
+        assert o["paths"] == ranks[0]["paths"]
+        assert o["stats"]["run_grid_searches"] == ranks[0]["stats"]["run_grid_searches"]
+        assert o["stats"]["run_bundle_searches"] == ranks[0]["stats"]["run_bundle_searches"]
+
+
+def test_c5_shard_paths_independent_of_host_lead(c5, monkeypatch):
+    """Rank 0's shard of the 8-way job alone (a 1-rank context, allow_unequal, as
+    tools/shard_probe.py runs it), 30 iterations from its unseeded first search: with the host
+    throttled before every enqueue (ICP_TEST_ENQUEUE_DELAY_US: the device always drained) and
+    unthrottled, the same path at every iteration and the same level-1 queue, the same bits."""
+    amd, m, p, _, _ = c5
+    b, c = amd.shard_range(N, 0, W)
+    out = []
+    for delay in ("0", "3000"):
+        monkeypatch.setenv("ICP_TEST_ENQUEUE_DELAY_US", delay)
+        with amd.Context(0) as ctx:
+            ctx.set_allow_unequal(True)
+            ctx.set_model(m)
+            ctx.set_scene(np.ascontiguousarray(p[b:b + c]), np_total=c)
+            res, e = ctx.run(ITERS, -1.0)
+            st = ctx.stats()
+            out.append((st["run_path_bits"], st["level1_queued"], st["run_bundle_searches"], e, ctx.get_scene()))
+    (pa, qa, ba, ea, sa), (pb, qb, bb, eb, sb) = out
+    assert pa == pb and qa == qb and ba == bb, (hex(pa), hex(pb), qa, qb, ba, bb)
+    assert np.array_equal(ea, eb) and np.array_equal(sa, sb)
 
 
 def test_c5_shards_equal_single_context(c5):

@@ -239,6 +239,20 @@ def test_other_bounds_are_below_the_true_distance(centre, extent):
     assert worst < 1.0
 
 
+def test_motion_bound_rounds_up():
+    """The kernel's fp32 motion bound is at least the exact |q' - q| (the fp64 square rounded up to
+    fp32, a root at most an ulp low, times 1 + 2^-21), over motions from 1e-12 to 1e3."""
+    rng = np.random.default_rng(9)
+    for _ in range(3000):
+        q = rng.uniform(-1e4, 1e4, 3)
+        d = rng.normal(size=3)
+        d *= 10.0 ** rng.uniform(-12, 3) / np.linalg.norm(d)
+        qn = q + d
+        m = motion_bound(q, qn)
+        m_low = float(np.nextafter(np.float32(m / (1.0 + 2.0 ** -21)), F(0))) * (1.0 + 2.0 ** -21)  # (a root an ulp low)
+        assert Fraction(min(m, m_low)) ** 2 >= exact_d2(q, qn)
+
+
 def test_motion_decrement_rounds_down():
     """Rc = (R - mot (1 + 2^-40)) - R 2^-48 is at most the exact R - |q' - q|, even in near
     cancellation (mot within an ulp of R)."""
@@ -258,11 +272,22 @@ def test_motion_decrement_rounds_down():
 
 
 # ---- the certificate over a trajectory (state machine against brute force) ----------------------
-def walk(q, pts, h_seed, lo, inv_h, g, c, em, skin, two=True):
-    """A walk of the fused kernel for one query: the exact first minimum over the scanned points,
-    the new pair and bound.  Every scanned point other than the winner is an "other" with its
-    d32 (the kernel's lanes mix in D64 rounded down for candidates; both bound from below)."""
-    e = float(d64(q, pts[h_seed]))
+def f32_rd(x):
+    """__double2float_rd: the largest float32 <= x."""
+    f = np.float32(x)
+    return float(np.nextafter(f, F(-np.inf))) if float(f) > x else float(f)
+
+
+def state_bound(r):
+    return f32_rd(r) if r > 0 else -1.0
+
+
+def walk(q, pts, seed, lo, inv_h, g, c, em, skin, two=True):
+    """A walk of nn_grid_iter2_kernel for one query: the exact first minimum over the scanned
+    points and the next state (R1, R3, winner, second point).  Every scanned point other than the
+    winner is an "other" with its d32 (the kernel's lanes mix in D64 rounded down for candidates;
+    both bound from below); R1 bounds every point but the winner, R3 every point outside the pair."""
+    e = float(d64(q, pts[seed]))
     rs = math.sqrt(e) + skin
     ew = rs * rs
     c0, c1 = complete_box(q, ew, lo, inv_h, g)
@@ -279,16 +304,48 @@ def walk(q, pts, h_seed, lo, inv_h, g, c, em, skin, two=True):
     win = int(scanned[order[0]])
     eq = math.ldexp(max(abs(q[a] - c[a]) for a in range(3)), -23) + em
     others = sorted((float(d32(q, pts[j], c)), int(j)) for j in scanned if j != win)
-    R = math.sqrt(ew) * (1.0 - 2.0 ** -40)
-    h2 = -1
-    if two:
-        if others:
-            h2 = others[0][1]
-        if len(others) > 1:
-            R = min(R, bound_from(others[1][0], eq))
-    elif others:
-        R = min(R, bound_from(others[0][0], eq))
-    return win, h2, float(np.float32(np.nextafter(F(R), F(-np.inf)))) if R > 0 else -1.0
+    u0 = math.sqrt(ew) * (1.0 - 2.0 ** -40)
+
+    def lower(k):
+        return min(u0, bound_from(others[k][0], eq)) if len(others) > k else u0
+
+    r1, r3 = lower(0), (lower(1) if two else -1.0)
+    h2 = others[0][1] if two and others else -1
+    return win, h2, state_bound(r1), state_bound(r3)
+
+
+def motion_bound(q, qn):
+    """The kernel's motion: the fp64 square rounded up to fp32, its fp32 root, times 1 + 2^-21."""
+    m2 = float(d64(q, qn))
+    m2f = np.float32(m2)
+    if float(m2f) < m2:
+        m2f = np.nextafter(m2f, F(np.inf))
+    return float(np.float32(np.sqrt(m2f) * F(1.0 + 2.0 ** -21)))
+
+
+def inside(d2, r):
+    return r > 0.0 and d2 * (1.0 + 2.0 ** -38) < r * r * (1.0 - 2.0 ** -50)
+
+
+def certify(qn, pts, st, mot, two):
+    """The kernel's phase-A certificate: (winner, next state) or None (the query walks)."""
+    h, h2, R1, R3 = st
+    if not (R1 > 0 or R3 > 0):
+        return None
+    R1c = (R1 - mot) - R1 * 2.0 ** -48
+    R3c = (R3 - mot) - R3 * 2.0 ** -48
+    e = float(d64(qn, pts[h]))
+    if inside(e, R1c):
+        return h, (h, h2, state_bound(R1c), state_bound(R3c))
+    if two and h2 >= 0 and R3c > 0:
+        d2 = float(d64(qn, pts[h2]))
+        swap = d2 < e or (d2 == e and h2 < h)
+        if inside(d2 if swap else e, R3c):
+            lb = min(R3c, math.sqrt(e if swap else d2) * (1.0 - 2.0 ** -40))
+            if swap:
+                return h2, (h2, h, state_bound(lb), state_bound(R3c))
+            return h, (h, h2, state_bound(max(R1c, lb)), state_bound(R3c))
+    return None
 
 
 def first_min(q, pts):
@@ -335,21 +392,13 @@ def test_certified_queries_keep_the_first_minimum(model, two):
         tmv = rng.normal(size=3) * step * 10.0 ** rng.uniform(-4, -1.5)
         qn = (q - centre) @ Rm.T + centre + tmv
         for i in range(nq):
-            h, h2, R = state[i]
-            mot = math.sqrt(float(d64(q[i], qn[i])))
-            Rc = (R - mot * (1.0 + 2.0 ** -40)) - R * 2.0 ** -48 if R > 0 else -1.0
-            best, bi = float(d64(qn[i], pts[h])), h
-            if two and h2 >= 0:
-                d2 = float(d64(qn[i], pts[h2]))
-                if d2 < best or (d2 == best and h2 < bi):
-                    best, bi = d2, h2
-            if R > 0 and math.sqrt(best) * (1.0 + 2.0 ** -40) < Rc:
-                assert bi == first_min(qn[i], pts), (model, it, i)
+            got = certify(qn[i], pts, state[i], motion_bound(q[i], qn[i]), two)
+            if got is not None:
+                assert got[0] == first_min(qn[i], pts), (model, it, i)
                 certified += 1
-                R2 = float(np.float32(np.nextafter(F(Rc), F(-np.inf))))
-                state[i] = (bi, h if bi == h2 else h2, R2)
+                state[i] = got[1]
             else:
-                state[i] = walk(qn[i], pts, bi, lo, inv_h, g, c, em, skin, two)
+                state[i] = walk(qn[i], pts, state[i][0], lo, inv_h, g, c, em, skin, two)
                 assert state[i][0] == first_min(qn[i], pts)
         q = qn
     assert certified > 0  # (the certificate does fire on these trajectories)
