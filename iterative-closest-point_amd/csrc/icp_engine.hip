@@ -2800,8 +2800,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                         unsigned long long h[16];
                         HIPCHK(hipStreamSynchronize(ctx->st));
                         HIPCHK(hipMemcpy(h, iter_dbg, sizeof(h), hipMemcpyDeviceToHost));
-                        fprintf(stderr, "[iter2_debug] it %d tasks %llu walkers %llu batches %llu pair %llu | wave-us A %.1f D %.1f G %.1f\n",
-                                enqueued, h[0], h[1], h[2], h[3], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01);
+                        fprintf(stderr, "[iter2_debug] it %d tasks %llu walkers %llu batches %llu pair %llu | wave-us A %.1f D %.1f out %.1f G %.1f\n",
+                                enqueued, h[0], h[1], h[2], h[3], h[5] * 0.01, h[6] * 0.01, h[4] * 0.01, h[7] * 0.01);
                         HIPCHK(hipMemset(iter_dbg, 0, sizeof(h)));
                     }
                     LAUNCHCHK("nn_grid_iter");

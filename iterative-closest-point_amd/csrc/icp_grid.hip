@@ -1428,6 +1428,15 @@ static_assert(32 * kIter2Slot + 32 / 2 <= kIter2Tile, "the hand-off slots and th
                         //  record decided at once -- no screen, no candidate round trip: 7,300 against
                         //  8,038 it/s, profiles/r06/r06j_ab.txt)
 #endif
+#ifndef ICP_ITER2_KU
+#define ICP_ITER2_KU 4 // (the walk: points a lane loads together; 2 / 3: 7,950 / 8,225 against 8,235 it/s, profiles/r06/r06m_ab.txt)
+#endif
+#ifndef ICP_ITER2_KR
+#define ICP_ITER2_KR ICP_ITER_KR // (the walk: rows whose bounds a lane reads together)
+#endif
+#ifndef ICP_ITER2_KCAND
+#define ICP_ITER2_KCAND ICP_ITER_KCAND // (candidate records a lane loads together)
+#endif
 #ifndef ICP_ITER2_WAVES
 #define ICP_ITER2_WAVES 4 // (waves a SIMD nn_grid_iter2_kernel is compiled for)
 #endif
@@ -1442,7 +1451,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     unsigned long long *__restrict__ dbg)
 {
     static_assert(CH == 1 || CH == 2, "one or two chunks a task");
-    // (ICP_ITER2_DBG: dcnt = tasks, walkers, walk batches, pair tests, -, clocks A, D, G (100 MHz))
+    // (ICP_ITER2_DBG: dcnt = tasks, walkers, walk batches, pair tests, clocks: merge + outputs, A, D, G (100 MHz))
     constexpr bool kDbg = ICP_ITER2_DBG != 0;
     unsigned long long dcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tclk = 0;
@@ -1648,7 +1657,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                 const double eq = eq_of();
                 const float T = seeded_bound32(wb, eq);
                 const int ny = c1[1] - c0[1] + 1, nrq = ny * (c1[2] - c0[2] + 1);
-                constexpr int kCand = ICP_ITER_KCAND;
+                constexpr int kCand = ICP_ITER2_KCAND;
                 int cand[kCand], nc = 0;
                 auto flush = [&]() {
                     double4 r[kCand];
@@ -1787,6 +1796,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                 if constexpr (!ICP_ITER2_F64)
                     if (nc) flush();
             }
+            lap(6); // (ICP_ITER2_DBG: D = the walk; the merge and the outputs count as "-" below)
             // the walker's G lanes: the (D64, index) minimum, its position and coordinates; with the
             // certificate also the others (the two lists, and the sub-group winner that loses a merge
             // -- one with no position here was scanned by a lane of another sub-group, which holds it)
@@ -1891,7 +1901,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             }
             wave_sync();
         }
-        lap(6);
+        lap(4);
         // ---- G: this task's 18 leaves a query into the chunk tile, then the chunk tree
         if (active) {
             y[0] = sl[4];
@@ -2019,11 +2029,11 @@ bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
             return e && atoi(e) == 1 ? 1 : 2;
         }();
         if (ch == 2)
-            nn_grid_iter2_kernel<ICP_ITER_KR, ICP_ITER_KU, 2><<<R, kBlock, 0, st>>>(
+            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 2><<<R, kBlock, 0, st>>>(
                 n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
                 xform, xcd_l, ca, dbg);
         else
-            nn_grid_iter2_kernel<ICP_ITER_KR, ICP_ITER_KU, 1><<<R, kBlock, 0, st>>>(
+            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 1><<<R, kBlock, 0, st>>>(
                 n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
                 xform, xcd_l, ca, dbg);
         return ca.state != nullptr;
