@@ -53,11 +53,32 @@ import roofline as RF  # noqa: E402
 GRID_SEEDED_KERNEL = "nn_grid_seeded_kernel"  # (tools/roofline.py GRID_KERNELS: its algorithmic bytes)
 # the fused grid iteration (transform + seeded search + moments, one launch per seeded iteration:
 # icp_run's canonical schedule); ICP_GRID_ITER=0 runs the separate kernels
-GRID_ITER_KERNEL = "nn_grid_iter_kernel"
+GRID_ITER_KERNEL = "nn_grid_iter2_kernel"  # (round 6: the exclusion certificate + packed walkers)
+GRID_ITER_KERNEL_R5 = "nn_grid_iter_kernel"  # (ICP_ITER_V2=0: round 5's two-lane kernel, every query walks)
 
 
 def grid_kernel():
-    return GRID_SEEDED_KERNEL if os.environ.get("ICP_GRID_ITER") == "0" else GRID_ITER_KERNEL
+    if os.environ.get("ICP_GRID_ITER") == "0":
+        return GRID_SEEDED_KERNEL
+    return GRID_ITER_KERNEL_R5 if os.environ.get("ICP_ITER_V2") == "0" else GRID_ITER_KERNEL
+
+
+def path_description(st):
+    """What the timed registrations ran, from one registration's counters (icp_stats): the
+    searches by kind, the fused iterations' certified / walked queries."""
+    g, b = st["run_grid_searches"], st["run_bundle_searches"]
+    cert, walk = st["run_certified"], st["run_walked"]
+    parts = []
+    if g:
+        parts.append(f"{g} exact fp64 grid searches (fp32 screen, candidates decided in fp64: the first "
+                     "from cell seeds, the seeded ones the fused grid iteration "
+                     f"{grid_kernel()}" + (f", {cert / max(cert + walk, 1):.0%} of its queries kept their "
+                                           "correspondence by the exclusion certificate without a walk"
+                                           if cert + walk else "") + ")")
+    if b:
+        parts.append(f"{b} searches through the f16 hi/lo-split MFMA bundle bound + pair filter (fp32 "
+                     "accumulate) with the fp64 certificate")
+    return ("; ".join(parts) or "no search") + "; fp64 transform and reductions"
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32 MFMA peak
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense
@@ -256,8 +277,10 @@ def grid_roofline(n_local, n_model, avg_ms, traffic, traffic_src, explicit_varia
     gbytes = bq * n_local + bm * n_model
     t = avg_ms * 1e-3
     ach = gbytes / t / 1e9 if t > 0 else 0.0
-    what = ("fused grid iteration: transform + seeded search + moments, every query" if kern == GRID_ITER_KERNEL
-            else "seeded, every query")
+    what = {GRID_ITER_KERNEL: "fused grid iteration: transform + exclusion certificate + packed walks of the rest "
+                              "+ moments, every query",
+            GRID_ITER_KERNEL_R5: "fused grid iteration: transform + seeded search + moments, every query"}.get(
+        kern, "seeded, every query")
     return {"bound": "hbm", "kernel": f"{kern} ({what})",
             "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
             "traffic": traffic, "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE)",
@@ -266,7 +289,8 @@ def grid_roofline(n_local, n_model, avg_ms, traffic, traffic_src, explicit_varia
                                 "(tools/roofline.py GRID_KERNELS)",
             "path": "ICP_NN_VARIANT_GRID" if explicit_variant else
                     "AUTO: icp_run's policy (seeded iterations once the scene is near the model)",
-            "note": "latency-bound gather: each query walks the grid rows of its box (dependent loads)"}
+            "note": "latency-bound: the walkers' dependent loads (cell table, points, candidate records) set each "
+                    "wave's time (DESIGN §3.8)"}
 
 
 def full_nxm_rate(device, m, p, steps=5, warmup=2):
@@ -644,6 +668,11 @@ def main():
     reg = registration(ctx, m, p[b:b + c], args.n, iters=REGISTRATION_ITERS) if args.registration else None
     # the headline step's phases (device-resident clouds), untimed by the headline
     reg_dev = registration(ctx, m, p[b:b + c], args.n, iters=REGISTRATION_ITERS, device=(dm, dps))
+    # what a timed step ran: one more registration's counters (the searches by kind, the fused
+    # iterations' certified / walked queries), for the line's dtype
+    ctx.reset_stats()
+    registration_step()
+    path_st = ctx.stats()
     progress("registration timed")
     host_reduce = world > 1 and os.environ.get("ICP_BENCH_HOST_REDUCE") == "1"
     its = args.steps * REGISTRATION_ITERS
@@ -704,7 +733,8 @@ def main():
             "ms_per_step": dt * 1e3 / args.steps,
             "step": f"one complete registration of {REGISTRATION_ITERS} ICP iterations from device-resident clouds: "
                     "icp_set_model_device (every model image) + icp_set_scene_device + icp_run(30); "
-                    "value = steps x 30 iterations / the max-over-ranks wall time",
+                    "value = steps x 30 iterations / the max-over-ranks wall time; the clock EXCLUDES the PCIe "
+                    "copy of the clouds (value_pcie_inclusive: the same registration from host arrays)",
             "iterations_per_step": REGISTRATION_ITERS,
             "ms_per_iteration": dt * 1e3 / its,
             "steady_state": {"iterations_per_s": STEADY_ITERS / dt_ss, "ms_per_iteration": dt_ss * 1e3 / STEADY_ITERS,
@@ -743,6 +773,11 @@ def main():
             "final_err": float(errs[-1]) if errs.size else None,
         }
         out["step_phases"] = dict(reg_dev)
+        out["step_paths"] = {"run_grid_searches": path_st["run_grid_searches"],
+                             "run_bundle_searches": path_st["run_bundle_searches"],
+                             "run_certified": path_st["run_certified"], "run_walked": path_st["run_walked"],
+                             "run_path_bits": hex(path_st["run_path_bits"]),
+                             "note": "one registration after the timed region (icp_stats)"}
         out["step_phases"]["note"] = ("the headline step's phases from device-resident clouds (median of 3 "
                                       "registrations after the timed region): set_model_device, set_scene_device, "
                                       "first (unseeded) iteration, seeded iterations")
@@ -757,6 +792,7 @@ def main():
                                             "registration_ms": worst["registration_ms"],
                                             "set_model_ms_max": max(r["set_model_ms"] for r in regs)})
                 out["registration"]["iterations_per_s_inclusive"] = reg["iterations"] / (worst["registration_ms"] * 1e-3)
+            out["value_pcie_inclusive"] = out["registration"]["iterations_per_s_inclusive"]
         if level1 == "bundle" and nn_s > 0:
             out["roofline"].update(bundle_roofline(c, args.n, nn_s, work, v1=bundle_v1()))
         if level1 == "mfma16" and nn_s > 0:
@@ -781,10 +817,7 @@ def main():
                                     "kernels": {k: v for k, v in rf["kernels"].items() if k in keep}}
         if level1 == "grid":
             out["roofline"] = grid_roofline(c, args.n, nn_avg_ms, traffic, traffic_src, args.variant == "grid")
-            out["dtype"] = ("f64 (exact grid search of every query)" if args.variant == "grid" else
-                            "f64 exact grid search in the seeded iterations (icp_run's policy); the first searches: "
-                            "f16 hi/lo-split MFMA bundle bound + pair filter (fp32 accumulate) with the fp64 "
-                            "certificate; fp64 reductions")
+            out["dtype"] = "f64 (" + path_description(path_st) + ")"
         if world == 1 and not args.no_cow:
             out["cow_frame_rate"] = cow_frame_rate(local)
         if world == 1 and not args.no_cases:

@@ -47,3 +47,41 @@ def test_documented_torchrun_commands_parse(doc):
         assert args.training_script == "bench.py"
         checked += 1
     assert checked > 0
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_dtype_describes_what_ran():
+    """The line's dtype is composed from one registration's counters (icp_stats), not fixed text:
+    a C4 registration that ran only grid searches names the grid kernel and its certified share and
+    no bundle filter; one whose early searches took the bundle cascade names both."""
+    bench = _bench_module()
+    grid_only = {"run_grid_searches": 30, "run_bundle_searches": 0, "run_certified": 750, "run_walked": 250}
+    d = bench.path_description(grid_only)
+    assert "30 exact fp64 grid searches" in d and bench.grid_kernel() in d and "75%" in d
+    assert "bundle" not in d
+    mixed = {"run_grid_searches": 27, "run_bundle_searches": 3, "run_certified": 0, "run_walked": 0}
+    d = bench.path_description(mixed)
+    assert "27 exact fp64 grid searches" in d and "3 searches through the f16" in d
+
+
+def test_committed_bench_line_dtype_matches_its_counters():
+    """The round-6 GPU bench line (profiles/r06/*bench*.log, newest) carries step_paths, and its
+    dtype is the description of exactly those counters."""
+    import json
+    logs = sorted((ROOT / "profiles" / "r06").glob("*bench*.log"))
+    lines = [json.loads(x) for f in logs for x in f.read_text().splitlines() if x.startswith("{")]
+    lines = [x for x in lines if "step_paths" in x]
+    if not lines:
+        pytest.skip("no round-6 bench line with step_paths committed yet")
+    bench = _bench_module()
+    last = lines[-1]
+    sp = {k: last["step_paths"][k] for k in ("run_grid_searches", "run_bundle_searches", "run_certified",
+                                             "run_walked")}
+    assert last["dtype"] == "f64 (" + bench.path_description(sp) + ")"
