@@ -72,10 +72,10 @@ def test_dtype_describes_what_ran():
 
 
 def test_committed_bench_line_dtype_matches_its_counters():
-    """The round-6 GPU bench line (profiles/r06/*bench*.log, newest) carries step_paths, and its
+    """The round-6 GPU bench lines (profiles/r06*/*bench*.log) carry step_paths, and the last one's
     dtype is the description of exactly those counters."""
     import json
-    logs = sorted((ROOT / "profiles" / "r06").glob("*bench*.log"))
+    logs = sorted(ROOT.glob("profiles/r06*/*bench*.log"))
     lines = [json.loads(x) for f in logs for x in f.read_text().splitlines() if x.startswith("{")]
     lines = [x for x in lines if "step_paths" in x]
     if not lines:
