@@ -2800,8 +2800,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                         unsigned long long h[16];
                         HIPCHK(hipStreamSynchronize(ctx->st));
                         HIPCHK(hipMemcpy(h, iter_dbg, sizeof(h), hipMemcpyDeviceToHost));
-                        fprintf(stderr, "[iter2_debug] it %d tasks %llu walkers %llu batches %llu pair %llu | wave-us A %.1f D %.1f out %.1f G %.1f\n",
-                                enqueued, h[0], h[1], h[2], h[3], h[5] * 0.01, h[6] * 0.01, h[4] * 0.01, h[7] * 0.01);
+                        fprintf(stderr, "[iter2_debug] it %d tasks %llu walkers %llu batches %llu pair tests %llu (lane 0's)\n",
+                                enqueued, h[0], h[1], h[2], h[3]);
                         HIPCHK(hipMemset(iter_dbg, 0, sizeof(h)));
                     }
                     LAUNCHCHK("nn_grid_iter");
@@ -3113,8 +3113,8 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                 h[0], h[1], h[2], h[3], h[4], h[10], h[11], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01, h[8] * 0.01,
                 h[9] * 0.01);
         fprintf(stderr, "[iter2_debug] (nn_grid_iter2_kernel, an ICP_ITER2_DBG build) tasks %llu walkers %llu batches %llu "
-                        "pair tests %llu | wave-us A %.1f D %.1f G %.1f\n",
-                h[0], h[1], h[2], h[3], h[5] * 0.01, h[6] * 0.01, h[7] * 0.01);
+                        "pair tests %llu (lane 0's)\n",
+                h[0], h[1], h[2], h[3]);
     }
     // (every transform of a policy run wrote the seed distances, whatever its form; the next run
     // may start from them)

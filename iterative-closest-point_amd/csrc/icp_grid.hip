@@ -1451,17 +1451,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     unsigned long long *__restrict__ dbg)
 {
     static_assert(CH == 1 || CH == 2, "one or two chunks a task");
-    // (ICP_ITER2_DBG: dcnt = tasks, walkers, walk batches, pair tests, clocks: merge + outputs, A, D, G (100 MHz))
+    // (ICP_ITER2_DBG: dcnt = tasks, walkers, walk batches, pair tests -- lane 0's counts, i.e. the
+    // walkers and batches of the task and the pair tests of one lane in 64.  Phase clocks were
+    // tried here: s_memrealtime reads slowed the kernel 10x, so their phases meant nothing)
     constexpr bool kDbg = ICP_ITER2_DBG != 0;
-    unsigned long long dcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tclk = 0;
-    auto lap = [&](int f) {
-        if (kDbg && dbg) {
-            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (f >= 0) dcnt[f] += now - tclk;
-            tclk = now;
-        }
-    };
+    unsigned long long dcnt[4] = {0, 0, 0, 0};
     constexpr int NW = kBlock / 64, QL = 2 / CH; // (lanes a query in phases A and G)
     __shared__ double s_tile[NW][CH * kIter2Tile];
     if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
@@ -1484,7 +1478,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     for (int c = s; s < S && c < C; c += CH * S) {
         const int t = slot_t(c, u);
         const bool active = c + (u >> 5) * S < C && t < n;
-        lap(-1);
         if (kDbg) dcnt[0] += 1;
         // ---- A: the previous transform, its residual = the seed distance, the certificate
         double q[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
@@ -1602,7 +1595,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         const int nW = __popcll(wm);
         if (walker && sub == 0) wl[__popcll(wm & ((1ull << lane) - 1ull))] = u;
         wave_sync();
-        lap(5);
         if (kDbg) dcnt[1] += nW;
         // ---- D: the walkers, at most 32 at a time, G = 64 / 2^k lanes each
         for (int b0 = 0; b0 < nW; b0 += 32) {
@@ -1796,7 +1788,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
                 if constexpr (!ICP_ITER2_F64)
                     if (nc) flush();
             }
-            lap(6); // (ICP_ITER2_DBG: D = the walk; the merge and the outputs count as "-" below)
             // the walker's G lanes: the (D64, index) minimum, its position and coordinates; with the
             // certificate also the others (the two lists, and the sub-group winner that loses a merge
             // -- one with no position here was scanned by a lane of another sub-group, which holds it)
@@ -1901,7 +1892,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             }
             wave_sync();
         }
-        lap(4);
         // ---- G: this task's 18 leaves a query into the chunk tile, then the chunk tree
         if (active) {
             y[0] = sl[4];
@@ -1945,10 +1935,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             if (CH == 2 && c + S < C) acc = acc + tb;
         }
         wave_sync(); // (the next task's slots alias the tiles)
-        lap(7);
     }
     if (kDbg && dbg && lane == 0)
-        for (int f = 0; f < 8; ++f)
+        for (int f = 0; f < 4; ++f)
             if (dcnt[f]) atomicAdd(dbg + f, dcnt[f]);
     // the workgroup's four strands -> its row (column k from lane k of each wave)
     __shared__ double sh[NW][kCanonCols];
