@@ -212,7 +212,11 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
     double a[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = 0.0;
-    constexpr int U = 4; // (R <= 2,048 rows: at most four a thread)
+    // (R <= kCanonStrandsMax / 4 = 4,096 rows: U = 4 rows a thread per pass of 2,048, the rest in a
+    // second pass -- thread t adds rows t, t + 512, ... in order either way, so the bits do not
+    // depend on how many passes)
+    constexpr int U = 4;
+    static_assert(kCanonStrandsMax / 4 <= 2 * U * kFoldThreads, "at most two passes of the fold's rows");
     for (int r0 = threadIdx.x; r0 < R; r0 += U * kFoldThreads) {
         double v[U][K];
 #pragma unroll
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const dou
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, k = blockIdx.x;
     const double *col = rows + (size_t)k * R;
     double a = 0.0;
-    constexpr int U = 4;
+    constexpr int U = 4; // (as canon_fold_kernel: rows t, t + 512, ... in order, R <= 4,096)
     for (int r0 = threadIdx.x; r0 < R; r0 += U * kFoldThreads) {
         double v[U];
 #pragma unroll

@@ -2276,6 +2276,9 @@ constexpr int kTailAborted = -1000; // run_loop: a fused tail's grid barrier tim
 
 int icp_run(icp_ctx *ctx, int max_iter, double threshold, double *err_trace, icp_result *res)
 {
+    // (icp_set_progress: reset once per icp_run -- a rerun below replays the same iterations bit for
+    // bit, and report_progress skips the ones the aborted attempt already reported)
+    if (ctx) ctx->progress_next = 0;
     const int r = run_loop(ctx, max_iter, threshold, err_trace, res, false);
     if (r != kTailAborted) return r;
     // A grid barrier of the fused mid-size tail timed out (its workgroups were not all resident:
@@ -2312,7 +2315,6 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         HIPCHK(hipHostGetDevicePointer((void **)&ctx->d_trace, ctx->h_trace, 0));
     }
     std::memset(ctx->h_iter, 0, sizeof(IterState));
-    ctx->progress_next = 0;
     if (!ctx->h_flags) {
         HIPCHK(hipHostMalloc((void **)&ctx->h_flags, sizeof(int) * 4 * kRing,
                              hipHostMallocMapped | hipHostMallocCoherent));
@@ -2575,6 +2577,15 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     if (canon) {
         TRY(grow(ctx, &ctx->canon_rowbuf, &ctx->canon_rowbuf_cap, (size_t)canon_rows(n) * kCanonCols));
         if (!ctx->h_far) HIPCHK(hipHostMalloc((void **)&ctx->h_far, sizeof(int), hipHostMallocDefault));
+        // the first iteration's shift of p: the scene's centroid (all ranks'), where run_init put the
+        // model's centre c -- a scene far from the model would otherwise cancel (D / sigma)^2 of the
+        // one-pass moments' precision (the shift of y stays c: the correspondences are model points)
+        launch_sum3(P.x, P.y, P.z, (int)n, red_target(ctx, n, ctx->sums + kSumScene), ctx->st, 1);
+        red_finish(ctx, n, 3, ctx->sums + kSumScene);
+        LAUNCHCHK("scene_sum");
+        TRY(allreduce(ctx, ctx->sums + kSumScene, 3));
+        launch_first_shift(sd, ctx->sums + kSumScene, N, ctx->st);
+        LAUNCHCHK("first_shift");
     }
     const bool lag_sched = lag || canon;
     // The fused grid iteration's exclusion certificate (icp_grid.hip): the state one fused

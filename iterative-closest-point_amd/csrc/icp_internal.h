@@ -40,5 +40,8 @@ constexpr int kSumP = 0, kSumY = 3, kSumS = 6, kSumDcaps = 15, kSumSp = 16, kSum
 // [18] the search policy's far count of the iteration's transform (icp_run's canonical schedule on
 // several ranks: all-reduced with the 18 sums, so that every rank takes the same path)
 constexpr int kSumFar = 18;
+// [20..22] the scene's coordinate sums at a run's start (all ranks'): the canonical first
+// iteration's shift of p (its one-pass moments around the scene's own centroid)
+constexpr int kSumScene = 20;
 
 } // namespace icp

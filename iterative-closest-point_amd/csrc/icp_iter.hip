@@ -1759,6 +1759,18 @@ __global__ void run_init_kernel(IterState *__restrict__ s, int *__restrict__ cnt
     }
 }
 
+// the canonical first iteration's shift of p: the scene's centroid (sums[0..2] / N, all ranks'), so
+// that its one-pass moments do not cancel when the scene sits far from the model's centre c
+__global__ void first_shift_kernel(IterState *__restrict__ s, const double *__restrict__ sums, double N)
+{
+    if (threadIdx.x < 3) s->shift_p[threadIdx.x] = sums[threadIdx.x] / N;
+}
+
+void launch_first_shift(IterState *st_dev, const double *sums3, double N, hipStream_t st)
+{
+    first_shift_kernel<<<1, 64, 0, st>>>(st_dev, sums3, N);
+}
+
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st, const double *c)
 {
     run_init_kernel<<<1, 64, 0, st>>>(st_dev, amb_count, c ? c[0] : 0.0, c ? c[1] : 0.0, c ? c[2] : 0.0);

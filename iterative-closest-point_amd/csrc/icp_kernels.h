@@ -696,6 +696,8 @@ void launch_small_err(const double *y_aos, double *p_aos, int n, const Xform &xf
 void launch_small_alignment(const double *p_aos, const double *y_aos, int n, double *out, hipStream_t st);
 // zero a run's IterState and the NN queue counters (amb_count[0..3])
 void launch_run_init(IterState *st_dev, int *amb_count, hipStream_t st, const double *c = nullptr);
+// st->shift_p = sums3 / N (the scene's centroid: the canonical first iteration's shift of p)
+void launch_first_shift(IterState *st_dev, const double *sums3, double N, hipStream_t st);
 
 // exact NN of nq (few) queries, one workgroup each: q_aos (3 x nq) in, idx and y = m[idx]
 // (3 x nq) out -- all three may be mapped host memory

@@ -49,6 +49,26 @@ for name, n, frac in (("whole", 1 << 17, 1), ("shard", 1 << 19, 8), ("big", 1 <<
         out[name + "_scene"] = ctx.get_scene()
         out[name + "_xf"] = np.concatenate([[res.s], np.array(res.R[:]), np.array(res.t[:])])
         out[name + "_grid"] = np.array([ctx.stats()["run_grid_searches"]])
+# a scene 1e3 model spreads away (ADVICE r05: the first iteration's one-pass moments around a shift
+# far from the scene cancel (D / sigma)^2 of their precision), and a positive threshold that stops
+# the run mid-way (ADVICE r05: the lagged error test of the canonical schedule)
+m, p = icp_amd.synthetic_pair(1 << 17, seed=33, angle_deg=6.0)
+for name, scene, thr in (("far", p + np.array([1000.0, -700.0, 500.0]), -1.0), ("thresh", p, None)):
+    if thr is None:  # (the threshold: between the trajectory's 6th and 7th errors)
+        with icp_amd.Context(0) as ctx:
+            ctx.set_model(m)
+            ctx.set_scene(scene)
+            _, e = ctx.run(12, -1.0)
+        thr = float(0.5 * (e[5] + e[6]))
+        out["thresh_full_errs"] = e
+    with icp_amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(scene)
+        res, errs = ctx.run(12 if name == "thresh" else 6, thr)
+        out[name + "_errs"] = errs
+        out[name + "_iters"] = np.array([res.iterations, res.converged])
+        out[name + "_scene"] = ctx.get_scene()
+        out[name + "_xf"] = np.concatenate([[res.s], np.array(res.R[:]), np.array(res.t[:])])
 np.savez(sys.argv[2], **out)
 print("canon ok")
 """
@@ -88,3 +108,31 @@ def test_canonical_matches_round4_schedule(settings, case):
     assert np.array_equal(a[case + "_dig"], b[case + "_dig"])
     np.testing.assert_allclose(a[case + "_errs"], b[case + "_errs"], rtol=1e-12)
     np.testing.assert_allclose(a[case + "_scene"], b[case + "_scene"], rtol=0, atol=1e-12)
+
+
+def test_far_scene_first_iteration_matches_two_pass(settings):
+    """A scene 1e3 spreads from the model: the canonical first iteration sums its moments around the
+    scene's own centroid (all ranks' sum, icp_engine.hip run_loop), so its (s, R, t) agree with the
+    reference's two passes (gpu.cc:98-104, the round-4 schedule) to rounding."""
+    a, b = settings["fused"], settings["round4"]
+    np.testing.assert_allclose(a["far_errs"], b["far_errs"], rtol=1e-12)
+    np.testing.assert_allclose(a["far_xf"], b["far_xf"], rtol=1e-12, atol=1e-12)
+    ext = float(np.abs(b["far_scene"]).max())
+    np.testing.assert_allclose(a["far_scene"], b["far_scene"], rtol=0, atol=1e-12 * ext)
+
+
+def test_threshold_stops_where_the_reference_breaks(settings):
+    """A positive threshold on a slot-order scene (2^17): the run stops after the first iteration whose
+    err is below it (gpu.cc:79-80) -- the lagged error test of the canonical schedule freezes the
+    scene at the same point -- with the round-4 schedule's iteration count, errors (rtol 1e-12),
+    scene and transform."""
+    a, b = settings["fused"], settings["round4"]
+    full = a["thresh_full_errs"]
+    thr = 0.5 * (full[5] + full[6])
+    want = int(np.argmax(full < thr)) + 1
+    assert a["thresh_iters"][0] == b["thresh_iters"][0] == want
+    assert a["thresh_iters"][1] == b["thresh_iters"][1] == 1
+    np.testing.assert_allclose(a["thresh_errs"], b["thresh_errs"], rtol=1e-12)
+    np.testing.assert_allclose(a["thresh_errs"], full[:want], rtol=0)
+    np.testing.assert_allclose(a["thresh_scene"], b["thresh_scene"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(a["thresh_xf"], b["thresh_xf"], rtol=1e-12, atol=1e-12)
