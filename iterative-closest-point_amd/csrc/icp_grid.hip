@@ -1493,9 +1493,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
             if (cert_in) cs4 = ca.state[t];
             if (xform) {
                 transform_point(st->xf, p0, p1, p2, q[0], q[1], q[2]);
-                // (the motion rounded up: the square up to fp32, its fp32 root one ulp low at most)
+                // (the motion rounded up: the square up to fp32, its root by v_sqrt_f32 -- within an
+                // ulp or two -- and 2^-21 of room; tests/test_iter_prune.py restates it)
                 if (cert_in)
-                    mot = (double)(sqrtf(__double2float_ru(residual2(p0, p1, p2, q[0], q[1], q[2]))) * (1.0f + 0x1.0p-21f));
+                    mot = (double)(__builtin_amdgcn_sqrtf(__double2float_ru(residual2(p0, p1, p2, q[0], q[1], q[2]))) *
+                                   (1.0f + 0x1.0p-21f));
             } else { // (a run's first iteration: no pending transform, the point as it is)
                 q[0] = p0;
                 q[1] = p1;
@@ -1514,7 +1516,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         if (active && sub == 0) { // the policy's far count (SeedArgs::far_box's rule, or the distance rule)
             if (far_d2 >= 0.0) {
                 if (xform) far += e > far_d2 ? 1 : 0;
-            } else {
+            } else if (!(h >= 0 && e * (gv.inv_h * gv.inv_h) < 2.2)) {
+                // (a seed distance under 1.483 cells -- (e inv_h^2 < 2.2, rounding aside) -- spans at most
+                // 2 r / h + 2 < 5 cells an axis, at most 125 cells: never far; the rest are boxed exactly)
                 int b0[3], b1[3];
                 far += h >= 0 && e == e && e < INFINITY && complete_box(q, e, gv, box, b0, b1) ? 0 : 1;
             }

@@ -241,7 +241,8 @@ def test_other_bounds_are_below_the_true_distance(centre, extent):
 
 def test_motion_bound_rounds_up():
     """The kernel's fp32 motion bound is at least the exact |q' - q| (the fp64 square rounded up to
-    fp32, a root at most an ulp low, times 1 + 2^-21), over motions from 1e-12 to 1e3."""
+    fp32, its v_sqrt_f32 root -- taken two ulps low here -- times 1 + 2^-21), over motions from
+    1e-12 to 1e3."""
     rng = np.random.default_rng(9)
     for _ in range(3000):
         q = rng.uniform(-1e4, 1e4, 3)
@@ -249,7 +250,8 @@ def test_motion_bound_rounds_up():
         d *= 10.0 ** rng.uniform(-12, 3) / np.linalg.norm(d)
         qn = q + d
         m = motion_bound(q, qn)
-        m_low = float(np.nextafter(np.float32(m / (1.0 + 2.0 ** -21)), F(0))) * (1.0 + 2.0 ** -21)  # (a root an ulp low)
+        r = np.float32(m / (1.0 + 2.0 ** -21))
+        m_low = float(np.nextafter(np.nextafter(r, F(0)), F(0))) * (1.0 + 2.0 ** -21)  # (v_sqrt_f32 two ulps low)
         assert Fraction(min(m, m_low)) ** 2 >= exact_d2(q, qn)
 
 
@@ -402,3 +404,25 @@ def test_certified_queries_keep_the_first_minimum(model, two):
                 assert state[i][0] == first_min(qn[i], pts)
         q = qn
     assert certified > 0  # (the certificate does fire on these trajectories)
+
+
+def test_far_count_shortcut_is_exact():
+    """nn_grid_iter2_kernel counts a query far (its complete box over 125 cells) only when e inv_h^2
+    >= 2.2: below that the box spans at most 4 cells an axis.  Checked against complete_box on
+    seed distances just under the cut, queries on and off cell faces, boxes far from the origin."""
+    rng = np.random.default_rng(13)
+    for centre, g in ((0.0, 80), (1e3, 64), (-5e4, 200)):
+        lo = [centre - 1.0] * 3
+        inv_h = (g - 0.5) / 2.0
+        gg = [g, g, g]
+        for _ in range(3000):
+            q = rng.uniform(np.array(lo) - 0.1, np.array(lo) + 2.1)
+            if rng.random() < 0.5:
+                a = rng.integers(3)
+                q[a] = lo[a] + rng.integers(0, g) / inv_h
+            e = 2.2 * (1.0 - 10.0 ** rng.uniform(-15, 0)) / (inv_h * inv_h)
+            if not e * (inv_h * inv_h) < 2.2:
+                continue
+            c0, c1 = complete_box(q, e, lo, inv_h, gg)
+            cells = (c1[0] - c0[0] + 1) * (c1[1] - c0[1] + 1) * (c1[2] - c0[2] + 1)
+            assert cells <= 64, (q, e, cells)
