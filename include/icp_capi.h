@@ -328,6 +328,12 @@ int icp_get_comm_info(icp_ctx *ctx, int *comm_count, int *comm_rank, char *bus_i
  * device by icp_set_model): kd_out[P] = the original index of kd position P (nm entries); 32
  * consecutive positions form a bundle.  ICP_E_NO_MODEL if the model has no bundle images. */
 int icp_get_model_order(icp_ctx *ctx, int32_t *kd_out);
+/* The engine's stable LSD radix sort (icp_sort.hip: the grid build's cell lists and the scene's
+ * slot order), exposed for its tests: order_out[k] = the input position of the k-th pair when
+ * the n keys are sorted by their low `bits` bits (ties in input order); keys_out (nullable) =
+ * the keys in that order.  Host arrays; runs on `device` (synchronous).  ICP_E_ARG for bits
+ * outside [0, 32] or n > INT_MAX. */
+int icp_sort_pairs(int device, const uint32_t *keys, size_t n, int bits, uint32_t *keys_out, int32_t *order_out);
 
 #ifdef __cplusplus
 }

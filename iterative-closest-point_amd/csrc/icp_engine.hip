@@ -18,6 +18,7 @@
 #include <thread>
 #include <cmath>
 #include <cstdio>
+#include <climits>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -3583,6 +3584,26 @@ int icp_get_model_order(icp_ctx *ctx, int32_t *kd_out)
     HIPCHK(hipMemcpyAsync(kd_out, ctx->b_kd, sizeof(int32_t) * ctx->nm, hipMemcpyDeviceToHost, ctx->st));
     HIPCHK(hipStreamSynchronize(ctx->st));
     return ICP_OK;
+}
+
+int icp_sort_pairs(int device, const uint32_t *keys, size_t n, int bits, uint32_t *keys_out, int32_t *order_out)
+{
+    if (bits < 0 || bits > 32 || n > (size_t)INT_MAX || (n && (!keys || !order_out))) return ICP_E_ARG;
+    if (n == 0) return ICP_OK;
+    if (hipSetDevice(device) != hipSuccess) return ICP_E_HIP;
+    size_t temp = 0;
+    (void)icp::sort_pairs_u32(nullptr, temp, nullptr, nullptr, nullptr, nullptr, (int)n, bits, nullptr);
+    char *buf = nullptr;
+    const size_t kb = ((n * 4 + 255) & ~(size_t)255);
+    if (hipMalloc(&buf, 3 * kb + temp) != hipSuccess) return ICP_E_HIP;
+    unsigned *k0 = (unsigned *)buf, *k1 = (unsigned *)(buf + kb);
+    int *v1 = (int *)(buf + 2 * kb);
+    bool ok = hipMemcpy(k0, keys, n * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              icp::sort_pairs_u32(buf + 3 * kb, temp, k0, k1, nullptr, v1, (int)n, bits, nullptr) == hipSuccess &&
+              hipMemcpy(order_out, v1, n * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+              (!keys_out || hipMemcpy(keys_out, k1, n * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    ok = hipFree(buf) == hipSuccess && ok;
+    return ok ? ICP_OK : ICP_E_HIP;
 }
 
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out)

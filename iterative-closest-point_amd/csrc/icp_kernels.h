@@ -247,8 +247,8 @@ void launch_nn_bundle2(const void *qop, const void *gop, int np, const void *bim
 // 256^3 grid over the box [lo, hi] (icp_order.hip), and pos (nullable) its inverse (pos[order[k]]
 // = k); scratch: query_order_scratch_bytes(n)
 size_t query_order_scratch_bytes(int n);
-// stable LSD radix sort of (key, value) pairs on the low `bits` key bits (rocprim onesweep at
-// every size): temp == nullptr -> temp_bytes = the storage it needs
+// stable LSD radix sort of (key, value) pairs on the low `bits` key bits (icp_sort.hip; v0 ==
+// nullptr: the values are the input positions): temp == nullptr -> temp_bytes = the storage it needs
 hipError_t sort_pairs_u32(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
                           int n, int bits, hipStream_t st);
 int launch_query_order(const double *px, const double *py, const double *pz, int n, const double lo[3],

@@ -5,8 +5,6 @@
 // of a search batch lie close together whatever order the cloud came in.  The order only decides
 // which queries share a batch; every result is the exact first minimum regardless.
 #include <hip/hip_runtime.h>
-#include <hipcub/device/device_radix_sort.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "icp_kernels.h"
 
@@ -144,20 +142,8 @@ void launch_permute_cloud(const int *order, int n, int inverse, const double *sx
                                                                         dy, dz, df, didx);
 }
 
-// The query orders' sort: stable LSD radix sort of (key, index) pairs.  rocprim's default sends
-// n <= 2^20 -- a whole C4 scene -- to its merge sort (a block sort and 10 merge passes: 173 us for
-// 2^20 pairs, profiles/r05h); a merge-sort limit of 0 takes onesweep's digit passes at every size
-// above one block.  Both are stable: the same order either way.
-using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                rocprim::default_config, 0>;
-
-hipError_t sort_pairs_u32(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
-                          int n, int bits, hipStream_t st)
-{
-    return rocprim::radix_sort_pairs<OnesweepSort>(temp, temp_bytes, k0, k1, v0, v1, (size_t)n, 0u, (unsigned)bits, st,
-                                                   false);
-}
-
+// The query orders' sort: the stable LSD radix sort of (key, index) pairs (icp_sort.hip; rounds
+// 4-5 ran rocprim's onesweep here, the same order).
 static hipError_t sort_pairs(void *temp, size_t &temp_bytes, const unsigned *k0, unsigned *k1, const int *v0, int *v1,
                              int n, int bits, hipStream_t st)
 {
@@ -222,8 +208,7 @@ int launch_slot_order_aos(const double *aos, int n, const double lo[3], const do
 size_t mid_order_scratch_bytes(int n)
 {
     size_t temp = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const unsigned *)nullptr, (unsigned *)nullptr,
-                                             (const int *)nullptr, (int *)nullptr, n, 0, kOrderBits);
+    (void)sort_pairs(nullptr, temp, nullptr, nullptr, nullptr, nullptr, n, kOrderBits, nullptr);
     return keys_bytes(n, 4) + ((temp + 255) & ~(size_t)255);
 }
 
@@ -241,7 +226,7 @@ int launch_mid_order(const double *px, const double *py, const double *pz, int n
     size_t temp_bytes = bytes - keys_bytes(n, 4);
     const int g = (n + kBlock - 1) / kBlock;
     order_keys_kernel<<<g, kBlock, 0, st>>>(px, py, pz, n, bx, k0, v0);
-    if (hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k0, k1, v0, v1, n, 0, kOrderBits, st) != hipSuccess)
+    if (sort_pairs(temp, temp_bytes, k0, k1, v0, v1, n, kOrderBits, st) != hipSuccess)
         return -1;
     order_pos_kernel<<<g, kBlock, 0, st>>>(v1, n, pos);
     return 0;

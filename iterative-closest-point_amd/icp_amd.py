@@ -67,7 +67,7 @@ EXPORTED = [
     "icp_ensure_model", "icp_subtract_col", "icp_get_indices", "icp_set_index_digest",
     "icp_get_index_digest", "icp_set_cert_audit", "icp_set_run_mode", "icp_set_nn_rule",
     "icp_get_comm_info", "icp_set_bundle_counters", "icp_get_bundle_counters", "icp_get_model_order",
-    "icp_bundle_audit",
+    "icp_bundle_audit", "icp_sort_pairs",
 ]
 
 
@@ -164,6 +164,7 @@ def lib() -> C.CDLL:
     L.icp_subtract_col.argtypes = [vp, dp, sz, dp, dp]
     L.icp_get_indices.argtypes = [vp, C.POINTER(C.c_int32)]
     L.icp_get_model_order.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.icp_sort_pairs.argtypes = [C.c_int, C.POINTER(C.c_uint32), sz, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
     L.icp_set_index_digest.argtypes = [vp, sz]
     L.icp_get_index_digest.argtypes = [vp, C.POINTER(C.c_uint64), sz]
     L.icp_set_cert_audit.argtypes = [vp, C.c_int]
@@ -207,6 +208,17 @@ def device_count() -> int:
     n = C.c_int(0)
     lib().icp_device_count(C.byref(n))
     return n.value
+
+
+def sort_pairs(keys, bits: int, device: int = 0):
+    """The engine's stable LSD radix sort (icp_sort_pairs) -> (order int32, sorted keys uint32)."""
+    k = np.ascontiguousarray(keys, dtype=np.uint32)
+    order = np.empty(k.size, dtype=np.int32); out = np.empty(k.size, dtype=np.uint32)
+    rc = lib().icp_sort_pairs(device, k.ctypes.data_as(C.POINTER(C.c_uint32)), k.size, bits,
+                              out.ctypes.data_as(C.POINTER(C.c_uint32)), order.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc != ICP_OK:
+        raise ICPError(rc, strerror(rc))
+    return order, out
 
 
 def horn_solve(S, mu_p, mu_y, d_caps: float, sp: float):
