@@ -327,7 +327,9 @@ struct icp_ctx {
     hipEvent_t order_ev = nullptr; // icp_set_*_device_stream: the producer stream's point to wait for
     int4 *cert_state = nullptr;
     size_t cert_state_cap = 0;
-    unsigned long long *cert_counts = nullptr;
+    unsigned *cert_counts = nullptr; // (2 per canonical row: certified, walked -- CertArgs::counts)
+    size_t cert_counts_cap = 0;
+    int cert_counts_rows = 0; // (rows the last run counted into cert_counts, not yet in stats)
     char *tail_backup = nullptr;              // icp_run with the fused tail: the starting scene / idx
     size_t tail_backup_cap = 0;
     double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
@@ -760,6 +762,33 @@ constexpr size_t kInlineFallbackModel = 8192; // (16 lanes scan it; a larger mod
 // the exact first minimum.  With the seed distances (seedd) the passes also write each query's
 // correspondence y (the moments stream it); without them kpos is kept when the bundle's kd tables
 // exist (the moments then gather from the kd-ordered model).
+// The fused iteration's per-row certificate counts of the last run (CertArgs::counts) summed:
+// (certified, walked); cert_counts_rows = 0: none pending
+static int sum_cert_counts(const icp_ctx *ctx, long long out[2])
+{
+    out[0] = out[1] = 0;
+    if (ctx->cert_counts_rows <= 0 || !ctx->cert_counts) return ICP_OK;
+    std::vector<unsigned> h(2 * (size_t)ctx->cert_counts_rows);
+    if (hipStreamSynchronize(ctx->st) != hipSuccess ||
+        hipMemcpy(h.data(), ctx->cert_counts, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+        return ICP_E_HIP;
+    for (size_t r = 0; r < h.size(); r += 2) {
+        out[0] += h[r];
+        out[1] += h[r + 1];
+    }
+    return ICP_OK;
+}
+
+static int fold_cert_counts(icp_ctx *ctx)
+{
+    long long c[2];
+    TRY(sum_cert_counts(ctx, c));
+    ctx->stats.run_certified += c[0];
+    ctx->stats.run_walked += c[1];
+    ctx->cert_counts_rows = 0;
+    return ICP_OK;
+}
+
 constexpr int kSeededBox = 125;
 static int grid_seeded_search(icp_ctx *ctx, const DevCloud &q, size_t n, const int *stop, const double *seedd,
                               hipEvent_t ev1)
@@ -2615,8 +2644,11 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     bool cert_prev = false;
     if (canon && cert_env && grid_iter_on() && ctx->g_pts32) {
         TRY(grow(ctx, &ctx->cert_state, &ctx->cert_state_cap, n));
-        if (!ctx->cert_counts) HIPCHK(hipMalloc((void **)&ctx->cert_counts, 2 * sizeof(unsigned long long)));
-        HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * sizeof(unsigned long long), ctx->st));
+        TRY(fold_cert_counts(ctx)); // (an earlier run's counts into the stats first)
+        const int crows = canon_rows(n);
+        TRY(grow(ctx, &ctx->cert_counts, &ctx->cert_counts_cap, 2 * (size_t)crows));
+        HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * (size_t)crows * sizeof(unsigned), ctx->st));
+        ctx->cert_counts_rows = crows;
         cert.state = ctx->cert_state;
         cert.two = cert_two;
         cert.skin = cert_skin / ctx->grid.inv_h;
@@ -3130,12 +3162,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }
     // (every transform of a policy run wrote the seed distances, whatever its form; the next run
     // may start from them)
-    if (cert.counts) {
-        unsigned long long cc[2] = {0ull, 0ull};
-        HIPCHK(hipMemcpy(cc, ctx->cert_counts, sizeof(cc), hipMemcpyDeviceToHost));
-        ctx->stats.run_certified += (long long)cc[0];
-        ctx->stats.run_walked += (long long)cc[1];
-    }
+    // (cert_counts: folded into the stats when they are read or the next run starts)
     ctx->seedd_valid = grid_policy && ws.seedd;
     ctx->last_far = far_obs;
     ctx->last_q2 = q2_obs;
@@ -3610,6 +3637,10 @@ int icp_get_stats(const icp_ctx *ctx, icp_stats *out)
 {
     if (!ctx || !out) return ICP_E_ARG;
     *out = ctx->stats;
+    long long cc[2]; // (the last run's certificate counts, not yet folded)
+    if (sum_cert_counts(ctx, cc) != ICP_OK) return ICP_E_HIP;
+    out->run_certified += cc[0];
+    out->run_walked += cc[1];
     out->cert_max_err_ratio = -1.0;
     out->cert_min_margin = -1.0;
     out->cert_audited = 0;
@@ -3634,6 +3665,7 @@ int icp_reset_stats(icp_ctx *ctx)
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->cert_audit) TRY(cert_audit_reset(ctx));
     ctx->stats = icp_stats{};
+    ctx->cert_counts_rows = 0; // (the last run's certificate counts go with the rest)
     ctx->stats.last_filter = -1;
     return ICP_OK;
 }

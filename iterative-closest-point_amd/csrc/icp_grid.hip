@@ -1971,8 +1971,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         if (threadIdx.x < 2) {
             int *dst = threadIdx.x == 0 ? far_acc : big_count;
             if (tot && dst) atomicAdd(dst, tot);
-        } else if (tot && ca.counts) {
-            atomicAdd(ca.counts + (threadIdx.x - 2), (unsigned long long)tot);
+        } else if (ca.counts) { // (this row's own counters: stream order separates the launches)
+            ca.counts[2 * wr + (threadIdx.x - 2)] += (unsigned)tot;
         }
     }
 }

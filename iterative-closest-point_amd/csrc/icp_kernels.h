@@ -541,13 +541,15 @@ struct GridView;
 // point without a walk.  valid: the state is the one the previous fused iteration of this run
 // wrote (else every query walks and the state is written fresh); two = 0: the one-point form
 // (R3 and pair.y unused); skin: the radius a walk scans beyond its seed distance (model units);
-// counts (nullable): += (queries certified, queries walked).
+// counts (nullable): per canonical row r (= workgroup), counts[2 r] += queries certified,
+// counts[2 r + 1] += queries walked -- plain adds by the row's own workgroup (a device atomic
+// per workgroup on one address serialised the launch's tail: 15 us a launch at C4).
 struct CertArgs {
     int4 *state = nullptr;
     int valid = 0;
     int two = 1;
     double skin = 0.0;
-    unsigned long long *counts = nullptr;
+    unsigned *counts = nullptr;
 };
 // Returns true when the launch wrote the certificate state (ca.state non-null, the certificate form).
 bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
