@@ -202,9 +202,22 @@ __global__ __launch_bounds__(kBlock) void canon_transform_kernel(
 // columns): + the error step of the previous iteration and this iteration's Horn step; MODE 2
 // (one rank, the residual column): + the error step (the run's last iteration).
 constexpr int kFoldThreads = 512; // (the Horn solve on thread 0 fits 256 VGPRs without spills)
+
+// Row r of column `col` of the canonical rows: col[r], or -- S > 0, the rows as strands (the
+// fused iteration's one-wave workgroups, nn_grid_iter2_kernel) -- (strand 4r + strand 4r + 1) +
+// (strand 4r + 2 + strand 4r + 3), a strand past S 0.0: the four-wave workgroup's own sum,
+// the same bits
+__device__ __forceinline__ double canon_row_value(const double *__restrict__ col, int S, int r)
+{
+    if (S <= 0) return col[r];
+    const int s = 4 * r;
+    const double a = col[s], b = s + 1 < S ? col[s + 1] : 0.0, c = s + 2 < S ? col[s + 2] : 0.0,
+                 d = s + 3 < S ? col[s + 3] : 0.0;
+    return (a + b) + (c + d);
+}
 template <int K0, int K, int MODE>
 __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *__restrict__ rows, int R,
-                                                                  double *__restrict__ sums, CanonStep cs)
+                                                                  double *__restrict__ sums, CanonStep cs, int S)
 {
     __shared__ double sh[kFoldThreads / 64][K];
     __shared__ double s_sum[kCanonCols];
@@ -223,7 +236,8 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
         for (int u = 0; u < U; ++u) {
             const int r = r0 + u * kFoldThreads;
 #pragma unroll
-            for (int k = 0; k < K; ++k) v[u][k] = r < R ? rows[(size_t)(K0 + k) * R + r] : 0.0;
+            for (int k = 0; k < K; ++k)
+                v[u][k] = r < R ? canon_row_value(rows + (size_t)(K0 + k) * (S > 0 ? S : R), S, r) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -269,13 +283,13 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
 // the Horn step on the 18 sums.  MODE 0: the sums only (several ranks: the all-reduce follows).
 template <int MODE>
 __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const double *__restrict__ rows, int R,
-                                                                       double *__restrict__ sums, CanonStep cs)
+                                                                       double *__restrict__ sums, CanonStep cs, int S)
 {
     __shared__ double sh[kFoldThreads / 64];
     __shared__ double s_sum[kCanonCols];
     __shared__ int s_last;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, k = blockIdx.x;
-    const double *col = rows + (size_t)k * R;
+    const double *col = rows + (size_t)k * (S > 0 ? S : R);
     double a = 0.0;
     constexpr int U = 4; // (as canon_fold_kernel: rows t, t + 512, ... in order, R <= 4,096)
     for (int r0 = threadIdx.x; r0 < R; r0 += U * kFoldThreads) {
@@ -283,7 +297,7 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const dou
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = r0 + u * kFoldThreads;
-            v[u] = r < R ? col[r] : 0.0;
+            v[u] = r < R ? canon_row_value(col, S, r) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -348,7 +362,8 @@ void launch_canon_transform(double *px, double *py, double *pz, const double *yx
         canon_transform_kernel<false><<<R, kBlock, 0, st>>>(px, py, pz, yx, yy, yz, n, xf, done, p32, rows, sa);
 }
 
-void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st)
+void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st,
+                       int strands)
 {
     const int R = canon_rows((size_t)(n > 0 ? n : 1));
     // (ICP_FOLD_ONE=1: the 18 columns in one workgroup, A/B)
@@ -357,17 +372,17 @@ void launch_canon_fold(const double *rows, int n, double *sums, int mode, const 
         return e && atoi(e) == 1;
     }();
     if (!one && cs.fold_ticket && (mode == 0 || mode == 1 || mode == 4)) {
-        if (mode == 0) canon_fold_cols_kernel<0><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
-        else if (mode == 1) canon_fold_cols_kernel<1><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
-        else canon_fold_cols_kernel<4><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs);
+        if (mode == 0) canon_fold_cols_kernel<0><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands);
+        else if (mode == 1) canon_fold_cols_kernel<1><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands);
+        else canon_fold_cols_kernel<4><<<kCanonCols, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands);
         return;
     }
     switch (mode) {
-    case 0: canon_fold_kernel<0, kCanonCols, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
-    case 1: canon_fold_kernel<0, kCanonCols, 1><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
-    case 4: canon_fold_kernel<0, kCanonCols, 4><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
-    case 2: canon_fold_kernel<kSumErr, 1, 2><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
-    default: canon_fold_kernel<kSumErr, 1, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs); break;
+    case 0: canon_fold_kernel<0, kCanonCols, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands); break;
+    case 1: canon_fold_kernel<0, kCanonCols, 1><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands); break;
+    case 4: canon_fold_kernel<0, kCanonCols, 4><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands); break;
+    case 2: canon_fold_kernel<kSumErr, 1, 2><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands); break;
+    default: canon_fold_kernel<kSumErr, 1, 0><<<1, kFoldThreads, 0, st>>>(rows, R, sums, cs, strands); break;
     }
 }
 

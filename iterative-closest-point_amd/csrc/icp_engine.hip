@@ -2605,7 +2605,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }();
     const bool canon = canon_env && ctx->scene_slot && n > 0;
     if (canon) {
-        TRY(grow(ctx, &ctx->canon_rowbuf, &ctx->canon_rowbuf_cap, (size_t)canon_rows(n) * kCanonCols));
+        TRY(grow(ctx, &ctx->canon_rowbuf, &ctx->canon_rowbuf_cap, (size_t)canon_strands(n) * kCanonCols)); // (rows, or strands)
         if (!ctx->h_far) HIPCHK(hipHostMalloc((void **)&ctx->h_far, sizeof(int), hipHostMallocDefault));
         // the first iteration's shift of p: the scene's centroid (all ranks'), where run_init put the
         // model's centre c -- a scene far from the model would otherwise cancel (D / sigma)^2 of the
@@ -2645,7 +2645,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     if (canon && cert_env && grid_iter_on() && ctx->g_pts32) {
         TRY(grow(ctx, &ctx->cert_state, &ctx->cert_state_cap, n));
         TRY(fold_cert_counts(ctx)); // (an earlier run's counts into the stats first)
-        const int crows = canon_rows(n);
+        const int crows = canon_strands(n); // (rows or strands: nn_grid_iter2_kernel NWG)
         TRY(grow(ctx, &ctx->cert_counts, &ctx->cert_counts_cap, 2 * (size_t)crows));
         HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * (size_t)crows * sizeof(unsigned), ctx->st));
         ctx->cert_counts_rows = crows;
@@ -2680,6 +2680,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         HIPCHK(hipMemsetAsync(ctx->canon_ticket, 0, sizeof(int), ctx->st));
     }
     cs.fold_ticket = ctx->canon_ticket;
+    int rows_strands = 0; // (> 0: the last fused launch wrote the canonical rows as this many strands)
     // the canonical transform of the last Horn step's (s, R, t), in the form sa_t (its residual into
     // the rows' kSumErr column, and what the next search reads)
     auto canon_transform = [&](SeedArgs sa_t) -> int {
@@ -2702,12 +2703,14 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
         slot_ticket[sl] = ++ctx->flag_ticket;
         cs.hflag = ctx->d_flags + 4 * sl;
         cs.ticket = slot_ticket[sl];
+        const int strands = rows_strands; // (the fused kernel wrote the rows as strands)
+        rows_strands = 0;
         if (!lag) {
-            launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, horn ? 1 : 2, cs, ctx->st);
+            launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, horn ? 1 : 2, cs, ctx->st, strands);
             LAUNCHCHK("canon_fold");
             return ICP_OK;
         }
-        launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, horn ? 0 : 3, cs, ctx->st);
+        launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, horn ? 0 : 3, cs, ctx->st, strands);
         LAUNCHCHK("canon_fold");
         const bool tm = horn && slot >= 0 && ar_timed[slot];
         if (tm) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 3], ctx->st));
@@ -2730,12 +2733,14 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     // around the shifts run_init set (c), no error step before it (round 4: the reference's two
     // passes and an unshifted Horn step, four more launches)
     auto canon_first = [&]() -> int {
+        const int strands = rows_strands;
+        rows_strands = 0;
         if (!lag) {
-            launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, 4, cs, ctx->st);
+            launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, 4, cs, ctx->st, strands);
             LAUNCHCHK("canon_fold");
             return ICP_OK;
         }
-        launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, 0, cs, ctx->st);
+        launch_canon_fold(ctx->canon_rowbuf, (int)n, ctx->sums, 0, cs, ctx->st, strands);
         LAUNCHCHK("canon_fold");
         TRY(allreduce(ctx, ctx->sums, kNumSums));
         launch_horn_step(ctx->sums, N, ctx->c, true, ctx->amb_count, sd, ctx->st);
@@ -2800,7 +2805,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                                     grid_budget(ctx), (int)ctx->nm, ctx->m4, ctx->canon_rowbuf,
                                                     grid_policy ? &sd->far_acc : nullptr,
                                                     sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2,
-                                                    ctx->st, iter_dbg, 0, cert);
+                                                    ctx->st, iter_dbg, 0, cert, &rows_strands);
                     LAUNCHCHK("nn_grid_iter (first)");
                     if (timed) HIPCHK(hipEventRecord(ctx->iter_ev[5 * slot + 1], ctx->st));
                     ws = SeedState{};
@@ -2839,7 +2844,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
                                                     grid_budget(ctx), (int)ctx->nm, ctx->m4, ctx->canon_rowbuf,
                                                     grid_policy ? &sd->far_acc : nullptr,
                                                     sa_grid.far_box > 0 ? -1.0 : sa_grid.far_d2, ctx->amb_count + 2,
-                                                    ctx->st, iter_dbg, 1, cert);
+                                                    ctx->st, iter_dbg, 1, cert, &rows_strands);
                     if (iter_dbg && iter_debug_each) { // (ICP_ITER_DEBUG=2: each launch's counts, synchronising)
                         unsigned long long h[16];
                         HIPCHK(hipStreamSynchronize(ctx->st));

@@ -1440,10 +1440,16 @@ static_assert(32 * kIter2Slot + 32 / 2 <= kIter2Tile, "the hand-off slots and th
 #ifndef ICP_ITER2_WAVES
 #define ICP_ITER2_WAVES 4 // (waves a SIMD nn_grid_iter2_kernel is compiled for)
 #endif
+#ifndef ICP_ITER2_NWG_DEFAULT
+#define ICP_ITER2_NWG_DEFAULT 1 // (waves a workgroup of nn_grid_iter2_kernel; ICP_ITER2_NWG=4 at run time: a row)
+#endif
 // CH chunks a task (1: a chunk, two lanes a query in phases A and G; 2: chunks c and c + S of the
 // strand together, a lane a query -- the walkers of 64 queries packed, one task a wave at C4)
-template <int KR, int KU, int CH>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER2_WAVES))) void nn_grid_iter2_kernel(
+// NWG waves a workgroup: 4, the four strands of one canonical row (their sum formed in LDS), or
+// 1, one strand (its sums written as the strand's; the fold forms the rows, canon_row_value: the
+// same bits) -- a wave then frees its slot when it ends, not when its row's slowest wave does
+template <int KR, int KU, int CH, int NWG>
+__global__ __launch_bounds__(64 * NWG) __attribute__((amdgpu_waves_per_eu(ICP_ITER2_WAVES))) void nn_grid_iter2_kernel(
     int n, double *__restrict__ px, double *__restrict__ py, double *__restrict__ pz, double *__restrict__ yx,
     double *__restrict__ yy, double *__restrict__ yz, int *__restrict__ idx, const IterState *__restrict__ st,
     float4 *__restrict__ p32, GridView gv, int box, int budget, int nm, const double4 *__restrict__ m4,
@@ -1456,13 +1462,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     // tried here: s_memrealtime reads slowed the kernel 10x, so their phases meant nothing)
     constexpr bool kDbg = ICP_ITER2_DBG != 0;
     unsigned long long dcnt[4] = {0, 0, 0, 0};
-    constexpr int NW = kBlock / 64, QL = 2 / CH; // (lanes a query in phases A and G)
+    static_assert(NWG == 4 || NWG == 1, "a row or a strand a workgroup");
+    constexpr int NW = NWG, QL = 2 / CH; // (lanes a query in phases A and G)
     __shared__ double s_tile[NW][CH * kIter2Tile];
     if (st->done) return; // a frozen (converged) ICP iteration: nothing moves, nothing is searched
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, u = lane / QL, sub = lane % QL;
     const int C = canon_chunks((size_t)n), S = canon_strands((size_t)n), R = canon_rows((size_t)n);
-    const int wr = xcd_row((int)blockIdx.x, R, xcd_l); // (as nn_grid_iter_kernel: runs of rows an XCD)
-    const int s = wr * 4 + wave;
+    // (as nn_grid_iter_kernel: runs of rows an XCD -- for one-strand workgroups runs of 4 L strands)
+    const int s = NWG == 4 ? xcd_row((int)blockIdx.x, R, xcd_l) * 4 + wave
+                           : xcd_row((int)blockIdx.x, S, xcd_l > 0 ? 4 * xcd_l : xcd_l);
+    const int wr = s >> 2;
     double *const tile = s_tile[wave];
     double *const slots = tile;                            // (phases A-D) 32 CH slots of kIter2Slot doubles
     int *const wl = (int *)(tile + 32 * CH * kIter2Slot);  // (phase D) the task's walkers, in query order
@@ -1943,13 +1952,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
     if (kDbg && dbg && lane == 0)
         for (int f = 0; f < 4; ++f)
             if (dcnt[f]) atomicAdd(dbg + f, dcnt[f]);
-    // the workgroup's four strands -> its row (column k from lane k of each wave)
-    __shared__ double sh[NW][kCanonCols];
-    if (lane < kCanonCols) sh[wave][lane] = acc;
-    __syncthreads();
-    if (threadIdx.x < kCanonCols) {
-        const int k = threadIdx.x;
-        rows[(size_t)k * R + wr] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+    if constexpr (NWG == 4) { // the workgroup's four strands -> its row (column k from lane k of each wave)
+        __shared__ double sh[NW][kCanonCols];
+        if (lane < kCanonCols) sh[wave][lane] = acc;
+        __syncthreads();
+        if (threadIdx.x < kCanonCols) {
+            const int k = threadIdx.x;
+            rows[(size_t)k * R + wr] = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+        }
+    } else if (s < S && lane < kCanonCols) { // the strand's sums (strands by column: k S + s)
+        rows[(size_t)lane * S + s] = acc;
     }
     // the far count (the policy's), the big boxes and the certificate's counts: one atomic each
     __shared__ int s_cnt[4][NW];
@@ -1971,8 +1983,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
         if (threadIdx.x < 2) {
             int *dst = threadIdx.x == 0 ? far_acc : big_count;
             if (tot && dst) atomicAdd(dst, tot);
-        } else if (ca.counts) { // (this row's own counters: stream order separates the launches)
-            ca.counts[2 * wr + (threadIdx.x - 2)] += (unsigned)tot;
+        } else if (ca.counts && (NWG == 4 || s < S)) { // (this row's / strand's own counters: stream order separates the launches)
+            ca.counts[2 * (NWG == 4 ? wr : s) + (threadIdx.x - 2)] += (unsigned)tot;
         }
     }
 }
@@ -1982,8 +1994,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ICP_ITER
 bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,
                          const IterState *st_dev, float4 *p32, const GridView &gv, int box, int budget, int nm,
                          const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
-                         unsigned long long *dbg, int xform, const CertArgs &ca)
+                         unsigned long long *dbg, int xform, const CertArgs &ca, int *strands)
 {
+    if (strands) *strands = 0;
     if (n <= 0) return false;
     // ICP_ITER_STAGE=1: the task's union of boxes staged in LDS (measured slower: the staging's two
     // dependent round trips and the LDS-limited occupancy cost more than the gathers they save)
@@ -2021,12 +2034,27 @@ bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
             const char *e = getenv("ICP_ITER2_CH");
             return e && atoi(e) == 1 ? 1 : 2;
         }();
-        if (ch == 2)
-            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 2><<<R, kBlock, 0, st>>>(
+        // ICP_ITER2_NWG: waves a workgroup (1: a strand, the rows written as strands -- *strands; 4: a row)
+        static const int nwg = [] {
+            const char *e = getenv("ICP_ITER2_NWG");
+            return e && atoi(e) == 4 ? 4 : ICP_ITER2_NWG_DEFAULT;
+        }();
+        const int S = canon_strands((size_t)n);
+        if (strands) *strands = nwg == 1 ? S : 0;
+        if (ch == 2 && nwg == 1)
+            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 2, 1><<<S, 64, 0, st>>>(
+                n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
+                xform, xcd_l, ca, dbg);
+        else if (ch == 2)
+            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 2, 4><<<R, kBlock, 0, st>>>(
+                n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
+                xform, xcd_l, ca, dbg);
+        else if (nwg == 1)
+            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 1, 1><<<S, 64, 0, st>>>(
                 n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
                 xform, xcd_l, ca, dbg);
         else
-            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 1><<<R, kBlock, 0, st>>>(
+            nn_grid_iter2_kernel<ICP_ITER2_KR, ICP_ITER2_KU, 1, 4><<<R, kBlock, 0, st>>>(
                 n, px, py, pz, yx, yy, yz, idx, st_dev, p32, gv, box, budget, nm, m4, rows, far_acc, far_d2, big_count,
                 xform, xcd_l, ca, dbg);
         return ca.state != nullptr;

@@ -525,7 +525,8 @@ void launch_canon_moments(const int *idx, const double4 *m4, const double *px, c
 void launch_canon_transform(double *px, double *py, double *pz, const double *yx, const double *yy, const double *yz,
                             int n, const Xform *xf, const int *done, float4 *p32, double *rows, const SeedArgs &sa,
                             hipStream_t st);
-void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st);
+void launch_canon_fold(const double *rows, int n, double *sums, int mode, const CanonStep &cs, hipStream_t st,
+                       int strands = 0); // (strands > 0: rows given as canon_strands(n) strands, canon_row_value)
 // the fused grid iteration (icp_grid.hip, nn_grid_iter_kernel): the previous transform (st->xf) of
 // the scene in slot order, the exact seeded grid search of every point (box: cells a query's own
 // box may have before the whole wave takes it; budget: cells before every model point), and the
@@ -557,7 +558,8 @@ bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, 
                          const double4 *m4, double *rows, int *far_acc, double far_d2, int *big_count, hipStream_t st,
                          unsigned long long *dbg = nullptr, // (dbg: ICP_ITER_DEBUG's 12 counters)
                          int xform = 1, // (0: no pending transform -- a run's first iteration, seeds in idx / y)
-                         const CertArgs &ca = CertArgs{}); // (ca.state null: no certificate, every query walks)
+                         const CertArgs &ca = CertArgs{}, // (ca.state null: no certificate, every query walks)
+                         int *strands = nullptr); // (out: canon_strands(n) when rows were written as strands, else 0)
 // One-pass moments around the shifts of *st (identical on every rank): y = m[idx];
 // partial [sum (p - cp) (3), sum (y - cy) (3), sum (p - cp)(y - cy)^T (9), sum ||y - cy||^2,
 // sum ||p - cp||^2] (17, sums slots 0..16; horn_step(shifted) removes the shift)
