@@ -582,8 +582,8 @@ __device__ __forceinline__ int xcd_row(int b, int nb, int L)
 // coordinates to y (the correspondence cloud the moments then stream: no gather there), re-read
 // from pts at the position the scan met it (an L2 hit).
 // A box over `budget` cells (or a non-finite seed) queues the query for the second pass.
-template <int G, int KR, int KU, int W>
-__global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
+template <int G, int KR, int KU, int W, int TB = kBlock>
+__global__ __launch_bounds__(TB, W) void nn_grid_seeded_kernel(
     int n, const double *__restrict__ px, const double *__restrict__ py, const double *__restrict__ pz, GridView gv,
     int budget, const double *__restrict__ seedd, const double4 *__restrict__ m4, int *__restrict__ idx,
     double *__restrict__ yx, double *__restrict__ yy, double *__restrict__ yz, int *far_count,
@@ -591,9 +591,9 @@ __global__ __launch_bounds__(kBlock, W) void nn_grid_seeded_kernel(
 {
     if (stop && *stop) return; // a frozen (converged) ICP iteration
     const int sub = threadIdx.x & (G - 1);
-    const int groups = gridDim.x * (kBlock / G);
+    const int groups = gridDim.x * (TB / G);
     const int bx = xcd_row((int)blockIdx.x, (int)gridDim.x, xcd_remap);
-    for (int t = (bx * kBlock + threadIdx.x) / G; t < n; t += groups) {
+    for (int t = (bx * TB + threadIdx.x) / G; t < n; t += groups) {
         const int h = idx[t];
         const double q[3] = {px[t], py[t], pz[t]};
         double best = seedd[t];
@@ -2347,6 +2347,20 @@ void launch_nn_grid_seeded(int n, const double *px, const double *py, const doub
 #define SEEDED(K, ...)                                                                                       \
     K<__VA_ARGS__><<<blocks, kBlock, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz, far_count, \
                                               far_list, far_hint, stop, xcd_l, trim)
+    // One-wave workgroups for the whole-scene default form (a wave frees its slot alone: the first
+    // iteration 0.336-0.345 against 0.363-0.365 ms at C4; a sparse shard's form keeps 256 threads,
+    // slower there, profiles/r06/r06stb).  ICP_SEEDED_TB=256 / 64 forces either (A/B).
+    static const int seeded_tb = [] {
+        const char *e = getenv("ICP_SEEDED_TB");
+        return e ? atoi(e) : 0;
+    }();
+    if (f == 0 && (seeded_tb == 64 || (seeded_tb != 256 && !xcd_remap))) {
+        int b64 = std::max(1, std::min((n + 64 / 2 - 1) / (64 / 2), 65536));
+        if (xcd_remap) b64 = (b64 + 7) / 8 * 8;
+        nn_grid_seeded_kernel<2, 2, 2, 1, 64><<<b64, 64, 0, st>>>(n, px, py, pz, gv, budget, seedd, m4, idx, yx, yy, yz,
+                                                                  far_count, far_list, far_hint, stop, xcd_l, trim);
+        return;
+    }
     switch (f) {
     case 1: SEEDED(nn_grid_seeded_kernel, 4, 2, 2, 1); break;
     case 2: SEEDED(nn_grid_seeded_kernel, 4, 2, 4, 1); break;
