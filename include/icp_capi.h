@@ -171,7 +171,11 @@ int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm);
 int icp_set_scene_device(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total);
 /* ... reading the array after the work enqueued so far on `producer` only (a hipStream_t of the
  * context's device; NULL = the legacy default stream): the context's stream waits for an event
- * recorded there, with no device synchronisation.  Work on other streams is not waited for. */
+ * recorded there, with no device synchronisation.  Work on other streams is not waited for.
+ * These two are stream-ordered: they may return before the array has been read (the model
+ * setter still waits for its bounding box; the scene setter does not wait at all), so the array
+ * must stay valid and unmodified until a synchronising call on the context returns (icp_run,
+ * icp_get_*); errors of the enqueued work surface there. */
 int icp_set_model_device_stream(icp_ctx *ctx, const double *m_xyz_dev, size_t nm, void *producer);
 int icp_set_scene_device_stream(icp_ctx *ctx, const double *p_xyz_dev, size_t np_local, size_t np_total,
                                 void *producer);

@@ -1649,7 +1649,11 @@ static bool kd_host()
 // model has passed its checks.
 // aos_dev (nullable): the model's AoS copy in device memory (icp_set_model_device), else ctx->stage.
 // m_xyz: the host copy, for the host-side images (small models, ICP_KD_HOST, the CPU rule)
-static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const double *aos_dev = nullptr)
+// stream_ordered (icp_set_model_device_stream): no closing synchronisation when no host buffer
+// feeds the device work -- the images are built on the context's stream, which every later call
+// uses, and the caller's array is read there (its contract: unchanged until icp_run returns)
+static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const double *aos_dev = nullptr,
+                            bool stream_ordered = false)
 {
     const double *aos = aos_dev ? aos_dev : ctx->stage;
     if (!ctx->mstat_part) {
@@ -1755,7 +1759,7 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
             ctx->pm_seed_big = 4.0 * d2[nb16 / 2];
         }
     }
-    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (!stream_ordered || !pm.empty() || !kd_h.empty()) HIPCHK(hipStreamSynchronize(ctx->st));
     if (nm <= (size_t)std::max(kPersistMaxModel, kPersistMidMaxModel) || ctx->nn_rule == ICP_NN_RULE_CPU_SQRT)
         ctx->model_host.assign(m_xyz, m_xyz + 3 * nm);
     else
@@ -1776,7 +1780,7 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
                         ctx->c[2], ctx->scene.f, ctx->st);
         LAUNCHCHK("make_f32");
         ctx->p32_stale = false;
-        HIPCHK(hipStreamSynchronize(ctx->st));
+        if (!stream_ordered) HIPCHK(hipStreamSynchronize(ctx->st));
     }
     return ICP_OK;
 }
@@ -1826,7 +1830,7 @@ static int set_model_device_impl(icp_ctx *ctx, const double *m_xyz_dev, size_t n
         HIPCHK(hipMemcpyAsync(host.data(), m_xyz_dev, sizeof(double) * 3 * nm, hipMemcpyDeviceToHost, ctx->st));
         HIPCHK(hipStreamSynchronize(ctx->st));
     }
-    return set_model_staged(ctx, host.empty() ? nullptr : host.data(), nm, m_xyz_dev);
+    return set_model_staged(ctx, host.empty() ? nullptr : host.data(), nm, m_xyz_dev, !any_stream);
 }
 
 int icp_set_model_device(icp_ctx *ctx, const double *m_xyz_dev, size_t nm)
@@ -1931,8 +1935,9 @@ static int set_scene_device_impl(icp_ctx *ctx, const double *p_xyz_dev, size_t n
     TRY(grow_cloud(ctx, ctx->scene, np_local, true));
     bool slot = false;
     TRY(scene_from_aos(ctx, p_xyz_dev, np_local, &slot)); // (the caller's array: no copy)
-    // the caller's array is read on the context's stream: done before the call returns
-    if (np_local) HIPCHK(hipStreamSynchronize(ctx->st));
+    // the caller's array is read on the context's stream: done before icp_set_scene_device returns;
+    // icp_set_scene_device_stream is stream-ordered (the array unchanged until icp_run returns)
+    if (np_local && any_stream) HIPCHK(hipStreamSynchronize(ctx->st));
     return set_scene_common(ctx, np_local, np_total, slot);
 }
 

@@ -346,7 +346,8 @@ class Context:
         pointer, e.g. a torch tensor's data_ptr()).  stream None: read after all work enqueued so
         far on the device (a device synchronisation); else a HIP stream handle (e.g.
         torch.cuda.current_stream().cuda_stream): read after the work enqueued on that stream
-        (icp_set_model_device_stream, no host synchronisation)."""
+        (icp_set_model_device_stream, no host synchronisation; stream-ordered: keep the array alive
+        and unmodified until run() or another synchronising call returns)."""
         if stream is None or not hasattr(lib(), "icp_set_model_device_stream"):
             self._check(lib().icp_set_model_device(self._h, C.c_void_p(ptr), nm))
         else:

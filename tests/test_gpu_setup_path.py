@@ -99,6 +99,33 @@ def test_device_arrays_written_on_another_stream(amd, form):
     assert_same(a, b)
 
 
+def test_scene_stream_setter_is_stream_ordered(amd):
+    """icp_set_scene_device_stream returns before the producer's copy has landed (no host wait: the
+    context's stream waits for the producer's event) and the run still reads the copied scene."""
+    n = 1 << 16
+    m, p = amd.synthetic_pair(n, seed=21)
+    with amd.Context(0) as ctx:
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        a = trajectory(ctx)
+    dm = torch.from_numpy(m).to("cuda:0")
+    dp = torch.zeros((n, 3), dtype=torch.float64, device="cuda:0")
+    hp = torch.from_numpy(p).pin_memory()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with amd.Context(0) as ctx:
+        ctx.set_model_device(dm.data_ptr(), n, stream=side.cuda_stream)
+        done = torch.cuda.Event()
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(400_000_000)  # (cycles: ~0.2 s)
+            dp.copy_(hp, non_blocking=True)
+            done.record(side)
+        ctx.set_scene_device(dp.data_ptr(), n, stream=side.cuda_stream)
+        assert not done.query()  # the setter did not wait for the producer
+        b = trajectory(ctx)
+    assert_same(a, b)
+
+
 def test_scene_before_model_matches_after(amd):
     n = 1 << 16
     m0, _ = amd.synthetic_pair(n, seed=3)
