@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_kernel(const double *
 // The same fold, one column a workgroup (18 workgroups: the rows' 295 KB read by 18 CUs instead
 // of one): workgroup k computes column k exactly as canon_fold_kernel does (thread t's rows in
 // order, the wave trees, the 8 waves' pairwise tree: the same bits).  MODE 1: the last workgroup
-// to finish (an agent-scope ticket, release before and acquire after) runs the error step and
+// to finish (a relaxed ticket after write-through column sums, icp_fold.h's hand-off) runs the error step and
 // the Horn step on the 18 sums.  MODE 0: the sums only (several ranks: the all-reduce follows).
 template <int MODE>
 __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const double *__restrict__ rows, int R,
@@ -315,21 +315,23 @@ __global__ __launch_bounds__(kFoldThreads) void canon_fold_cols_kernel(const dou
         for (int span = 1; span < kFoldThreads / 64; span <<= 1)
 #pragma unroll
             for (int i = 0; i < kFoldThreads / 64; i += 2 * span) t[i] = t[i] + t[i + span];
-        __hip_atomic_store(sums + k, t[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pub_store(sums + k, t[0]); // (write-through: the hand-off of icp_fold.h, no release fence)
         if (MODE == 0 && k == 0) // (several ranks: the far count rides on the all-reduce)
             sums[kSumFar] = (double)__hip_atomic_load(&cs.s->far_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (MODE != 0) {
-            __atomic_thread_fence(__ATOMIC_RELEASE); // (this column before the ticket)
-            s_last = __hip_atomic_fetch_add(cs.fold_ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // (this column has landed before the ticket)
+            s_last = __hip_atomic_fetch_add(cs.fold_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                      kCanonCols - 1;
         }
     }
     if constexpr (MODE == 0) return;
     __syncthreads();
     if (!s_last || threadIdx.x != 0) return;
-    __atomic_thread_fence(__ATOMIC_ACQUIRE); // (every column's sum)
-    for (int i = 0; i < kCanonCols; ++i) s_sum[i] = __hip_atomic_load(sums + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *cs.fold_ticket = 0; // (the next iteration's ticket: stream order puts the next fold after this kernel)
+    // every column's sum by write-through-coherent loads: no agent-scope release / acquire fences
+    // (their L2 write-back and invalidate; with the mirror's fewer host writes, icp_fold.h, the fold
+    // is 10.7 -> 10.1 us at C4, profiles/r06/r06fold3/)
+    for (int i = 0; i < kCanonCols; ++i) s_sum[i] = pub_load(sums + i);
+    __hip_atomic_store(cs.fold_ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // (the next iteration's ticket)
     if constexpr (MODE == 1)
         err_step_body(s_sum, cs.N, cs.threshold, cs.max_iter, cs.err_trace, cs.s, cs.hflag, cs.ticket, cs.h_state,
                       cs.h_trace);

@@ -80,9 +80,18 @@ __device__ __forceinline__ void err_step_body(const double *__restrict__ sums, d
         h_trace[s->iter] = err; // mapped host copies: the run's result needs no copy back
         s->iter += 1;
         if (err < threshold || s->iter >= max_iter) s->done = 1; // gpu.cc:79-80
-        const int *src = (const int *)s;
-        int *dst = (int *)h_state;
-        for (size_t k = 0; k < sizeof(IterState) / sizeof(int); ++k) dst[k] = src[k];
+        // the mirror: every field once the run is done (the result: iter, srt, nn_counts); before
+        // that only what the host reads while the run goes on (the policy's far_acc and queued2) --
+        // each field is a posted write over the host link that the ticket's release waits for
+        if (s->done) {
+            const int *src = (const int *)s;
+            int *dst = (int *)h_state;
+            for (size_t k = 0; k < sizeof(IterState) / sizeof(int); ++k) dst[k] = src[k];
+        } else {
+            h_state->iter = s->iter;
+            h_state->far_acc = s->far_acc;
+            h_state->queued2 = s->queued2;
+        }
         // (far_coherent: s is global and this launch's workgroups added to s->far_acc -- a fused
         // transform -- so its count is read at agent scope; s may be an LDS copy otherwise)
         if (far_coherent) h_state->far_acc = __hip_atomic_load(&s->far_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
