@@ -327,9 +327,9 @@ struct icp_ctx {
     hipEvent_t order_ev = nullptr; // icp_set_*_device_stream: the producer stream's point to wait for
     int4 *cert_state = nullptr;
     size_t cert_state_cap = 0;
-    unsigned *cert_counts = nullptr; // (2 per canonical row: certified, walked -- CertArgs::counts)
+    unsigned long long *cert_counts = nullptr; // (2 per strand: certified, walked -- CertArgs::counts)
     size_t cert_counts_cap = 0;
-    int cert_counts_rows = 0; // (rows the last run counted into cert_counts, not yet in stats)
+    int cert_counts_rows = 0; // (strands the runs since the last fold counted into cert_counts, not yet in stats)
     char *tail_backup = nullptr;              // icp_run with the fused tail: the starting scene / idx
     size_t tail_backup_cap = 0;
     double4 *b_gctr = nullptr;                // v2: per-group (centre, D)
@@ -768,9 +768,9 @@ static int sum_cert_counts(const icp_ctx *ctx, long long out[2])
 {
     out[0] = out[1] = 0;
     if (ctx->cert_counts_rows <= 0 || !ctx->cert_counts) return ICP_OK;
-    std::vector<unsigned> h(2 * (size_t)ctx->cert_counts_rows);
+    std::vector<unsigned long long> h(2 * (size_t)ctx->cert_counts_rows);
     if (hipStreamSynchronize(ctx->st) != hipSuccess ||
-        hipMemcpy(h.data(), ctx->cert_counts, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(h.data(), ctx->cert_counts, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost) != hipSuccess)
         return ICP_E_HIP;
     for (size_t r = 0; r < h.size(); r += 2) {
         out[0] += h[r];
@@ -2649,11 +2649,16 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     bool cert_prev = false;
     if (canon && cert_env && grid_iter_on() && ctx->g_pts32) {
         TRY(grow(ctx, &ctx->cert_state, &ctx->cert_state_cap, n));
-        TRY(fold_cert_counts(ctx)); // (an earlier run's counts into the stats first)
+        // the counts accumulate on the device over the runs of one scene size (64-bit: no wrap),
+        // read when the stats are; another size folds them into the stats first (a synchronisation
+        // the runs of a registration loop do not pay: 60 us a run at C4, profiles/r06/r06fold3)
         const int crows = canon_strands(n); // (rows or strands: nn_grid_iter2_kernel NWG)
-        TRY(grow(ctx, &ctx->cert_counts, &ctx->cert_counts_cap, 2 * (size_t)crows));
-        HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * (size_t)crows * sizeof(unsigned), ctx->st));
-        ctx->cert_counts_rows = crows;
+        if (ctx->cert_counts_rows != crows) {
+            TRY(fold_cert_counts(ctx));
+            TRY(grow(ctx, &ctx->cert_counts, &ctx->cert_counts_cap, 2 * (size_t)crows));
+            HIPCHK(hipMemsetAsync(ctx->cert_counts, 0, 2 * (size_t)crows * sizeof(ctx->cert_counts[0]), ctx->st));
+            ctx->cert_counts_rows = crows;
+        }
         cert.state = ctx->cert_state;
         cert.two = cert_two;
         cert.skin = cert_skin / ctx->grid.inv_h;
@@ -3172,7 +3177,7 @@ static int run_loop(icp_ctx *ctx, int max_iter, double threshold, double *err_tr
     }
     // (every transform of a policy run wrote the seed distances, whatever its form; the next run
     // may start from them)
-    // (cert_counts: folded into the stats when they are read or the next run starts)
+    // (cert_counts: read with the stats, or folded into them when a run of another size starts)
     ctx->seedd_valid = grid_policy && ws.seedd;
     ctx->last_far = far_obs;
     ctx->last_q2 = q2_obs;
@@ -3647,7 +3652,7 @@ int icp_get_stats(const icp_ctx *ctx, icp_stats *out)
 {
     if (!ctx || !out) return ICP_E_ARG;
     *out = ctx->stats;
-    long long cc[2]; // (the last run's certificate counts, not yet folded)
+    long long cc[2]; // (the runs' certificate counts still on the device)
     if (sum_cert_counts(ctx, cc) != ICP_OK) return ICP_E_HIP;
     out->run_certified += cc[0];
     out->run_walked += cc[1];
@@ -3675,7 +3680,7 @@ int icp_reset_stats(icp_ctx *ctx)
     HIPCHK(hipSetDevice(ctx->device));
     if (ctx->cert_audit) TRY(cert_audit_reset(ctx));
     ctx->stats = icp_stats{};
-    ctx->cert_counts_rows = 0; // (the last run's certificate counts go with the rest)
+    ctx->cert_counts_rows = 0; // (the device's certificate counts go with the rest: zeroed at the next run)
     ctx->stats.last_filter = -1;
     return ICP_OK;
 }

@@ -1984,7 +1984,7 @@ __global__ __launch_bounds__(64 * NWG) __attribute__((amdgpu_waves_per_eu(ICP_IT
             int *dst = threadIdx.x == 0 ? far_acc : big_count;
             if (tot && dst) atomicAdd(dst, tot);
         } else if (ca.counts && (NWG == 4 || s < S)) { // (this row's / strand's own counters: stream order separates the launches)
-            ca.counts[2 * (NWG == 4 ? wr : s) + (threadIdx.x - 2)] += (unsigned)tot;
+            ca.counts[2 * (NWG == 4 ? wr : s) + (threadIdx.x - 2)] += (unsigned long long)tot;
         }
     }
 }

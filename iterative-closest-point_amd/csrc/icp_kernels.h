@@ -542,7 +542,7 @@ struct GridView;
 // point without a walk.  valid: the state is the one the previous fused iteration of this run
 // wrote (else every query walks and the state is written fresh); two = 0: the one-point form
 // (R3 and pair.y unused); skin: the radius a walk scans beyond its seed distance (model units);
-// counts (nullable): per canonical row r (= workgroup), counts[2 r] += queries certified,
+// counts (nullable): per strand / row r (= workgroup), counts[2 r] += queries certified,
 // counts[2 r + 1] += queries walked -- plain adds by the row's own workgroup (a device atomic
 // per workgroup on one address serialised the launch's tail: 15 us a launch at C4).
 struct CertArgs {
@@ -550,7 +550,7 @@ struct CertArgs {
     int valid = 0;
     int two = 1;
     double skin = 0.0;
-    unsigned *counts = nullptr;
+    unsigned long long *counts = nullptr; // (64-bit: accumulated over the runs of one scene size)
 };
 // Returns true when the launch wrote the certificate state (ca.state non-null, the certificate form).
 bool launch_nn_grid_iter(int n, double *px, double *py, double *pz, double *yx, double *yy, double *yz, int *idx,

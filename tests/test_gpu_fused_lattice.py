@@ -104,3 +104,39 @@ def test_fused_iteration_matches_brute_force(amd, oracle, name):
         _, ref = oracle.closest_blocked(cur[sel], m)
         assert np.array_equal(got[sel], ref), (name, k, int(np.sum(got[sel] != ref)))
     assert certified > 0  # the certificate settled queries in these runs
+
+
+def test_certificate_counts_accumulate_over_runs(amd):
+    """The certificate's per-strand counts stay on the device across runs of one scene size (no
+    synchronisation at a run's start), fold into the stats at a size change, and reset with them."""
+    n = 1 << 17
+    m, p = amd.synthetic_pair(n, seed=5)
+    m2, p2 = amd.synthetic_pair(n // 2 + 77, seed=6)
+    def counts(st):
+        return st["run_certified"], st["run_walked"]
+    with amd.Context(0) as ctx:
+        ctx.set_nn_variant(amd.VARIANT_GRID)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        ctx.run(6, -1.0)
+        one = counts(ctx.stats())
+        assert one[0] > 0 and one[1] > 0
+        ctx.set_scene(p)
+        ctx.run(6, -1.0)
+        assert counts(ctx.stats()) == (2 * one[0], 2 * one[1])
+        with amd.Context(0) as c2:  # another size: its counts alone
+            c2.set_nn_variant(amd.VARIANT_GRID)
+            c2.set_model(m2)
+            c2.set_scene(p2)
+            c2.run(6, -1.0)
+            small = counts(c2.stats())
+        ctx.set_model(m2)
+        ctx.set_scene(p2)
+        ctx.run(6, -1.0)  # (a size change: the first two runs' counts fold into the stats)
+        assert counts(ctx.stats()) == (2 * one[0] + small[0], 2 * one[1] + small[1])
+        ctx.reset_stats()
+        assert counts(ctx.stats()) == (0, 0)
+        ctx.set_model(m)
+        ctx.set_scene(p)
+        ctx.run(6, -1.0)
+        assert counts(ctx.stats()) == one
