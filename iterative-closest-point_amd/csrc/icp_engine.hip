@@ -227,6 +227,12 @@ struct icp_ctx {
     size_t digest_cap = 0;
     double4 *m4 = nullptr;      // model as (x, y, z, 0) doubles: one read per random gather
     size_t m4_cap = 0;
+    // the next model's SoA copy and double4 rows, built while its checks are read back and
+    // swapped with model / m4 when they pass (set_model_staged)
+    DevCloud model_alt;
+    double4 *m4_alt = nullptr;
+    size_t m4_alt_cap = 0;
+    hipEvent_t mstat_ev = nullptr; // (the checks' read-back)
     unsigned *seed16 = nullptr; // seeded f16 filter: per-query shift (icp_run iterations >= 2)
     size_t seed16_cap = 0;
     bool last_search_timed = false; // the per-operation search recorded its events
@@ -1543,6 +1549,8 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     free_cloud(ctx->model);
+    free_cloud(ctx->model_alt);
+    if (ctx->m4_alt) (void)hipFree(ctx->m4_alt);
     free_cloud(ctx->scene);
     free_cloud(ctx->Y);
     free_cloud(ctx->qa);
@@ -1580,6 +1588,7 @@ void icp_ctx_destroy(icp_ctx *ctx)
     if (ctx->h_io) (void)hipHostFree(ctx->h_io);
     for (auto e : ctx->iter_ev) (void)hipEventDestroy(e);
     if (ctx->order_ev) (void)hipEventDestroy(ctx->order_ev);
+    if (ctx->mstat_ev) (void)hipEventDestroy(ctx->mstat_ev);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -1666,7 +1675,15 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     launch_model_stats(aos, (int)nm, ctx->mstat_part, ctx->mstat_out, ctx->st);
     LAUNCHCHK("model_stats");
     HIPCHK(hipMemcpyAsync(ctx->h_mstat, ctx->mstat_out, sizeof(double) * 10, hipMemcpyDeviceToHost, ctx->st));
-    HIPCHK(hipStreamSynchronize(ctx->st));
+    if (!ctx->mstat_ev) HIPCHK(hipEventCreateWithFlags(&ctx->mstat_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ctx->mstat_ev, ctx->st));
+    // the SoA fp64 copy and the double4 rows need no statistic: built into the spare buffers while
+    // the host waits for the checks (the wait was an idle gap of ~20 us at C4), swapped in below
+    TRY(grow_cloud(ctx, ctx->model_alt, nm, true));
+    TRY(grow(ctx, &ctx->m4_alt, &ctx->m4_alt_cap, nm));
+    launch_aos_to_soa4(aos, nm, ctx->model_alt.x, ctx->model_alt.y, ctx->model_alt.z, ctx->m4_alt, ctx->st);
+    LAUNCHCHK("aos_to_soa4");
+    HIPCHK(hipEventSynchronize(ctx->mstat_ev)); // (the checks only: the copy above runs on)
     if (ctx->h_mstat[9] != 0.0) return fail(ctx, ICP_E_RANGE, "model has non-finite coordinates");
     double c[3], lo[3], hi[3];
     for (int k = 0; k < 3; ++k) {
@@ -1696,9 +1713,9 @@ static int set_model_staged(icp_ctx *ctx, const double *m_xyz, size_t nm, const 
     // and its MFMA operand order, the f16 split image at S = 2^e with max |m - c| S in
     // [2^11, 2^12), the double4 rows, the grid
     const size_t nm_pad = (nm + kTile32 - 1) / kTile32 * kTile32;
-    TRY(grow_cloud(ctx, ctx->model, nm, true));
-    TRY(grow(ctx, &ctx->m4, &ctx->m4_cap, nm));
-    launch_aos_to_soa4(aos, nm, ctx->model.x, ctx->model.y, ctx->model.z, ctx->m4, ctx->st);
+    std::swap(ctx->model, ctx->model_alt);
+    std::swap(ctx->m4, ctx->m4_alt);
+    std::swap(ctx->m4_cap, ctx->m4_alt_cap);
     TRY(grow(ctx, &ctx->m32, &ctx->m32_cap, nm_pad));
     TRY(grow(ctx, &ctx->mperm, &ctx->mperm_cap, nm_pad));
     TRY(grow(ctx, &ctx->mm, &ctx->mm_cap, nm_pad));
