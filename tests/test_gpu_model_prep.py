@@ -158,3 +158,26 @@ def test_ensure_model_large_is_exact(amd):
         assert ctx.ensure_model(m3) is True
         _, i3 = ctx.closest_matrix(p[:1])
         assert i3[0] != i1[0]
+
+
+@pytest.mark.parametrize("bad", [np.nan, 1e300])
+def test_refused_model_keeps_the_resident_one(amd, bad):
+    """The model's SoA copy and double4 rows are built into spare buffers while its checks are
+    read back (set_model_staged): a refused model must leave the resident model whole -- large
+    enough for the device path (no host copy) and searched on the grid after the refusal."""
+    rng = np.random.default_rng(3)
+    good = rng.uniform(-1.0, 1.0, size=(1 << 17, 3))
+    m = rng.uniform(-1.0, 1.0, size=(1 << 17, 3))
+    m[777, 2] = bad
+    p = good[:4096] + 0.003
+    with amd.Context(0) as ctx:
+        ctx.set_model(good)
+        _, before = ctx.closest_matrix(p)
+        with pytest.raises(amd.ICPError) as e:
+            ctx.set_model(m)
+        assert e.value.code == amd.ICP_E_RANGE
+        _, after = ctx.closest_matrix(p)
+    assert np.array_equal(before, after)
+    sel = np.arange(0, 4096, 64)
+    d = ((p[sel, None, :] - good[None, :, :]) ** 2).sum(-1)
+    assert np.array_equal(after[sel], d.argmin(axis=1))
