@@ -309,6 +309,9 @@ typedef struct icp_bundle_audit_result {
 int icp_bundle_audit(icp_ctx *ctx, int groups, icp_bundle_audit_result *out);
 int icp_get_index_digest(icp_ctx *ctx, uint64_t *out, size_t cap);
 
+/* The counters since the context was created or icp_reset_stats.  run_certified / run_walked are
+ * kept on the device while the runs' scene size stays the same (no synchronisation at a run's
+ * start), so icp_get_stats synchronises the context's stream to read them. */
 int icp_get_stats(const icp_ctx *ctx, icp_stats *out);
 int icp_reset_stats(icp_ctx *ctx);
 /* Instrumentation of the bundle filter (ICP_NN_VARIANT_BUNDLE): with enable = 1 its searches
