@@ -1440,6 +1440,9 @@ static_assert(32 * kIter2Slot + 32 / 2 <= kIter2Tile, "the hand-off slots and th
 #ifndef ICP_ITER2_WAVES
 #define ICP_ITER2_WAVES 4 // (waves a SIMD nn_grid_iter2_kernel is compiled for)
 #endif
+#ifndef ICP_ITER2_GFLOOR
+#define ICP_ITER2_GFLOOR 1 // (1: G = floor(64 / walkers) lanes a walker; 0: the largest power of two that fits)
+#endif
 #ifndef ICP_ITER2_NWG_DEFAULT
 #define ICP_ITER2_NWG_DEFAULT 1 // (waves a workgroup of nn_grid_iter2_kernel; ICP_ITER2_NWG=4 at run time: a row)
 #endif
@@ -1613,8 +1616,12 @@ __global__ __launch_bounds__(64 * NWG) __attribute__((amdgpu_waves_per_eu(ICP_IT
         for (int b0 = 0; b0 < nW; b0 += 32) {
             if (kDbg) dcnt[2] += 1;
             const int nb = min(32, nW - b0);
+            // G lanes a walker: every lane the batch can use (17 walkers: 3 lanes each, not 2 -- a
+            // third fewer rows a lane); wi = lane / G exactly by the reciprocal (lane < 64, G <= 64)
             const int lg = nb > 16 ? 1 : nb > 8 ? 2 : nb > 4 ? 3 : nb > 2 ? 4 : nb > 1 ? 5 : 6;
-            const int G = 1 << lg, wi = lane >> lg, ws = lane & (G - 1);
+            const int G = ICP_ITER2_GFLOOR ? 64 / nb : 1 << lg;
+            const int ginv = (65536 + G - 1) / G;
+            const int wi = (lane * ginv) >> 16, ws = lane - wi * G, gbase = wi * G;
             const bool wact = wi < nb;
             const int wu = wl[b0 + (wact ? wi : 0)];
             const double *const ws_sl = slots + wu * kIter2Slot;
@@ -1804,13 +1811,18 @@ __global__ __launch_bounds__(64 * NWG) __attribute__((amdgpu_waves_per_eu(ICP_IT
             // the walker's G lanes: the (D64, index) minimum, its position and coordinates; with the
             // certificate also the others (the two lists, and the sub-group winner that loses a merge
             // -- one with no position here was scanned by a lane of another sub-group, which holds it)
+            // (recursive doubling over the next power of two: a partner past the walker's G lanes
+            // is the identity; lane ws = 0 ends with every lane of its walker, the only one read)
             for (int o = 1; o < G; o <<= 1) {
-                const double ob = __shfl_xor(wb, o, 64);
-                const int oi = __shfl_xor(wbi, o, 64), ok2 = __shfl_xor(bk, o, 64);
+                const int pw = ws ^ o;
+                const bool pin = pw < G;
+                const int pl = gbase + (pin ? pw : ws);
+                const double ob = pin ? __shfl(wb, pl, 64) : INFINITY;
+                const int oi = pin ? __shfl(wbi, pl, 64) : -1, ok2 = pin ? __shfl(bk, pl, 64) : -1;
                 const bool theirs = ob < wb || (ob == wb && (unsigned)oi < (unsigned)wbi);
                 if (cert_on) {
-                    const float oa1 = __shfl_xor(a1, o, 64), oa2 = __shfl_xor(a2, o, 64);
-                    const int ok1 = __shfl_xor(k1, o, 64);
+                    const float oa1 = pin ? __shfl(a1, pl, 64) : INFINITY, oa2 = pin ? __shfl(a2, pl, 64) : INFINITY;
+                    const int ok1 = pin ? __shfl(k1, pl, 64) : -1;
                     if (a1 <= oa1) {
                         a2 = fminf(a2, oa1);
                     } else {
@@ -1856,7 +1868,7 @@ __global__ __launch_bounds__(64 * NWG) __attribute__((amdgpu_waves_per_eu(ICP_IT
                     }
                 }
                 group_lex_min<64>(b2, bj);
-                if ((lane >> lg) == (bl >> lg)) {
+                if (wi == ((bl * ginv) >> 16)) {
                     wb = b2;
                     wbi = bj < 0 ? 0 : bj;
                     whole = true;
