@@ -1391,8 +1391,8 @@ __global__ __launch_bounds__(kBlock * G / 2) __attribute__((amdgpu_waves_per_eu(
 //   A  (two lanes a query) the transform, the residual (the seed distance), the policy's far
 //      count, p' written; the exclusion certificate (below) settles the query, or it is a walker:
 //      its state (p', seed, seed distance) goes to an LDS slot;
-//   D  (the walkers, packed) the task's walkers get G = 64 / 2^k lanes each (2^k >= their count):
-//      a task with 5..8 walkers walks each over 8 lanes, so a wave's walk takes as many load
+//   D  (the walkers, packed) the task's walkers get G = floor(64 / their count) lanes each (at most
+//      32 a batch): a task with 7 walkers walks each over 9 lanes, so a wave's walk takes as many load
 //      rounds as its busiest walker's rows / G, where the two-lane kernel took its busiest query's
 //      rows / 2 whatever the rest (the walk itself is that kernel's: a row's x-run cut to the seed
 //      sphere's chord, fp32 screen, candidates in fp64); the winner, its coordinates and the next
@@ -1612,7 +1612,7 @@ __global__ __launch_bounds__(64 * NWG) __attribute__((amdgpu_waves_per_eu(ICP_IT
         if (walker && sub == 0) wl[__popcll(wm & ((1ull << lane) - 1ull))] = u;
         wave_sync();
         if (kDbg) dcnt[1] += nW;
-        // ---- D: the walkers, at most 32 at a time, G = 64 / 2^k lanes each
+        // ---- D: the walkers, at most 32 at a time, G = floor(64 / walkers) lanes each
         for (int b0 = 0; b0 < nW; b0 += 32) {
             if (kDbg) dcnt[2] += 1;
             const int nb = min(32, nW - b0);
