@@ -1432,7 +1432,7 @@ static_assert(32 * kIter2Slot + 32 / 2 <= kIter2Tile, "the hand-off slots and th
 #define ICP_ITER2_KU 4 // (the walk: points a lane loads together; 2 / 3: 7,950 / 8,225 against 8,235 it/s, profiles/r06/r06m_ab.txt)
 #endif
 #ifndef ICP_ITER2_KR
-#define ICP_ITER2_KR ICP_ITER_KR // (the walk: rows whose bounds a lane reads together)
+#define ICP_ITER2_KR 3 // (the walk: rows whose bounds a lane reads together; with floor(64 / walkers) lanes a walker 3 beats 2 by 2% and 1 / 4 lose, profiles/r06/r06kr)
 #endif
 #ifndef ICP_ITER2_KCAND
 #define ICP_ITER2_KCAND ICP_ITER_KCAND // (candidate records a lane loads together)
